@@ -1,0 +1,171 @@
+"""bench.py -- device-resident pcap->flow Mpackets/s on MI355X (BASELINE.json metric).
+
+Step = one pass of the `fluere offline` hot path over one batch of synthetic
+pcap records already resident in HBM: parse (parse_keys + parse_fluereflow),
+exact flow key, update_flow aggregation, the record finalisation, and -- for
+N > 1 -- the flow-table merge (one RCCL all_gather of per-flow summaries over
+xGMI + device merge on rank 0).  Weak scaling: every rank owns a fixed
+per-GPU shard of one global capture (packet-range sharding with global packet
+indices).  The same sharded pipeline runs at N = 1 (the gather is a no-op).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5u]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# per-GPU workload of each BASELINE config
+CONFIGS = {
+    "c2": dict(kind=0, per_gpu=10_000_000, flows=1000, seed=0xF10E0002, use_mac=False,
+               workload="10M x 64B UDP, 1k 5-tuples per GPU (BASELINE configs[1])"),
+    "c3": dict(kind=1, per_gpu=10_000_000, flows=100_000, seed=0xF10E0003, use_mac=False,
+               workload="10M IMIX 64/576/1500 TCP+UDP, 100k flows per GPU (BASELINE configs[2])"),
+    "c4": dict(kind=1, per_gpu=12_500_000, flows=125_000, seed=0xF10E0004, use_mac=False,
+               workload="IMIX TCP+UDP, 12.5M packets / 125k flows per GPU (BASELINE configs[3] at 8 GPUs)"),
+    "c5u": dict(kind=3, per_gpu=10_000_000, flows=50_000, seed=0xF10E0005, use_mac=True,
+                workload="10M x 64B untagged, 50k MAC pairs, --useMAC (BASELINE configs[4], untagged)"),
+}
+BYTES_PER_PKT = 80  # algorithmic: 16 B pcap record header + min(caplen, 64) B header window
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import fluere_amd
+    from fluere_amd import dist as fdist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    C = CONFIGS[args.config]
+    n_total = C["per_gpu"] * world
+    cfg = fluere_amd.synth_cfg(C["kind"], n_total, C["flows"], C["seed"])
+    first, n = fdist.shard_range(n_total, rank, world)
+
+    # synthetic capture generated directly in HBM (untimed)
+    b, o, nbytes = fluere_amd.synth_device(cfg, first, n)
+    torch.cuda.synchronize()
+    ctx = fluere_amd.FlowContext(use_mac=C["use_mac"], max_flows=max(1 << 16, 2 * C["flows"]), device=local)
+    fdist.set_index_base(ctx, first)
+    ctx.add_device_batch(b, nbytes, o, n)
+
+    sums_buf = None
+    kernel_ms = []
+
+    def step():
+        nonlocal sums_buf
+        s, lo, hi = fdist.export_summaries(ctx, sums_buf)
+        sums_buf = s if sums_buf is None or s.numel() > sums_buf.numel() else sums_buf
+        kernel_ms.append(ctx.last_kernel_ms())
+        if world > 1:
+            return fdist.gather_and_merge(ctx, s, lo, hi)
+        return fdist.merge_summaries(ctx, s, lo, hi)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    kernel_ms.clear()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_avg = float(km.item())
+    else:
+        kernel_avg = sum(kernel_ms) / len(kernel_ms)
+
+    if rank == 0:
+        ms_per_step = 1e3 * elapsed / args.steps
+        mpps = n_total / (elapsed / args.steps) / 1e6
+        achieved = BYTES_PER_PKT * n / (kernel_avg * 1e-3) / 1e9  # per-GPU launch (GB/s)
+        recs, ne = ctx.records()
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(prof):
+            traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
+        line = {
+            "metric": "Mpackets/s device-resident pcap->flow parse+key, 64B & IMIX, 1/2/4/8 GPU",
+            "value": round(mpps, 1),
+            "unit": "Mpackets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter-based generator, device-resident)",
+            "config": {"workload": C["workload"], "packets_total": n_total, "flows": C["flows"],
+                       "parallelism": f"packet-range shards x{world}, RCCL all_gather merge",
+                       "use_mac": C["use_mac"]},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_parse_agg", "kernel_ms": round(kernel_avg, 4),
+                         "algorithmic_bytes_per_launch": BYTES_PER_PKT * n},
+            "parse_key_mpps_per_gpu": round(n / (kernel_avg * 1e-3) / 1e6, 1),
+            "records": int(len(recs)),
+            "records_ended": int(ne),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, C)
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, C):
+    """The oracle (C restatement of the reference CPU path, single thread, pinned
+    to one core) over the same workload, timed over the reference's "Converted in"
+    window (pcap open -> end of packet loop, offline_fluereflows.rs:49,178)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import fluere_amd
+    import pyoracle
+    n = min(cfg.n_packets, 4_000_000)
+    sample = fluere_amd.synth_cfg(cfg.kind, n, cfg.n_flows, cfg.seed)
+    data = fluere_amd.synth_pcap(sample)
+    old = os.sched_getaffinity(0)
+    try:
+        os.sched_setaffinity(0, {sorted(old)[0]})
+        best = min(pyoracle.offline(data, use_mac=C["use_mac"])["loop_seconds"] for _ in range(2))
+    finally:
+        os.sched_setaffinity(0, old)
+    return {"value": round(n / best / 1e6, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} packets of the same synthetic capture, in memory, best of 2"}
+
+
+if __name__ == "__main__":
+    main()

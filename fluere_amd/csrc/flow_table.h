@@ -1,0 +1,128 @@
+// flow_table.h -- exact flow dictionary for MI355X.
+//
+// The reference keys its active-flow HashMap by the full Key
+// (src/net/types/key.rs:5-14: two IpAddr, two ports, protocol, two MACs) and
+// looks a packet up under Key and its reverse (offline_fluereflows.rs:97-130).
+// On the device both directions map to one *canonical* key (lower endpoint
+// first, endpoint = (ip, port, mac)) plus a direction bit, and the canonical
+// key is turned into a dense flow id through a chain of write-once hash
+// tables whose entries are single 64-bit words:
+//
+//   IPv4, no MAC:  T0[(lo_ip << 32) | hi_ip]                      -> s0
+//                  T1[(s0 << 40) | (lo_port << 24) | (hi_port << 8) | proto] -> s1 -> dense id
+//   otherwise:     the canonical key serialised to 32-bit units; level 0 takes
+//                  units 0 and 1, level k >= 1 takes (s_{k-1} << 32) | unit k+1.
+//
+// Each level is exact (the stored word *is* the key material), so the chain
+// is an injective map without any full-key compare, and every cross-workgroup
+// interaction is a 64-bit CAS whose returned value is authoritative: a plain
+// (possibly stale) load can only show EMPTY for a filled slot, never a wrong
+// key, because slots are written once.  No release/acquire hand-off between
+// workgroups is needed inside the launch (MI355X_MICROARCH.md, inter-workgroup
+// visibility).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fl {
+
+constexpr uint64_t EMPTY = ~0ull;
+constexpr uint64_t PENDING = ~0ull - 1;
+constexpr int N_TABLES = 14;        // 0,1: IPv4 fast chain; 2..13: generic levels 0..11
+constexpr int MAX_PROBE = 4096;
+constexpr uint32_t FAIL = 0xFFFFFFFFu;
+
+enum : uint32_t { ERR_TABLE_FULL = 1, ERR_FLOWS_FULL = 2, ERR_SPIN = 4 };
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct TableSet {
+    unsigned long long* tab[N_TABLES];  // (C + 1) entries of {key, val}; entry C holds the word EMPTY
+    uint32_t C;                          // power of two, <= 1 << 23
+    uint32_t fmax;                       // dense id capacity
+    uint32_t* n_flows;
+    uint32_t* err;
+    uint8_t* flow_key;                   // [fmax][56] canonical key of each dense id
+};
+
+// Returns the slot of `w` in table t, inserting it if absent (insert=true).
+__device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t w, bool insert) {
+    unsigned long long* tab = T.tab[t];
+    if (w == EMPTY) return T.C;  // the sentinel word has a dedicated slot
+    uint32_t h = (uint32_t)mix64(w) & (T.C - 1);
+    for (int p = 0; p < MAX_PROBE; p++) {
+        unsigned long long k = tab[2 * h];
+        if (k == w) return h;
+        if (k == EMPTY) {
+            if (!insert) return FAIL;
+            unsigned long long old = atomicCAS(&tab[2 * h], EMPTY, (unsigned long long)w);
+            if (old == EMPTY || old == w) return h;
+        }
+        h = (h + 1) & (T.C - 1);
+    }
+    atomicOr(T.err, ERR_TABLE_FULL);
+    return FAIL;
+}
+
+// Dense id of a final-level slot; the first caller assigns it.
+__device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t s, bool insert,
+                                             const uint8_t* key56) {
+    unsigned long long* val = &T.tab[t][2 * s + 1];
+    unsigned long long v = *val;
+    if (v < PENDING) return (uint32_t)v;
+    if (!insert) {
+        v = atomicOr(val, 0ull);
+        return v < PENDING ? (uint32_t)v : FAIL;
+    }
+    v = atomicCAS(val, EMPTY, PENDING);
+    if (v == EMPTY) {
+        uint32_t d = atomicAdd(T.n_flows, 1u);
+        if (d >= T.fmax) {
+            atomicOr(T.err, ERR_FLOWS_FULL);
+            d = FAIL;
+        } else {
+            uint32_t* dst = (uint32_t*)(T.flow_key + (size_t)d * 56);
+            const uint32_t* src = (const uint32_t*)key56;
+            for (int k = 0; k < 14; k++) dst[k] = src[k];
+        }
+        atomicExch(val, (unsigned long long)d);
+        return d;
+    }
+    for (int it = 0; v == PENDING && it < (1 << 20); it++) {
+        __builtin_amdgcn_s_sleep(2);
+        v = atomicOr(val, 0ull);  // memory-side read: coherent across XCDs
+    }
+    if (v >= PENDING) {
+        atomicOr(T.err, ERR_SPIN);
+        return FAIL;
+    }
+    return (uint32_t)v;
+}
+
+// Canonical key: 14 little-endian u32 words (also fluere_flow_summary.key):
+//   w[0..4) lo_ip, w[4..8) hi_ip (big-endian numeric words, IPv4 in w[0] / w[4])
+//   w[8]  = lo_port << 16 | hi_port
+//   w[9]  = kind << 8 | proto          (kind bit0: IPv6, bit1: MACs in key)
+//   w[10] = lo_mac[0..4) BE, w[11] = lo_mac[4..6) BE << 16
+//   w[12] = hi_mac[0..4) BE, w[13] = hi_mac[4..6) BE << 16
+struct CKey {
+    uint32_t w[14];
+};
+
+// Endpoint comparison (ip, port, mac) lexicographic in key-field order;
+// returns true when src > dst (the packet travels hi -> lo).
+__device__ __forceinline__ bool src_gt_dst(const uint32_t* sip, const uint32_t* dip, uint32_t sp, uint32_t dp,
+                                          uint64_t smac, uint64_t dmac, bool v6, bool macs) {
+    int n = v6 ? 4 : 1;
+    for (int k = 0; k < n; k++)
+        if (sip[k] != dip[k]) return sip[k] > dip[k];
+    if (sp != dp) return sp > dp;
+    if (macs && smac != dmac) return smac > dmac;
+    return false;
+}
+
+}  // namespace fl

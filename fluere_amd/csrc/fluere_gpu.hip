@@ -1,0 +1,1595 @@
+// fluere_gpu.hip -- MI355X kernels and the C ABI (include/fluere_gpu.h) for
+// the `fluere offline` hot path.
+//
+// Pipeline for one capture (all batches attached to a context):
+//   k_parse_agg   one streaming pass over the pcap records in HBM: parse
+//                 (parse_keys + parse_fluereflow), canonical flow key, exact
+//                 dense flow id (flow_table.h), and the update_flow sums /
+//                 min / max / flag counts / first-last packet indices,
+//                 pre-aggregated in LDS per workgroup and flushed with
+//                 coalesced atomics.                        <- roofline kernel
+//   k_finalize    one thread per flow: if the order-free aggregate is exactly
+//                 what the reference state machine would produce (certificate
+//                 below) build the FluereRecord, else mark the flow complex.
+//   complex flows (Mode A: no expiry can fire): their packets are gathered,
+//                 radix-sorted by (flow, packet index) and replayed by an exact
+//                 per-flow state machine (SYN gate, FIN/RST split).
+//   Mode B (capture span >= timeout, so expiries can fire): the exact global
+//                 state machine over per-packet metadata (k_seq_*).
+//
+// Certificate (Mode A, per flow): first create-eligible packet == first
+// packet of the flow (TCP: the first packet carries SYN) and no FIN/RST before
+// the last packet.  Then the reference creates the flow at its first packet,
+// every later packet updates it, and it is closed (if at all) by its last
+// packet -- so the record is the order-free aggregate, with orientation / ports
+// / tos / first taken from the first packet and `last` from the last one
+// (offline_fluereflows.rs:97-157, flows.rs:11-42).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/fluere_gpu.h"
+#include "flow_table.h"
+#include "parse.h"
+#include "synth.h"
+
+using namespace fl;
+
+namespace {
+
+constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
+constexpr int H = 2048;          // LDS direct-mapped flow slots (dense ids < H)
+constexpr int WIN_ITERS = 32;    // flush LDS every 32 x 1024 packets (u32 byte sums cannot wrap)
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr unsigned long long NONE64 = ~0ull;
+constexpr uint64_t IDX_MASK = (1ull << 40) - 1;
+
+struct Batch {
+    const uint8_t* bytes;
+    const uint32_t* offs;
+    uint64_t nbytes;
+    uint64_t n;
+    uint64_t first;  // global index of packet 0
+    uint32_t snap;
+    uint32_t flags;  // bit0 byte-swapped headers, bit1 nanosecond timestamps
+};
+
+struct Acc {
+    uint32_t* pk[2];
+    unsigned long long* by[2];
+    uint32_t* mn[2];  // min pkt, min ttl
+    uint32_t* mx[2];  // max pkt, max ttl
+    uint32_t* fl[8];  // fin syn rst psh ack urg ece cwr
+    unsigned long long* fa;  // first packet (any)
+    unsigned long long* fc;  // first create-eligible packet
+    unsigned long long* fr;  // first FIN/RST packet
+    unsigned long long* la;  // last packet
+    uint32_t* slots;         // [fmax][N_TABLES] chain slots (cleanup)
+};
+
+struct Glob {
+    unsigned long long valid, dropped, raw;
+    unsigned long long tmin, tmax;
+    unsigned long long n_rec;
+    unsigned long long n_complex, n_complex_pkts;
+    unsigned long long n_keys, n_heads;
+    unsigned long long generic_used;
+};
+
+#define HIPCHECK(x)                                  \
+    do {                                             \
+        hipError_t e_ = (x);                         \
+        if (e_ != hipSuccess) return FLUERE_E_HIP;   \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// per-packet front end shared by every kernel
+// ---------------------------------------------------------------------------
+struct Parsed {
+    PktInfo pi;
+    uint64_t t;
+    uint64_t smac, dmac;  // big-endian packed MACs of the keyed frame
+    uint32_t L;
+    uint8_t cls;          // 0 valid, 1 dropped (NetError), 2 raw class
+};
+
+__device__ __forceinline__ uint32_t hdr_word(uint32_t w, bool swapped) { return swapped ? bswap32(w) : w; }
+
+__device__ __forceinline__ void load_win(const Batch& B, uint32_t off, Win& W) {
+    const uint8_t* p = B.bytes + off;
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if ((uint64_t)off + 16 * c < B.nbytes) __builtin_memcpy(&v, p + 16 * c, 16);
+        W.w[4 * c + 0] = v.x; W.w[4 * c + 1] = v.y; W.w[4 * c + 2] = v.z; W.w[4 * c + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
+    uint64_t m = 0;
+    for (int k = 0; k < 6; k++) m = (m << 8) | p[k];
+    return m;
+}
+
+// mode: 0 production (fast path first), 1 general parser only
+__device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool macs, int mode, Parsed& P) {
+    uint32_t off = B.offs[li];
+    Win W;
+    load_win(B, off, W);
+    bool sw = B.flags & 1;
+    uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
+    uint32_t L = min(incl, B.snap);
+    uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
+    if (L > avail) L = (uint32_t)avail;
+    P.L = L;
+    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);  // time.rs:5-7
+    const uint8_t* fr = B.bytes + off + 16;
+    bool fast = (mode == 0) && parse_fast(W, L, P.pi);
+    if (!fast) {
+        PktInfo g;  // only this copy lives on the stack (parse_general is out of line)
+        parse_general(fr, L, g);
+        P.pi = g;
+    }
+    const PktInfo& pi = P.pi;
+    bool kbad = pi.kst != ST_OK && pi.kst != ST_RAW;
+    bool fbad = pi.fst != ST_OK && pi.fst != ST_RAW;
+    P.cls = (kbad || fbad) ? 1 : ((pi.kst == ST_RAW || pi.fst == ST_RAW) ? 2 : 0);
+    P.smac = P.dmac = 0;
+    if (macs && P.cls == 0) {
+        if (fast) {
+            // frame bytes 0..12 = record bytes 16..28
+            uint64_t d = 0, s = 0;
+            for (int k = 0; k < 6; k++) d = (d << 8) | W.b(16 + k);
+            for (int k = 0; k < 6; k++) s = (s << 8) | W.b(22 + k);
+            P.dmac = d; P.smac = s;
+        } else {
+            P.dmac = mac_be(fr + pi.frame_off);
+            P.smac = mac_be(fr + pi.frame_off + 6);
+        }
+    }
+}
+
+__device__ __forceinline__ int find_batch(const Batch* bs, int nb, uint64_t gi) {
+    int b = 0;
+    while (b + 1 < nb && bs[b + 1].first <= gi) b++;
+    return b;
+}
+
+__device__ __forceinline__ uint8_t canon_dir(const Parsed& P, bool macs) {
+    const PktInfo& pi = P.pi;
+    return src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs) ? 1 : 0;
+}
+
+// Canonical key of a parsed packet.  dir = 1 when the packet travels from the
+// higher endpoint to the lower one.
+__device__ __forceinline__ void canon_key(const Parsed& P, bool macs, CKey& k, uint8_t& dir) {
+    const PktInfo& pi = P.pi;
+    bool gt = src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs);
+    dir = gt ? 1 : 0;
+    const uint32_t* lo = gt ? pi.dip : pi.sip;
+    const uint32_t* hi = gt ? pi.sip : pi.dip;
+    uint32_t lop = gt ? pi.kdp : pi.ksp, hip = gt ? pi.ksp : pi.kdp;
+    uint64_t lom = gt ? P.dmac : P.smac, him = gt ? P.smac : P.dmac;
+    for (int j = 0; j < 4; j++) { k.w[j] = lo[j]; k.w[4 + j] = hi[j]; }
+    k.w[8] = (lop << 16) | hip;
+    uint32_t kind = (pi.v6 ? 1u : 0u) | (macs ? 2u : 0u);
+    k.w[9] = (kind << 8) | pi.kproto;
+    k.w[10] = macs ? (uint32_t)(lom >> 16) : 0; k.w[11] = macs ? (uint32_t)(lom & 0xFFFF) << 16 : 0;
+    k.w[12] = macs ? (uint32_t)(him >> 16) : 0; k.w[13] = macs ? (uint32_t)(him & 0xFFFF) << 16 : 0;
+}
+
+// Exact dense flow id of a canonical key (flow_table.h chains).
+__device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& k, bool insert, uint32_t* chain_out,
+                                                 unsigned long long* generic_used) {
+    const uint32_t kind = k.w[9] >> 8;
+    const bool v6 = kind & 1, macs = kind & 2;
+    uint32_t chain[N_TABLES];
+    for (int j = 0; j < N_TABLES; j++) chain[j] = NONE32;
+    uint32_t s;
+    int ft;
+    if (!v6 && !macs) {
+        s = tab_slot(T, 0, ((uint64_t)k.w[0] << 32) | k.w[4], insert);
+        if (s == FAIL) return FAIL;
+        chain[0] = s;
+        s = tab_slot(T, 1, ((uint64_t)s << 40) | ((uint64_t)k.w[8] << 8) | (k.w[9] & 0xFF), insert);
+        if (s == FAIL) return FAIL;
+        chain[1] = s;
+        ft = 1;
+    } else {
+        if (generic_used && insert) *generic_used = 1;
+        // 32-bit units: kind|proto, ports, lo_ip, hi_ip, [lo_mac, hi_mac]
+        uint32_t u[13];
+        u[0] = k.w[9];
+        u[1] = k.w[8];
+        const uint32_t m0 = k.w[10], m1 = k.w[11] | (k.w[12] >> 16), m2 = (k.w[12] << 16) | (k.w[13] >> 16);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            u[2 + j] = v6 ? k.w[j] : (j == 0 ? k.w[0] : j == 1 ? k.w[4] : j == 2 ? m0 : m1);
+            u[6 + j] = v6 ? k.w[4 + j] : (j == 0 ? m2 : 0);
+        }
+        u[10] = m0; u[11] = m1; u[12] = m2;
+        const int m = v6 ? (macs ? 13 : 10) : 7;
+        s = tab_slot(T, 2, ((uint64_t)u[0] << 32) | u[1], insert);
+        if (s == FAIL) return FAIL;
+        chain[2] = s;
+        ft = 2;
+#pragma unroll
+        for (int j = 2; j < 13; j++) {
+            if (j < m) {
+                s = tab_slot(T, j + 1, ((uint64_t)s << 32) | u[j], insert);
+                if (s == FAIL) return FAIL;
+                chain[j + 1] = s;
+                ft = j + 1;
+            }
+        }
+    }
+    uint32_t d = dense_id(T, ft, s, insert, (const uint8_t*)k.w);
+    if (chain_out && d != FAIL && d < T.fmax) {
+        for (int j = 0; j < N_TABLES; j++) chain_out[(size_t)d * N_TABLES + j] = chain[j];
+    }
+    return d;
+}
+
+__device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, bool macs, bool insert,
+                                           uint8_t& dir, uint32_t* chain_out, unsigned long long* generic_used) {
+    CKey k;
+    canon_key(P, macs, k, dir);
+    return dense_of_key(T, k, insert, chain_out, generic_used);
+}
+
+// ---------------------------------------------------------------------------
+// k_parse_agg: the hot kernel
+// ---------------------------------------------------------------------------
+struct AggArgs {
+    Batch B;
+    TableSet T;
+    Acc A;
+    Glob* g;
+    int macs;
+};
+
+__global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
+    __shared__ uint32_t s_pk[2][H], s_by[2][H], s_mn[2][H], s_mx[2][H], s_fl[4][H];
+    __shared__ uint32_t s_fa[H], s_fc[H], s_fr[H], s_la[H];
+    __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < H; e += BLOCK) {
+        s_pk[0][e] = s_pk[1][e] = s_by[0][e] = s_by[1][e] = 0;
+        s_mn[0][e] = s_mn[1][e] = NONE32;
+        s_mx[0][e] = s_mx[1][e] = 0;
+        s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
+        s_fa[e] = s_fc[e] = s_fr[e] = NONE32;
+        s_la[e] = 0;
+    }
+    if (tid < 3) s_cnt[tid] = 0;
+    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; }
+    __syncthreads();
+
+    const Batch& B = a.B;
+    const bool macs = a.macs != 0;
+    const uint64_t n = B.n;
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t beg = per * blockIdx.x;
+    const uint64_t end = min(n, beg + per);
+    unsigned long long c_valid = 0, c_drop = 0, c_raw = 0, tmin = NONE64, tmax = 0;
+
+    for (uint64_t wbase = beg; wbase < end; wbase += (uint64_t)BLOCK * WIN_ITERS) {
+        const uint64_t wend = min(end, wbase + (uint64_t)BLOCK * WIN_ITERS);
+        for (uint64_t li = wbase + tid; li < wend; li += BLOCK) {
+            Parsed P;
+            parse_record(B, li, macs, 0, P);
+            if (P.cls == 1) { c_drop++; continue; }
+            if (P.cls == 2) { c_raw++; continue; }
+            c_valid++;
+            tmin = min(tmin, (unsigned long long)P.t);
+            tmax = max(tmax, (unsigned long long)P.t);
+            uint8_t dir;
+            uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
+            if (d == FAIL || d >= a.T.fmax) continue;  // error flag already set
+            const PktInfo& pi = P.pi;
+            const uint32_t tf = pi.tflags;
+            const bool elig = pi.rprot != 6 || (tf & 2);
+            const uint32_t pkt = pi.rpkt, ttl = pi.rttl;
+            const uint64_t gi = B.first + li;
+            if (d < H) {
+                const uint32_t loc = (uint32_t)(li - wbase);
+                atomicAdd(&s_pk[dir][d], 1u);
+                atomicAdd(&s_by[dir][d], pi.doctets);
+                if (pkt < s_mn[0][d]) atomicMin(&s_mn[0][d], pkt);
+                if (pkt > s_mx[0][d]) atomicMax(&s_mx[0][d], pkt);
+                if (ttl < s_mn[1][d]) atomicMin(&s_mn[1][d], ttl);
+                if (ttl > s_mx[1][d]) atomicMax(&s_mx[1][d], ttl);
+                if (tf) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
+                        if (w) atomicAdd(&s_fl[q][d], w);
+                    }
+                    if (tf & 5) atomicMin(&s_fr[d], loc);
+                }
+                if (loc < s_fa[d]) atomicMin(&s_fa[d], loc);
+                if (elig && loc < s_fc[d]) atomicMin(&s_fc[d], loc);
+                atomicMax(&s_la[d], loc + 1);
+            } else {
+                atomicAdd(&a.A.pk[dir][d], 1u);
+                atomicAdd(&a.A.by[dir][d], (unsigned long long)pi.doctets);
+                if (pkt < a.A.mn[0][d]) atomicMin(&a.A.mn[0][d], pkt);
+                if (pkt > a.A.mx[0][d]) atomicMax(&a.A.mx[0][d], pkt);
+                if (ttl < a.A.mn[1][d]) atomicMin(&a.A.mn[1][d], ttl);
+                if (ttl > a.A.mx[1][d]) atomicMax(&a.A.mx[1][d], ttl);
+                if (tf) {
+                    for (int q = 0; q < 8; q++)
+                        if ((tf >> q) & 1) atomicAdd(&a.A.fl[q][d], 1u);
+                    if (tf & 5) atomicMin(&a.A.fr[d], (unsigned long long)gi);
+                }
+                if (gi < a.A.fa[d]) atomicMin(&a.A.fa[d], (unsigned long long)gi);
+                if (elig && gi < a.A.fc[d]) atomicMin(&a.A.fc[d], (unsigned long long)gi);
+                atomicMax(&a.A.la[d], (unsigned long long)gi);
+            }
+        }
+        __syncthreads();
+        // flush: lanes walk consecutive flow ids -> coalesced global atomics
+        const uint64_t gbase = B.first + wbase;
+        for (int e = tid; e < H; e += BLOCK) {
+            uint32_t c0 = s_pk[0][e], c1 = s_pk[1][e];
+            if (c0 + c1 == 0) continue;
+            if (c0) { atomicAdd(&a.A.pk[0][e], c0); atomicAdd(&a.A.by[0][e], (unsigned long long)s_by[0][e]); }
+            if (c1) { atomicAdd(&a.A.pk[1][e], c1); atomicAdd(&a.A.by[1][e], (unsigned long long)s_by[1][e]); }
+            for (int q = 0; q < 2; q++) {
+                if (s_mn[q][e] < a.A.mn[q][e]) atomicMin(&a.A.mn[q][e], s_mn[q][e]);
+                if (s_mx[q][e] > a.A.mx[q][e]) atomicMax(&a.A.mx[q][e], s_mx[q][e]);
+            }
+            for (int q = 0; q < 4; q++) {
+                uint32_t w = s_fl[q][e];
+                if (w & 0xFFFF) atomicAdd(&a.A.fl[2 * q][e], w & 0xFFFF);
+                if (w >> 16) atomicAdd(&a.A.fl[2 * q + 1][e], w >> 16);
+            }
+            if (s_fa[e] != NONE32) atomicMin(&a.A.fa[e], gbase + s_fa[e]);
+            if (s_fc[e] != NONE32) atomicMin(&a.A.fc[e], gbase + s_fc[e]);
+            if (s_fr[e] != NONE32) atomicMin(&a.A.fr[e], gbase + s_fr[e]);
+            atomicMax(&a.A.la[e], gbase + s_la[e] - 1);
+            s_pk[0][e] = s_pk[1][e] = s_by[0][e] = s_by[1][e] = 0;
+            s_mn[0][e] = s_mn[1][e] = NONE32;
+            s_mx[0][e] = s_mx[1][e] = 0;
+            s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
+            s_fa[e] = s_fc[e] = s_fr[e] = NONE32;
+            s_la[e] = 0;
+        }
+        __syncthreads();
+    }
+    // statistics: one global atomic per workgroup
+    atomicAdd(&s_cnt[0], c_valid);
+    atomicAdd(&s_cnt[1], c_drop);
+    atomicAdd(&s_cnt[2], c_raw);
+    if (c_valid) { atomicMin(&s_tmin, tmin); atomicMax(&s_tmax, tmax); }
+    __syncthreads();
+    if (tid == 0) {
+        if (s_cnt[0]) atomicAdd(&a.g->valid, s_cnt[0]);
+        if (s_cnt[1]) atomicAdd(&a.g->dropped, s_cnt[1]);
+        if (s_cnt[2]) atomicAdd(&a.g->raw, s_cnt[2]);
+        if (s_cnt[0]) { atomicMin(&a.g->tmin, s_tmin); atomicMax(&a.g->tmax, s_tmax); }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// finalize (certified flows -> records; others -> complex)
+// ---------------------------------------------------------------------------
+struct FinArgs {
+    const Batch* bs;
+    int nb;
+    TableSet T;
+    Acc A;
+    Glob* g;
+    fluere_record* out;
+    uint8_t* complex;
+    int macs;
+};
+
+__device__ void fill_seed(fluere_record& r, const Parsed& P) {
+    const PktInfo& pi = P.pi;
+    memset(&r, 0, sizeof r);
+    r.src_v6 = r.dst_v6 = pi.rv6;
+    for (int k = 0; k < 4; k++) {
+        uint32_t s = pi.rsip[k], d = pi.rdip[k];
+        for (int b = 0; b < 4; b++) {
+            r.source[4 * k + b] = (uint8_t)(s >> (24 - 8 * b));
+            r.destination[4 * k + b] = (uint8_t)(d >> (24 - 8 * b));
+        }
+    }
+    r.prot = pi.rprot; r.tos = pi.rtos;
+    r.src_port = pi.rsp; r.dst_port = pi.rdp;
+    r.min_pkt = r.max_pkt = pi.rpkt;
+    r.min_ttl = r.max_ttl = pi.rttl;
+    r.first = r.last = P.t;
+}
+
+__device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t gi, bool macs, Parsed& P) {
+    int b = find_batch(bs, nb, gi);
+    parse_record(bs[b], gi - bs[b].first, macs, 0, P);
+}
+
+__global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
+    uint32_t nf = *a.T.n_flows;
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= nf || d >= a.T.fmax) return;
+    const Acc& A = a.A;
+    unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
+    if (fc == NONE64) return;  // TCP flow without any SYN: every packet is dropped (:101-113)
+    bool certified = fc == fa && (fr == NONE64 || fr == la);
+    if (!certified) {
+        a.complex[d] = 1;
+        atomicAdd(&a.g->n_complex, 1ull);
+        atomicAdd(&a.g->n_complex_pkts, (unsigned long long)(A.pk[0][d] + A.pk[1][d]));
+        return;
+    }
+    const bool macs = a.macs != 0;
+    Parsed P;
+    parse_global(a.bs, a.nb, fc, macs, P);
+    const uint8_t cd = canon_dir(P, macs);
+    fluere_record r;
+    fill_seed(r, P);
+    Parsed Q;
+    parse_global(a.bs, a.nb, la, macs, Q);
+    uint32_t p0 = A.pk[0][d], p1 = A.pk[1][d];
+    unsigned long long b0 = A.by[0][d], b1 = A.by[1][d];
+    r.d_pkts = p0 + p1;
+    r.d_octets = b0 + b1;
+    r.out_pkts = cd ? p1 : p0; r.in_pkts = cd ? p0 : p1;
+    r.out_bytes = cd ? b1 : b0; r.in_bytes = cd ? b0 : b1;
+    r.min_pkt = A.mn[0][d]; r.max_pkt = A.mx[0][d];
+    r.min_ttl = (uint8_t)A.mn[1][d]; r.max_ttl = (uint8_t)A.mx[1][d];
+    for (int q = 0; q < 8; q++) r.cnt[q] = A.fl[q][d];
+    r.cnt[8] = 0;
+    r.last = Q.t;
+    r.order_key = (fr == la) ? la : NONE64;
+    unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
+    a.out[pos] = r;
+}
+
+// ---------------------------------------------------------------------------
+// complex flows, Mode A: gather -> sort by (flow, index) -> per-flow replay
+// ---------------------------------------------------------------------------
+struct CollectArgs {
+    Batch B;
+    TableSet T;
+    Glob* g;
+    const uint8_t* complex;
+    unsigned long long* keys;
+    unsigned long long cap;
+    int macs;
+};
+
+__global__ void __launch_bounds__(256) k_collect(CollectArgs a) {
+    uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= a.B.n) return;
+    const bool macs = a.macs != 0;
+    Parsed P;
+    parse_record(a.B, li, macs, 0, P);
+    if (P.cls != 0) return;
+    uint8_t dir;
+    uint32_t d = flow_of(a.T, P, macs, false, dir, nullptr, nullptr);
+    if (d == FAIL || !a.complex[d]) return;
+    unsigned long long pos = atomicAdd(&a.g->n_keys, 1ull);
+    if (pos < a.cap) a.keys[pos] = ((unsigned long long)d << 40) | (a.B.first + li);
+}
+
+__global__ void k_heads(const unsigned long long* keys, unsigned long long n, unsigned long long* heads, Glob* g) {
+    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0 || (keys[i] >> 40) != (keys[i - 1] >> 40)) heads[atomicAdd(&g->n_heads, 1ull)] = i;
+}
+
+__device__ __forceinline__ void update_flow(fluere_record& r, bool rev, const PktInfo& pi, uint64_t t) {
+    // src/net/flows.rs:11-42 (u32 counters wrap like the release build)
+    r.d_pkts += 1;
+    r.d_octets += pi.doctets;
+    r.max_pkt = max(r.max_pkt, pi.rpkt);
+    r.min_pkt = min(r.min_pkt, pi.rpkt);
+    r.max_ttl = max(r.max_ttl, pi.rttl);
+    r.min_ttl = min(r.min_ttl, pi.rttl);
+    for (int q = 0; q < 8; q++) r.cnt[q] += (pi.tflags >> q) & 1;
+    r.last = t;
+    if (rev) { r.in_pkts += 1; r.in_bytes += pi.doctets; }
+    else { r.out_pkts += 1; r.out_bytes += pi.doctets; }
+}
+
+struct FsmArgs {
+    const Batch* bs;
+    int nb;
+    TableSet T;
+    Glob* g;
+    const unsigned long long* keys;
+    unsigned long long n_keys;
+    const unsigned long long* heads;
+    fluere_record* out;
+    unsigned long long out_cap;
+    int macs;
+};
+
+__global__ void __launch_bounds__(64) k_fsm_flows(FsmArgs a) {
+    unsigned long long h = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= a.g->n_heads) return;
+    const bool macs = a.macs != 0;
+    unsigned long long i = a.heads[h];
+    const unsigned long long d = a.keys[i] >> 40;
+    bool active = false;
+    uint8_t cdir = 0;
+    fluere_record r;
+    for (; i < a.n_keys && (a.keys[i] >> 40) == d; i++) {
+        uint64_t gi = a.keys[i] & IDX_MASK;
+        Parsed P;
+        parse_global(a.bs, a.nb, gi, macs, P);
+        const uint8_t dir = canon_dir(P, macs);
+        bool rev;
+        if (active) {
+            rev = dir != cdir;
+        } else {
+            if (P.pi.rprot == 6 && !(P.pi.tflags & 2)) continue;  // offline_fluereflows.rs:101-113
+            active = true;
+            cdir = dir;
+            fill_seed(r, P);
+            rev = false;
+        }
+        update_flow(r, rev, P.pi, P.t);
+        if (P.pi.tflags & 5) {  // is_finished: fin or rst (types/flags.rs:27-30)
+            r.order_key = gi;
+            unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
+            if (pos < a.out_cap) a.out[pos] = r;
+            active = false;
+        }
+    }
+    if (active) {
+        r.order_key = NONE64;
+        unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
+        if (pos < a.out_cap) a.out[pos] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Mode B: exact global state machine (expiries can fire)
+// ---------------------------------------------------------------------------
+struct SeqMeta {
+    uint32_t d;       // dense flow id, NONE32 = not a valid packet
+    uint8_t dir, tflags, rprot_tcp, ttl;
+    uint32_t pkt, doctets;
+    uint64_t t;
+};
+
+struct SeqMetaArgs {
+    Batch B;
+    TableSet T;
+    SeqMeta* meta;
+    uint64_t base;
+    int macs;
+};
+
+__global__ void __launch_bounds__(256) k_seq_meta(SeqMetaArgs a) {
+    uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= a.B.n) return;
+    const bool macs = a.macs != 0;
+    Parsed P;
+    parse_record(a.B, li, macs, 0, P);
+    SeqMeta m;
+    m.d = NONE32;
+    m.dir = 0; m.tflags = 0; m.rprot_tcp = 0; m.ttl = 0; m.pkt = 0; m.doctets = 0; m.t = P.t;
+    if (P.cls == 0) {
+        uint8_t dir;
+        uint32_t d = flow_of(a.T, P, macs, false, dir, nullptr, nullptr);
+        m.d = d == FAIL ? NONE32 : d;
+        m.dir = dir; m.tflags = P.pi.tflags; m.rprot_tcp = P.pi.rprot == 6; m.ttl = P.pi.rttl;
+        m.pkt = P.pi.rpkt; m.doctets = P.pi.doctets;
+    }
+    a.meta[a.B.first + li - a.base] = m;
+}
+
+struct HeapEnt {
+    unsigned long long exp, seq;
+    uint32_t d;
+    uint32_t dir;
+};
+
+struct SeqArgs {
+    const Batch* bs;
+    int nb;
+    const SeqMeta* meta;
+    unsigned long long n;
+    uint8_t* active;   // [fmax]
+    uint8_t* cdir;     // [fmax]
+    fluere_record* cur;  // [fmax]
+    HeapEnt* heap;     // capacity n
+    fluere_record* out;
+    unsigned long long out_cap;
+    Glob* g;
+    unsigned long long timeout_us;
+    uint64_t base;
+    uint32_t n_flows;
+    int macs;
+};
+
+__device__ __forceinline__ bool h_less(const HeapEnt& x, const HeapEnt& y) {
+    return x.exp < y.exp || (x.exp == y.exp && x.seq < y.seq);
+}
+
+__global__ void __launch_bounds__(64) k_seq_run(SeqArgs a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned long long hn = 0, seq = 0, nout = 0;
+    auto emit = [&](const fluere_record& r) {
+        if (nout < a.out_cap) { a.out[nout] = r; a.out[nout].order_key = nout; }
+        nout++;
+    };
+    for (unsigned long long gi = 0; gi < a.n; gi++) {  // offline_fluereflows.rs:68-176
+        SeqMeta m = a.meta[gi];
+        if (m.d == NONE32) continue;
+        uint32_t d = m.d;
+        bool rev;
+        if (a.active[d]) {
+            rev = m.dir != a.cdir[d];
+        } else {
+            if (m.rprot_tcp && !(m.tflags & 2)) continue;  // :101-113 (no sweep either)
+            Parsed P;
+            parse_global(a.bs, a.nb, gi + a.base, a.macs != 0, P);
+            fill_seed(a.cur[d], P);
+            a.active[d] = 1;
+            a.cdir[d] = m.dir;
+            HeapEnt e{m.t + a.timeout_us, seq++, d, m.dir};
+            unsigned long long i = hn++;
+            a.heap[i] = e;
+            while (i) {
+                unsigned long long p = (i - 1) / 2;
+                if (!h_less(a.heap[i], a.heap[p])) break;
+                HeapEnt t = a.heap[i]; a.heap[i] = a.heap[p]; a.heap[p] = t; i = p;
+            }
+            rev = false;
+        }
+        fluere_record& r = a.cur[d];
+        PktInfo pi;
+        pi.doctets = m.doctets; pi.rpkt = m.pkt; pi.rttl = m.ttl; pi.tflags = m.tflags;
+        update_flow(r, rev, pi, m.t);
+        if (m.tflags & 5) { emit(r); a.active[d] = 0; }
+        while (hn && a.heap[0].exp <= m.t) {  // :161-175
+            HeapEnt top = a.heap[0];
+            // the entry holds the creator Key: it removes whatever flow is now
+            // stored under that exact (oriented) key
+            if (a.active[top.d] && a.cdir[top.d] == top.dir) { emit(a.cur[top.d]); a.active[top.d] = 0; }
+            a.heap[0] = a.heap[--hn];
+            unsigned long long i = 0;
+            for (;;) {
+                unsigned long long l = 2 * i + 1, rr = l + 1, mm = i;
+                if (l < hn && h_less(a.heap[l], a.heap[mm])) mm = l;
+                if (rr < hn && h_less(a.heap[rr], a.heap[mm])) mm = rr;
+                if (mm == i) break;
+                HeapEnt t = a.heap[i]; a.heap[i] = a.heap[mm]; a.heap[mm] = t; i = mm;
+            }
+        }
+    }
+    unsigned long long ended = nout;
+    for (uint32_t d = 0; d < a.n_flows; d++)
+        if (a.active[d]) {
+            if (nout < a.out_cap) { a.out[nout] = a.cur[d]; a.out[nout].order_key = NONE64; }
+            nout++;
+        }
+    a.g->n_rec = nout;
+    a.g->n_heads = ended;  // reused: number of ended records
+}
+
+// ---------------------------------------------------------------------------
+// cleanup: clear exactly the table slots and accumulators this run touched
+// ---------------------------------------------------------------------------
+struct CleanArgs {
+    TableSet T;
+    Acc A;
+    uint8_t* complex;
+    uint8_t* active;
+};
+
+__global__ void __launch_bounds__(256) k_cleanup(CleanArgs a) {
+    uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= nf) return;
+    for (int t = 0; t < N_TABLES; t++) {
+        uint32_t s = a.A.slots[(size_t)d * N_TABLES + t];
+        if (s != NONE32) { a.T.tab[t][2 * s] = EMPTY; a.T.tab[t][2 * s + 1] = EMPTY; }
+        a.A.slots[(size_t)d * N_TABLES + t] = NONE32;
+    }
+    a.A.pk[0][d] = a.A.pk[1][d] = 0;
+    a.A.by[0][d] = a.A.by[1][d] = 0;
+    a.A.mn[0][d] = a.A.mn[1][d] = NONE32;
+    a.A.mx[0][d] = a.A.mx[1][d] = 0;
+    for (int q = 0; q < 8; q++) a.A.fl[q][d] = 0;
+    a.A.fa[d] = a.A.fc[d] = a.A.fr[d] = NONE64;
+    a.A.la[d] = 0;
+    a.complex[d] = 0;
+    if (a.active) a.active[d] = 0;
+}
+
+__global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// ---------------------------------------------------------------------------
+// library seam: per-packet parse_keys / parse_fluereflow view
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_parse_batch(Batch B, fluere_pkt_meta* out, int mode) {
+    uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= B.n) return;
+    Parsed P;
+    parse_record(B, li, true, mode, P);
+    const PktInfo& pi = P.pi;
+    fluere_pkt_meta m;
+    memset(&m, 0, sizeof m);
+    m.k_status = pi.kst;
+    m.f_status = pi.fst;
+    m.raw_used = (pi.kst == ST_RAW || pi.fst == ST_RAW) ? 1 : 0;
+    const uint8_t* fr = B.bytes + B.offs[li] + 16;
+    if (pi.kst == ST_OK) {
+        m.key_v6 = pi.v6; m.key_proto = pi.kproto; m.key_sport = pi.ksp; m.key_dport = pi.kdp;
+        for (int k = 0; k < 4; k++)
+            for (int b = 0; b < 4; b++) {
+                m.key_src[4 * k + b] = (uint8_t)(pi.sip[k] >> (24 - 8 * b));
+                m.key_dst[4 * k + b] = (uint8_t)(pi.dip[k] >> (24 - 8 * b));
+            }
+        for (int b = 0; b < 6; b++) {
+            m.key_dmac[b] = fr[pi.frame_off + b];
+            m.key_smac[b] = fr[pi.frame_off + 6 + b];
+        }
+    }
+    if (pi.fst == ST_OK) {
+        m.rec_v6 = pi.rv6; m.rec_prot = pi.rprot; m.rec_tos = pi.rtos; m.rec_ttl = pi.rttl;
+        for (int k = 0; k < 4; k++)
+            for (int b = 0; b < 4; b++) {
+                m.rec_src[4 * k + b] = (uint8_t)(pi.rsip[k] >> (24 - 8 * b));
+                m.rec_dst[4 * k + b] = (uint8_t)(pi.rdip[k] >> (24 - 8 * b));
+            }
+        m.rec_sport = pi.rsp; m.rec_dport = pi.rdp; m.rec_pkt = pi.rpkt;
+        m.doctets = pi.doctets;
+        m.time = P.t;
+        m.flags = pi.tflags;
+    }
+    out[li] = m;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic captures on the device
+// ---------------------------------------------------------------------------
+__global__ void k_synth_len(fluere_synth_cfg c, uint64_t first, uint64_t n, uint32_t* lens) {
+    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) lens[j] = 16 + synth::frame_len(c, first + j);
+}
+__global__ void k_synth_write(fluere_synth_cfg c, uint64_t first, uint64_t n, uint8_t* bytes, const uint32_t* offs) {
+    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) synth::write_record(c, first + j, bytes + offs[j]);
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU: per-flow summaries (export on every shard, merge on one)
+// ---------------------------------------------------------------------------
+struct FirstPay {
+    unsigned long long t_first, t_last;
+    uint16_t sp, dp;
+    uint8_t dir, prot, tos, pad;
+};
+
+__global__ void __launch_bounds__(256) k_export(FinArgs a, fluere_flow_summary* out) {
+    uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= nf) return;
+    const Acc& A = a.A;
+    fluere_flow_summary s;
+    memset(&s, 0, sizeof s);
+    const uint32_t* key = (const uint32_t*)(a.T.flow_key + (size_t)d * 56);
+    for (int j = 0; j < 14; j++) s.key[j] = key[j];
+    s.pkts[0] = A.pk[0][d]; s.pkts[1] = A.pk[1][d];
+    s.bytes[0] = A.by[0][d]; s.bytes[1] = A.by[1][d];
+    s.min_pkt = A.mn[0][d]; s.max_pkt = A.mx[0][d]; s.min_ttl = A.mn[1][d]; s.max_ttl = A.mx[1][d];
+    for (int q = 0; q < 8; q++) s.flag_cnt[q] = A.fl[q][d];
+    s.first_all = A.fa[d]; s.first_create = A.fc[d]; s.finrst_min = A.fr[d]; s.last = A.la[d];
+    const bool macs = a.macs != 0;
+    if (s.first_create != NONE64) {
+        Parsed P;
+        parse_global(a.bs, a.nb, s.first_create, macs, P);
+        s.first_dir = canon_dir(P, macs);
+        s.first_sport = P.pi.rsp; s.first_dport = P.pi.rdp;
+        s.first_prot = P.pi.rprot; s.first_tos = P.pi.rtos;
+        s.first_time = P.t;
+    }
+    Parsed Q;
+    parse_global(a.bs, a.nb, s.last, macs, Q);
+    s.last_time = Q.t;
+    out[d] = s;
+}
+
+struct MergeArgs {
+    TableSet T;
+    Acc A;
+    const fluere_flow_summary* in;
+    unsigned long long n;
+    uint32_t* sd;
+    FirstPay* pay;
+    Glob* g;
+    fluere_record* out;
+    uint8_t* complex;
+};
+
+__global__ void __launch_bounds__(256) k_merge_insert(MergeArgs a) {
+    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const fluere_flow_summary& s = a.in[i];
+    CKey k;
+    for (int j = 0; j < 14; j++) k.w[j] = s.key[j];
+    uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+    a.sd[i] = d;
+    if (d == FAIL || d >= a.T.fmax) return;
+    const Acc& A = a.A;
+    for (int q = 0; q < 2; q++) {
+        if (s.pkts[q]) { atomicAdd(&A.pk[q][d], s.pkts[q]); atomicAdd(&A.by[q][d], (unsigned long long)s.bytes[q]); }
+    }
+    atomicMin(&A.mn[0][d], s.min_pkt); atomicMax(&A.mx[0][d], s.max_pkt);
+    atomicMin(&A.mn[1][d], s.min_ttl); atomicMax(&A.mx[1][d], s.max_ttl);
+    for (int q = 0; q < 8; q++) if (s.flag_cnt[q]) atomicAdd(&A.fl[q][d], s.flag_cnt[q]);
+    atomicMin(&A.fa[d], (unsigned long long)s.first_all);
+    atomicMin(&A.fc[d], (unsigned long long)s.first_create);
+    atomicMin(&A.fr[d], (unsigned long long)s.finrst_min);
+    atomicMax(&A.la[d], (unsigned long long)s.last);
+}
+
+__global__ void __launch_bounds__(256) k_merge_payload(MergeArgs a) {
+    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    uint32_t d = a.sd[i];
+    if (d == FAIL || d >= a.T.fmax) return;
+    const fluere_flow_summary& s = a.in[i];
+    // packet indices are global and unique: exactly one shard holds each
+    if (s.first_create != NONE64 && s.first_create == a.A.fc[d]) {
+        a.pay[d].t_first = s.first_time;
+        a.pay[d].sp = s.first_sport; a.pay[d].dp = s.first_dport;
+        a.pay[d].dir = s.first_dir; a.pay[d].prot = s.first_prot; a.pay[d].tos = s.first_tos;
+    }
+    if (s.last == a.A.la[d]) a.pay[d].t_last = s.last_time;
+}
+
+__global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
+    uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= nf) return;
+    const Acc& A = a.A;
+    unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
+    if (fc == NONE64) return;
+    if (!(fc == fa && (fr == NONE64 || fr == la))) {
+        a.complex[d] = 1;
+        atomicAdd(&a.g->n_complex, 1ull);
+        return;
+    }
+    const FirstPay p = a.pay[d];
+    const uint32_t* key = (const uint32_t*)(a.T.flow_key + (size_t)d * 56);
+    fluere_record r;
+    memset(&r, 0, sizeof r);
+    const bool v6 = (key[9] >> 8) & 1;
+    r.src_v6 = r.dst_v6 = v6;
+    const uint32_t* src = p.dir ? key + 4 : key;  // the creating packet's source endpoint
+    const uint32_t* dst = p.dir ? key : key + 4;
+    for (int k = 0; k < 4; k++)
+        for (int b = 0; b < 4; b++) {
+            r.source[4 * k + b] = (uint8_t)(src[k] >> (24 - 8 * b));
+            r.destination[4 * k + b] = (uint8_t)(dst[k] >> (24 - 8 * b));
+        }
+    r.prot = p.prot; r.tos = p.tos; r.src_port = p.sp; r.dst_port = p.dp;
+    uint32_t p0 = A.pk[0][d], p1 = A.pk[1][d];
+    unsigned long long b0 = A.by[0][d], b1 = A.by[1][d];
+    r.d_pkts = p0 + p1;
+    r.d_octets = b0 + b1;
+    r.out_pkts = p.dir ? p1 : p0; r.in_pkts = p.dir ? p0 : p1;
+    r.out_bytes = p.dir ? b1 : b0; r.in_bytes = p.dir ? b0 : b1;
+    r.min_pkt = A.mn[0][d]; r.max_pkt = A.mx[0][d];
+    r.min_ttl = (uint8_t)A.mn[1][d]; r.max_ttl = (uint8_t)A.mx[1][d];
+    for (int q = 0; q < 8; q++) r.cnt[q] = A.fl[q][d];
+    r.first = p.t_first;
+    r.last = p.t_last;
+    r.order_key = (fr == la) ? la : NONE64;
+    unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
+    a.out[pos] = r;
+}
+
+unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+// ===========================================================================
+// host side
+// ===========================================================================
+struct HostBatch {
+    Batch b;
+    void* own_bytes = nullptr;
+    void* own_offs = nullptr;
+};
+
+struct fluere_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint64_t timeout_ms = 600000;
+    int use_mac = 0;
+    uint32_t C = 0, fmax = 0;
+    int n_cu = 256;
+    std::vector<HostBatch> batches;
+    uint64_t n_total = 0;
+    uint64_t index_base = 0;
+    // device state
+    unsigned long long* d_tab = nullptr;
+    void* d_acc = nullptr;
+    Acc acc{};
+    uint32_t* d_nflows = nullptr;  // [0] n_flows, [1] err
+    Glob* d_glob = nullptr;
+    uint8_t* d_flow_key = nullptr;
+    uint8_t* d_complex = nullptr;
+    uint8_t* d_active = nullptr;
+    Batch* d_batches = nullptr;
+    int d_batches_cap = 0;
+    fluere_record* d_recs = nullptr;
+    uint64_t d_recs_cap = 0;
+    void* d_pay = nullptr;      // FirstPay[fmax] (merge)
+    bool generic_dirty = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    // results
+    std::vector<fluere_record> recs;
+    uint64_t n_ended = 0;
+    bool have_results = false;
+};
+
+static TableSet tables_of(fluere_ctx* c) {
+    TableSet T;
+    for (int t = 0; t < N_TABLES; t++) T.tab[t] = c->d_tab + (size_t)t * 2 * (c->C + 1);
+    T.C = c->C;
+    T.fmax = c->fmax;
+    T.n_flows = c->d_nflows;
+    T.err = c->d_nflows + 1;
+    T.flow_key = c->d_flow_key;
+    return T;
+}
+
+extern "C" int fluere_abi_version(void) { return FLUERE_ABI_VERSION; }
+
+extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
+    if (!out) return FLUERE_E_ARG;
+    *out = nullptr;
+    fluere_ctx* c = new (std::nothrow) fluere_ctx();
+    if (!c) return FLUERE_E_NOMEM;
+    fluere_opts def{};
+    def.timeout_ms = 600000;
+    if (!o) o = &def;
+    c->device = o->device;
+    c->timeout_ms = o->timeout_ms;
+    c->use_mac = o->use_mac ? 1 : 0;
+    uint64_t mf = o->max_flows ? o->max_flows : (1ull << 21);
+    uint32_t C = 1u << 16;
+    while (C < 2 * mf && C < (1u << 23)) C <<= 1;
+    c->C = C;
+    c->fmax = (uint32_t)std::min<uint64_t>(mf, C);
+    int rc = FLUERE_OK;
+    auto fail = [&](int r) { rc = r; fluere_close(c); return r; };
+    if (hipSetDevice(c->device) != hipSuccess) return fail(FLUERE_E_HIP);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (o->stream) c->stream = (hipStream_t)o->stream;
+    else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLUERE_E_HIP);
+        c->own_stream = true;
+    }
+    size_t tab_words = (size_t)N_TABLES * 2 * (C + 1);
+    if (hipMalloc(&c->d_tab, tab_words * 8) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    size_t F = c->fmax;
+    size_t acc_bytes = F * (4 * 2 + 8 * 2 + 4 * 4 + 4 * 8 + 8 * 4 + 4 * N_TABLES);
+    if (hipMalloc(&c->d_acc, acc_bytes) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    char* p = (char*)c->d_acc;
+    auto take = [&](size_t bytes) { char* r = p; p += bytes; return r; };
+    for (int q = 0; q < 2; q++) c->acc.by[q] = (unsigned long long*)take(F * 8);
+    c->acc.fa = (unsigned long long*)take(F * 8);
+    c->acc.fc = (unsigned long long*)take(F * 8);
+    c->acc.fr = (unsigned long long*)take(F * 8);
+    c->acc.la = (unsigned long long*)take(F * 8);
+    for (int q = 0; q < 2; q++) c->acc.pk[q] = (uint32_t*)take(F * 4);
+    for (int q = 0; q < 2; q++) c->acc.mn[q] = (uint32_t*)take(F * 4);
+    for (int q = 0; q < 2; q++) c->acc.mx[q] = (uint32_t*)take(F * 4);
+    for (int q = 0; q < 8; q++) c->acc.fl[q] = (uint32_t*)take(F * 4);
+    c->acc.slots = (uint32_t*)take(F * 4 * N_TABLES);
+    if (hipMalloc(&c->d_nflows, 64) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_glob, sizeof(Glob)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev2) != hipSuccess)
+        return fail(FLUERE_E_HIP);
+    // initial state: every table EMPTY, accumulators at their identities
+    hipStream_t s = c->stream;
+    k_fill_u64<<<grid_for(tab_words, 256), 256, 0, s>>>(c->d_tab, tab_words, EMPTY);
+    k_fill_u64<<<grid_for(4 * F, 256), 256, 0, s>>>(c->acc.fa, 4 * F, NONE64);
+    k_fill_u64<<<grid_for(F, 256), 256, 0, s>>>(c->acc.la, F, 0);
+    k_fill_u64<<<grid_for(2 * F, 256), 256, 0, s>>>(c->acc.by[0], 2 * F, 0);
+    k_fill_u32<<<grid_for(2 * F, 256), 256, 0, s>>>(c->acc.pk[0], 2 * F, 0);
+    k_fill_u32<<<grid_for(2 * F, 256), 256, 0, s>>>(c->acc.mn[0], 2 * F, NONE32);
+    k_fill_u32<<<grid_for(2 * F, 256), 256, 0, s>>>(c->acc.mx[0], 2 * F, 0);
+    k_fill_u32<<<grid_for(8 * F, 256), 256, 0, s>>>(c->acc.fl[0], 8 * F, 0);
+    k_fill_u32<<<grid_for(F * N_TABLES, 256), 256, 0, s>>>(c->acc.slots, F * N_TABLES, NONE32);
+    if (hipMemsetAsync(c->d_complex, 0, F, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    if (hipMemsetAsync(c->d_nflows, 0, 64, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(FLUERE_E_HIP);
+    (void)rc;
+    *out = c;
+    return FLUERE_OK;
+}
+
+static void free_batches(fluere_ctx* c) {
+    for (auto& hb : c->batches) {
+        if (hb.own_bytes) hipFree(hb.own_bytes);
+        if (hb.own_offs) hipFree(hb.own_offs);
+    }
+    c->batches.clear();
+    c->n_total = 0;
+}
+
+extern "C" int fluere_close(fluere_ctx* c) {
+    if (!c) return FLUERE_OK;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_batches(c);
+    hipFree(c->d_tab);
+    hipFree(c->d_acc);
+    hipFree(c->d_nflows);
+    hipFree(c->d_glob);
+    hipFree(c->d_flow_key);
+    hipFree(c->d_complex);
+    hipFree(c->d_active);
+    hipFree(c->d_batches);
+    hipFree(c->d_recs);
+    hipFree(c->d_pay);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->ev2) hipEventDestroy(c->ev2);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return FLUERE_OK;
+}
+
+// Clear flow state touched by the previous run (O(flows), not O(capacity)).
+static int clear_flows(fluere_ctx* c) {
+    hipStream_t s = c->stream;
+    uint32_t hn[2];
+    HIPCHECK(hipMemcpyAsync(hn, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    uint32_t nf = std::min(hn[0], c->fmax);
+    if (hn[1] & (ERR_TABLE_FULL | ERR_SPIN)) {
+        // a failed run may have left slots without a dense id: clear everything
+        size_t tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
+        k_fill_u64<<<grid_for(tab_words, 256), 256, 0, s>>>(c->d_tab, tab_words, EMPTY);
+        nf = c->fmax;
+    }
+    if (nf) {
+        CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active};
+        k_cleanup<<<grid_for(nf, 256), 256, 0, s>>>(a);
+    }
+    HIPCHECK(hipMemsetAsync(c->d_nflows, 0, 64, s));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_reset(fluere_ctx* c) {
+    if (!c) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    int rc = clear_flows(c);
+    if (rc) return rc;
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    free_batches(c);
+    c->recs.clear();
+    c->have_results = false;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_add_device_batch(fluere_ctx* c, const uint8_t* d_bytes, uint64_t nbytes,
+                                       const uint32_t* d_offsets, uint64_t n, uint32_t snaplen, int swapped,
+                                       int nsec_ts) {
+    if (!c || (!d_bytes && n) || (!d_offsets && n) || nbytes >= (1ull << 32)) return FLUERE_E_ARG;
+    HostBatch hb;
+    hb.b.bytes = d_bytes;
+    hb.b.offs = d_offsets;
+    hb.b.nbytes = nbytes;
+    hb.b.n = n;
+    hb.b.first = c->index_base + c->n_total;
+    hb.b.snap = snaplen ? snaplen : 262144;
+    hb.b.flags = (swapped ? 1u : 0u) | (nsec_ts ? 2u : 0u);
+    c->batches.push_back(hb);
+    c->n_total += n;
+    c->have_results = false;
+    return FLUERE_OK;
+}
+
+// libpcap offline walk: stop at the first truncated or
+// oversized record.  Returns records, fills offsets (relative to file start).
+static int64_t pcap_walk(const uint8_t* f, uint64_t nbytes, uint64_t* offs, uint64_t cap, uint32_t* snap_out,
+                         int* swapped_out, int* nsec_out) {
+    if (!f || nbytes < 24) return FLUERE_E_PCAP;
+    uint32_t magic;
+    memcpy(&magic, f, 4);
+    int sw = 0, ns = 0;
+    if (magic == 0xa1b2c3d4u) {
+    } else if (magic == 0xd4c3b2a1u) sw = 1;
+    else if (magic == 0xa1b23c4du) ns = 1;
+    else if (magic == 0x4d3cb2a1u) { sw = 1; ns = 1; }
+    else return FLUERE_E_PCAP;
+    auto rd = [&](uint64_t o) { uint32_t v; memcpy(&v, f + o, 4); return sw ? __builtin_bswap32(v) : v; };
+    uint32_t snap = rd(16);
+    const uint32_t kMax = 262144;
+    if (snap == 0 || snap > kMax) snap = kMax;
+    if (snap_out) *snap_out = snap;
+    if (swapped_out) *swapped_out = sw;
+    if (nsec_out) *nsec_out = ns;
+    uint64_t off = 24;
+    int64_t n = 0;
+    while (off + 16 <= nbytes) {
+        uint32_t incl = rd(off + 8);
+        if (incl > kMax || off + 16 + (uint64_t)incl > nbytes) break;
+        if (offs && (uint64_t)n < cap) offs[n] = off;
+        n++;
+        off += 16 + (uint64_t)incl;
+    }
+    return n;
+}
+
+extern "C" int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint64_t* offsets, uint64_t cap) {
+    return pcap_walk(file, nbytes, offsets, cap, nullptr, nullptr, nullptr);
+}
+
+extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t nbytes) {
+    if (!c || !file) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    uint32_t snap;
+    int sw, ns;
+    int64_t n = pcap_walk(file, nbytes, nullptr, 0, &snap, &sw, &ns);
+    if (n < 0) return (int)n;
+    std::vector<uint64_t> offs((size_t)n);
+    pcap_walk(file, nbytes, offs.data(), (uint64_t)n, nullptr, nullptr, nullptr);
+    // split into batches of < 4 GiB (u32 offsets relative to the batch start)
+    size_t i = 0;
+    const uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
+    while (i < (size_t)n || (n == 0 && i == 0)) {
+        if (n == 0) break;
+        uint64_t base = offs[i];
+        size_t j = i;
+        while (j < (size_t)n) {
+            uint32_t incl;
+            memcpy(&incl, file + offs[j] + 8, 4);
+            if (sw) incl = __builtin_bswap32(incl);
+            if (offs[j] + 16 + incl - base > kMaxBatch) break;
+            j++;
+        }
+        uint64_t endb = (j < (size_t)n) ? offs[j] : nbytes;
+        uint64_t nb = endb - base;
+        std::vector<uint32_t> rel(j - i);
+        for (size_t k = i; k < j; k++) rel[k - i] = (uint32_t)(offs[k] - base);
+        HostBatch hb;
+        if (hipMalloc(&hb.own_bytes, nb + 256) != hipSuccess) return FLUERE_E_NOMEM;
+        if (hipMalloc(&hb.own_offs, std::max<size_t>(rel.size(), 1) * 4) != hipSuccess) {
+            hipFree(hb.own_bytes);
+            return FLUERE_E_NOMEM;
+        }
+        HIPCHECK(hipMemcpyAsync(hb.own_bytes, file + base, nb, hipMemcpyHostToDevice, c->stream));
+        HIPCHECK(hipMemsetAsync((uint8_t*)hb.own_bytes + nb, 0, 256, c->stream));
+        HIPCHECK(hipMemcpyAsync(hb.own_offs, rel.data(), rel.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHECK(hipStreamSynchronize(c->stream));
+        hb.b.bytes = (const uint8_t*)hb.own_bytes;
+        hb.b.offs = (const uint32_t*)hb.own_offs;
+        hb.b.nbytes = nb;
+        hb.b.n = j - i;
+        hb.b.first = c->index_base + c->n_total;
+        hb.b.snap = snap;
+        hb.b.flags = (sw ? 1u : 0u) | (ns ? 2u : 0u);
+        c->batches.push_back(hb);
+        c->n_total += hb.b.n;
+        i = j;
+    }
+    c->have_results = false;
+    return FLUERE_OK;
+}
+
+static int upload_batches(fluere_ctx* c) {
+    int nb = (int)c->batches.size();
+    if (nb > c->d_batches_cap) {
+        hipFree(c->d_batches);
+        c->d_batches = nullptr;
+        int cap = std::max(16, nb);
+        if (hipMalloc(&c->d_batches, sizeof(Batch) * cap) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_batches_cap = cap;
+    }
+    std::vector<Batch> hb(nb);
+    for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
+    if (nb) HIPCHECK(hipMemcpyAsync(c->d_batches, hb.data(), sizeof(Batch) * nb, hipMemcpyHostToDevice, c->stream));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_parse_batch(fluere_ctx* c, fluere_pkt_meta* d_out, uint64_t cap) {
+    if (!c || !d_out || cap < c->n_total) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    const char* m = getenv("FLUERE_PARSE_MODE");
+    int mode = (m && m[0] == '1') ? 1 : 0;
+    for (auto& hb : c->batches) {
+        if (!hb.b.n) continue;
+        k_parse_batch<<<grid_for(hb.b.n, 256), 256, 0, c->stream>>>(hb.b, d_out + hb.b.first, mode);
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    return FLUERE_OK;
+}
+
+static int launch_parse_agg(fluere_ctx* c) {
+    AggArgs a;
+    a.T = tables_of(c);
+    a.A = c->acc;
+    a.g = c->d_glob;
+    a.macs = c->use_mac;
+    for (auto& hb : c->batches) {
+        if (!hb.b.n) continue;
+        a.B = hb.b;
+        uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
+        unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
+        k_parse_agg<<<grid, BLOCK, 0, c->stream>>>(a);
+    }
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+static int init_glob(fluere_ctx* c) {
+    Glob g{};
+    g.tmin = NONE64;
+    HIPCHECK(hipMemcpyAsync(c->d_glob, &g, sizeof g, hipMemcpyHostToDevice, c->stream));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
+    if (!c) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    int rc = clear_flows(c);
+    if (rc) return rc;
+    rc = init_glob(c);
+    if (rc) return rc;
+    HIPCHECK(hipEventRecord(c->ev0, c->stream));
+    rc = launch_parse_agg(c);
+    HIPCHECK(hipEventRecord(c->ev1, c->stream));
+    return rc;
+}
+
+extern "C" double fluere_last_kernel_ms(fluere_ctx* c) {
+    if (!c) return -1.0;
+    float ms = -1.0f;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0;
+    return ms;
+}
+
+static int ensure_recs(fluere_ctx* c, uint64_t need) {
+    if (need <= c->d_recs_cap) return FLUERE_OK;
+    hipFree(c->d_recs);
+    c->d_recs = nullptr;
+    uint64_t cap = std::max<uint64_t>(need, 1024);
+    if (hipMalloc(&c->d_recs, cap * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
+    c->d_recs_cap = cap;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
+    if (!c) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = clear_flows(c))) return rc;
+    if ((rc = init_glob(c))) return rc;
+    if ((rc = upload_batches(c))) return rc;
+    HIPCHECK(hipEventRecord(c->ev0, s));
+    if ((rc = launch_parse_agg(c))) return rc;
+    HIPCHECK(hipEventRecord(c->ev1, s));
+    Glob g;
+    uint32_t nf_err[2];
+    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) return FLUERE_E_TABLE_FULL;
+    if (nf_err[1] & ERR_FLOWS_FULL) return FLUERE_E_TABLE_FULL;
+    uint32_t nf = nf_err[0];
+    const TableSet T = tables_of(c);
+    const int nb = (int)c->batches.size();
+    const uint64_t timeout_us = c->timeout_ms * 1000ull;
+    // Mode B if any flow could expire inside the capture (offline_fluereflows.rs:161-175)
+    bool modeB = g.valid && (g.tmax - g.tmin) >= timeout_us;
+    uint64_t n_ended = 0, n_rec = 0;
+    fluere_stats out{};
+    if (!modeB) {
+        if ((rc = ensure_recs(c, std::max<uint64_t>(nf, 1)))) return rc;
+        FinArgs fa{c->d_batches, nb, T, c->acc, c->d_glob, c->d_recs, c->d_complex, c->use_mac};
+        if (nf) k_finalize<<<grid_for(nf, 256), 256, 0, s>>>(fa);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (g.n_complex) {
+            uint64_t nk = g.n_complex_pkts;
+            unsigned long long *keys = nullptr, *keys2 = nullptr, *heads = nullptr;
+            void* tmp = nullptr;
+            size_t tmp_bytes = 0;
+            if (hipMalloc(&keys, nk * 8) != hipSuccess || hipMalloc(&keys2, nk * 8) != hipSuccess ||
+                hipMalloc(&heads, nk * 8) != hipSuccess) {
+                hipFree(keys); hipFree(keys2); hipFree(heads);
+                return FLUERE_E_NOMEM;
+            }
+            for (auto& hb : c->batches) {
+                if (!hb.b.n) continue;
+                CollectArgs ca{hb.b, T, c->d_glob, c->d_complex, keys, nk, c->use_mac};
+                k_collect<<<grid_for(hb.b.n, 256), 256, 0, s>>>(ca);
+            }
+            hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys2, (int)nk, 0, 64, s);
+            if (hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)) != hipSuccess) {
+                hipFree(keys); hipFree(keys2); hipFree(heads);
+                return FLUERE_E_NOMEM;
+            }
+            hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys2, (int)nk, 0, 64, s);
+            k_heads<<<grid_for(nk, 256), 256, 0, s>>>(keys2, nk, heads, c->d_glob);
+            // records: certified ones already written + at most one per complex packet
+            uint64_t need = g.n_rec + nk;
+            fluere_record* old = c->d_recs;
+            uint64_t old_n = g.n_rec;
+            if (need > c->d_recs_cap) {
+                fluere_record* nr = nullptr;
+                if (hipMalloc(&nr, need * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
+                HIPCHECK(hipMemcpyAsync(nr, old, old_n * sizeof(fluere_record), hipMemcpyDeviceToDevice, s));
+                HIPCHECK(hipStreamSynchronize(s));
+                hipFree(old);
+                c->d_recs = nr;
+                c->d_recs_cap = need;
+            }
+            FsmArgs fs{c->d_batches, nb, T, c->d_glob, keys2, nk, heads, c->d_recs, c->d_recs_cap, c->use_mac};
+            k_fsm_flows<<<grid_for(g.n_complex, 64), 64, 0, s>>>(fs);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            hipFree(tmp); hipFree(keys); hipFree(keys2); hipFree(heads);
+        }
+        n_rec = g.n_rec;
+        c->recs.resize(n_rec);
+        if (n_rec)
+            HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipEventRecord(c->ev2, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        // ended prefix in emission order (packet index of the closing packet), then active
+        std::stable_sort(c->recs.begin(), c->recs.end(), [](const fluere_record& x, const fluere_record& y) {
+            if (x.order_key != y.order_key) return x.order_key < y.order_key;
+            return x.first < y.first;
+        });
+        for (auto& r : c->recs) if (r.order_key != NONE64) n_ended++;
+        out.complex_flows = g.n_complex;
+    } else {
+        // exact global state machine
+        uint64_t N = c->n_total;
+        SeqMeta* meta = nullptr;
+        HeapEnt* heap = nullptr;
+        fluere_record* cur = nullptr;
+        if (!c->d_active && hipMalloc(&c->d_active, c->fmax) != hipSuccess) return FLUERE_E_NOMEM;
+        uint8_t* cdir = nullptr;
+        if (hipMalloc(&meta, std::max<uint64_t>(N, 1) * sizeof(SeqMeta)) != hipSuccess ||
+            hipMalloc(&heap, std::max<uint64_t>(N, 1) * sizeof(HeapEnt)) != hipSuccess ||
+            hipMalloc(&cur, std::max<uint32_t>(nf, 1) * sizeof(fluere_record)) != hipSuccess ||
+            hipMalloc(&cdir, std::max<uint32_t>(nf, 1)) != hipSuccess) {
+            hipFree(meta); hipFree(heap); hipFree(cur); hipFree(cdir);
+            return FLUERE_E_NOMEM;
+        }
+        HIPCHECK(hipMemsetAsync(c->d_active, 0, c->fmax, s));
+        for (auto& hb : c->batches) {
+            if (!hb.b.n) continue;
+            SeqMetaArgs ma{hb.b, T, meta, c->index_base, c->use_mac};
+            k_seq_meta<<<grid_for(hb.b.n, 256), 256, 0, s>>>(ma);
+        }
+        if ((rc = ensure_recs(c, g.valid + 1))) return rc;
+        SeqArgs sa{c->d_batches, nb, meta, N, c->d_active, cdir, cur, heap, c->d_recs, c->d_recs_cap,
+                   c->d_glob, timeout_us, c->index_base, nf, c->use_mac};
+        k_seq_run<<<1, 64, 0, s>>>(sa);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        n_rec = g.n_rec;
+        n_ended = g.n_heads;
+        c->recs.resize(n_rec);
+        if (n_rec)
+            HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipEventRecord(c->ev2, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        for (uint64_t i = n_ended; i < n_rec; i++) c->recs[i].order_key = NONE64;
+        hipFree(meta); hipFree(heap); hipFree(cur); hipFree(cdir);
+        out.sequential_mode = 1;
+    }
+    c->n_ended = n_ended;
+    c->have_results = true;
+    float ms_parse = 0, ms_total = 0;
+    hipEventElapsedTime(&ms_parse, c->ev0, c->ev1);
+    hipEventElapsedTime(&ms_total, c->ev0, c->ev2);
+    out.packets = c->n_total;
+    out.valid = g.valid;
+    out.dropped_parse = g.dropped;
+    out.unsupported = g.raw;
+    out.flows = nf;
+    out.records = n_rec;
+    out.ended = n_ended;
+    out.parse_ms = ms_parse;
+    out.total_ms = ms_total;
+    uint64_t upd = 0;
+    for (auto& r : c->recs) upd += r.d_pkts;
+    out.updates = upd;
+    if (st) *st = out;
+    return g.raw ? FLUERE_E_UNSUPPORTED : FLUERE_OK;
+}
+
+extern "C" int fluere_get_records(fluere_ctx* c, fluere_record** out, uint64_t* n, uint64_t* n_ended) {
+    if (!c || !out || !n) return FLUERE_E_ARG;
+    if (!c->have_results) return FLUERE_E_STATE;
+    *n = c->recs.size();
+    if (n_ended) *n_ended = c->n_ended;
+    *out = (fluere_record*)malloc(std::max<size_t>(1, c->recs.size()) * sizeof(fluere_record));
+    if (!*out) return FLUERE_E_NOMEM;
+    if (!c->recs.empty()) memcpy(*out, c->recs.data(), c->recs.size() * sizeof(fluere_record));
+    return FLUERE_OK;
+}
+
+extern "C" void fluere_records_free(fluere_record* r) { free(r); }
+
+// ---------------------------------------------------------------------------
+// synthetic captures
+// ---------------------------------------------------------------------------
+extern "C" uint64_t fluere_synth_range_bytes(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n) {
+    if (!cfg) return 0;
+    if (cfg->kind != FLUERE_SYNTH_IMIX) return n * 80;
+    uint64_t s = 0;
+    for (uint64_t i = first; i < first + n; i++) s += 16 + synth::frame_len(*cfg, i);
+    return s;
+}
+
+extern "C" uint64_t fluere_synth_file_size(const fluere_synth_cfg* cfg) {
+    return cfg ? 24 + fluere_synth_range_bytes(cfg, 0, cfg->n_packets) : 0;
+}
+
+extern "C" int fluere_synth_host(const fluere_synth_cfg* cfg, uint8_t* file, uint64_t cap) {
+    if (!cfg || !file) return FLUERE_E_ARG;
+    if (cap < fluere_synth_file_size(cfg)) return FLUERE_E_ARG;
+    uint32_t hdr[6] = {0xa1b2c3d4u, 2u | (4u << 16), 0, 0, synth::kSnap, 1};
+    memcpy(file, hdr, 24);
+    uint64_t off = 24;
+    for (uint64_t i = 0; i < cfg->n_packets; i++) off += synth::write_record(*cfg, i, file + off);
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_synth_device(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n, uint8_t* d_bytes,
+                                   uint32_t* d_offsets, void* stream) {
+    if (!cfg || !d_bytes || !d_offsets) return FLUERE_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (!n) return FLUERE_OK;
+    uint32_t* lens = nullptr;
+    HIPCHECK(hipMalloc(&lens, n * 4));
+    k_synth_len<<<grid_for(n, 256), 256, 0, s>>>(*cfg, first, n, lens);
+    size_t tb = 0;
+    void* tmp = nullptr;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lens, d_offsets, (int)n, s);
+    if (hipMalloc(&tmp, std::max<size_t>(tb, 16)) != hipSuccess) { hipFree(lens); return FLUERE_E_NOMEM; }
+    hipcub::DeviceScan::ExclusiveSum(tmp, tb, lens, d_offsets, (int)n, s);
+    k_synth_write<<<grid_for(n, 256), 256, 0, s>>>(*cfg, first, n, d_bytes, d_offsets);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    hipFree(tmp);
+    hipFree(lens);
+    return FLUERE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU merge
+// ---------------------------------------------------------------------------
+extern "C" int fluere_set_index_base(fluere_ctx* c, uint64_t base) {
+    if (!c) return FLUERE_E_ARG;
+    if (!c->batches.empty()) return FLUERE_E_STATE;
+    c->index_base = base;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out, uint64_t cap, uint64_t* n,
+                                       uint64_t* tmin, uint64_t* tmax) {
+    if (!c || !n) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = upload_batches(c))) return rc;
+    Glob g;
+    uint32_t nf_err[2];
+    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (nf_err[1]) return FLUERE_E_TABLE_FULL;
+    if (g.raw) return FLUERE_E_UNSUPPORTED;
+    uint32_t nf = std::min(nf_err[0], c->fmax);
+    *n = nf;
+    if (tmin) *tmin = g.tmin;
+    if (tmax) *tmax = g.tmax;
+    if (!d_out) return FLUERE_OK;
+    if (cap < nf) return FLUERE_E_ARG;
+    FinArgs fa{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
+    if (nf) k_export<<<grid_for(nf, 256), 256, 0, s>>>(fa, d_out);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+static int collect_records(fluere_ctx* c, uint64_t n_rec) {
+    hipStream_t s = c->stream;
+    c->recs.resize(n_rec);
+    if (n_rec)
+        HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipEventRecord(c->ev2, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    std::stable_sort(c->recs.begin(), c->recs.end(), [](const fluere_record& x, const fluere_record& y) {
+        if (x.order_key != y.order_key) return x.order_key < y.order_key;
+        return x.first < y.first;
+    });
+    uint64_t ne = 0;
+    for (auto& r : c->recs) if (r.order_key != NONE64) ne++;
+    c->n_ended = ne;
+    c->have_results = true;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
+                                      uint64_t tmax, fluere_stats* st) {
+    if (!c || (!d_in && n)) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = clear_flows(c))) return rc;
+    if ((rc = init_glob(c))) return rc;
+    if (!c->d_pay && hipMalloc(&c->d_pay, (size_t)c->fmax * sizeof(FirstPay)) != hipSuccess) return FLUERE_E_NOMEM;
+    uint32_t* sd = nullptr;
+    if (hipMalloc(&sd, std::max<uint64_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
+    if ((rc = ensure_recs(c, std::max<uint64_t>(n, 1)))) { hipFree(sd); return rc; }
+    HIPCHECK(hipEventRecord(c->ev0, s));
+    MergeArgs ma{tables_of(c), c->acc, d_in, n, sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex};
+    if (n) {
+        k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
+        k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
+    }
+    HIPCHECK(hipEventRecord(c->ev1, s));
+    uint32_t nf_err[2];
+    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    hipFree(sd);
+    if (nf_err[1]) return FLUERE_E_TABLE_FULL;
+    uint32_t nf = std::min(nf_err[0], c->fmax);
+    if (nf) k_merge_finalize<<<grid_for(nf, 256), 256, 0, s>>>(ma);
+    HIPCHECK(hipGetLastError());
+    Glob g;
+    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if ((rc = collect_records(c, g.n_rec))) return rc;
+    fluere_stats out{};
+    float ms_parse = 0, ms_total = 0;
+    hipEventElapsedTime(&ms_parse, c->ev0, c->ev1);
+    hipEventElapsedTime(&ms_total, c->ev0, c->ev2);
+    out.flows = nf;
+    out.records = c->recs.size();
+    out.ended = c->n_ended;
+    out.complex_flows = g.n_complex;
+    out.parse_ms = ms_parse;
+    out.total_ms = ms_total;
+    for (auto& r : c->recs) out.updates += r.d_pkts;
+    if (st) *st = out;
+    // expiries or order-dependent flows across shards need the per-packet
+    // state machine, which the sharded path does not run yet
+    if (g.n_complex || (tmax >= tmin && tmax - tmin >= c->timeout_ms * 1000ull)) return FLUERE_E_UNSUPPORTED;
+    return FLUERE_OK;
+}

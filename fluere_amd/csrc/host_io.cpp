@@ -1,0 +1,171 @@
+// host_io.cpp -- egress and the whole `fluere offline` mode.
+//
+//   fluere_format_csv / fluere_write_csv   <- fluere_exporter
+//       (src/utils/fluere_csv_exporter.rs:5-81): csv 1.3 Writer defaults
+//       (',' delimiter, '\n' terminator, quote only when necessary -- never
+//       for these fields), column order of the header at :10-38, IpAddr via
+//       Rust std Display (IPv6: RFC 5952 compression, ::ffff:a.b.c.d).
+//   fluere_offline_file                     <- fluereflow_fileparse
+//       (src/net/offline_fluereflows.rs:26-196): open the capture, create
+//       ./output-style directory, convert, write <stem>_converted.csv.
+#include <sys/stat.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fluere_gpu.h"
+
+namespace {
+
+struct Out {
+    char* buf;
+    uint64_t cap, n;
+    void put(const char* s, uint64_t len) {
+        if (buf && n + len <= cap) memcpy(buf + n, s, len);
+        n += len;
+    }
+    void put(const char* s) { put(s, strlen(s)); }
+    void u(uint64_t v) {
+        char t[24];
+        int i = 24;
+        do { t[--i] = (char)('0' + v % 10); v /= 10; } while (v);
+        put(t + i, (uint64_t)(24 - i));
+    }
+    void hex(unsigned v) {
+        char t[8];
+        int i = 8;
+        do { t[--i] = "0123456789abcdef"[v & 15]; v >>= 4; } while (v);
+        put(t + i, (uint64_t)(8 - i));
+    }
+    // std::net::IpAddr Display
+    void ip(uint8_t v6, const uint8_t* b) {
+        if (!v6) {
+            for (int i = 0; i < 4; i++) { if (i) put(".", 1); u(b[i]); }
+            return;
+        }
+        unsigned seg[8];
+        for (int i = 0; i < 8; i++) seg[i] = (unsigned)(b[2 * i] << 8) | b[2 * i + 1];
+        bool mapped = seg[0] == 0 && seg[1] == 0 && seg[2] == 0 && seg[3] == 0 && seg[4] == 0 && seg[5] == 0xFFFF;
+        if (mapped) {
+            put("::ffff:");
+            for (int i = 12; i < 16; i++) { if (i > 12) put(".", 1); u(b[i]); }
+            return;
+        }
+        int bs = 0, bl = 0, cs = 0, cl = 0;  // longest zero run, first wins ties
+        for (int i = 0; i < 8; i++) {
+            if (seg[i] == 0) {
+                if (!cl) cs = i;
+                if (++cl > bl) { bl = cl; bs = cs; }
+            } else cl = 0;
+        }
+        if (bl > 1) {
+            for (int i = 0; i < bs; i++) { if (i) put(":", 1); hex(seg[i]); }
+            put("::", 2);
+            for (int i = bs + bl; i < 8; i++) { if (i > bs + bl) put(":", 1); hex(seg[i]); }
+        } else {
+            for (int i = 0; i < 8; i++) { if (i) put(":", 1); hex(seg[i]); }
+        }
+    }
+};
+
+const char* kHeader =
+    "source,destination,src_port,dst_port,prot,d_pkts,d_octets,in_pkts,out_pkts,in_bytes,out_bytes,"
+    "first,last,min_pkt,max_pkt,min_ttl,max_ttl,fin_cnt,syn_cnt,rst_cnt,psh_cnt,ack_cnt,urg_cnt,"
+    "ece_cnt,cwr_cnt,ns_cnt,tos\n";
+
+}  // namespace
+
+extern "C" uint64_t fluere_format_csv(const fluere_record* recs, uint64_t n, char* buf, uint64_t cap) {
+    Out o{buf, cap, 0};
+    o.put(kHeader);
+    for (uint64_t i = 0; i < n; i++) {
+        const fluere_record& r = recs[i];
+        o.ip(r.src_v6, r.source);
+        o.put(",", 1);
+        o.ip(r.dst_v6, r.destination);
+        const uint64_t v[] = {r.src_port, r.dst_port, r.prot, r.d_pkts, r.d_octets, r.in_pkts, r.out_pkts,
+                              r.in_bytes, r.out_bytes, r.first, r.last, r.min_pkt, r.max_pkt, r.min_ttl,
+                              r.max_ttl, r.cnt[0], r.cnt[1], r.cnt[2], r.cnt[3], r.cnt[4], r.cnt[5],
+                              r.cnt[6], r.cnt[7], r.cnt[8], r.tos};
+        for (uint64_t x : v) { o.put(",", 1); o.u(x); }
+        o.put("\n", 1);
+    }
+    return o.n;
+}
+
+extern "C" int fluere_write_csv(const fluere_record* recs, uint64_t n, const char* path) {
+    if (!path || (!recs && n)) return FLUERE_E_ARG;
+    uint64_t need = fluere_format_csv(recs, n, nullptr, 0);
+    std::vector<char> b(need);
+    fluere_format_csv(recs, n, b.data(), need);
+    FILE* f = fopen(path, "wb");
+    if (!f) return FLUERE_E_IO;
+    size_t w = fwrite(b.data(), 1, need, f);
+    int rc = fclose(f);
+    return (w == need && rc == 0) ? FLUERE_OK : FLUERE_E_IO;
+}
+
+static std::string file_stem(const std::string& p) {
+    // Path::file_stem(): final component without its last extension;
+    // a leading dot alone is not an extension.
+    size_t s = p.find_last_of('/');
+    std::string name = s == std::string::npos ? p : p.substr(s + 1);
+    if (name.empty() || name == "." || name == "..") return "output";
+    size_t d = name.find_last_of('.');
+    if (d == std::string::npos || d == 0) return name;
+    return name.substr(0, d);
+}
+
+static int mkdir_p(const std::string& dir) {
+    std::string cur;
+    for (size_t i = 0; i <= dir.size(); i++) {
+        if (i == dir.size() || dir[i] == '/') {
+            if (!cur.empty() && mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return -1;
+        }
+        if (i < dir.size()) cur.push_back(dir[i]);
+    }
+    return 0;
+}
+
+extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, int use_mac, const char* out_dir,
+                                   fluere_stats* stats) {
+    if (!pcap_path) return FLUERE_E_ARG;
+    FILE* f = fopen(pcap_path, "rb");
+    if (!f) return FLUERE_E_IO;
+    std::vector<uint8_t> file;
+    {
+        uint8_t chunk[1 << 16];
+        size_t r;
+        while ((r = fread(chunk, 1, sizeof chunk, f)) > 0) file.insert(file.end(), chunk, chunk + r);
+        fclose(f);
+    }
+    std::string dir = out_dir ? out_dir : "./output";
+    if (mkdir_p(dir) != 0) return FLUERE_E_IO;
+    std::string out = dir + "/" + file_stem(pcap_path) + "_converted.csv";
+    fluere_opts o{};
+    o.timeout_ms = timeout_ms;
+    o.use_mac = use_mac;
+    int64_t n = fluere_pcap_index(file.data(), file.size(), nullptr, 0);
+    if (n < 0) return (int)n;
+    o.max_flows = (uint64_t)std::max<int64_t>(1 << 16, std::min<int64_t>(n, 1 << 22));
+    fluere_ctx* c = nullptr;
+    int rc = fluere_open(&o, &c);
+    if (rc) return rc;
+    rc = fluere_add_host_pcap(c, file.data(), file.size());
+    fluere_stats st{};
+    if (!rc) rc = fluere_run(c, &st);
+    if (stats) *stats = st;
+    if (rc && rc != FLUERE_E_UNSUPPORTED) { fluere_close(c); return rc; }
+    int run_rc = rc;
+    fluere_record* recs = nullptr;
+    uint64_t nr = 0, ne = 0;
+    rc = fluere_get_records(c, &recs, &nr, &ne);
+    if (!rc) rc = fluere_write_csv(recs, nr, out.c_str());
+    fluere_records_free(recs);
+    fluere_close(c);
+    return rc ? rc : run_rc;
+}

@@ -1,0 +1,187 @@
+// synth.h -- counter-based synthetic pcap generator.
+//
+// Every byte of packet i is a pure function of (cfg, i), so the host image
+// (fluere_synth_host) and the device generator (fluere_synth_device) produce
+// identical captures and any packet range can be generated independently on
+// any GPU shard.  Compiled for host and device from the same source.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/fluere_gpu.h"
+
+#ifndef FL_HD
+#define FL_HD __host__ __device__ inline
+#endif
+
+namespace synth {
+
+constexpr uint32_t kT0 = 1700000000u;  // capture start (s); +1 us per packet
+constexpr uint32_t kSnap = 65535;
+
+FL_HD uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+FL_HD uint64_t rnd(uint64_t seed, uint64_t stream, uint64_t i) {
+    return mix64(mix64(seed + stream * 0x9E3779B97F4A7C15ull) + i * 0xD1B54A32D192ED03ull);
+}
+
+struct Flow {
+    uint32_t a_ip, b_ip;
+    uint16_t a_port, b_port;
+    uint8_t proto;
+    uint8_t closer;  // 0 none, 1 FIN+ACK, 2 RST (IMIX TCP flows only)
+    uint8_t a_mac[6], b_mac[6];
+};
+
+FL_HD uint16_t pick_port(uint64_t r) {
+    uint16_t p = (uint16_t)(1024 + r % 64000);
+    return p == 4789 ? 4790 : p;  // 53 and 4789 never appear
+}
+
+FL_HD Flow flow(const fluere_synth_cfg& c, uint32_t f) {
+    Flow F;
+    F.a_ip = 0x0A000000u | (f & 0x7FFFFFu);                        // 10.0-127.x.x, unique per f
+    F.b_ip = 0x0A800000u | (uint32_t)(rnd(c.seed, 3, f) & 0x7FFFFFu);  // 10.128-255.x.x
+    F.a_port = pick_port(rnd(c.seed, 4, f));
+    F.b_port = pick_port(rnd(c.seed, 5, f));
+    F.proto = 17;
+    F.closer = 0;
+    if (c.kind == FLUERE_SYNTH_IMIX) {
+        F.proto = (rnd(c.seed, 6, f) & 1) ? 6 : 17;
+        if (F.proto == 6) {
+            uint32_t r = (uint32_t)(rnd(c.seed, 15, f) % 100);
+            F.closer = r < 20 ? 1 : (r < 25 ? 2 : 0);
+        }
+    }
+    uint64_t ma = rnd(c.seed, 7, f), mb = rnd(c.seed, 8, f);
+    for (int k = 0; k < 6; k++) {
+        F.a_mac[k] = (uint8_t)(ma >> (8 * k));
+        F.b_mac[k] = (uint8_t)(mb >> (8 * k));
+    }
+    F.a_mac[0] = (uint8_t)((F.a_mac[0] & 0xFC) | 0x02);  // unicast, locally administered
+    F.b_mac[0] = (uint8_t)((F.b_mac[0] & 0xFC) | 0x02);
+    return F;
+}
+
+// Frame length of packet i (bytes on the wire, == caplen == orig_len).
+FL_HD uint32_t frame_len(const fluere_synth_cfg& c, uint64_t i) {
+    if (c.kind != FLUERE_SYNTH_IMIX) return 64;
+    uint32_t r = (uint32_t)(rnd(c.seed, 14, i) % 12);
+    return r < 7 ? 64 : (r < 11 ? 576 : 1500);
+}
+
+// Schedule: which flow packet i belongs to, its direction and TCP flags.
+struct Slot {
+    uint32_t f;
+    uint8_t rev;
+    uint8_t tcp_flags;
+};
+
+FL_HD Slot slot(const fluere_synth_cfg& c, uint64_t i) {
+    Slot s;
+    uint64_t F = c.n_flows ? c.n_flows : 1;
+    s.rev = (uint8_t)((rnd(c.seed, 2, i) % 100) < c.rev_pct);
+    s.tcp_flags = (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0));  // ACK (+PSH)
+    if (c.kind == FLUERE_SYNTH_IMIX && c.n_packets >= 2 * F) {
+        // [0, F): opening packet of flow i (forward; SYN for TCP)
+        // [N-F, N): one packet per flow; TCP closers send FIN+ACK / RST here
+        // otherwise: random flow, ACK (+PSH) for TCP
+        if (i < F) {
+            s.f = (uint32_t)i;
+            s.rev = 0;
+            s.tcp_flags = 0x02;
+        } else if (i >= c.n_packets - F) {
+            s.f = (uint32_t)(i - (c.n_packets - F));
+            s.tcp_flags = 0xFF;  // resolved from the flow's closer kind
+        } else {
+            s.f = (uint32_t)(rnd(c.seed, 1, i) % F);
+        }
+        return s;
+    }
+    s.f = (uint32_t)(rnd(c.seed, 1, i) % F);
+    return s;
+}
+
+FL_HD void put16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+FL_HD void put32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+FL_HD void put32le(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+
+// Writes the 16-byte pcap record header and the frame of packet i at dst.
+// Returns bytes written (16 + frame_len).
+FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst) {
+    uint32_t L = frame_len(c, i);
+    put32le(dst + 0, kT0 + (uint32_t)(i / 1000000u));
+    put32le(dst + 4, (uint32_t)(i % 1000000u));
+    put32le(dst + 8, L);
+    put32le(dst + 12, L);
+    uint8_t* e = dst + 16;
+    Slot s = slot(c, i);
+    Flow F = flow(c, s.f);
+    uint8_t tflags = s.tcp_flags;
+    if (tflags == 0xFF)
+        tflags = F.closer == 1 ? 0x11 : (F.closer == 2 ? 0x04 : (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0)));
+    uint32_t sip = s.rev ? F.b_ip : F.a_ip, dip = s.rev ? F.a_ip : F.b_ip;
+    uint16_t sp = s.rev ? F.b_port : F.a_port, dp = s.rev ? F.a_port : F.b_port;
+    const uint8_t* smac = s.rev ? F.b_mac : F.a_mac;
+    const uint8_t* dmac = s.rev ? F.a_mac : F.b_mac;
+    for (int k = 0; k < 6; k++) { e[k] = dmac[k]; e[6 + k] = smac[k]; }
+    uint32_t o = 12;
+    if (c.kind == FLUERE_SYNTH_VLAN64) {
+        put16(e + 12, 0x8100);
+        put16(e + 14, (uint32_t)(rnd(c.seed, 17, s.f) & 0x0FFF));
+        o = 16;
+    }
+    put16(e + o, 0x0800);
+    uint8_t* ip = e + o + 2;
+    uint32_t iplen = L - (o + 2);
+    uint32_t dsel = (uint32_t)(rnd(c.seed, 10, i) & 3);  // DSCP 0, 10, 46, 1 (1 is unmapped -> tos 0)
+    ip[0] = 0x45;
+    ip[1] = (uint8_t)((dsel == 0 ? 0 : dsel == 1 ? 10 : dsel == 2 ? 46 : 1) << 2);
+    put16(ip + 2, iplen);
+    put16(ip + 4, (uint32_t)(rnd(c.seed, 11, i) & 0xFFFF));
+    put16(ip + 6, 0x4000);  // DF
+    ip[8] = (uint8_t)(32 + rnd(c.seed, 9, i) % 97);
+    ip[9] = F.proto;
+    put16(ip + 10, 0);
+    put32(ip + 12, sip);
+    put32(ip + 16, dip);
+    uint32_t sum = 0;
+    for (int k = 0; k < 20; k += 2) sum += ((uint32_t)ip[k] << 8) | ip[k + 1];
+    while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+    put16(ip + 10, ~sum & 0xFFFF);
+    uint8_t* l4 = ip + 20;
+    uint32_t l4len = iplen - 20, hl;
+    put16(l4, sp);
+    put16(l4 + 2, dp);
+    if (F.proto == 6) {
+        put32(l4 + 4, (uint32_t)rnd(c.seed, 18, i));
+        put32(l4 + 8, (uint32_t)rnd(c.seed, 19, i));
+        l4[12] = 0x50;
+        l4[13] = tflags;
+        put16(l4 + 14, 0xFFFF);
+        put16(l4 + 16, 0);
+        put16(l4 + 18, 0);
+        hl = 20;
+    } else {
+        put16(l4 + 4, l4len);
+        put16(l4 + 6, 0);
+        hl = 8;
+    }
+    uint8_t* pay = l4 + hl;
+    uint32_t plen = l4len - hl;
+    uint64_t base = rnd(c.seed, 12, i);
+    for (uint32_t k = 0; k < plen; k += 8) {
+        uint64_t w = mix64(base + k * 0x9E3779B97F4A7C15ull);
+        for (uint32_t b = 0; b < 8 && k + b < plen; b++) pay[k + b] = (uint8_t)(w >> (8 * b));
+    }
+    if (plen && pay[0] == 0x08) pay[0] = 0x09;  // never a VXLAN prefix
+    return 16 + L;
+}
+
+}  // namespace synth

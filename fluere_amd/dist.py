@@ -1,0 +1,76 @@
+"""Packet-range sharding over GPUs: one process per GPU (torch.distributed,
+backend "nccl" = RCCL on ROCm), flow-table merge as one all_gather of per-flow
+summaries over xGMI followed by a device merge on rank 0.
+
+Reference: the offline loop is one sequential pass (offline_fluereflows.rs:68-176);
+shard r processes packets [r*N/G, (r+1)*N/G) with global packet indices, so the
+order-dependent record fields (first / last packet, FIN/RST position) merge as
+min / max of global indices.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from ._lib import SUMMARY_BYTES, Stats, check
+
+
+def shard_range(n_packets: int, rank: int, world: int):
+    per = (n_packets + world - 1) // world
+    first = min(n_packets, rank * per)
+    return first, min(n_packets, first + per) - first
+
+
+def set_index_base(ctx, base: int):
+    check(_lib.lib().fluere_set_index_base(ctx._h, base), "fluere_set_index_base")
+
+
+def export_summaries(ctx, out=None):
+    """parse+key+aggregate this shard and export its flows -> (uint8 cuda tensor [n*192], tmin, tmax)."""
+    import torch
+    L = _lib.lib()
+    ctx.parse_aggregate()
+    n, lo, hi = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    check(L.fluere_export_summaries(ctx._h, None, 0, ctypes.byref(n), ctypes.byref(lo), ctypes.byref(hi)),
+          "fluere_export_summaries")
+    if out is None or out.numel() < n.value * SUMMARY_BYTES:
+        out = torch.empty(max(n.value, 1) * SUMMARY_BYTES, dtype=torch.uint8, device="cuda")
+    check(L.fluere_export_summaries(ctx._h, out.data_ptr(), n.value, ctypes.byref(n), None, None),
+          "fluere_export_summaries")
+    return out[: n.value * SUMMARY_BYTES], lo.value, hi.value
+
+
+def merge_summaries(ctx, summaries, tmin: int, tmax: int) -> dict:
+    st = Stats()
+    n = summaries.numel() // SUMMARY_BYTES
+    check(_lib.lib().fluere_merge_summaries(ctx._h, summaries.data_ptr() if n else None, n, tmin, tmax,
+                                            ctypes.byref(st)), "fluere_merge_summaries")
+    return st.as_dict()
+
+
+def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int = 0):
+    """All-gather every shard's summaries (RCCL over xGMI) and merge on rank dst.
+
+    Returns the merge stats on dst, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = summaries.device
+    meta = torch.tensor([summaries.numel() // SUMMARY_BYTES, tmin, tmax], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    counts = [int(m[0]) for m in metas]
+    gmin = min(int(m[1]) for m in metas)
+    gmax = max(int(m[2]) for m in metas)
+    cap = max(max(counts), 1) * SUMMARY_BYTES
+    send = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    send[: summaries.numel()] = summaries
+    recv = torch.empty(world * cap, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    if rank != dst:
+        return None
+    parts = [recv[r * cap: r * cap + counts[r] * SUMMARY_BYTES] for r in range(world)]
+    allsum = torch.cat(parts) if parts else recv[:0]
+    torch.cuda.current_stream().synchronize()
+    return merge_summaries(ctx, allsum, gmin, gmax)

@@ -1,0 +1,241 @@
+/*
+ * fluere_gpu.h -- C ABI of the MI355X-native `fluere offline` hot path.
+ *
+ * Plain pointers and sizes only; no torch or HIP types in the signatures
+ * (streams are passed as void*, hipStream_t underneath).  A Rust host links
+ * this through `extern "C"` (INTEGRATION.md shows the bindgen-free stub).
+ *
+ * Reference interfaces replaced (paths relative to SkuldNorniern/fluere):
+ *   fluere_offline_file   <- pub async fn fluereflow_fileparse(arg: Args)
+ *                            src/net/offline_fluereflows.rs:26 (mode seam,
+ *                            called from execute_mode src/lib.rs:61)
+ *   fluere_parse_batch    <- pub fn parse_keys(packet) src/net/parser/keys.rs:98
+ *                            + pub fn parse_fluereflow(packet)
+ *                            src/net/parser/fluereflows.rs:30 (library seam,
+ *                            batched; re-exported at src/net/parser/mod.rs:15,17)
+ *   fluere_run / fluere_get_records
+ *                         <- the loop body of offline_fluereflows.rs:68-184:
+ *                            update_flow (src/net/flows.rs:11) + the active /
+ *                            expiry tables (:60-62) + the final flush (:182-184)
+ *   fluere_record         <- FluereRecord fluereflow/src/types/fluereflow.rs:31-60
+ *   fluere_write_csv      <- fluere_exporter src/utils/fluere_csv_exporter.rs:5
+ *
+ * Error convention: every call returns 0 on success, a negative FLUERE_E_*
+ * code on failure (never panics or aborts).  Per-packet NetError results
+ * (src/net/mod.rs:28-36) surface as fluere_pkt_meta.k_status / f_status.
+ */
+#ifndef FLUERE_GPU_H
+#define FLUERE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLUERE_ABI_VERSION 1
+
+enum fluere_status {
+    FLUERE_OK = 0,
+    FLUERE_E_ARG = -1,         /* bad argument */
+    FLUERE_E_IO = -2,          /* file open/read/write failed (FluereError::Io) */
+    FLUERE_E_PCAP = -3,        /* not a classic pcap file (FluereError::Pcap) */
+    FLUERE_E_HIP = -4,         /* HIP runtime error / no device */
+    FLUERE_E_NOMEM = -5,       /* device or host allocation failed */
+    FLUERE_E_TABLE_FULL = -6,  /* flow dictionary capacity exceeded: reopen with larger max_flows */
+    FLUERE_E_UNSUPPORTED = -7, /* input needs a parser class not yet on the GPU (see stats) */
+    FLUERE_E_STATE = -8        /* call order violated */
+};
+
+/* NetError per packet (src/net/mod.rs:28-36). */
+enum fluere_pkt_status {
+    FLUERE_PKT_OK = 0,
+    FLUERE_PKT_EMPTY = 1,         /* NetError::EmptyPacket */
+    FLUERE_PKT_INVALID = 2,       /* NetError::InvalidPacket */
+    FLUERE_PKT_UNKNOWN_ETHER = 3, /* NetError::UnknownEtherType */
+    FLUERE_PKT_RAW = 0xFE         /* needs src/net/parser/raw (not yet on the GPU) */
+};
+
+/* The fluereflow record with a C layout.  IpAddr is {v6 flag, 16 bytes}
+ * (IPv4 in the first 4).  cnt[] = fin, syn, rst, psh, ack, urg, ece, cwr, ns. */
+typedef struct fluere_record {
+    uint8_t src_v6, dst_v6, prot, tos;
+    uint8_t min_ttl, max_ttl;
+    uint16_t src_port, dst_port;
+    uint8_t source[16];
+    uint8_t destination[16];
+    uint16_t pad0;
+    uint32_t d_pkts, min_pkt, max_pkt, in_pkts, out_pkts;
+    uint32_t cnt[9];
+    uint64_t d_octets, first, last, in_bytes, out_bytes;
+    /* emission order: ended records carry the global index of the packet that
+     * closed them (FIN/RST or the sweep); active records carry UINT64_MAX. */
+    uint64_t order_key;
+} fluere_record; /* 152 bytes */
+
+/* Per-packet view of parse_keys + parse_fluereflow (library seam). 128 B. */
+typedef struct fluere_pkt_meta {
+    uint8_t k_status, f_status, key_v6, key_proto;
+    uint16_t key_sport, key_dport;
+    uint8_t key_src[16], key_dst[16];
+    uint8_t key_smac[6], key_dmac[6];
+    uint8_t rec_v6, rec_prot, rec_tos, rec_ttl;
+    uint8_t rec_src[16], rec_dst[16];
+    uint16_t rec_sport, rec_dport;
+    uint32_t rec_pkt;
+    uint64_t doctets;
+    uint64_t time;
+    uint16_t flags; /* bit i = parse_flags()[i], fin..ns */
+    uint8_t raw_used;
+    uint8_t pad[13];
+} fluere_pkt_meta;
+
+typedef struct fluere_opts {
+    int device;            /* HIP device ordinal */
+    void* stream;          /* hipStream_t to run on (NULL: the library creates one) */
+    uint64_t timeout_ms;   /* -t (Args.parameters.timeout), default 600000 */
+    int use_mac;           /* -M (Args.parameters.use_mac) */
+    uint64_t max_flows;    /* flow dictionary capacity (0: 1<<21) */
+} fluere_opts;
+
+typedef struct fluere_stats {
+    uint64_t packets;          /* pcap records handed to the device */
+    uint64_t valid;            /* passed parse_keys and parse_fluereflow */
+    uint64_t updates;          /* valid and not dropped by the TCP SYN gate */
+    uint64_t dropped_parse;    /* parse_keys or parse_fluereflow returned Err */
+    uint64_t unsupported;      /* packets in FLUERE_PKT_RAW class */
+    uint64_t flows;            /* distinct canonical flow keys */
+    uint64_t complex_flows;    /* flows resolved by the exact per-flow state machine */
+    uint64_t records;          /* emitted records */
+    uint64_t ended;            /* records in the ended prefix */
+    uint32_t sequential_mode;  /* 1 if expiries fired (global sequential state machine) */
+    uint32_t pad;
+    double parse_ms;           /* device time of the fused parse+key+aggregate kernel */
+    double total_ms;           /* device time of the whole run */
+} fluere_stats;
+
+typedef struct fluere_ctx fluere_ctx;
+
+int fluere_abi_version(void);
+int fluere_open(const fluere_opts* opts, fluere_ctx** out);
+int fluere_close(fluere_ctx* ctx);
+/* Forget all packets and flows (keeps allocations). */
+int fluere_reset(fluere_ctx* ctx);
+
+/* ---- ingress ------------------------------------------------------------- */
+/* Index a classic pcap held in host memory: record offsets (relative to the
+ * buffer) follow libpcap offline semantics (stop at the first bad record).
+ * offsets may be NULL to count.  Returns number of records or <0. */
+int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint64_t* offsets, uint64_t cap);
+
+/* Attach a device-resident batch: `d_bytes` holds pcap records (the 24-byte
+ * file header excluded or not: offsets decide), `d_offsets[i]` is the byte
+ * offset of record i's 16-byte header inside d_bytes.  Batches must be
+ * appended in capture order; the library does not copy them and they must
+ * stay valid until fluere_reset/fluere_close.  nbytes < 4 GiB, and the
+ * buffer must stay readable 16 bytes past nbytes (records are read with
+ * 16-byte loads).  snaplen: the file header's snaplen (0: 262144);
+ * swapped: byte-swapped pcap; nsec_ts: nanosecond timestamps. */
+int fluere_add_device_batch(fluere_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes,
+                            const uint32_t* d_offsets, uint64_t n_packets, uint32_t snaplen, int swapped,
+                            int nsec_ts);
+
+/* Copy a host pcap file image to the device (owned by ctx) and attach it. */
+int fluere_add_host_pcap(fluere_ctx* ctx, const uint8_t* file, uint64_t nbytes);
+
+/* ---- compute ------------------------------------------------------------- */
+/* Per-packet parse_keys/parse_fluereflow of every attached packet into a
+ * device array of n fluere_pkt_meta (test / library seam). */
+int fluere_parse_batch(fluere_ctx* ctx, fluere_pkt_meta* d_out, uint64_t cap);
+
+/* Run the hot path over every attached batch: parse + flow key + aggregate
+ * + state machine.  Asynchronous on the ctx stream except where the exact
+ * state machine needs host decisions. */
+int fluere_run(fluere_ctx* ctx, fluere_stats* stats);
+
+/* Only the fused parse+key+aggregate kernel over the attached batches (the
+ * roofline kernel); leaves the flow table populated. Asynchronous. */
+int fluere_parse_aggregate(fluere_ctx* ctx);
+/* Device time (HIP events on the ctx stream) of the fused kernel launches of
+ * the last fluere_run / fluere_parse_aggregate, in ms. */
+double fluere_last_kernel_ms(fluere_ctx* ctx);
+
+/* Records of the last fluere_run, host memory, ended prefix first (in the
+ * reference's emission order), then active flows.  Caller frees with
+ * fluere_records_free. */
+int fluere_get_records(fluere_ctx* ctx, fluere_record** out, uint64_t* n, uint64_t* n_ended);
+void fluere_records_free(fluere_record* recs);
+
+/* ---- multi-GPU merge (one process per GPU; RCCL moves the bytes) -------- */
+/* Packet-range sharding: rank r attaches packets [b_r, e_r) of the capture
+ * with fluere_set_index_base(ctx, b_r) first, so every index is global.
+ * After fluere_parse_aggregate each rank exports one summary per local flow;
+ * the summaries of all ranks are gathered (RCCL all_gather over xGMI) and
+ * merged on one rank, which then emits the records. */
+typedef struct fluere_flow_summary {
+    uint32_t key[14];           /* canonical key words (DESIGN.md "Flow key") */
+    uint32_t pkts[2];           /* per canonical direction */
+    uint64_t bytes[2];
+    uint32_t min_pkt, max_pkt, min_ttl, max_ttl;
+    uint32_t flag_cnt[8];       /* fin syn rst psh ack urg ece cwr */
+    uint64_t first_all, first_create, finrst_min, last; /* global packet indices */
+    uint64_t first_time, last_time; /* times of packets first_create / last */
+    uint16_t first_sport, first_dport; /* FluereRecord ports of the creating packet */
+    uint8_t first_dir, first_prot, first_tos, pad0;
+    uint32_t pad1;
+} fluere_flow_summary;          /* 192 bytes */
+
+int fluere_set_index_base(fluere_ctx* ctx, uint64_t first_global_index);
+/* Export this context's flows after fluere_parse_aggregate.  tmin/tmax: time
+ * range of the valid packets (for the expiry-mode decision). */
+int fluere_export_summaries(fluere_ctx* ctx, fluere_flow_summary* d_out, uint64_t cap, uint64_t* n,
+                            uint64_t* tmin, uint64_t* tmax);
+/* Merge n device-resident summaries (from every shard) into this context's
+ * (cleared) flow table and build the records; then fluere_get_records. */
+int fluere_merge_summaries(fluere_ctx* ctx, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
+                           uint64_t tmax, fluere_stats* stats);
+
+/* ---- egress -------------------------------------------------------------- */
+/* Write the CSV exactly as fluere_exporter does (header + one row per record). */
+int fluere_write_csv(const fluere_record* recs, uint64_t n, const char* path);
+/* Format into a caller buffer; returns bytes needed (buf may be NULL). */
+uint64_t fluere_format_csv(const fluere_record* recs, uint64_t n, char* buf, uint64_t cap);
+
+/* The whole `fluere offline` mode: read pcap, run, write
+ * <out_dir>/<file_stem>_converted.csv (offline_fluereflows.rs:44-58,186-190). */
+int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, int use_mac, const char* out_dir,
+                        fluere_stats* stats);
+
+/* ---- synthetic captures (bench / tests) ---------------------------------- */
+typedef struct fluere_synth_cfg {
+    uint64_t seed;
+    uint64_t n_packets;
+    uint32_t n_flows;
+    uint32_t kind;       /* FLUERE_SYNTH_* */
+    uint32_t rev_pct;    /* % of packets sent in the reverse direction */
+    uint32_t pad;
+} fluere_synth_cfg;
+
+enum {
+    FLUERE_SYNTH_UDP64 = 0,     /* 64-B Ethernet/IPv4/UDP */
+    FLUERE_SYNTH_IMIX = 1,      /* 64/576/1500 (7:4:1), TCP+UDP, SYN first, FIN/RST last */
+    FLUERE_SYNTH_VLAN64 = 2,    /* 802.1Q-tagged 64-B IPv4/UDP, MAC pairs */
+    FLUERE_SYNTH_MAC64 = 3      /* untagged 64-B IPv4/UDP, MAC pairs */
+};
+
+/* Size of the synthetic pcap file (24-B header + records). */
+uint64_t fluere_synth_file_size(const fluere_synth_cfg* cfg);
+/* Write the whole synthetic pcap file into host memory. */
+int fluere_synth_host(const fluere_synth_cfg* cfg, uint8_t* file, uint64_t cap);
+/* Generate packets [first, first+n) directly in device memory as a batch
+ * (bytes + offsets), identical to the host image.  d_bytes needs
+ * fluere_synth_range_bytes(); d_offsets n entries. */
+uint64_t fluere_synth_range_bytes(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n);
+int fluere_synth_device(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n, uint8_t* d_bytes,
+                        uint32_t* d_offsets, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

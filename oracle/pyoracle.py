@@ -1,0 +1,99 @@
+"""TEST INFRASTRUCTURE: ctypes access to the C restatement of the reference
+CPU path (oracle/fluere_oracle.c).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg import this module."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+CLI = os.path.join(HERE, "_build", "fluere_oracle")
+
+PKT_META_DTYPE = np.dtype([
+    ("k_status", "u1"), ("f_status", "u1"), ("key_v6", "u1"), ("key_proto", "u1"),
+    ("key_sport", "<u2"), ("key_dport", "<u2"), ("key_src", "u1", 16), ("key_dst", "u1", 16),
+    ("key_smac", "u1", 6), ("key_dmac", "u1", 6), ("rec_v6", "u1"), ("rec_prot", "u1"), ("rec_tos", "u1"),
+    ("rec_ttl", "u1"), ("rec_src", "u1", 16), ("rec_dst", "u1", 16), ("rec_sport", "<u2"), ("rec_dport", "<u2"),
+    ("rec_pkt", "<u4"), ("doctets", "<u8"), ("time", "<u8"), ("flags", "<u2"), ("raw_used", "u1"),
+    ("pad", "u1", 13),
+])
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [("recs", ctypes.c_void_p), ("n", ctypes.c_uint64), ("n_ended", ctypes.c_uint64),
+                ("packets", ctypes.c_uint64), ("valid", ctypes.c_uint64), ("raw_used", ctypes.c_uint64),
+                ("loop_seconds", ctypes.c_double), ("cap", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.or_offline_buffer.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                        ctypes.POINTER(_Result)]
+        L.or_offline_buffer.restype = ctypes.c_int
+        L.or_result_free.argtypes = [ctypes.POINTER(_Result)]
+        L.or_format_csv.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.or_format_csv.restype = ctypes.c_uint64
+        L.or_parse_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.POINTER(ctypes.c_uint64)]
+        L.or_parse_batch.restype = ctypes.c_int
+        L.or_pcap_index.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+        L.or_pcap_index.restype = ctypes.c_int64
+        _lib = L
+    return _lib
+
+
+def offline(pcap: bytes, timeout_ms: int = 600000, use_mac: bool = False):
+    """-> dict(csv=str, n_ended=int, n=int, packets, valid, raw_used, loop_seconds)."""
+    L = lib()
+    buf = (ctypes.c_uint8 * max(len(pcap), 1)).from_buffer_copy(pcap + b"\0")
+    r = _Result()
+    if L.or_offline_buffer(buf, len(pcap), timeout_ms, 1 if use_mac else 0, ctypes.byref(r)) != 0:
+        raise ValueError("oracle: not a classic pcap")
+    try:
+        need = L.or_format_csv(r.recs, r.n, None, 0)
+        out = ctypes.create_string_buffer(need)
+        L.or_format_csv(r.recs, r.n, out, need)
+        return dict(csv=out.raw[:need].decode(), n=r.n, n_ended=r.n_ended, packets=r.packets, valid=r.valid,
+                    raw_used=r.raw_used, loop_seconds=r.loop_seconds)
+    finally:
+        L.or_result_free(ctypes.byref(r))
+
+
+def parse_batch(pcap: bytes) -> np.ndarray:
+    L = lib()
+    buf = (ctypes.c_uint8 * max(len(pcap), 1)).from_buffer_copy(pcap + b"\0")
+    cnt = L.or_pcap_index(buf, len(pcap), ctypes.byref(ctypes.c_void_p()))
+    n = max(int(cnt), 0)
+    out = np.zeros(max(n, 1), dtype=PKT_META_DTYPE)
+    got = ctypes.c_uint64()
+    if L.or_parse_batch(buf, len(pcap), out.ctypes.data, n, ctypes.byref(got)) != 0:
+        raise ValueError("oracle: not a classic pcap")
+    return out[: got.value]
+
+
+def time_offline_cli(path: str, timeout_ms: int = 600000, use_mac: bool = False, repeat: int = 1, core: int = 0):
+    """CPU baseline: the "Converted in" window on one pinned core."""
+    import json
+    cmd = [CLI, "-f", path, "-t", str(timeout_ms), "--repeat", str(repeat)] + (["-M"] if use_mac else [])
+    try:
+        os.sched_setaffinity(0, os.sched_getaffinity(0))  # no-op probe
+        cmd = ["taskset", "-c", str(core)] + cmd
+    except Exception:
+        pass
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+    return json.loads(out.strip().splitlines()[-1])

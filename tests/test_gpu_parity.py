@@ -1,0 +1,172 @@
+"""GPU parity: the HIP path through the C ABI against the oracle and the
+committed goldens.  Bit-exact (integer / byte work): per-packet
+parse_keys/parse_fluereflow views and the flow CSV (header equal, ended
+prefix equal in order, active suffix equal as a multiset)."""
+import numpy as np
+import pyoracle
+import pytest
+import torch
+from util import assert_csv_equal, golden_csv, golden_pcap, manifest
+
+import fluere_amd
+from fluere_amd import _lib
+from fluere_amd._lib import FluereError
+
+pytestmark = pytest.mark.gpu
+
+KEY_FIELDS = ["key_v6", "key_proto", "key_sport", "key_dport", "key_src", "key_dst", "key_smac", "key_dmac"]
+REC_FIELDS = ["rec_v6", "rec_prot", "rec_tos", "rec_ttl", "rec_src", "rec_dst", "rec_sport", "rec_dport", "rec_pkt",
+              "doctets", "time", "flags"]
+
+
+def _check_meta(got, want, what):
+    assert len(got) == len(want), what
+    for i, (g, w) in enumerate(zip(got, want)):
+        if g["k_status"] == 0xFE or g["f_status"] == 0xFE:
+            assert w["raw_used"] == 1, f"{what}[{i}]: GPU says raw class, oracle did not use the raw parser"
+        if g["k_status"] != 0xFE:
+            assert g["k_status"] == w["k_status"], f"{what}[{i}] k_status {g['k_status']} != {w['k_status']}"
+            if g["k_status"] == 0:
+                for f in KEY_FIELDS:
+                    assert np.array_equal(g[f], w[f]), f"{what}[{i}].{f}: {g[f]} != {w[f]}"
+        if g["f_status"] != 0xFE:
+            assert g["f_status"] == w["f_status"], f"{what}[{i}] f_status {g['f_status']} != {w['f_status']}"
+            if g["f_status"] == 0:
+                for f in REC_FIELDS:
+                    assert np.array_equal(g[f], w[f]), f"{what}[{i}].{f}: {g[f]} != {w[f]}"
+
+
+def _gpu_csv(data, timeout_ms=600000, use_mac=False):
+    with fluere_amd.FlowContext(timeout_ms=timeout_ms, use_mac=use_mac, max_flows=1 << 16) as ctx:
+        ctx.add_host_pcap(data)
+        st = ctx.run()
+        recs, ne = ctx.records()
+    return fluere_amd.format_csv(recs), ne, st
+
+
+@pytest.mark.parametrize("name", sorted(manifest()))
+@pytest.mark.parametrize("general", [False, True])
+def test_parse_batch_matches_oracle(gpu, name, general):
+    data = golden_pcap(name)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_host_pcap(data)
+        got = ctx.parse_batch(general_only=general)
+    _check_meta(got, pyoracle.parse_batch(data), name)
+
+
+@pytest.mark.parametrize("name", sorted(manifest()))
+def test_fixture_csv_matches_golden(gpu, name):
+    m = manifest()[name]
+    data = golden_pcap(name)
+    for run in m["runs"]:
+        try:
+            csv, ne, st = _gpu_csv(data, run["timeout_ms"], run["use_mac"])
+        except FluereError as e:
+            assert e.code == _lib.E_UNSUPPORTED and m["raw_packets"] > 0, f"{name}: {e}"
+            continue
+        assert_csv_equal(csv, ne, golden_csv(run["csv"]), run["n_ended"], f"{name} t={run['timeout_ms']}")
+
+
+SYNTH = {
+    "c1_udp64_1flow": (_lib.SYNTH_UDP64, 10_000, 1, 0xF10E0001, False),
+    "c2_udp64_small": (_lib.SYNTH_UDP64, 300_000, 1000, 0xF10E0002, False),
+    "c3_imix_small": (_lib.SYNTH_IMIX, 200_000, 5000, 0xF10E0003, False),
+    "c5_vlan_small": (_lib.SYNTH_VLAN64, 100_000, 2000, 0xF10E0005, True),
+    "c5u_mac_small": (_lib.SYNTH_MAC64, 100_000, 5000, 0xF10E0005, True),
+    "many_flows": (_lib.SYNTH_UDP64, 200_000, 50_000, 0xF10E0006, False),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SYNTH))
+def test_synthetic_csv_matches_oracle(gpu, name):
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=use_mac)
+    csv, ne, st = _gpu_csv(data, use_mac=use_mac)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
+    assert st["packets"] == n
+
+
+@pytest.mark.parametrize("kind", [_lib.SYNTH_UDP64, _lib.SYNTH_IMIX, _lib.SYNTH_VLAN64])
+def test_device_generator_matches_host(gpu, kind):
+    cfg = fluere_amd.synth_cfg(kind, 50_000, 300, 0xABCDEF)
+    host = fluere_amd.synth_pcap(cfg)
+    first, n = 12_345, 20_000
+    b, o, nbytes = fluere_amd.synth_device(cfg, first, n)
+    torch.cuda.synchronize()
+    offs = o.cpu().numpy().astype(np.int64)
+    idx = np.zeros(cfg.n_packets, dtype=np.uint64)
+    import ctypes
+    buf = (ctypes.c_uint8 * len(host)).from_buffer_copy(host)
+    _lib.lib().fluere_pcap_index(buf, len(host), idx.ctypes.data, len(idx))
+    base = int(idx[first])
+    dev = bytes(b[:nbytes].cpu().numpy())
+    assert dev == host[base: base + nbytes]
+    assert np.array_equal(offs, idx[first: first + n].astype(np.int64) - base)
+
+
+def test_multi_batch_equals_single(gpu):
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 120_000, 3000, 0x1234)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        for first, n in ((0, 50_000), (50_000, 1), (50_001, 69_999)):
+            b, o, nbytes = fluere_amd.synth_device(cfg, first, n)
+            ctx.add_device_batch(b, nbytes, o, n)
+        torch.cuda.synchronize()
+        ctx.run()
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "multi-batch")
+
+
+def test_rerun_is_idempotent(gpu):
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 50_000, 1000, 77))
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_host_pcap(data)
+        outs = []
+        for _ in range(3):
+            ctx.run()
+            recs, ne = ctx.records()
+            outs.append((fluere_amd.format_csv(recs), ne))
+    assert outs[0] == outs[1] == outs[2]
+
+
+def test_sharded_merge_equals_single(gpu):
+    """G logical shards on one device through the summary export/merge path."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    G = 4
+    per = cfg.n_packets // G
+    sums, tmin, tmax = [], None, None
+    for r in range(G):
+        with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+            b, o, nbytes = fluere_amd.synth_device(cfg, r * per, per)
+            _lib.check(_lib.lib().fluere_set_index_base(ctx._h, r * per), "base")
+            ctx.add_device_batch(b, nbytes, o, per)
+            torch.cuda.synchronize()
+            s, lo, hi = fluere_amd.dist.export_summaries(ctx)
+            sums.append(s)
+            tmin = lo if tmin is None else min(tmin, lo)
+            tmax = hi if tmax is None else max(tmax, hi)
+    allsum = torch.cat(sums)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        fluere_amd.dist.merge_summaries(ctx, allsum, tmin, tmax)
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "sharded")
+
+
+def test_c2_full_size_parity(gpu):
+    """BASELINE configs[1] at full size (10M x 64 B, 1k tuples), device-resident,
+    against the oracle on the identical host image."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_UDP64, 10_000_000, 1000, 0xF10E0002)
+    b, o, nbytes = fluere_amd.synth_device(cfg, 0, cfg.n_packets)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_device_batch(b, nbytes, o, cfg.n_packets)
+        torch.cuda.synchronize()
+        st = ctx.run()
+        recs, ne = ctx.records()
+    assert st["records"] == 1000 and st["valid"] == cfg.n_packets
+    assert int(recs["d_pkts"].sum()) == cfg.n_packets
+    assert int(recs["d_octets"].sum()) == cfg.n_packets * 50
+    assert np.all(recs["in_pkts"] + recs["out_pkts"] == recs["d_pkts"])
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "c2-10M")
