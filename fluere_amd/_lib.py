@@ -80,7 +80,15 @@ PKT_META_DTYPE = np.dtype([
 ])
 assert PKT_META_DTYPE.itemsize == 128
 
-SUMMARY_BYTES = 192  # struct fluere_flow_summary
+SUMMARY_DTYPE = np.dtype([
+    ("key", "<u4", 14), ("pkts", "<u4", 2), ("bytes", "<u8", 2), ("min_pkt", "<u4"), ("max_pkt", "<u4"),
+    ("min_ttl", "<u4"), ("max_ttl", "<u4"), ("flag_cnt", "<u4", 8), ("first_all", "<u8"), ("first_create", "<u8"),
+    ("finrst_min", "<u8"), ("last", "<u8"), ("first_time", "<u8"), ("last_time", "<u8"), ("first_sport", "<u2"),
+    ("first_dport", "<u2"), ("first_dir", "u1"), ("first_prot", "u1"), ("first_tos", "u1"), ("pad0", "u1"),
+    ("pad1", "<u4"), ("pad2", "<u4"),
+])
+SUMMARY_BYTES = SUMMARY_DTYPE.itemsize  # struct fluere_flow_summary
+assert SUMMARY_BYTES == 192
 
 _lib = None
 
@@ -120,6 +128,7 @@ def lib() -> ctypes.CDLL:
         "fluere_synth_device": (I, [ctypes.POINTER(SynthCfg), U64, U64, P, P, P]),
         "fluere_set_index_base": (I, [P, U64]),
         "fluere_last_kernel_ms": (ctypes.c_double, [P]),
+        "fluere_debug_dense_ids": (I, [P, P, U64, P]),
         "fluere_export_summaries": (I, [P, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "fluere_merge_summaries": (I, [P, P, U64, U64, U64, ctypes.POINTER(Stats)]),
     }

@@ -68,41 +68,6 @@ __device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t 
     return FAIL;
 }
 
-// Dense id of a final-level slot; the first caller assigns it.
-__device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t s, bool insert,
-                                             const uint8_t* key56) {
-    unsigned long long* val = &T.tab[t][2 * s + 1];
-    unsigned long long v = *val;
-    if (v < PENDING) return (uint32_t)v;
-    if (!insert) {
-        v = atomicOr(val, 0ull);
-        return v < PENDING ? (uint32_t)v : FAIL;
-    }
-    v = atomicCAS(val, EMPTY, PENDING);
-    if (v == EMPTY) {
-        uint32_t d = atomicAdd(T.n_flows, 1u);
-        if (d >= T.fmax) {
-            atomicOr(T.err, ERR_FLOWS_FULL);
-            d = FAIL;
-        } else {
-            uint32_t* dst = (uint32_t*)(T.flow_key + (size_t)d * 56);
-            const uint32_t* src = (const uint32_t*)key56;
-            for (int k = 0; k < 14; k++) dst[k] = src[k];
-        }
-        atomicExch(val, (unsigned long long)d);
-        return d;
-    }
-    for (int it = 0; v == PENDING && it < (1 << 20); it++) {
-        __builtin_amdgcn_s_sleep(2);
-        v = atomicOr(val, 0ull);  // memory-side read: coherent across XCDs
-    }
-    if (v >= PENDING) {
-        atomicOr(T.err, ERR_SPIN);
-        return FAIL;
-    }
-    return (uint32_t)v;
-}
-
 // Canonical key: 14 little-endian u32 words (also fluere_flow_summary.key):
 //   w[0..4) lo_ip, w[4..8) hi_ip (big-endian numeric words, IPv4 in w[0] / w[4])
 //   w[8]  = lo_port << 16 | hi_port
@@ -112,6 +77,76 @@ __device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t 
 struct CKey {
     uint32_t w[14];
 };
+
+// Dense id of a final-level slot; the first caller assigns it.
+//
+// CDNA waves have no independent thread scheduling, and a retry loop nested
+// inside a single-lane branch proved fragile, so the only loop here is
+// wave-uniform: each iteration elects one leader per distinct value word
+// (ballot), the leader makes ONE attempt -- claim (CAS EMPTY->PENDING, then
+// take a dense id and publish it in the same branch) or read the published
+// id -- and broadcasts the outcome.  A PENDING word was claimed by another
+// wave, which publishes right after its claim, so retrying (bounded) always
+// terminates.  Every step that another workgroup can observe is a 64-bit
+// atomic (memory-side on MI355X, coherent across XCDs).
+__device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t s, bool insert, const CKey& key,
+                                             const uint32_t (&chain)[N_TABLES], uint32_t* chain_out) {
+    unsigned long long* val = &T.tab[t][2 * s + 1];
+    unsigned long long v0 = *val;  // stale reads can only show EMPTY/PENDING, never a wrong id
+    if (v0 < PENDING) return (uint32_t)v0;
+    if (!insert) {
+        v0 = atomicOr(val, 0ull);
+        return v0 < PENDING ? (uint32_t)v0 : FAIL;
+    }
+    uint32_t res = FAIL;
+    const uint64_t addr = (uint64_t)val;
+    const int lane = __lane_id();
+    bool need = true;
+    int spins = 0;
+    for (;;) {
+        const uint64_t mask = __ballot(need);
+        if (mask == 0 || spins > (1 << 20)) break;
+        const int leader = __ffsll((unsigned long long)mask) - 1;
+        const uint64_t laddr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(addr >> 32), leader) << 32) |
+                               (uint32_t)__shfl((int)(uint32_t)addr, leader);
+        uint32_t r = FAIL;
+        int ok = 0;
+        if (lane == leader) {
+            unsigned long long v = atomicCAS(val, EMPTY, PENDING);
+            if (v == EMPTY) {
+                uint32_t d = atomicAdd(T.n_flows, 1u);
+                if (d >= T.fmax) {
+                    atomicOr(T.err, ERR_FLOWS_FULL);
+                    d = FAIL;
+                } else {
+                    uint32_t* dst = (uint32_t*)(T.flow_key + (size_t)d * 56);
+#pragma unroll
+                    for (int k = 0; k < 14; k++) dst[k] = key.w[k];
+                    if (chain_out) {  // table slots of this flow's chain, for O(flows) cleanup
+#pragma unroll
+                        for (int j = 0; j < N_TABLES; j++) chain_out[(size_t)d * N_TABLES + j] = chain[j];
+                    }
+                }
+                atomicExch(val, (unsigned long long)d);
+                r = d;
+                ok = 1;
+            } else if (v != PENDING) {
+                r = (uint32_t)v;
+                ok = 1;
+            }
+        }
+        ok = __shfl(ok, leader);
+        r = (uint32_t)__shfl((int)r, leader);
+        if (ok) {
+            if (need && addr == laddr) { res = r; need = false; }
+        } else {
+            spins++;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (need) atomicOr(T.err, ERR_SPIN);
+    return res;
+}
 
 // Endpoint comparison (ip, port, mac) lexicographic in key-field order;
 // returns true when src > dst (the packet travels hi -> lo).

@@ -42,6 +42,10 @@
 
 using namespace fl;
 
+static_assert(sizeof(fluere_record) == 152, "fluere_record ABI");
+static_assert(sizeof(fluere_pkt_meta) == 128, "fluere_pkt_meta ABI");
+static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
+
 namespace {
 
 constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
@@ -81,6 +85,7 @@ struct Glob {
     unsigned long long n_complex, n_complex_pkts;
     unsigned long long n_keys, n_heads;
     unsigned long long generic_used;
+    unsigned long long n_slow;
 };
 
 #define HIPCHECK(x)                                  \
@@ -230,11 +235,7 @@ __device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& 
             }
         }
     }
-    uint32_t d = dense_id(T, ft, s, insert, (const uint8_t*)k.w);
-    if (chain_out && d != FAIL && d < T.fmax) {
-        for (int j = 0; j < N_TABLES; j++) chain_out[(size_t)d * N_TABLES + j] = chain[j];
-    }
-    return d;
+    return dense_id(T, ft, s, insert, k, chain, chain_out);
 }
 
 __device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, bool macs, bool insert,
@@ -252,13 +253,61 @@ struct AggArgs {
     TableSet T;
     Acc A;
     Glob* g;
+    uint32_t* slow;            // packets (batch-local indices) parse_fast did not take
+    unsigned long long* slow_n;
     int macs;
 };
+
+// Front end of the hot kernel: record header + five 16-byte loads + the
+// static-offset parser.  Returns false when the general parser is needed.
+__device__ __forceinline__ bool parse_fast_record(const Batch& B, uint64_t li, bool macs, Parsed& P) {
+    uint32_t off = B.offs[li];
+    Win W;
+    load_win(B, off, W);
+    bool sw = B.flags & 1;
+    uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
+    uint32_t L = min(incl, B.snap);
+    uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
+    if (L > avail) L = (uint32_t)avail;
+    P.L = L;
+    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);
+    if (!parse_fast(W, L, P.pi)) return false;
+    const PktInfo& pi = P.pi;
+    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;  // the fast path never needs the raw parser
+    P.smac = P.dmac = 0;
+    if (macs) {
+        uint64_t d = 0, s = 0;
+        for (int k = 0; k < 6; k++) d = (d << 8) | W.b(16 + k);
+        for (int k = 0; k < 6; k++) s = (s << 8) | W.b(22 + k);
+        P.dmac = d; P.smac = s;
+    }
+    return true;
+}
+
+// update_flow's order-free part straight into the global accumulators
+// (flows.rs:11-42); first/last/FIN-RST positions as min/max packet indices.
+__device__ __forceinline__ void agg_global(const Acc& A, uint32_t d, uint8_t dir, const PktInfo& pi, uint64_t gi) {
+    const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
+    atomicAdd(&A.pk[dir][d], 1u);
+    atomicAdd(&A.by[dir][d], (unsigned long long)pi.doctets);
+    if (pkt < A.mn[0][d]) atomicMin(&A.mn[0][d], pkt);  // a stale read can only skip a no-op
+    if (pkt > A.mx[0][d]) atomicMax(&A.mx[0][d], pkt);
+    if (ttl < A.mn[1][d]) atomicMin(&A.mn[1][d], ttl);
+    if (ttl > A.mx[1][d]) atomicMax(&A.mx[1][d], ttl);
+    if (tf) {
+        for (int q = 0; q < 8; q++)
+            if ((tf >> q) & 1) atomicAdd(&A.fl[q][d], 1u);
+        if (tf & 5) atomicMin(&A.fr[d], (unsigned long long)gi);
+    }
+    if (gi < A.fa[d]) atomicMin(&A.fa[d], (unsigned long long)gi);
+    if ((pi.rprot != 6 || (tf & 2)) && gi < A.fc[d]) atomicMin(&A.fc[d], (unsigned long long)gi);
+    atomicMax(&A.la[d], (unsigned long long)gi);
+}
 
 __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint32_t s_pk[2][H], s_by[2][H], s_mn[2][H], s_mx[2][H], s_fl[4][H];
     __shared__ uint32_t s_fa[H], s_fc[H], s_fr[H], s_la[H];
-    __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
+    __shared__ unsigned long long s_cnt[2], s_tmin, s_tmax;
     const int tid = threadIdx.x;
     for (int e = tid; e < H; e += BLOCK) {
         s_pk[0][e] = s_pk[1][e] = s_by[0][e] = s_by[1][e] = 0;
@@ -268,7 +317,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         s_fa[e] = s_fc[e] = s_fr[e] = NONE32;
         s_la[e] = 0;
     }
-    if (tid < 3) s_cnt[tid] = 0;
+    if (tid < 2) s_cnt[tid] = 0;
     if (tid == 0) { s_tmin = NONE64; s_tmax = 0; }
     __syncthreads();
 
@@ -278,15 +327,17 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t beg = per * blockIdx.x;
     const uint64_t end = min(n, beg + per);
-    unsigned long long c_valid = 0, c_drop = 0, c_raw = 0, tmin = NONE64, tmax = 0;
+    unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
 
     for (uint64_t wbase = beg; wbase < end; wbase += (uint64_t)BLOCK * WIN_ITERS) {
         const uint64_t wend = min(end, wbase + (uint64_t)BLOCK * WIN_ITERS);
         for (uint64_t li = wbase + tid; li < wend; li += BLOCK) {
             Parsed P;
-            parse_record(B, li, macs, 0, P);
-            if (P.cls == 1) { c_drop++; continue; }
-            if (P.cls == 2) { c_raw++; continue; }
+            if (!parse_fast_record(B, li, macs, P)) {
+                a.slow[atomicAdd(a.slow_n, 1ull)] = (uint32_t)li;
+                continue;
+            }
+            if (P.cls) { c_drop++; continue; }
             c_valid++;
             tmin = min(tmin, (unsigned long long)P.t);
             tmax = max(tmax, (unsigned long long)P.t);
@@ -294,11 +345,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
             if (d == FAIL || d >= a.T.fmax) continue;  // error flag already set
             const PktInfo& pi = P.pi;
-            const uint32_t tf = pi.tflags;
-            const bool elig = pi.rprot != 6 || (tf & 2);
-            const uint32_t pkt = pi.rpkt, ttl = pi.rttl;
-            const uint64_t gi = B.first + li;
             if (d < H) {
+                const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
                 const uint32_t loc = (uint32_t)(li - wbase);
                 atomicAdd(&s_pk[dir][d], 1u);
                 atomicAdd(&s_by[dir][d], pi.doctets);
@@ -315,23 +363,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     if (tf & 5) atomicMin(&s_fr[d], loc);
                 }
                 if (loc < s_fa[d]) atomicMin(&s_fa[d], loc);
-                if (elig && loc < s_fc[d]) atomicMin(&s_fc[d], loc);
+                if ((pi.rprot != 6 || (tf & 2)) && loc < s_fc[d]) atomicMin(&s_fc[d], loc);
                 atomicMax(&s_la[d], loc + 1);
             } else {
-                atomicAdd(&a.A.pk[dir][d], 1u);
-                atomicAdd(&a.A.by[dir][d], (unsigned long long)pi.doctets);
-                if (pkt < a.A.mn[0][d]) atomicMin(&a.A.mn[0][d], pkt);
-                if (pkt > a.A.mx[0][d]) atomicMax(&a.A.mx[0][d], pkt);
-                if (ttl < a.A.mn[1][d]) atomicMin(&a.A.mn[1][d], ttl);
-                if (ttl > a.A.mx[1][d]) atomicMax(&a.A.mx[1][d], ttl);
-                if (tf) {
-                    for (int q = 0; q < 8; q++)
-                        if ((tf >> q) & 1) atomicAdd(&a.A.fl[q][d], 1u);
-                    if (tf & 5) atomicMin(&a.A.fr[d], (unsigned long long)gi);
-                }
-                if (gi < a.A.fa[d]) atomicMin(&a.A.fa[d], (unsigned long long)gi);
-                if (elig && gi < a.A.fc[d]) atomicMin(&a.A.fc[d], (unsigned long long)gi);
-                atomicMax(&a.A.la[d], (unsigned long long)gi);
+                agg_global(a.A, d, dir, pi, B.first + li);
             }
         }
         __syncthreads();
@@ -367,15 +402,40 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     // statistics: one global atomic per workgroup
     atomicAdd(&s_cnt[0], c_valid);
     atomicAdd(&s_cnt[1], c_drop);
-    atomicAdd(&s_cnt[2], c_raw);
     if (c_valid) { atomicMin(&s_tmin, tmin); atomicMax(&s_tmax, tmax); }
     __syncthreads();
     if (tid == 0) {
         if (s_cnt[0]) atomicAdd(&a.g->valid, s_cnt[0]);
         if (s_cnt[1]) atomicAdd(&a.g->dropped, s_cnt[1]);
-        if (s_cnt[2]) atomicAdd(&a.g->raw, s_cnt[2]);
         if (s_cnt[0]) { atomicMin(&a.g->tmin, s_tmin); atomicMax(&a.g->tmax, s_tmax); }
     }
+}
+
+// The packets parse_fast declined (IPv6, IPv4 options, ARP, VXLAN, VLAN,
+// short frames ...): general parser + direct global aggregation.  Grid-stride
+// over the device-side count, so no host round trip between the two kernels.
+__global__ void __launch_bounds__(256) k_parse_agg_slow(AggArgs a) {
+    const unsigned long long n = *a.slow_n;
+    const bool macs = a.macs != 0;
+    unsigned long long c_valid = 0, c_drop = 0, c_raw = 0, tmin = NONE64, tmax = 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const uint64_t li = a.slow[i];
+        Parsed P;
+        parse_record(a.B, li, macs, 1, P);
+        if (P.cls == 1) { c_drop++; continue; }
+        if (P.cls == 2) { c_raw++; continue; }
+        c_valid++;
+        tmin = min(tmin, (unsigned long long)P.t);
+        tmax = max(tmax, (unsigned long long)P.t);
+        uint8_t dir;
+        uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
+        if (d == FAIL || d >= a.T.fmax) continue;
+        agg_global(a.A, d, dir, P.pi, a.B.first + li);
+    }
+    if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
+    if (c_drop) atomicAdd(&a.g->dropped, c_drop);
+    if (c_raw) atomicAdd(&a.g->raw, c_raw);
 }
 
 // ---------------------------------------------------------------------------
@@ -901,6 +961,16 @@ __global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
     a.out[pos] = r;
 }
 
+// test seam: insert canonical keys, return dense ids (flow dictionary checks)
+__global__ void __launch_bounds__(256) k_dense_test(TableSet T, const uint32_t* keys, unsigned long long n,
+                                                    uint32_t* out, uint32_t* slots) {
+    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    CKey k;
+    for (int j = 0; j < 14; j++) k.w[j] = keys[i * 14 + j];
+    out[i] = dense_of_key(T, k, true, slots, nullptr);
+}
+
 unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
@@ -939,6 +1009,8 @@ struct fluere_ctx {
     fluere_record* d_recs = nullptr;
     uint64_t d_recs_cap = 0;
     void* d_pay = nullptr;      // FirstPay[fmax] (merge)
+    uint32_t* d_slow = nullptr; // slow-path packet list (one batch)
+    uint64_t d_slow_cap = 0;
     bool generic_dirty = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     // results
@@ -1052,6 +1124,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_batches);
     hipFree(c->d_recs);
     hipFree(c->d_pay);
+    hipFree(c->d_slow);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->ev2) hipEventDestroy(c->ev2);
@@ -1234,12 +1307,24 @@ static int launch_parse_agg(fluere_ctx* c) {
     a.A = c->acc;
     a.g = c->d_glob;
     a.macs = c->use_mac;
+    uint64_t maxn = 1;
+    for (auto& hb : c->batches) maxn = std::max<uint64_t>(maxn, hb.b.n);
+    if (maxn > c->d_slow_cap) {
+        hipFree(c->d_slow);
+        c->d_slow = nullptr;
+        if (hipMalloc(&c->d_slow, maxn * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_slow_cap = maxn;
+    }
+    a.slow = c->d_slow;
+    a.slow_n = &c->d_glob->n_slow;
     for (auto& hb : c->batches) {
         if (!hb.b.n) continue;
         a.B = hb.b;
+        HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 8, c->stream));
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
         unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
         k_parse_agg<<<grid, BLOCK, 0, c->stream>>>(a);
+        k_parse_agg_slow<<<(unsigned)std::max(1, c->n_cu * 4), 256, 0, c->stream>>>(a);
     }
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
@@ -1592,4 +1677,15 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     // state machine, which the sharded path does not run yet
     if (g.n_complex || (tmax >= tmin && tmax - tmin >= c->timeout_ms * 1000ull)) return FLUERE_E_UNSUPPORTED;
     return FLUERE_OK;
+}
+
+extern "C" int fluere_debug_dense_ids(fluere_ctx* c, const uint32_t* d_keys, uint64_t n, uint32_t* d_out) {
+    if (!c || (!d_keys && n) || (!d_out && n)) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    if (n) k_dense_test<<<grid_for(n, 256), 256, 0, c->stream>>>(tables_of(c), d_keys, n, d_out, c->acc.slots);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    uint32_t nf_err[2];
+    HIPCHECK(hipMemcpy(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost));
+    return nf_err[1] ? FLUERE_E_TABLE_FULL : FLUERE_OK;
 }

@@ -196,6 +196,10 @@ int fluere_export_summaries(fluere_ctx* ctx, fluere_flow_summary* d_out, uint64_
 int fluere_merge_summaries(fluere_ctx* ctx, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
                            uint64_t tmax, fluere_stats* stats);
 
+/* Test seam: insert n canonical keys (14 u32 words each, device memory) into
+ * the flow dictionary and write each key's dense flow id. */
+int fluere_debug_dense_ids(fluere_ctx* ctx, const uint32_t* d_keys, uint64_t n, uint32_t* d_out);
+
 /* ---- egress -------------------------------------------------------------- */
 /* Write the CSV exactly as fluere_exporter does (header + one row per record). */
 int fluere_write_csv(const fluere_record* recs, uint64_t n, const char* path);

@@ -170,3 +170,30 @@ def test_c2_full_size_parity(gpu):
     assert np.all(recs["in_pkts"] + recs["out_pkts"] == recs["d_pkts"])
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "c2-10M")
+
+
+@pytest.mark.parametrize("n_keys,dup", [(64, 1), (5000, 1), (5000, 4), (100_000, 3)])
+def test_flow_dictionary_ids(gpu, n_keys, dup):
+    """Exactness of the flow dictionary: equal keys -> equal ids, distinct keys
+    -> distinct dense ids 0..F-1, under heavy concurrent insertion."""
+    rng = np.random.default_rng(n_keys * 7 + dup)
+    base = np.zeros((n_keys, 14), dtype=np.uint32)
+    base[:, 0] = rng.integers(0, 2**32, n_keys, dtype=np.uint32)
+    base[:, 4] = rng.integers(0, 2**32, n_keys, dtype=np.uint32)
+    base[:, 8] = rng.integers(0, 2**32, n_keys, dtype=np.uint32)
+    base[:, 9] = 17
+    base[n_keys // 2:, 9] = (2 << 8) | 6          # half of them MAC-keyed (generic chain)
+    base[n_keys // 2:, 10] = rng.integers(0, 2**32, n_keys - n_keys // 2, dtype=np.uint32)
+    keys = np.repeat(base, dup, axis=0)
+    perm = rng.permutation(len(keys))
+    keys = np.ascontiguousarray(keys[perm])
+    dk = torch.from_numpy(keys.view(np.int32)).cuda()
+    out = torch.empty(len(keys), dtype=torch.int32, device="cuda")
+    with fluere_amd.FlowContext(max_flows=1 << 18) as ctx:
+        _lib.check(_lib.lib().fluere_debug_dense_ids(ctx._h, dk.data_ptr(), len(keys), out.data_ptr()), "dense")
+    ids = out.cpu().numpy().view(np.uint32)
+    inv = np.argsort(perm)
+    ids_by_key = ids[inv].reshape(n_keys, dup)
+    assert np.all(ids_by_key == ids_by_key[:, :1]), "equal keys got different ids"
+    uniq = ids_by_key[:, 0]
+    assert len(np.unique(uniq)) == n_keys and uniq.max() == n_keys - 1
