@@ -50,14 +50,22 @@ struct TableSet {
 };
 
 // Returns the slot of `w` in table t, inserting it if absent (insert=true).
-__device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t w, bool insert) {
+// Each probe loads the whole 16-byte entry {key, val}; *val_out receives the
+// value word seen with the matching key (possibly stale: EMPTY/PENDING), so a
+// final-level lookup of a published flow costs one round trip.
+__device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t w, bool insert,
+                                            unsigned long long* val_out = nullptr) {
     unsigned long long* tab = T.tab[t];
+    if (val_out) *val_out = EMPTY;
     if (w == EMPTY) return T.C;  // the sentinel word has a dedicated slot
     uint32_t h = (uint32_t)mix64(w) & (T.C - 1);
     for (int p = 0; p < MAX_PROBE; p++) {
-        unsigned long long k = tab[2 * h];
-        if (k == w) return h;
-        if (k == EMPTY) {
+        const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&tab[2 * h]);
+        if (e.x == w) {
+            if (val_out) *val_out = e.y;
+            return h;
+        }
+        if (e.x == EMPTY) {
             if (!insert) return FAIL;
             unsigned long long old = atomicCAS(&tab[2 * h], EMPTY, (unsigned long long)w);
             if (old == EMPTY || old == w) return h;
@@ -80,38 +88,31 @@ struct CKey {
 
 // Dense id of a final-level slot; the first caller assigns it.
 //
-// CDNA waves have no independent thread scheduling, and a retry loop nested
-// inside a single-lane branch proved fragile, so the only loop here is
-// wave-uniform: each iteration elects one leader per distinct value word
-// (ballot), the leader makes ONE attempt -- claim (CAS EMPTY->PENDING, then
-// take a dense id and publish it in the same branch) or read the published
-// id -- and broadcasts the outcome.  A PENDING word was claimed by another
-// wave, which publishes right after its claim, so retrying (bounded) always
-// terminates.  Every step that another workgroup can observe is a 64-bit
-// atomic (memory-side on MI355X, coherent across XCDs).
+// CDNA waves have no independent thread scheduling, and a retry loop whose
+// exit is per-lane proved fragile here, so the only loop is wave-uniform
+// (exit decided by a ballot).  In each iteration every lane that still needs
+// an id makes ONE attempt: CAS EMPTY->PENDING; the winner takes a dense id
+// and publishes it in the same branch, lanes that read a published id are
+// done, lanes that read PENDING retry next iteration (the claimer -- in this
+// wave or another -- publishes right after its claim, so the bounded retry
+// terminates).  Everything another workgroup can observe is a 64-bit atomic
+// (memory-side on MI355X, coherent across XCDs).
 __device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t s, bool insert, const CKey& key,
-                                             const uint32_t (&chain)[N_TABLES], uint32_t* chain_out) {
+                                             const uint32_t (&chain)[N_TABLES], uint32_t* chain_out,
+                                             unsigned long long v0) {
+    // v0: the value word loaded with the key (stale reads can only show
+    // EMPTY/PENDING, never a wrong id)
     unsigned long long* val = &T.tab[t][2 * s + 1];
-    unsigned long long v0 = *val;  // stale reads can only show EMPTY/PENDING, never a wrong id
     if (v0 < PENDING) return (uint32_t)v0;
     if (!insert) {
         v0 = atomicOr(val, 0ull);
         return v0 < PENDING ? (uint32_t)v0 : FAIL;
     }
     uint32_t res = FAIL;
-    const uint64_t addr = (uint64_t)val;
-    const int lane = __lane_id();
     bool need = true;
-    int spins = 0;
-    for (;;) {
-        const uint64_t mask = __ballot(need);
-        if (mask == 0 || spins > (1 << 20)) break;
-        const int leader = __ffsll((unsigned long long)mask) - 1;
-        const uint64_t laddr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(addr >> 32), leader) << 32) |
-                               (uint32_t)__shfl((int)(uint32_t)addr, leader);
-        uint32_t r = FAIL;
-        int ok = 0;
-        if (lane == leader) {
+    for (int spins = 0; spins < (1 << 20); spins++) {
+        if (__ballot(need) == 0) break;
+        if (need) {
             unsigned long long v = atomicCAS(val, EMPTY, PENDING);
             if (v == EMPTY) {
                 uint32_t d = atomicAdd(T.n_flows, 1u);
@@ -128,21 +129,14 @@ __device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t 
                     }
                 }
                 atomicExch(val, (unsigned long long)d);
-                r = d;
-                ok = 1;
+                res = d;
+                need = false;
             } else if (v != PENDING) {
-                r = (uint32_t)v;
-                ok = 1;
+                res = (uint32_t)v;
+                need = false;
             }
         }
-        ok = __shfl(ok, leader);
-        r = (uint32_t)__shfl((int)r, leader);
-        if (ok) {
-            if (need && addr == laddr) { res = r; need = false; }
-        } else {
-            spins++;
-            __builtin_amdgcn_s_sleep(1);
-        }
+        if (__ballot(need) != 0) __builtin_amdgcn_s_sleep(1);
     }
     if (need) atomicOr(T.err, ERR_SPIN);
     return res;
@@ -152,9 +146,12 @@ __device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t 
 // returns true when src > dst (the packet travels hi -> lo).
 __device__ __forceinline__ bool src_gt_dst(const uint32_t* sip, const uint32_t* dip, uint32_t sp, uint32_t dp,
                                           uint64_t smac, uint64_t dmac, bool v6, bool macs) {
-    int n = v6 ? 4 : 1;
-    for (int k = 0; k < n; k++)
-        if (sip[k] != dip[k]) return sip[k] > dip[k];
+    if (sip[0] != dip[0]) return sip[0] > dip[0];
+    if (v6) {
+#pragma unroll
+        for (int k = 1; k < 4; k++)
+            if (sip[k] != dip[k]) return sip[k] > dip[k];
+    }
     if (sp != dp) return sp > dp;
     if (macs && smac != dmac) return smac > dmac;
     return false;

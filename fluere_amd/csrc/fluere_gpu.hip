@@ -49,7 +49,9 @@ static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
 namespace {
 
 constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
-constexpr int H = 2048;          // LDS direct-mapped flow slots (dense ids < H)
+constexpr int H = 1280;          // LDS direct-mapped aggregation slots (dense ids < H), 80 KiB
+constexpr int KC = 2048;         // LDS flow-key cache entries (canonical IPv4 key -> dense id), 64 KiB
+constexpr int KC_PROBE = 4;
 constexpr int WIN_ITERS = 32;    // flush LDS every 32 x 1024 packets (u32 byte sums cannot wrap)
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
@@ -107,12 +109,16 @@ struct Parsed {
 
 __device__ __forceinline__ uint32_t hdr_word(uint32_t w, bool swapped) { return swapped ? bswap32(w) : w; }
 
+// Five unconditional 16-byte loads (unaligned global_load_dwordx4): record
+// header + the first 64 frame bytes.  Unconditional so the compiler can count
+// outstanding loads and keep the next packet's window in flight; batches are
+// readable 80 bytes past their end (fluere_add_device_batch contract).
 __device__ __forceinline__ void load_win(const Batch& B, uint32_t off, Win& W) {
     const uint8_t* p = B.bytes + off;
 #pragma unroll
     for (int c = 0; c < 5; c++) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if ((uint64_t)off + 16 * c < B.nbytes) __builtin_memcpy(&v, p + 16 * c, 16);
+        uint4 v;
+        __builtin_memcpy(&v, p + 16 * c, 16);
         W.w[4 * c + 0] = v.x; W.w[4 * c + 1] = v.y; W.w[4 * c + 2] = v.z; W.w[4 * c + 3] = v.w;
     }
 }
@@ -178,11 +184,13 @@ __device__ __forceinline__ void canon_key(const Parsed& P, bool macs, CKey& k, u
     const PktInfo& pi = P.pi;
     bool gt = src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs);
     dir = gt ? 1 : 0;
-    const uint32_t* lo = gt ? pi.dip : pi.sip;
-    const uint32_t* hi = gt ? pi.sip : pi.dip;
     uint32_t lop = gt ? pi.kdp : pi.ksp, hip = gt ? pi.ksp : pi.kdp;
     uint64_t lom = gt ? P.dmac : P.smac, him = gt ? P.smac : P.dmac;
-    for (int j = 0; j < 4; j++) { k.w[j] = lo[j]; k.w[4 + j] = hi[j]; }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // per-word selects keep the IP arrays in registers
+        k.w[j] = gt ? pi.dip[j] : pi.sip[j];
+        k.w[4 + j] = gt ? pi.sip[j] : pi.dip[j];
+    }
     k.w[8] = (lop << 16) | hip;
     uint32_t kind = (pi.v6 ? 1u : 0u) | (macs ? 2u : 0u);
     k.w[9] = (kind << 8) | pi.kproto;
@@ -199,11 +207,12 @@ __device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& 
     for (int j = 0; j < N_TABLES; j++) chain[j] = NONE32;
     uint32_t s;
     int ft;
+    unsigned long long v = EMPTY;
     if (!v6 && !macs) {
         s = tab_slot(T, 0, ((uint64_t)k.w[0] << 32) | k.w[4], insert);
         if (s == FAIL) return FAIL;
         chain[0] = s;
-        s = tab_slot(T, 1, ((uint64_t)s << 40) | ((uint64_t)k.w[8] << 8) | (k.w[9] & 0xFF), insert);
+        s = tab_slot(T, 1, ((uint64_t)s << 40) | ((uint64_t)k.w[8] << 8) | (k.w[9] & 0xFF), insert, &v);
         if (s == FAIL) return FAIL;
         chain[1] = s;
         ft = 1;
@@ -221,21 +230,21 @@ __device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& 
         }
         u[10] = m0; u[11] = m1; u[12] = m2;
         const int m = v6 ? (macs ? 13 : 10) : 7;
-        s = tab_slot(T, 2, ((uint64_t)u[0] << 32) | u[1], insert);
+        s = tab_slot(T, 2, ((uint64_t)u[0] << 32) | u[1], insert, &v);
         if (s == FAIL) return FAIL;
         chain[2] = s;
         ft = 2;
 #pragma unroll
         for (int j = 2; j < 13; j++) {
             if (j < m) {
-                s = tab_slot(T, j + 1, ((uint64_t)s << 32) | u[j], insert);
+                s = tab_slot(T, j + 1, ((uint64_t)s << 32) | u[j], insert, &v);
                 if (s == FAIL) return FAIL;
                 chain[j + 1] = s;
                 ft = j + 1;
             }
         }
     }
-    return dense_id(T, ft, s, insert, k, chain, chain_out);
+    return dense_id(T, ft, s, insert, k, chain, chain_out, v);
 }
 
 __device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, bool macs, bool insert,
@@ -258,12 +267,10 @@ struct AggArgs {
     int macs;
 };
 
-// Front end of the hot kernel: record header + five 16-byte loads + the
-// static-offset parser.  Returns false when the general parser is needed.
-__device__ __forceinline__ bool parse_fast_record(const Batch& B, uint64_t li, bool macs, Parsed& P) {
-    uint32_t off = B.offs[li];
-    Win W;
-    load_win(B, off, W);
+// Front end of the hot kernel: the static-offset parser over a record window
+// already in registers (header + first 64 frame bytes).  Returns false when
+// the general parser is needed.
+__device__ __forceinline__ bool parse_fast_window(const Batch& B, uint32_t off, const Win& W, bool macs, Parsed& P) {
     bool sw = B.flags & 1;
     uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
     uint32_t L = min(incl, B.snap);
@@ -304,11 +311,16 @@ __device__ __forceinline__ void agg_global(const Acc& A, uint32_t d, uint8_t dir
     atomicMax(&A.la[d], (unsigned long long)gi);
 }
 
+// ABL (diagnostics only): 0 full kernel; 1 parse only; 2 parse + flow id; 3 parse + flow id, global atomics only
+template <int ABL>
 __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint32_t s_pk[2][H], s_by[2][H], s_mn[2][H], s_mx[2][H], s_fl[4][H];
     __shared__ uint32_t s_fa[H], s_fc[H], s_fr[H], s_la[H];
+    __shared__ uint4 s_kc_key[KC];   // (lo_ip, hi_ip, lo_port<<16|hi_port, proto)
+    __shared__ uint2 s_kc_meta[KC];  // (dense id, tag): tag 0 empty, 1 being filled, else ready|hash
     __shared__ unsigned long long s_cnt[2], s_tmin, s_tmax;
     const int tid = threadIdx.x;
+    for (int e = tid; e < KC; e += BLOCK) s_kc_meta[e] = make_uint2(0, 0);
     for (int e = tid; e < H; e += BLOCK) {
         s_pk[0][e] = s_pk[1][e] = s_by[0][e] = s_by[1][e] = 0;
         s_mn[0][e] = s_mn[1][e] = NONE32;
@@ -331,21 +343,71 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 
     for (uint64_t wbase = beg; wbase < end; wbase += (uint64_t)BLOCK * WIN_ITERS) {
         const uint64_t wend = min(end, wbase + (uint64_t)BLOCK * WIN_ITERS);
-        for (uint64_t li = wbase + tid; li < wend; li += BLOCK) {
+        // one packet: parse (registers only), flow key, LDS key cache / flow
+        // dictionary, LDS or global aggregation
+        auto process = [&](const Win& W, const uint32_t off, const uint64_t li) {
             Parsed P;
-            if (!parse_fast_record(B, li, macs, P)) {
+            if (!parse_fast_window(B, off, W, macs, P)) {
                 a.slow[atomicAdd(a.slow_n, 1ull)] = (uint32_t)li;
-                continue;
+                return;
             }
-            if (P.cls) { c_drop++; continue; }
+            if (P.cls) { c_drop++; return; }
             c_valid++;
             tmin = min(tmin, (unsigned long long)P.t);
             tmax = max(tmax, (unsigned long long)P.t);
             uint8_t dir;
-            uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
-            if (d == FAIL || d >= a.T.fmax) continue;  // error flag already set
+            CKey k;
+            canon_key(P, macs, k, dir);
+            if (ABL == 1) {
+                uint32_t x = k.w[0] ^ k.w[4] ^ k.w[8] ^ k.w[9] ^ P.pi.doctets ^ P.pi.rpkt ^ P.pi.rttl ^ dir;
+                asm volatile("" ::"v"(x));
+                return;
+            }
+            uint32_t d = FAIL;
+            if (!macs) {
+                // per-workgroup flow-key cache: entries are written once (empty ->
+                // filling -> ready) and never replaced inside the launch, so a
+                // ready entry whose key words match is exact
+                const uint32_t hk = (uint32_t)(mix64(((uint64_t)k.w[0] << 32 | k.w[4]) ^
+                                                     ((uint64_t)k.w[8] << 24) ^ k.w[9]) >> 32);
+                const uint32_t tag = hk | 0x80000000u;
+                uint32_t e = hk & (KC - 1);
+                bool found = false, free_slot = false;
+#pragma unroll
+                for (int q = 0; q < KC_PROBE; q++) {
+                    // meta is read before the key words and a wave's LDS reads are
+                    // served in issue order, so a ready tag implies final key words
+                    const uint2 m = s_kc_meta[e];
+                    asm volatile("" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint4 kk = s_kc_key[e];
+                    if (m.y == tag && kk.x == k.w[0] && kk.y == k.w[4] && kk.z == k.w[8] && kk.w == k.w[9]) {
+                        d = m.x;
+                        found = true;
+                        break;
+                    }
+                    if (m.y == 0) { free_slot = true; break; }
+                    e = (e + 1) & (KC - 1);
+                }
+                if (!found) {
+                    d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
+                    if (free_slot && d != FAIL && atomicCAS(&s_kc_meta[e].y, 0u, 1u) == 0u) {
+                        s_kc_key[e] = make_uint4(k.w[0], k.w[4], k.w[8], k.w[9]);
+                        s_kc_meta[e].x = d;
+                        __threadfence_block();
+                        atomicExch(&s_kc_meta[e].y, tag);
+                    }
+                }
+            } else {
+                d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+            }
+            if (d == FAIL || d >= a.T.fmax) return;  // error flag already set
             const PktInfo& pi = P.pi;
-            if (d < H) {
+            if (ABL == 2) {
+                asm volatile("" ::"v"(d), "v"(pi.doctets), "v"(pi.rpkt));
+                return;
+            }
+            if (d < H && ABL == 0) {
                 const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
                 const uint32_t loc = (uint32_t)(li - wbase);
                 atomicAdd(&s_pk[dir][d], 1u);
@@ -368,6 +430,29 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             } else {
                 agg_global(a.A, d, dir, pi, B.first + li);
             }
+        };
+        // software pipeline, unrolled by two so the in-flight window never has
+        // to be copied (a copy would wait on the load): while packet li is
+        // processed from one window, packet li+BLOCK streams into the other
+        // and the offset of li+2*BLOCK is loaded
+        const uint64_t lastp = n - 1;  // prefetches past the end re-read the last packet (in bounds)
+        uint64_t li = wbase + tid;
+        uint32_t oA = B.offs[min(li, lastp)];
+        uint32_t oB = B.offs[min(li + BLOCK, lastp)];
+        Win WA, WB;
+        load_win(B, oA, WA);
+        while (li < wend) {
+            const uint32_t curA = oA;
+            load_win(B, oB, WB);
+            oA = B.offs[min(li + 2 * BLOCK, lastp)];
+            process(WA, curA, li);
+            li += BLOCK;
+            if (li >= wend) break;
+            const uint32_t curB = oB;
+            load_win(B, oA, WA);
+            oB = B.offs[min(li + 2 * BLOCK, lastp)];
+            process(WB, curB, li);
+            li += BLOCK;
         }
         __syncthreads();
         // flush: lanes walk consecutive flow ids -> coalesced global atomics
@@ -1323,7 +1408,11 @@ static int launch_parse_agg(fluere_ctx* c) {
         HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 8, c->stream));
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
         unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
-        k_parse_agg<<<grid, BLOCK, 0, c->stream>>>(a);
+        static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
+        if (abl == 1) k_parse_agg<1><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 2) k_parse_agg<2><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 3) k_parse_agg<3><<<grid, BLOCK, 0, c->stream>>>(a);
+        else k_parse_agg<0><<<grid, BLOCK, 0, c->stream>>>(a);
         k_parse_agg_slow<<<(unsigned)std::max(1, c->n_cu * 4), 256, 0, c->stream>>>(a);
     }
     HIPCHECK(hipGetLastError());

@@ -134,8 +134,8 @@ int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint64_t* offset
  * offset of record i's 16-byte header inside d_bytes.  Batches must be
  * appended in capture order; the library does not copy them and they must
  * stay valid until fluere_reset/fluere_close.  nbytes < 4 GiB, and the
- * buffer must stay readable 16 bytes past nbytes (records are read with
- * 16-byte loads).  snaplen: the file header's snaplen (0: 262144);
+ * buffer must stay readable 80 bytes past nbytes (every record is read as
+ * one unconditional 80-byte window: header + first 64 frame bytes).  snaplen: the file header's snaplen (0: 262144);
  * swapped: byte-swapped pcap; nsec_ts: nanosecond timestamps. */
 int fluere_add_device_batch(fluere_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes,
                             const uint32_t* d_offsets, uint64_t n_packets, uint32_t snaplen, int swapped,
