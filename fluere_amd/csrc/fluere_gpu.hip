@@ -50,8 +50,9 @@ namespace {
 
 constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
 constexpr int H = 1280;          // LDS direct-mapped aggregation slots (dense ids < H), 80 KiB
-constexpr int KC = 2048;         // LDS flow-key cache entries (canonical IPv4 key -> dense id), 64 KiB
+constexpr int KC = 4096;         // LDS flow-key cache entries (canonical IPv4 key -> dense id), 64 KiB
 constexpr int KC_PROBE = 4;
+constexpr uint32_t KC_READY = 1u << 23, KC_ID = KC_READY - 1, KC_CLAIM = 1u << 22;  // ids < 2^22 are cached
 constexpr int WIN_ITERS = 32;    // flush LDS every 32 x 1024 packets (u32 byte sums cannot wrap)
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
@@ -311,18 +312,26 @@ __device__ __forceinline__ void agg_global(const Acc& A, uint32_t d, uint8_t dir
     atomicMax(&A.la[d], (unsigned long long)gi);
 }
 
+// Workgroup barrier for LDS-only hand-offs: waits for this wave's LDS
+// operations, not for its outstanding global loads (__syncthreads would drain
+// the prefetched windows).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ABL (diagnostics only): 0 full kernel; 1 parse only; 2 parse + flow id; 3 parse + flow id, global atomics only
-template <int ABL>
+template <int ABL, bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
-    __shared__ uint32_t s_pk[2][H], s_by[2][H], s_mn[2][H], s_mx[2][H], s_fl[4][H];
+    __shared__ uint32_t s_pk[H];  // packets per canonical direction, 16-bit halves (window <= 32768)
+    __shared__ uint32_t s_by[2][H], s_mn[2][H], s_mx[2][H], s_fl[4][H];
     __shared__ uint32_t s_fa[H], s_fc[H], s_fr[H], s_la[H];
-    __shared__ uint4 s_kc_key[KC];   // (lo_ip, hi_ip, lo_port<<16|hi_port, proto)
-    __shared__ uint2 s_kc_meta[KC];  // (dense id, tag): tag 0 empty, 1 being filled, else ready|hash
+    // flow-key cache entry: (lo_ip, hi_ip, lo_port<<16|hi_port, proto<<24 | READY | dense id)
+    __shared__ uint4 s_kc[KC];
     __shared__ unsigned long long s_cnt[2], s_tmin, s_tmax;
     const int tid = threadIdx.x;
-    for (int e = tid; e < KC; e += BLOCK) s_kc_meta[e] = make_uint2(0, 0);
+    for (int e = tid; e < KC; e += BLOCK) s_kc[e] = make_uint4(0, 0, 0, 0);
     for (int e = tid; e < H; e += BLOCK) {
-        s_pk[0][e] = s_pk[1][e] = s_by[0][e] = s_by[1][e] = 0;
+        s_pk[e] = s_by[0][e] = s_by[1][e] = 0;
         s_mn[0][e] = s_mn[1][e] = NONE32;
         s_mx[0][e] = s_mx[1][e] = 0;
         s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
@@ -334,132 +343,115 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __syncthreads();
 
     const Batch& B = a.B;
-    const bool macs = a.macs != 0;
+    constexpr bool macs = MACS;  // key family fixed per instantiation (IPv4 fast path: 5-tuple or MAC pair)
     const uint64_t n = B.n;
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t beg = per * blockIdx.x;
     const uint64_t end = min(n, beg + per);
     unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
 
-    for (uint64_t wbase = beg; wbase < end; wbase += (uint64_t)BLOCK * WIN_ITERS) {
-        const uint64_t wend = min(end, wbase + (uint64_t)BLOCK * WIN_ITERS);
-        // one packet: parse (registers only), flow key, LDS key cache / flow
-        // dictionary, LDS or global aggregation
-        auto process = [&](const Win& W, const uint32_t off, const uint64_t li) {
-            Parsed P;
-            if (!parse_fast_window(B, off, W, macs, P)) {
-                a.slow[atomicAdd(a.slow_n, 1ull)] = (uint32_t)li;
-                return;
-            }
-            if (P.cls) { c_drop++; return; }
-            c_valid++;
-            tmin = min(tmin, (unsigned long long)P.t);
-            tmax = max(tmax, (unsigned long long)P.t);
-            uint8_t dir;
-            CKey k;
-            canon_key(P, macs, k, dir);
-            if (ABL == 1) {
-                uint32_t x = k.w[0] ^ k.w[4] ^ k.w[8] ^ k.w[9] ^ P.pi.doctets ^ P.pi.rpkt ^ P.pi.rttl ^ dir;
-                asm volatile("" ::"v"(x));
-                return;
-            }
-            uint32_t d = FAIL;
-            if (!macs) {
-                // per-workgroup flow-key cache: entries are written once (empty ->
-                // filling -> ready) and never replaced inside the launch, so a
-                // ready entry whose key words match is exact
-                const uint32_t hk = (uint32_t)(mix64(((uint64_t)k.w[0] << 32 | k.w[4]) ^
-                                                     ((uint64_t)k.w[8] << 24) ^ k.w[9]) >> 32);
-                const uint32_t tag = hk | 0x80000000u;
-                uint32_t e = hk & (KC - 1);
-                bool found = false, free_slot = false;
-#pragma unroll
-                for (int q = 0; q < KC_PROBE; q++) {
-                    // meta is read before the key words and a wave's LDS reads are
-                    // served in issue order, so a ready tag implies final key words
-                    const uint2 m = s_kc_meta[e];
-                    asm volatile("" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                    const uint4 kk = s_kc_key[e];
-                    if (m.y == tag && kk.x == k.w[0] && kk.y == k.w[4] && kk.z == k.w[8] && kk.w == k.w[9]) {
-                        d = m.x;
-                        found = true;
-                        break;
-                    }
-                    if (m.y == 0) { free_slot = true; break; }
-                    e = (e + 1) & (KC - 1);
-                }
-                if (!found) {
-                    d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
-                    if (free_slot && d != FAIL && atomicCAS(&s_kc_meta[e].y, 0u, 1u) == 0u) {
-                        s_kc_key[e] = make_uint4(k.w[0], k.w[4], k.w[8], k.w[9]);
-                        s_kc_meta[e].x = d;
-                        __threadfence_block();
-                        atomicExch(&s_kc_meta[e].y, tag);
-                    }
-                }
-            } else {
-                d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
-            }
-            if (d == FAIL || d >= a.T.fmax) return;  // error flag already set
-            const PktInfo& pi = P.pi;
-            if (ABL == 2) {
-                asm volatile("" ::"v"(d), "v"(pi.doctets), "v"(pi.rpkt));
-                return;
-            }
-            if (d < H && ABL == 0) {
-                const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
-                const uint32_t loc = (uint32_t)(li - wbase);
-                atomicAdd(&s_pk[dir][d], 1u);
-                atomicAdd(&s_by[dir][d], pi.doctets);
-                if (pkt < s_mn[0][d]) atomicMin(&s_mn[0][d], pkt);
-                if (pkt > s_mx[0][d]) atomicMax(&s_mx[0][d], pkt);
-                if (ttl < s_mn[1][d]) atomicMin(&s_mn[1][d], ttl);
-                if (ttl > s_mx[1][d]) atomicMax(&s_mx[1][d], ttl);
-                if (tf) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
-                        if (w) atomicAdd(&s_fl[q][d], w);
-                    }
-                    if (tf & 5) atomicMin(&s_fr[d], loc);
-                }
-                if (loc < s_fa[d]) atomicMin(&s_fa[d], loc);
-                if ((pi.rprot != 6 || (tf & 2)) && loc < s_fc[d]) atomicMin(&s_fc[d], loc);
-                atomicMax(&s_la[d], loc + 1);
-            } else {
-                agg_global(a.A, d, dir, pi, B.first + li);
-            }
-        };
-        // software pipeline, unrolled by two so the in-flight window never has
-        // to be copied (a copy would wait on the load): while packet li is
-        // processed from one window, packet li+BLOCK streams into the other
-        // and the offset of li+2*BLOCK is loaded
-        const uint64_t lastp = n - 1;  // prefetches past the end re-read the last packet (in bounds)
-        uint64_t li = wbase + tid;
-        uint32_t oA = B.offs[min(li, lastp)];
-        uint32_t oB = B.offs[min(li + BLOCK, lastp)];
-        Win WA, WB;
-        load_win(B, oA, WA);
-        while (li < wend) {
-            const uint32_t curA = oA;
-            load_win(B, oB, WB);
-            oA = B.offs[min(li + 2 * BLOCK, lastp)];
-            process(WA, curA, li);
-            li += BLOCK;
-            if (li >= wend) break;
-            const uint32_t curB = oB;
-            load_win(B, oA, WA);
-            oB = B.offs[min(li + 2 * BLOCK, lastp)];
-            process(WB, curB, li);
-            li += BLOCK;
+    // The packet loop is uniform over the workgroup (nsteps steps of BLOCK
+    // packets); every WIN_ITERS steps the LDS aggregates are flushed.  Loads
+    // are issued in the order the loop consumes them -- the offset of packet
+    // li+2*BLOCK before the window of li+BLOCK -- so that with in-order vmcnt
+    // accounting a wait for one never drains the other, and the prefetch runs
+    // straight through the flushes.
+    const uint64_t nsteps = end > beg ? (end - beg + BLOCK - 1) / BLOCK : 0;
+    uint64_t wbase = beg;
+    auto process = [&](const Win& W, const uint32_t off, const uint64_t li) {
+        Parsed P;
+        if (!parse_fast_window(B, off, W, macs, P)) {
+            a.slow[atomicAdd(a.slow_n, 1ull)] = (uint32_t)li;
+            return;
         }
-        __syncthreads();
+        if (P.cls) { c_drop++; return; }
+        c_valid++;
+        tmin = min(tmin, (unsigned long long)P.t);
+        tmax = max(tmax, (unsigned long long)P.t);
+        uint8_t dir;
+        CKey k;
+        canon_key(P, macs, k, dir);
+        if (ABL == 1) {
+            uint32_t x = k.w[0] ^ k.w[4] ^ k.w[8] ^ k.w[9] ^ P.pi.doctets ^ P.pi.rpkt ^ P.pi.rttl ^ dir;
+            asm volatile("" ::"v"(x));
+            return;
+        }
+        uint32_t d = FAIL;
+        if (!macs) {
+            // per-workgroup flow-key cache.  An entry is one 16-byte LDS word
+            // group written once inside the launch: claim (CAS the last word
+            // 0 -> KC_CLAIM), write the key words, publish (last word =
+            // proto | READY | id).  A reader takes the entry only if its
+            // single 16-byte read shows READY and all key words match, so
+            // the id it uses belongs to exactly its key.
+            const uint32_t hk = (uint32_t)(mix64(((uint64_t)k.w[0] << 32 | k.w[4]) ^
+                                                 ((uint64_t)k.w[8] << 24) ^ k.w[9]) >> 32);
+            const uint32_t want3 = (k.w[9] & 0xFF) << 24;
+            uint32_t e = hk & (KC - 1);
+            bool found = false, free_slot = false;
+#pragma unroll
+            for (int q = 0; q < KC_PROBE; q++) {
+                const uint4 kk = s_kc[e];
+                if ((kk.w & KC_READY) && kk.x == k.w[0] && kk.y == k.w[4] && kk.z == k.w[8] &&
+                    (kk.w & 0xFF000000u) == want3) {
+                    d = kk.w & KC_ID;
+                    found = true;
+                    break;
+                }
+                if (kk.w == 0) { free_slot = true; break; }
+                e = (e + 1) & (KC - 1);
+            }
+            if (!found) {
+                d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
+                if (free_slot && d <= KC_ID && atomicCAS(&s_kc[e].w, 0u, KC_CLAIM) == 0u) {
+                    s_kc[e].x = k.w[0];
+                    s_kc[e].y = k.w[4];
+                    s_kc[e].z = k.w[8];
+                    __threadfence_block();
+                    atomicExch(&s_kc[e].w, want3 | KC_READY | d);
+                }
+            }
+        } else {
+            d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+        }
+        if (d == FAIL || d >= a.T.fmax) return;  // error flag already set
+        const PktInfo& pi = P.pi;
+        if (ABL == 2) {
+            asm volatile("" ::"v"(d), "v"(pi.doctets), "v"(pi.rpkt));
+            return;
+        }
+        if (d < H && ABL == 0) {
+            const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
+            const uint32_t loc = (uint32_t)(li - wbase);
+            atomicAdd(&s_pk[d], 1u << (16 * dir));
+            atomicAdd(&s_by[dir][d], pi.doctets);
+            if (pkt < s_mn[0][d]) atomicMin(&s_mn[0][d], pkt);
+            if (pkt > s_mx[0][d]) atomicMax(&s_mx[0][d], pkt);
+            if (ttl < s_mn[1][d]) atomicMin(&s_mn[1][d], ttl);
+            if (ttl > s_mx[1][d]) atomicMax(&s_mx[1][d], ttl);
+            if (tf) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
+                    if (w) atomicAdd(&s_fl[q][d], w);
+                }
+                if (tf & 5) atomicMin(&s_fr[d], loc);
+            }
+            if (loc < s_fa[d]) atomicMin(&s_fa[d], loc);
+            if ((pi.rprot != 6 || (tf & 2)) && loc < s_fc[d]) atomicMin(&s_fc[d], loc);
+            atomicMax(&s_la[d], loc + 1);
+        } else {
+            agg_global(a.A, d, dir, pi, B.first + li);
+        }
+    };
+    auto flush = [&]() {
+        lds_barrier();
         // flush: lanes walk consecutive flow ids -> coalesced global atomics
         const uint64_t gbase = B.first + wbase;
         for (int e = tid; e < H; e += BLOCK) {
-            uint32_t c0 = s_pk[0][e], c1 = s_pk[1][e];
-            if (c0 + c1 == 0) continue;
+            const uint32_t pk = s_pk[e];
+            if (pk == 0) continue;
+            const uint32_t c0 = pk & 0xFFFF, c1 = pk >> 16;
             if (c0) { atomicAdd(&a.A.pk[0][e], c0); atomicAdd(&a.A.by[0][e], (unsigned long long)s_by[0][e]); }
             if (c1) { atomicAdd(&a.A.pk[1][e], c1); atomicAdd(&a.A.by[1][e], (unsigned long long)s_by[1][e]); }
             for (int q = 0; q < 2; q++) {
@@ -475,15 +467,39 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             if (s_fc[e] != NONE32) atomicMin(&a.A.fc[e], gbase + s_fc[e]);
             if (s_fr[e] != NONE32) atomicMin(&a.A.fr[e], gbase + s_fr[e]);
             atomicMax(&a.A.la[e], gbase + s_la[e] - 1);
-            s_pk[0][e] = s_pk[1][e] = s_by[0][e] = s_by[1][e] = 0;
+            s_pk[e] = s_by[0][e] = s_by[1][e] = 0;
             s_mn[0][e] = s_mn[1][e] = NONE32;
             s_mx[0][e] = s_mx[1][e] = 0;
             s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
             s_fa[e] = s_fc[e] = s_fr[e] = NONE32;
             s_la[e] = 0;
         }
-        __syncthreads();
+        lds_barrier();
+        wbase += (uint64_t)BLOCK * WIN_ITERS;
+    };
+    const uint64_t lastp = n - 1;  // prefetches past the end re-read the last packet (in bounds)
+    uint64_t li = beg + tid;
+    uint32_t oA = B.offs[min(li, lastp)];
+    uint32_t oB = B.offs[min(li + BLOCK, lastp)];
+    Win WA, WB;
+    load_win(B, oA, WA);
+    for (uint64_t st = 0; st < nsteps; st += 2) {
+        // software pipeline, unrolled by two so the in-flight window is never
+        // copied (a copy would wait on the load)
+        const uint32_t curA = oA;
+        oA = B.offs[min(li + 2 * BLOCK, lastp)];
+        load_win(B, oB, WB);
+        if (li < end) process(WA, curA, li);
+        li += BLOCK;
+        if (st + 1 == nsteps) break;
+        const uint32_t curB = oB;
+        oB = B.offs[min(li + 2 * BLOCK, lastp)];
+        load_win(B, oA, WA);
+        if (li < end) process(WB, curB, li);
+        li += BLOCK;
+        if ((st + 2) % WIN_ITERS == 0 && st + 2 < nsteps) flush();
     }
+    flush();
     // statistics: one global atomic per workgroup
     atomicAdd(&s_cnt[0], c_valid);
     atomicAdd(&s_cnt[1], c_drop);
@@ -1409,10 +1425,11 @@ static int launch_parse_agg(fluere_ctx* c) {
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
         unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
         static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
-        if (abl == 1) k_parse_agg<1><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 2) k_parse_agg<2><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 3) k_parse_agg<3><<<grid, BLOCK, 0, c->stream>>>(a);
-        else k_parse_agg<0><<<grid, BLOCK, 0, c->stream>>>(a);
+        if (a.macs) k_parse_agg<0, true><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 1) k_parse_agg<1, false><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 2) k_parse_agg<2, false><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 3) k_parse_agg<3, false><<<grid, BLOCK, 0, c->stream>>>(a);
+        else k_parse_agg<0, false><<<grid, BLOCK, 0, c->stream>>>(a);
         k_parse_agg_slow<<<(unsigned)std::max(1, c->n_cu * 4), 256, 0, c->stream>>>(a);
     }
     HIPCHECK(hipGetLastError());
