@@ -109,12 +109,19 @@ __device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t 
         return v0 < PENDING ? (uint32_t)v0 : FAIL;
     }
     uint32_t res = FAIL;
-    bool need = true;
+    bool need = true, try_cas = true;
     for (int spins = 0; spins < (1 << 20); spins++) {
         if (__ballot(need) == 0) break;
         if (need) {
-            unsigned long long v = atomicCAS(val, EMPTY, PENDING);
-            if (v == EMPTY) {
+            // Claim attempts are CAS; after a lost claim (PENDING) the lane polls
+            // with coherent atomic loads, so the many waiting workgroups do not
+            // queue read-modify-writes in front of the claimer's publish.  Only a
+            // CAS that returned EMPTY claims; a poll reading EMPTY retries the CAS.
+            const bool cas = try_cas;
+            unsigned long long v = cas ? atomicCAS(val, EMPTY, PENDING)
+                                       : __hip_atomic_load(val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            try_cas = v == EMPTY;
+            if (cas && v == EMPTY) {
                 uint32_t d = atomicAdd(T.n_flows, 1u);
                 if (d >= T.fmax) {
                     atomicOr(T.err, ERR_FLOWS_FULL);
@@ -131,12 +138,16 @@ __device__ __forceinline__ uint32_t dense_id(const TableSet& T, int t, uint32_t 
                 atomicExch(val, (unsigned long long)d);
                 res = d;
                 need = false;
-            } else if (v != PENDING) {
+            } else if (v != PENDING && v != EMPTY) {
                 res = (uint32_t)v;
                 need = false;
             }
         }
-        if (__ballot(need) != 0) __builtin_amdgcn_s_sleep(1);
+        if (__ballot(need) != 0) {  // back off: ~0.1 us, then ~0.5 us, then ~2 us between polls
+            if (spins < 4) __builtin_amdgcn_s_sleep(4);
+            else if (spins < 16) __builtin_amdgcn_s_sleep(16);
+            else __builtin_amdgcn_s_sleep(64);
+        }
     }
     if (need) atomicOr(T.err, ERR_SPIN);
     return res;

@@ -48,20 +48,26 @@ def merge_summaries(ctx, summaries, tmin: int, tmax: int) -> dict:
     return st.as_dict()
 
 
-def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int = 0):
-    """All-gather every shard's summaries (RCCL over xGMI) and merge on rank dst.
+NONE64 = (1 << 64) - 1  # tmin of a shard without valid packets
 
-    Returns the merge stats on dst, None elsewhere."""
+
+def gather_summaries(summaries, tmin: int, tmax: int, group=None, dst: int = 0):
+    """All-gather every shard's flow summaries (RCCL over xGMI on GPUs, gloo on
+    CPU) -> (concatenated summaries in rank order, global tmin, global tmax) on
+    rank dst, None elsewhere.  Shards may be empty (tmin NONE64)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = summaries.device
-    meta = torch.tensor([summaries.numel() // SUMMARY_BYTES, tmin, tmax], dtype=torch.int64, device=dev)
+    # timestamps are microseconds (< 2^63); an empty shard travels as -1
+    meta = torch.tensor([summaries.numel() // SUMMARY_BYTES, tmin if tmin < (1 << 63) else -1, tmax],
+                        dtype=torch.int64, device=dev)
     metas = [torch.empty_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
     counts = [int(m[0]) for m in metas]
-    gmin = min(int(m[1]) for m in metas)
+    lows = [int(m[1]) for m in metas if int(m[1]) >= 0]
+    gmin = min(lows) if lows else NONE64
     gmax = max(int(m[2]) for m in metas)
     cap = max(max(counts), 1) * SUMMARY_BYTES
     send = torch.zeros(cap, dtype=torch.uint8, device=dev)
@@ -71,6 +77,17 @@ def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int 
     if rank != dst:
         return None
     parts = [recv[r * cap: r * cap + counts[r] * SUMMARY_BYTES] for r in range(world)]
-    allsum = torch.cat(parts) if parts else recv[:0]
-    torch.cuda.current_stream().synchronize()
+    return torch.cat(parts), gmin, gmax
+
+
+def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int = 0):
+    """All-gather every shard's summaries and merge them on rank dst (device
+    merge, fluere_merge_summaries).  Returns the merge stats on dst, None
+    elsewhere."""
+    import torch
+    got = gather_summaries(summaries, tmin, tmax, group, dst)
+    if got is None:
+        return None
+    allsum, gmin, gmax = got
+    torch.cuda.current_stream().synchronize()  # the collective ran on torch's stream, the merge runs on ctx's
     return merge_summaries(ctx, allsum, gmin, gmax)
