@@ -71,13 +71,14 @@ def main():
     ctx.add_device_batch(b, nbytes, o, n)
 
     sums_buf = None
-    kernel_ms = []
+    kernel_ms, pass_ms = [], []
 
     def step():
         nonlocal sums_buf
         s, lo, hi = fdist.export_summaries(ctx, sums_buf)
         sums_buf = s if sums_buf is None or s.numel() > sums_buf.numel() else sums_buf
         kernel_ms.append(ctx.last_kernel_ms())
+        pass_ms.append(ctx.last_pass_ms())
         if world > 1:
             return fdist.gather_and_merge(ctx, s, lo, hi)
         return fdist.merge_summaries(ctx, s, lo, hi)
@@ -91,6 +92,7 @@ def main():
     for _ in range(args.warmup):
         step()
     kernel_ms.clear()
+    pass_ms.clear()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -137,6 +139,7 @@ def main():
                          "kernel": "k_parse_agg", "kernel_ms": round(kernel_avg, 4),
                          "algorithmic_bytes_per_launch": BYTES_PER_PKT * n},
             "parse_key_mpps_per_gpu": round(n / (kernel_avg * 1e-3) / 1e6, 1),
+            "aggregate_pass_ms": round(sum(pass_ms) / len(pass_ms), 4),
             "records": int(len(recs)),
             "records_ended": int(ne),
         }

@@ -49,10 +49,6 @@ static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
 namespace {
 
 constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
-constexpr int H = 1280;          // LDS direct-mapped aggregation slots (dense ids < H), 80 KiB
-constexpr int KC = 4096;         // LDS flow-key cache entries (canonical IPv4 key -> dense id), 64 KiB
-constexpr int KC_PROBE = 4;
-constexpr uint32_t KC_READY = 1u << 23, KC_ID = KC_READY - 1, KC_CLAIM = 1u << 22;  // ids < 2^22 are cached
 constexpr int WIN_ITERS = 32;    // flush LDS every 32 x 1024 packets (u32 byte sums cannot wrap)
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
@@ -89,7 +85,9 @@ struct Glob {
     unsigned long long n_keys, n_heads;
     unsigned long long generic_used;
     unsigned long long n_slow;
-    unsigned long long n_kc_miss;  // diagnostics: hot-kernel key-cache misses
+    unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
+    unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
+    unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
 };
 
 #define HIPCHECK(x)                                  \
@@ -259,10 +257,35 @@ __device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, 
 // ---------------------------------------------------------------------------
 // k_parse_agg: the hot kernel
 // ---------------------------------------------------------------------------
+// Per-window partial aggregates of the hot kernel's LDS flow tables, one "set"
+// per (workgroup, window), SoA over [set * NS + cell].  Within a set the
+// cells are grouped by merge owner (owner = hash(key) % O), so the owner of a
+// flow reads only its own segment of every set.  Written with plain stores;
+// merged per flow by k_merge_partials.
+// One staged partial: 80 bytes, written and read as five 16-byte accesses.
+struct alignas(16) Part {
+    uint32_t k0, k1, k2, tag;     // key words; tag = proto << 24 (0xFF << 24: k0 is a dense id)
+    uint32_t h, pk, by0, by1;     // key hash; packets per direction (16-bit halves); bytes per direction
+    uint32_t mn0, mn1, mx0, mx1;  // min / max pkt, min / max ttl
+    uint32_t fl[4];               // flag pairs, 16-bit halves
+    uint32_t pos[4];              // first any / first create / first FIN-RST (NONE32) and last+1 (0), window-relative
+};
+static_assert(sizeof(Part) == 80, "Part layout");
+
+struct Stage {
+    Part* part;                   // [set * NS + cell]
+    uint32_t* off;                // [(O + 1) * n_sets]: off[o * n_sets + set] = first cell of owner o's flows
+    unsigned long long* base;     // [set] global index of the window's first packet
+    uint32_t W;                   // sets per workgroup
+    uint32_t O;                   // merge owners (k_merge_partials workgroups)
+    uint32_t n_sets;
+};
+
 struct AggArgs {
     Batch B;
     TableSet T;
     Acc A;
+    Stage S;
     Glob* g;
     uint32_t* slow;            // packets (batch-local indices) parse_fast did not take
     unsigned long long* slow_n;
@@ -320,20 +343,50 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// ABL (diagnostics only): 0 full kernel; 1 parse only; 2 parse + flow id; 3 parse + flow id, global atomics only;
-// 4 parse + hashed stand-in id + LDS aggregation (no lookup); 5 full kernel with a 2-entry-bucket key cache;
-// 6 full kernel with a hashed stand-in id on key-cache misses (no dictionary walk)
+// Per-workgroup LDS flow table (k_parse_agg), two parts:
+//  * key table, LK entries of 16 bytes (3 key words + proto | state | slot),
+//    each written once per launch: claim (CAS of the state word) -> take an
+//    aggregate slot from an LDS counter -> key words -> publish.  Load stays
+//    low (<= NS / LK), so probe chains are short; two entries per probe step.
+//  * NS aggregate slots: the flow's update_flow aggregates for the current
+//    window and, once resolved, its dense id.
+// The hot loop never needs the dense id: ids are resolved (global dictionary
+// walk, all lanes in parallel) only when a window is flushed.  Keys that get
+// no slot (more than NS flows in this workgroup) or no key entry take the
+// global path per packet (dictionary walk + global atomics).
+//   non-MAC kernels: key = (lo_ip, hi_ip, lo_port<<16|hi_port), proto
+//   MAC kernels:     key = (dense id, 0, 0), proto 0xFF (the dictionary is
+//                    walked per packet; the table only pre-aggregates)
+constexpr int LK = 4096;                // key entries (64 KiB)
+constexpr int NS = 1280;                // aggregate slots (68 B each, 85 KiB)
+constexpr int LK_STEPS = 16;            // probe steps of two entries
+constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
+constexpr int MAX_OWNERS = 256;
+
+__device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) { return (h >> 8) % O; }
+
+__device__ __forceinline__ uint32_t lt_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag) {
+    uint32_t h = (k0 * 0x9E3779B1u) ^ (k1 * 0x85EBCA77u) ^ (k2 * 0xC2B2AE3Du) ^ tag;
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    return h;
+}
+
+// ABL (diagnostics only): 0 full kernel; 1 parse + canonical key only
 template <int ABL, bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
-    __shared__ uint32_t s_pk[H];  // packets per canonical direction, 16-bit halves (window <= 32768)
-    __shared__ uint32_t s_by[2][H], s_mn[2][H], s_mx[2][H], s_fl[4][H];
-    __shared__ uint32_t s_fa[H], s_fc[H], s_fr[H], s_la[H];
-    // flow-key cache entry: (lo_ip, hi_ip, lo_port<<16|hi_port, proto<<24 | READY | dense id)
-    __shared__ uint4 s_kc[KC];
+    __shared__ uint4 s_key[LK];
+    __shared__ uint32_t s_sk[NS];  // key entry of each slot
+    __shared__ uint32_t s_pk[NS];  // packets per canonical direction, 16-bit halves (window <= 32768)
+    __shared__ uint32_t s_by[2][NS], s_mn[2][NS], s_mx[2][NS], s_fl[4][NS];
+    __shared__ uint32_t s_fa[NS], s_fc[NS], s_fr[NS], s_la[NS];
+    __shared__ uint32_t s_nslot;
+    __shared__ uint32_t s_own[MAX_OWNERS + 1];  // flush: per-owner counts -> segment starts
     __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
     const int tid = threadIdx.x;
-    for (int e = tid; e < KC; e += BLOCK) s_kc[e] = make_uint4(0, 0, 0, 0);
-    for (int e = tid; e < H; e += BLOCK) {
+    for (int e = tid; e < LK; e += BLOCK) s_key[e] = make_uint4(0, 0, 0, 0);
+    for (int e = tid; e < NS; e += BLOCK) {
         s_pk[e] = s_by[0][e] = s_by[1][e] = 0;
         s_mn[0][e] = s_mn[1][e] = NONE32;
         s_mx[0][e] = s_mx[1][e] = 0;
@@ -342,7 +395,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         s_la[e] = 0;
     }
     if (tid < 3) s_cnt[tid] = 0;
-    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; }
+    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; }
     __syncthreads();
 
     const Batch& B = a.B;
@@ -379,129 +432,137 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             asm volatile("" ::"v"(x));
             return;
         }
-        uint32_t d = FAIL;
-        if (ABL == 4) {
-            d = ((k.w[0] * 0x9E3779B1u) ^ (k.w[4] * 0x85EBCA77u) ^ k.w[8]) % 1000u;  // diagnostics: no lookup
-        } else if (!macs && ABL == 5) {
-            uint32_t h = (k.w[0] * 0x9E3779B1u) ^ (k.w[4] * 0x85EBCA77u) ^ (k.w[8] * 0xC2B2AE3Du) ^ k.w[9];
-            h ^= h >> 16;
-            h *= 0x7FEB352Du;
-            h ^= h >> 15;
-            const uint32_t e = (h & (KC / 2 - 1)) * 2;
-            const uint32_t want3 = ((k.w[9] & 0xFF) << 24) | KC_READY;
-            const uint4 k0 = s_kc[e], k1 = s_kc[e + 1];
-            const bool m0 = (k0.w & (0xFF000000u | KC_READY)) == want3 && k0.x == k.w[0] && k0.y == k.w[4] &&
-                            k0.z == k.w[8];
-            const bool m1 = (k1.w & (0xFF000000u | KC_READY)) == want3 && k1.x == k.w[0] && k1.y == k.w[4] &&
-                            k1.z == k.w[8];
-            if (m0 || m1) {
-                d = (m0 ? k0.w : k1.w) & KC_ID;
-            } else {
-                c_miss++;
-                d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
-                const uint32_t fe = k0.w == 0 ? e : (k1.w == 0 ? e + 1 : KC);
-                if (fe < KC && d <= KC_ID && atomicCAS(&s_kc[fe].w, 0u, KC_CLAIM) == 0u) {
-                    s_kc[fe].x = k.w[0];
-                    s_kc[fe].y = k.w[4];
-                    s_kc[fe].z = k.w[8];
-                    __threadfence_block();
-                    atomicExch(&s_kc[fe].w, want3 | d);
-                }
-            }
-        } else if (!macs) {
-            // per-workgroup flow-key cache.  An entry is one 16-byte LDS word
-            // group written once inside the launch: claim (CAS the last word
-            // 0 -> KC_CLAIM), write the key words, publish (last word =
-            // proto | READY | id).  A reader takes the entry only if its
-            // single 16-byte read shows READY and all key words match, so
-            // the id it uses belongs to exactly its key.
-            const uint32_t hk = (uint32_t)(mix64(((uint64_t)k.w[0] << 32 | k.w[4]) ^
-                                                 ((uint64_t)k.w[8] << 24) ^ k.w[9]) >> 32);
-            const uint32_t want3 = (k.w[9] & 0xFF) << 24;
-            uint32_t e = hk & (KC - 1);
-            bool found = false, free_slot = false;
-#pragma unroll
-            for (int q = 0; q < KC_PROBE; q++) {
-                const uint4 kk = s_kc[e];
-                if ((kk.w & KC_READY) && kk.x == k.w[0] && kk.y == k.w[4] && kk.z == k.w[8] &&
-                    (kk.w & 0xFF000000u) == want3) {
-                    d = kk.w & KC_ID;
-                    found = true;
-                    break;
-                }
-                if (kk.w == 0) { free_slot = true; break; }
-                e = (e + 1) & (KC - 1);
-            }
-            if (!found) {
-                c_miss++;
-                if (ABL == 6)  // diagnostics: cheap stand-in for the dictionary walk
-                    d = ((k.w[0] * 0x9E3779B1u) ^ (k.w[4] * 0x85EBCA77u) ^ k.w[8]) % 1000u;
-                else
-                    d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
-                if (free_slot && d <= KC_ID && atomicCAS(&s_kc[e].w, 0u, KC_CLAIM) == 0u) {
-                    s_kc[e].x = k.w[0];
-                    s_kc[e].y = k.w[4];
-                    s_kc[e].z = k.w[8];
-                    __threadfence_block();
-                    atomicExch(&s_kc[e].w, want3 | KC_READY | d);
-                }
-            }
-        } else {
-            d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
-        }
-        if (d == FAIL || d >= a.T.fmax) return;  // error flag already set
         const PktInfo& pi = P.pi;
-        if (ABL == 2) {
-            asm volatile("" ::"v"(d), "v"(pi.doctets), "v"(pi.rpkt));
-            return;
+        uint32_t d = FAIL;
+        uint32_t k0 = k.w[0], k1 = k.w[4], k2 = k.w[8], tag = (k.w[9] & 0xFF) << 24;
+        if (macs) {  // MAC pairs: dictionary first, the table is keyed by the dense id
+            d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+            if (d == FAIL || d >= a.T.fmax) return;  // error flag already set
+            k0 = d; k1 = 0; k2 = 0; tag = 0xFFu << 24;
         }
-        if (d < H && (ABL == 0 || ABL >= 4)) {
+        // find or claim the key entry: wave-uniform retry loop (a lane that lost
+        // a claim, or saw an entry being written, reads the pair again next step)
+        uint32_t e = lt_hash(k0, k1, k2, tag) & (LK - 2);  // even: entries e, e+1 per step
+        uint32_t slot = NS;
+        int state = 0, steps = 0;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 gave up
+        for (int it = 0; it < 2 * LK_STEPS; it++) {
+            if (state == 0) {
+                const uint4 ka = s_key[e], kb = s_key[e + 1];
+                const bool ma = (ka.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && ka.x == k0 && ka.y == k1 &&
+                                ka.z == k2;
+                const bool mb = (kb.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && kb.x == k0 && kb.y == k1 &&
+                                kb.z == k2;
+                if (ma || mb) {
+                    slot = (ma ? ka.w : kb.w) & LT_SLOT;
+                    state = 1;
+                } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
+                    if (++steps == LK_STEPS) state = 2;
+                    else e = (e + 2) & (LK - 1);
+                } else {
+                    // first free entry of the pair; an entry being written (CLAIM) is re-read next step
+                    const uint32_t f = (ka.w == 0) ? e : ((ka.w & LT_READY) && kb.w == 0 ? e + 1 : LK);
+                    if (f < LK && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
+                        slot = atomicAdd(&s_nslot, 1u);
+                        if (slot >= NS) slot = NS;  // no slot left: the key is kept, its packets go global
+                        s_key[f].x = k0;
+                        s_key[f].y = k1;
+                        s_key[f].z = k2;
+                        if (slot < NS) s_sk[slot] = f;
+                        __threadfence_block();
+                        atomicExch(&s_key[f].w, tag | LT_READY | (slot < NS ? slot : LT_SLOT));
+                        state = 1;
+                    }
+                }
+            }
+            if (__ballot(state == 0) == 0) break;
+        }
+        if (slot >= NS) slot = NS;
+        if (state == 1 && slot < NS) {
             const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
             const uint32_t loc = (uint32_t)(li - wbase);
-            atomicAdd(&s_pk[d], 1u << (16 * dir));
-            atomicAdd(&s_by[dir][d], pi.doctets);
-            if (pkt < s_mn[0][d]) atomicMin(&s_mn[0][d], pkt);
-            if (pkt > s_mx[0][d]) atomicMax(&s_mx[0][d], pkt);
-            if (ttl < s_mn[1][d]) atomicMin(&s_mn[1][d], ttl);
-            if (ttl > s_mx[1][d]) atomicMax(&s_mx[1][d], ttl);
+            atomicAdd(&s_pk[slot], 1u << (16 * dir));
+            atomicAdd(&s_by[dir][slot], pi.doctets);
+            if (pkt < s_mn[0][slot]) atomicMin(&s_mn[0][slot], pkt);
+            if (pkt > s_mx[0][slot]) atomicMax(&s_mx[0][slot], pkt);
+            if (ttl < s_mn[1][slot]) atomicMin(&s_mn[1][slot], ttl);
+            if (ttl > s_mx[1][slot]) atomicMax(&s_mx[1][slot], ttl);
             if (tf) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
-                    if (w) atomicAdd(&s_fl[q][d], w);
+                    if (w) atomicAdd(&s_fl[q][slot], w);
                 }
-                if (tf & 5) atomicMin(&s_fr[d], loc);
+                if (tf & 5) atomicMin(&s_fr[slot], loc);
             }
-            if (loc < s_fa[d]) atomicMin(&s_fa[d], loc);
-            if ((pi.rprot != 6 || (tf & 2)) && loc < s_fc[d]) atomicMin(&s_fc[d], loc);
-            atomicMax(&s_la[d], loc + 1);
-        } else {
-            agg_global(a.A, d, dir, pi, B.first + li);
+            if (loc < s_fa[slot]) atomicMin(&s_fa[slot], loc);
+            if ((pi.rprot != 6 || (tf & 2)) && loc < s_fc[slot]) atomicMin(&s_fc[slot], loc);
+            atomicMax(&s_la[slot], loc + 1);
+            return;
         }
+        c_miss++;  // no slot: this packet goes to the global accumulators
+        if (!macs) d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
+        if (d == FAIL || d >= a.T.fmax) return;
+        agg_global(a.A, d, dir, pi, B.first + li);
     };
+    unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_start = clock64();
+    uint32_t win = 0;
     auto flush = [&]() {
+        // the window's partial aggregates -> this workgroup's staging set
+        // (plain coalesced stores, lane per slot); k_merge_partials merges them
+        const unsigned long long f0 = clock64();
         lds_barrier();
-        // flush: lanes walk consecutive flow ids -> coalesced global atomics
-        const uint64_t gbase = B.first + wbase;
-        for (int e = tid; e < H; e += BLOCK) {
+        const Stage& S = a.S;
+        const uint32_t set = blockIdx.x * S.W + win;
+        const uint32_t ns = min(s_nslot, (uint32_t)NS), O = S.O;
+        // counting sort of this window's flows by merge owner
+        for (uint32_t o = tid; o <= O; o += BLOCK) s_own[o] = 0;
+        lds_barrier();
+        for (uint32_t e = tid; e < ns; e += BLOCK) {
+            if (s_pk[e] == 0) continue;
+            const uint4 kk = s_key[s_sk[e]];
+            atomicAdd(&s_own[owner_of(lt_hash(kk.x, kk.y, kk.z, kk.w & 0xFF000000u), O)], 1u);
+        }
+        lds_barrier();
+        if (tid < 64) {  // exclusive scan over the owners (one wave, 4 per lane)
+            uint32_t v[4], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t o = tid * 4 + q;
+                v[q] = o < O ? s_own[o] : 0;
+                sum += v[q];
+            }
+            uint32_t incl = sum;
+#pragma unroll
+            for (int dlt = 1; dlt < 64; dlt <<= 1) {
+                const uint32_t y = __shfl_up(incl, dlt, 64);
+                if (tid >= dlt) incl += y;
+            }
+            uint32_t run = incl - sum;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t o = tid * 4 + q;
+                if (o < O) s_own[o] = run;
+                run += v[q];
+            }
+            if (tid == 63) s_own[O] = incl;
+        }
+        lds_barrier();
+        for (uint32_t o = tid; o <= O; o += BLOCK) S.off[(size_t)o * S.n_sets + set] = s_own[o];
+        if (tid == 0) S.base[set] = B.first + wbase;
+        lds_barrier();
+        for (uint32_t e = tid; e < ns; e += BLOCK) {
             const uint32_t pk = s_pk[e];
             if (pk == 0) continue;
-            const uint32_t c0 = pk & 0xFFFF, c1 = pk >> 16;
-            if (c0) { atomicAdd(&a.A.pk[0][e], c0); atomicAdd(&a.A.by[0][e], (unsigned long long)s_by[0][e]); }
-            if (c1) { atomicAdd(&a.A.pk[1][e], c1); atomicAdd(&a.A.by[1][e], (unsigned long long)s_by[1][e]); }
-            for (int q = 0; q < 2; q++) {
-                if (s_mn[q][e] < a.A.mn[q][e]) atomicMin(&a.A.mn[q][e], s_mn[q][e]);
-                if (s_mx[q][e] > a.A.mx[q][e]) atomicMax(&a.A.mx[q][e], s_mx[q][e]);
-            }
-            for (int q = 0; q < 4; q++) {
-                uint32_t w = s_fl[q][e];
-                if (w & 0xFFFF) atomicAdd(&a.A.fl[2 * q][e], w & 0xFFFF);
-                if (w >> 16) atomicAdd(&a.A.fl[2 * q + 1][e], w >> 16);
-            }
-            if (s_fa[e] != NONE32) atomicMin(&a.A.fa[e], gbase + s_fa[e]);
-            if (s_fc[e] != NONE32) atomicMin(&a.A.fc[e], gbase + s_fc[e]);
-            if (s_fr[e] != NONE32) atomicMin(&a.A.fr[e], gbase + s_fr[e]);
-            atomicMax(&a.A.la[e], gbase + s_la[e] - 1);
+            const uint4 kk = s_key[s_sk[e]];
+            const uint32_t tag = kk.w & 0xFF000000u;
+            const uint32_t h = lt_hash(kk.x, kk.y, kk.z, tag);
+            const size_t o = (size_t)set * NS + atomicAdd(&s_own[owner_of(h, O)], 1u);
+            uint4* dst = reinterpret_cast<uint4*>(S.part + o);
+            dst[0] = make_uint4(kk.x, kk.y, kk.z, tag);
+            dst[1] = make_uint4(h, pk, s_by[0][e], s_by[1][e]);
+            dst[2] = make_uint4(s_mn[0][e], s_mn[1][e], s_mx[0][e], s_mx[1][e]);
+            dst[3] = make_uint4(s_fl[0][e], s_fl[1][e], s_fl[2][e], s_fl[3][e]);
+            dst[4] = make_uint4(s_fa[e], s_fc[e], s_fr[e], s_la[e]);
             s_pk[e] = s_by[0][e] = s_by[1][e] = 0;
             s_mn[0][e] = s_mn[1][e] = NONE32;
             s_mx[0][e] = s_mx[1][e] = 0;
@@ -510,7 +571,11 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             s_la[e] = 0;
         }
         lds_barrier();
+        const unsigned long long f1 = clock64() - f0;
+        if (win == 0) cyc_flush0 = f1;
+        cyc_flush += f1;
         wbase += (uint64_t)BLOCK * WIN_ITERS;
+        win++;
     };
     const uint64_t lastp = n - 1;  // prefetches past the end re-read the last packet (in bounds)
     uint64_t li = beg + tid;
@@ -535,6 +600,9 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         if ((st + 2) % WIN_ITERS == 0 && st + 2 < nsteps) flush();
     }
     flush();
+    // sets of windows this workgroup did not have: empty segments
+    for (uint32_t w = win; w < a.S.W; w++)
+        for (uint32_t o = tid; o <= a.S.O; o += BLOCK) a.S.off[(size_t)o * a.S.n_sets + blockIdx.x * a.S.W + w] = 0;
     // statistics: one global atomic per workgroup
     atomicAdd(&s_cnt[0], c_valid);
     atomicAdd(&s_cnt[1], c_drop);
@@ -545,7 +613,310 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         if (s_cnt[0]) atomicAdd(&a.g->valid, s_cnt[0]);
         if (s_cnt[1]) atomicAdd(&a.g->dropped, s_cnt[1]);
         if (s_cnt[2]) atomicAdd(&a.g->n_kc_miss, s_cnt[2]);
+        atomicAdd(&a.g->cyc_total, clock64() - cyc_start);
+        atomicAdd(&a.g->cyc_flush, cyc_flush);
+        atomicAdd(&a.g->cyc_flush0, cyc_flush0);
         if (s_cnt[0]) { atomicMin(&a.g->tmin, s_tmin); atomicMax(&a.g->tmax, s_tmax); }
+    }
+}
+
+// One flow's merged update_flow aggregate -> the global accumulators of dense
+// id d (flows.rs:11-42).  Positions are global packet indices.
+struct FlowPart {
+    uint32_t pk[2];
+    unsigned long long by[2];
+    uint32_t mn[2], mx[2];
+    uint32_t fl[8];
+    unsigned long long fa, fc, fr, la;  // NONE64 / 0 when absent (la = last + 1)
+};
+
+__device__ __forceinline__ void part_to_global(const Acc& A, uint32_t d, const FlowPart& f) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        if (f.pk[q]) {
+            atomicAdd(&A.pk[q][d], f.pk[q]);
+            atomicAdd(&A.by[q][d], f.by[q]);
+        }
+        if (f.mn[q] < A.mn[q][d]) atomicMin(&A.mn[q][d], f.mn[q]);
+        if (f.mx[q] > A.mx[q][d]) atomicMax(&A.mx[q][d], f.mx[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if (f.fl[q]) atomicAdd(&A.fl[q][d], f.fl[q]);
+    if (f.fa != NONE64) atomicMin(&A.fa[d], f.fa);
+    if (f.fc != NONE64) atomicMin(&A.fc[d], f.fc);
+    if (f.fr != NONE64) atomicMin(&A.fr[d], f.fr);
+    if (f.la) atomicMax(&A.la[d], f.la - 1);
+}
+
+__device__ __forceinline__ void part_of_stage(const Part& p, unsigned long long base, FlowPart& f) {
+    f.pk[0] = p.pk & 0xFFFF;
+    f.pk[1] = p.pk >> 16;
+    f.by[0] = p.by0;
+    f.by[1] = p.by1;
+    f.mn[0] = p.mn0;
+    f.mn[1] = p.mn1;
+    f.mx[0] = p.mx0;
+    f.mx[1] = p.mx1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        f.fl[2 * q] = p.fl[q] & 0xFFFF;
+        f.fl[2 * q + 1] = p.fl[q] >> 16;
+    }
+    f.fa = p.pos[0] == NONE32 ? NONE64 : base + p.pos[0];
+    f.fc = p.pos[1] == NONE32 ? NONE64 : base + p.pos[1];
+    f.fr = p.pos[2] == NONE32 ? NONE64 : base + p.pos[2];
+    f.la = p.pos[3] ? base + p.pos[3] : 0;
+}
+
+// Dense id of a staged key (flow_table.h dictionary; tag 0xFF: the key is the id).
+__device__ __forceinline__ uint32_t staged_id(const TableSet& T, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag,
+                                              uint32_t* slots) {
+    if (tag == 0xFF000000u) return k0;
+    CKey k;
+#pragma unroll
+    for (int j = 0; j < 14; j++) k.w[j] = 0;
+    k.w[0] = k0;
+    k.w[4] = k1;
+    k.w[8] = k2;
+    k.w[9] = tag >> 24;
+    return dense_of_key(T, k, true, slots, nullptr);
+}
+
+// k_merge_partials: the flow-table merge of the hot kernel's staged partials.
+// Flow f belongs to workgroup owner(hash(f)); each owner scans the compact
+// hash array (L2-resident), merges its flows' partials in LDS, resolves each
+// key ONCE in the dictionary (no key has two inserters, so no claim waits)
+// and applies one uncontended atomic update per field.  Partials of flows that
+// find no LDS entry merge straight into the global accumulators.
+constexpr int MB = 1024;   // merge kernel block
+constexpr int MT = 1024;   // merge table entries (120 B each)
+constexpr int MCH = 2048;  // sets per scan chunk
+
+// Exclusive scan of one value per thread over a 1024-thread block; returns
+// this thread's prefix, and leaves the block total in scratch[MB / 64].
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int dlt = 1; dlt < 64; dlt <<= 1) {
+        const uint32_t y = __shfl_up(incl, dlt, 64);
+        if (lane >= dlt) incl += y;
+    }
+    if (lane == 63) scratch[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t r = 0;
+        for (int w = 0; w < MB / 64; w++) {
+            const uint32_t t = scratch[w];
+            scratch[w] = r;
+            r += t;
+        }
+        scratch[MB / 64] = r;
+    }
+    __syncthreads();
+    return scratch[wv] + incl - v;
+}
+__global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
+    __shared__ uint4 m_key[MT];
+    __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
+    __shared__ unsigned long long m_by[2][MT], m_fa[MT], m_fc[MT], m_fr[MT], m_la[MT];
+    __shared__ uint32_t m_nclaim, m_base;
+    __shared__ uint32_t m_lo[MCH], m_start[MCH], m_scan[MB / 64 + 1];
+    const int tid = threadIdx.x;
+    const unsigned long long c0 = clock64();
+    for (int e = tid; e < MT; e += MB) {
+        m_key[e] = make_uint4(0, 0, 0, 0);
+        m_pk[0][e] = m_pk[1][e] = 0;
+        m_by[0][e] = m_by[1][e] = 0;
+        m_mn[0][e] = m_mn[1][e] = NONE32;
+        m_mx[0][e] = m_mx[1][e] = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
+        m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
+        m_la[e] = 0;
+    }
+    __syncthreads();
+    const Stage& S = a.S;
+    const uint32_t me = blockIdx.x;
+    // This owner's segment of every set, flattened: per chunk of MCH sets, an
+    // exclusive scan of the segment lengths; threads then take partials from
+    // the flattened index space (binary search for the set), so every thread
+    // has about (partials / MB) of them with all their loads in flight.
+    for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
+        const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
+        uint32_t len[MCH / MB], tot = 0;
+#pragma unroll
+        for (int q = 0; q < MCH / MB; q++) {
+            const uint32_t set = c0s + tid * (MCH / MB) + q;
+            uint32_t lo = 0, hi = 0;
+            if (set < c0s + nset) {
+                lo = S.off[(size_t)me * S.n_sets + set];
+                hi = S.off[(size_t)(me + 1) * S.n_sets + set];
+            }
+            m_lo[tid * (MCH / MB) + q] = lo;
+            len[q] = hi - lo;
+            tot += len[q];
+        }
+        uint32_t run = block_exclusive_scan(tot, m_scan) ;
+#pragma unroll
+        for (int q = 0; q < MCH / MB; q++) {
+            m_start[tid * (MCH / MB) + q] = run;
+            run += len[q];
+        }
+        __syncthreads();
+        const uint32_t total = m_scan[MB / 64];
+        for (uint32_t idx = tid; idx < total; idx += MB) {
+            uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                if (m_start[mid] <= idx) lo_i = mid;
+                else hi_i = mid - 1;
+            }
+            const uint32_t set = c0s + lo_i;
+            const unsigned long long base = S.base[set];
+            const size_t o = (size_t)set * NS + m_lo[lo_i] + (idx - m_start[lo_i]);
+            Part p;
+            {
+                const uint4* src = reinterpret_cast<const uint4*>(S.part + o);
+                uint4 v[5];
+#pragma unroll
+                for (int q = 0; q < 5; q++) v[q] = src[q];
+                __builtin_memcpy(&p, v, sizeof p);
+            }
+            const uint32_t h = p.h, k0 = p.k0, k1 = p.k1, k2 = p.k2, tag = p.tag;
+            FlowPart f;
+            part_of_stage(p, base, f);
+            // find or claim the merge entry (same protocol as the hot kernel)
+            uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
+            int state = 0, probes = 0;
+            for (int it = 0; it < 128; it++) {
+                if (state == 0) {
+                    const uint4 kk = m_key[e];
+                    if (kk.w & LT_READY) {
+                        if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2) state = 1;
+                        else if (++probes == 64) state = 2;
+                        else e = (e + 1) & (MT - 1);
+                    } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
+                        m_key[e].x = k0;
+                        m_key[e].y = k1;
+                        m_key[e].z = k2;
+                        __threadfence_block();
+                        atomicExch(&m_key[e].w, tag | LT_READY);
+                        state = 1;
+                    }
+                }
+                if (__ballot(state == 0) == 0) break;
+            }
+            if (state == 1) {
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    if (f.pk[q]) {
+                        atomicAdd(&m_pk[q][e], f.pk[q]);
+                        atomicAdd(&m_by[q][e], f.by[q]);
+                    }
+                    atomicMin(&m_mn[q][e], f.mn[q]);
+                    atomicMax(&m_mx[q][e], f.mx[q]);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
+                if (f.fa != NONE64) atomicMin(&m_fa[e], f.fa);
+                if (f.fc != NONE64) atomicMin(&m_fc[e], f.fc);
+                if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
+                if (f.la) atomicMax(&m_la[e], f.la);
+            } else {
+                const uint32_t d = staged_id(a.T, k0, k1, k2, tag, a.A.slots);
+                if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
+            }
+        }
+        __syncthreads();
+    }
+    // Dense ids: thread per entry (MT == MB).  The owner is the only inserter
+    // of its keys, so a claim (EMPTY -> PENDING) normally succeeds at once;
+    // the new ids of the whole workgroup come from ONE atomicAdd on the flow
+    // counter (a single hot address: per-flow increments would serialise).
+    static_assert(MT == MB, "one merge entry per thread");
+    if (tid == 0) m_nclaim = 0;
+    __syncthreads();
+    const unsigned long long c1 = clock64();
+    const int e = tid;
+    const uint4 kk = m_key[e];
+    const bool have = (kk.w & LT_READY) != 0;
+    const uint32_t tag = kk.w & 0xFF000000u;
+    uint32_t d = FAIL, s0 = FAIL, s1 = FAIL, rank = 0;
+    bool claimed = false, wait = false;
+    unsigned long long* val = nullptr;
+    if (have) {
+        if (tag == 0xFF000000u) {
+            d = kk.x;  // MAC kernels stage dense ids
+        } else {       // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
+            unsigned long long v = EMPTY;
+            s0 = tab_slot(a.T, 0, ((uint64_t)kk.x << 32) | kk.y, true);
+            if (s0 != FAIL) s1 = tab_slot(a.T, 1, ((uint64_t)s0 << 40) | ((uint64_t)kk.z << 8) | (tag >> 24), true, &v);
+            if (s1 != FAIL) {
+                val = &a.T.tab[1][2 * s1 + 1];
+                if (v >= PENDING) v = atomicCAS(val, EMPTY, PENDING);
+                if (v == EMPTY) {
+                    claimed = true;
+                    rank = atomicAdd(&m_nclaim, 1u);
+                } else if (v == PENDING) {
+                    wait = true;
+                } else {
+                    d = (uint32_t)v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) m_base = m_nclaim ? atomicAdd(a.T.n_flows, m_nclaim) : 0;
+    __syncthreads();
+    if (claimed) {
+        d = m_base + rank;
+        if (d >= a.T.fmax) {
+            atomicOr(a.T.err, ERR_FLOWS_FULL);
+            d = FAIL;
+        } else {
+            uint32_t* dst = (uint32_t*)(a.T.flow_key + (size_t)d * 56);
+#pragma unroll
+            for (int k = 0; k < 14; k++) dst[k] = k == 0 ? kk.x : k == 4 ? kk.y : k == 8 ? kk.z : k == 9 ? tag >> 24 : 0;
+#pragma unroll
+            for (int j = 0; j < N_TABLES; j++) a.A.slots[(size_t)d * N_TABLES + j] = j == 0 ? s0 : j == 1 ? s1 : NONE32;
+        }
+        atomicExch(val, (unsigned long long)d);
+    }
+    for (int sp = 0; sp < (1 << 20); sp++) {  // a claim held elsewhere: poll (wave-uniform)
+        if (__ballot(wait) == 0) break;
+        if (wait) {
+            const unsigned long long v = __hip_atomic_load(val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v != PENDING && v != EMPTY) {
+                d = (uint32_t)v;
+                wait = false;
+            }
+        }
+        if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(16);
+    }
+    if (wait) atomicOr(a.T.err, ERR_SPIN);
+    if (have && d != FAIL && d < a.T.fmax) {
+        FlowPart f;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            f.pk[q] = m_pk[q][e];
+            f.by[q] = m_by[q][e];
+            f.mn[q] = m_mn[q][e];
+            f.mx[q] = m_mx[q][e];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) f.fl[q] = m_fl[q][e];
+        f.fa = m_fa[e];
+        f.fc = m_fc[e];
+        f.fr = m_fr[e];
+        f.la = m_la[e];
+        part_to_global(a.A, d, f);
+    }
+    if (tid == 0) {
+        atomicAdd(&a.g->cyc_m_scan, c1 - c0);
+        atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
     }
 }
 
@@ -1149,8 +1520,11 @@ struct fluere_ctx {
     void* d_pay = nullptr;      // FirstPay[fmax] (merge)
     uint32_t* d_slow = nullptr; // slow-path packet list (one batch)
     uint64_t d_slow_cap = 0;
+    void* d_stage = nullptr;    // hot-kernel partial aggregates (Stage)
+    size_t d_stage_bytes = 0;
     bool generic_dirty = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the last k_parse_agg launch
     // results
     std::vector<fluere_record> recs;
     uint64_t n_ended = 0;
@@ -1218,7 +1592,8 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev2) != hipSuccess)
+        hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
+        hipEventCreate(&c->evk1) != hipSuccess)
         return fail(FLUERE_E_HIP);
     // initial state: every table EMPTY, accumulators at their identities
     hipStream_t s = c->stream;
@@ -1263,9 +1638,12 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_recs);
     hipFree(c->d_pay);
     hipFree(c->d_slow);
+    hipFree(c->d_stage);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->ev2) hipEventDestroy(c->ev2);
+    if (c->evk0) hipEventDestroy(c->evk0);
+    if (c->evk1) hipEventDestroy(c->evk1);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
     return FLUERE_OK;
@@ -1461,15 +1839,37 @@ static int launch_parse_agg(fluere_ctx* c) {
         HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 8, c->stream));
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
         unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
+        // staging: one set per (workgroup, window) -- k_parse_agg's loop bounds
+        const uint64_t per = (hb.b.n + grid - 1) / grid;
+        const uint64_t steps = (per + BLOCK - 1) / BLOCK;
+        const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
+        const size_t sets = (size_t)grid * W, cells = sets * NS;
+        const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
+        const size_t need = cells * sizeof(Part) + sets * sizeof(unsigned long long) +
+                            (size_t)(O + 1) * sets * sizeof(uint32_t) + 64;
+        if (need > c->d_stage_bytes) {
+            hipFree(c->d_stage);
+            c->d_stage = nullptr;
+            c->d_stage_bytes = 0;
+            if (hipMalloc(&c->d_stage, need) != hipSuccess) return FLUERE_E_NOMEM;
+            c->d_stage_bytes = need;
+        }
+        {
+            Stage& S = a.S;
+            S.part = (Part*)c->d_stage;
+            S.base = (unsigned long long*)(S.part + cells);
+            S.off = (uint32_t*)(S.base + sets);
+            S.W = W;
+            S.O = O;
+            S.n_sets = (uint32_t)sets;
+        }
         static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
+        HIPCHECK(hipEventRecord(c->evk0, c->stream));
         if (a.macs) k_parse_agg<0, true><<<grid, BLOCK, 0, c->stream>>>(a);
         else if (abl == 1) k_parse_agg<1, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 2) k_parse_agg<2, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 3) k_parse_agg<3, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 4) k_parse_agg<4, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 5) k_parse_agg<5, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 6) k_parse_agg<6, false><<<grid, BLOCK, 0, c->stream>>>(a);
         else k_parse_agg<0, false><<<grid, BLOCK, 0, c->stream>>>(a);
+        HIPCHECK(hipEventRecord(c->evk1, c->stream));
+        if (abl != 1) k_merge_partials<<<O, MB, 0, c->stream>>>(a);
         k_parse_agg_slow<<<(unsigned)std::max(1, c->n_cu * 4), 256, 0, c->stream>>>(a);
     }
     HIPCHECK(hipGetLastError());
@@ -1477,8 +1877,11 @@ static int launch_parse_agg(fluere_ctx* c) {
         Glob g;
         HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, c->stream));
         HIPCHECK(hipStreamSynchronize(c->stream));
-        fprintf(stderr, "[fluere] valid %llu dropped %llu slow %llu key-cache misses %llu\n", g.valid, g.dropped,
+        fprintf(stderr, "[fluere] valid %llu dropped %llu slow %llu LDS-table overflow packets %llu\n", g.valid, g.dropped,
                 g.n_slow, g.n_kc_miss);
+        fprintf(stderr, "[fluere] per-WG clock: total %.0f flush %.0f first flush %.0f | merge scan %.0f ids %.0f\n",
+                g.cyc_total / 256.0, g.cyc_flush / 256.0, g.cyc_flush0 / 256.0, g.cyc_m_scan / 256.0,
+                g.cyc_m_ids / 256.0);
     }
     return FLUERE_OK;
 }
@@ -1507,7 +1910,18 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     return rc;
 }
 
+// Duration of the last k_parse_agg launch (HIP events on the context stream).
 extern "C" double fluere_last_kernel_ms(fluere_ctx* c) {
+    if (!c) return -1.0;
+    float ms = -1.0f;
+    if (hipEventSynchronize(c->evk1) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, c->evk0, c->evk1) != hipSuccess) return -1.0;
+    return ms;
+}
+
+// Duration of the last parse_aggregate pass: k_parse_agg, k_merge_partials and
+// the slow-path kernel (HIP events on the context stream).
+extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
     if (!c) return -1.0;
     float ms = -1.0f;
     if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0;

@@ -87,8 +87,12 @@ class FlowContext:
         check(self._L.fluere_parse_aggregate(self._h), "fluere_parse_aggregate")
 
     def last_kernel_ms(self) -> float:
-        """HIP-event time of the fused parse+key+aggregate launches of the last run."""
+        """HIP-event time of the last k_parse_agg launch (the roofline kernel)."""
         return float(self._L.fluere_last_kernel_ms(self._h))
+
+    def last_pass_ms(self) -> float:
+        """HIP-event time of the whole last parse+key+aggregate pass."""
+        return float(self._L.fluere_last_pass_ms(self._h))
 
     def records(self):
         """(records ndarray[RECORD_DTYPE], n_ended): ended prefix first, then active."""

@@ -154,12 +154,15 @@ int fluere_parse_batch(fluere_ctx* ctx, fluere_pkt_meta* d_out, uint64_t cap);
  * state machine needs host decisions. */
 int fluere_run(fluere_ctx* ctx, fluere_stats* stats);
 
-/* Only the fused parse+key+aggregate kernel over the attached batches (the
- * roofline kernel); leaves the flow table populated. Asynchronous. */
+/* Only the parse+key+aggregate pass over the attached batches (k_parse_agg,
+ * the partial merge and the slow-path kernel); leaves the flow table
+ * populated. Asynchronous. */
 int fluere_parse_aggregate(fluere_ctx* ctx);
-/* Device time (HIP events on the ctx stream) of the fused kernel launches of
- * the last fluere_run / fluere_parse_aggregate, in ms. */
+/* Device time (HIP events on the ctx stream) of the last k_parse_agg launch
+ * (the roofline kernel) of the last fluere_run / fluere_parse_aggregate, ms. */
 double fluere_last_kernel_ms(fluere_ctx* ctx);
+/* Device time of the whole last parse+key+aggregate pass, ms. */
+double fluere_last_pass_ms(fluere_ctx* ctx);
 
 /* Records of the last fluere_run, host memory, ended prefix first (in the
  * reference's emission order), then active flows.  Caller frees with
