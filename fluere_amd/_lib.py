@@ -127,6 +127,7 @@ def lib() -> ctypes.CDLL:
         "fluere_synth_range_bytes": (U64, [ctypes.POINTER(SynthCfg), U64, U64]),
         "fluere_synth_device": (I, [ctypes.POINTER(SynthCfg), U64, U64, P, P, P]),
         "fluere_set_index_base": (I, [P, U64]),
+        "fluere_capacity": (U64, [P]),
         "fluere_last_kernel_ms": (ctypes.c_double, [P]),
         "fluere_last_pass_ms": (ctypes.c_double, [P]),
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),

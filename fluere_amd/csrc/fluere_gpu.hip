@@ -1258,13 +1258,10 @@ struct CleanArgs {
     uint8_t* active;
 };
 
-__global__ void __launch_bounds__(256) k_cleanup(CleanArgs a) {
-    uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= nf) return;
+__device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool tables) {
     for (int t = 0; t < N_TABLES; t++) {
         uint32_t s = a.A.slots[(size_t)d * N_TABLES + t];
-        if (s != NONE32) { a.T.tab[t][2 * s] = EMPTY; a.T.tab[t][2 * s + 1] = EMPTY; }
+        if (tables && s != NONE32) { a.T.tab[t][2 * s] = EMPTY; a.T.tab[t][2 * s + 1] = EMPTY; }
         a.A.slots[(size_t)d * N_TABLES + t] = NONE32;
     }
     a.A.pk[0][d] = a.A.pk[1][d] = 0;
@@ -1276,6 +1273,18 @@ __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a) {
     a.A.la[d] = 0;
     a.complex[d] = 0;
     if (a.active) a.active[d] = 0;
+}
+
+// Reset the flows of the last run, grid-stride over the device-side count.
+// After a failed run (error word set) some table slots may have no dense id,
+// so every table word is cleared instead of the recorded chains.
+__global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words) {
+    const bool failed = (*a.T.err & (ERR_TABLE_FULL | ERR_SPIN)) != 0;
+    const uint32_t nf = failed ? a.T.fmax : min(*a.T.n_flows, a.T.fmax);
+    const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (size_t d = t0; d < nf; d += stride) cleanup_one(a, (uint32_t)d, !failed);
+    if (failed)
+        for (size_t w = t0; w < tab_words; w += stride) a.T.tab[0][w] = EMPTY;  // tables are contiguous
 }
 
 __global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v) {
@@ -1350,10 +1359,7 @@ struct FirstPay {
     uint8_t dir, prot, tos, pad;
 };
 
-__global__ void __launch_bounds__(256) k_export(FinArgs a, fluere_flow_summary* out) {
-    uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= nf) return;
+__device__ __forceinline__ void export_one(const FinArgs& a, fluere_flow_summary* out, uint32_t d) {
     const Acc& A = a.A;
     fluere_flow_summary s;
     memset(&s, 0, sizeof s);
@@ -1377,6 +1383,12 @@ __global__ void __launch_bounds__(256) k_export(FinArgs a, fluere_flow_summary* 
     parse_global(a.bs, a.nb, s.last, macs, Q);
     s.last_time = Q.t;
     out[d] = s;
+}
+
+// grid-stride over the flows counted on the device (no host round trip)
+__global__ void __launch_bounds__(256) k_export(FinArgs a, fluere_flow_summary* out) {
+    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) export_one(a, out, d);
 }
 
 struct MergeArgs {
@@ -1428,10 +1440,7 @@ __global__ void __launch_bounds__(256) k_merge_payload(MergeArgs a) {
     if (s.last == a.A.la[d]) a.pay[d].t_last = s.last_time;
 }
 
-__global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
-    uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= nf) return;
+__device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t d) {
     const Acc& A = a.A;
     unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
     if (fc == NONE64) return;
@@ -1468,6 +1477,12 @@ __global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
     r.order_key = (fr == la) ? la : NONE64;
     unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
     a.out[pos] = r;
+}
+
+// grid-stride over the flows counted on the device (no host round trip)
+__global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
+    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) merge_finalize_one(a, d);
 }
 
 // test seam: insert canonical keys, return dense ids (flow dictionary checks)
@@ -1520,6 +1535,8 @@ struct fluere_ctx {
     void* d_pay = nullptr;      // FirstPay[fmax] (merge)
     uint32_t* d_slow = nullptr; // slow-path packet list (one batch)
     uint64_t d_slow_cap = 0;
+    uint32_t* d_sd = nullptr;   // merge scratch (summary -> dense id)
+    uint64_t d_sd_cap = 0;
     void* d_stage = nullptr;    // hot-kernel partial aggregates (Stage)
     size_t d_stage_bytes = 0;
     bool generic_dirty = false;
@@ -1639,6 +1656,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_pay);
     hipFree(c->d_slow);
     hipFree(c->d_stage);
+    hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->ev2) hipEventDestroy(c->ev2);
@@ -1650,22 +1668,17 @@ extern "C" int fluere_close(fluere_ctx* c) {
 }
 
 // Clear flow state touched by the previous run (O(flows), not O(capacity)).
+// Reset the flows of the previous run on the device (no host round trip):
+// k_cleanup reads the flow count and the error word itself.
+static unsigned flow_grid(fluere_ctx* c) {
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(c->fmax, 256), (uint64_t)c->n_cu * 16));
+}
+
 static int clear_flows(fluere_ctx* c) {
     hipStream_t s = c->stream;
-    uint32_t hn[2];
-    HIPCHECK(hipMemcpyAsync(hn, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    uint32_t nf = std::min(hn[0], c->fmax);
-    if (hn[1] & (ERR_TABLE_FULL | ERR_SPIN)) {
-        // a failed run may have left slots without a dense id: clear everything
-        size_t tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
-        k_fill_u64<<<grid_for(tab_words, 256), 256, 0, s>>>(c->d_tab, tab_words, EMPTY);
-        nf = c->fmax;
-    }
-    if (nf) {
-        CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active};
-        k_cleanup<<<grid_for(nf, 256), 256, 0, s>>>(a);
-    }
+    CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active};
+    k_cleanup<<<flow_grid(c), 256, 0, s>>>(a, (size_t)N_TABLES * 2 * (c->C + 1));
+    HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemsetAsync(c->d_nflows, 0, 64, s));
     return FLUERE_OK;
 }
@@ -2149,6 +2162,8 @@ extern "C" int fluere_synth_device(const fluere_synth_cfg* cfg, uint64_t first, 
 // ---------------------------------------------------------------------------
 // multi-GPU merge
 // ---------------------------------------------------------------------------
+extern "C" uint64_t fluere_capacity(fluere_ctx* c) { return c ? c->fmax : 0; }
+
 extern "C" int fluere_set_index_base(fluere_ctx* c, uint64_t base) {
     if (!c) return FLUERE_E_ARG;
     if (!c->batches.empty()) return FLUERE_E_STATE;
@@ -2163,6 +2178,11 @@ extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out
     hipStream_t s = c->stream;
     int rc;
     if ((rc = upload_batches(c))) return rc;
+    FinArgs fa{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
+    // a buffer for every possible flow: export first, then one readback
+    const bool one_pass = d_out && cap >= c->fmax;
+    if (one_pass) k_export<<<flow_grid(c), 256, 0, s>>>(fa, d_out);
+    HIPCHECK(hipGetLastError());
     Glob g;
     uint32_t nf_err[2];
     HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
@@ -2174,10 +2194,9 @@ extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out
     *n = nf;
     if (tmin) *tmin = g.tmin;
     if (tmax) *tmax = g.tmax;
-    if (!d_out) return FLUERE_OK;
+    if (!d_out || one_pass) return FLUERE_OK;
     if (cap < nf) return FLUERE_E_ARG;
-    FinArgs fa{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
-    if (nf) k_export<<<grid_for(nf, 256), 256, 0, s>>>(fa, d_out);
+    k_export<<<flow_grid(c), 256, 0, s>>>(fa, d_out);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(s));
     return FLUERE_OK;
@@ -2210,27 +2229,30 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     if ((rc = clear_flows(c))) return rc;
     if ((rc = init_glob(c))) return rc;
     if (!c->d_pay && hipMalloc(&c->d_pay, (size_t)c->fmax * sizeof(FirstPay)) != hipSuccess) return FLUERE_E_NOMEM;
-    uint32_t* sd = nullptr;
-    if (hipMalloc(&sd, std::max<uint64_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
-    if ((rc = ensure_recs(c, std::max<uint64_t>(n, 1)))) { hipFree(sd); return rc; }
+    if (std::max<uint64_t>(n, 1) > c->d_sd_cap) {
+        hipFree(c->d_sd);
+        c->d_sd = nullptr;
+        c->d_sd_cap = 0;
+        if (hipMalloc(&c->d_sd, std::max<uint64_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_sd_cap = std::max<uint64_t>(n, 1);
+    }
+    if ((rc = ensure_recs(c, std::max<uint64_t>(n, 1)))) return rc;
     HIPCHECK(hipEventRecord(c->ev0, s));
-    MergeArgs ma{tables_of(c), c->acc, d_in, n, sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex};
+    MergeArgs ma{tables_of(c), c->acc, d_in, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex};
     if (n) {
         k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
         k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
     }
     HIPCHECK(hipEventRecord(c->ev1, s));
-    uint32_t nf_err[2];
-    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    hipFree(sd);
-    if (nf_err[1]) return FLUERE_E_TABLE_FULL;
-    uint32_t nf = std::min(nf_err[0], c->fmax);
-    if (nf) k_merge_finalize<<<grid_for(nf, 256), 256, 0, s>>>(ma);
+    k_merge_finalize<<<flow_grid(c), 256, 0, s>>>(ma);
     HIPCHECK(hipGetLastError());
     Glob g;
+    uint32_t nf_err[2];
     HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
+    if (nf_err[1]) return FLUERE_E_TABLE_FULL;
+    const uint32_t nf = std::min(nf_err[0], c->fmax);
     if ((rc = collect_records(c, g.n_rec))) return rc;
     fluere_stats out{};
     float ms_parse = 0, ms_total = 0;

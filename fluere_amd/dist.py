@@ -25,16 +25,34 @@ def set_index_base(ctx, base: int):
     check(_lib.lib().fluere_set_index_base(ctx._h, base), "fluere_set_index_base")
 
 
+ONE_PASS_BYTES = 256 << 20  # export buffers up to this size hold every possible flow
+
+
 def export_summaries(ctx, out=None):
-    """parse+key+aggregate this shard and export its flows -> (uint8 cuda tensor [n*192], tmin, tmax)."""
+    """parse+key+aggregate this shard and export its flows -> (uint8 cuda tensor [n*192], tmin, tmax).
+
+    With a buffer for the context's whole flow capacity the export is one pass
+    with a single host round trip (fluere_capacity).  The buffer is cached on
+    the context unless `out` is given; the returned tensor is a view of it."""
     import torch
     L = _lib.lib()
     ctx.parse_aggregate()
     n, lo, hi = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    cap = int(L.fluere_capacity(ctx._h))
+    if out is None:
+        out = getattr(ctx, "_export_buf", None)
+    if cap * SUMMARY_BYTES <= ONE_PASS_BYTES:
+        if out is None or out.numel() < cap * SUMMARY_BYTES:
+            out = torch.empty(max(cap, 1) * SUMMARY_BYTES, dtype=torch.uint8, device="cuda")
+        ctx._export_buf = out
+        check(L.fluere_export_summaries(ctx._h, out.data_ptr(), cap, ctypes.byref(n), ctypes.byref(lo),
+                                        ctypes.byref(hi)), "fluere_export_summaries")
+        return out[: n.value * SUMMARY_BYTES], lo.value, hi.value
     check(L.fluere_export_summaries(ctx._h, None, 0, ctypes.byref(n), ctypes.byref(lo), ctypes.byref(hi)),
           "fluere_export_summaries")
     if out is None or out.numel() < n.value * SUMMARY_BYTES:
         out = torch.empty(max(n.value, 1) * SUMMARY_BYTES, dtype=torch.uint8, device="cuda")
+    ctx._export_buf = out
     check(L.fluere_export_summaries(ctx._h, out.data_ptr(), n.value, ctypes.byref(n), None, None),
           "fluere_export_summaries")
     return out[: n.value * SUMMARY_BYTES], lo.value, hi.value

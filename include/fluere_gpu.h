@@ -189,6 +189,10 @@ typedef struct fluere_flow_summary {
     uint32_t pad1;
 } fluere_flow_summary;          /* 192 bytes */
 
+/* Flow capacity of the context (max_flows clamped to the table size): a
+ * summary buffer of this many entries lets fluere_export_summaries run in one
+ * pass with a single host round trip. */
+uint64_t fluere_capacity(fluere_ctx* ctx);
 int fluere_set_index_base(fluere_ctx* ctx, uint64_t first_global_index);
 /* Export this context's flows after fluere_parse_aggregate.  tmin/tmax: time
  * range of the valid packets (for the expiry-mode decision). */
