@@ -2,11 +2,13 @@
 
 Step = one pass of the `fluere offline` hot path over one batch of synthetic
 pcap records already resident in HBM: parse (parse_keys + parse_fluereflow),
-exact flow key, update_flow aggregation, the record finalisation, and -- for
-N > 1 -- the flow-table merge (one RCCL all_gather of per-flow summaries over
-xGMI + device merge on rank 0).  Weak scaling: every rank owns a fixed
-per-GPU shard of one global capture (packet-range sharding with global packet
-indices).  The same sharded pipeline runs at N = 1 (the gather is a no-op).
+exact flow key, update_flow aggregation and the record finalisation (the
+records are materialised in HBM: the reference's "Converted in" window also
+ends before the CSV export, offline_fluereflows.rs:178).  For N > 1 each rank
+aggregates its shard and the step adds the flow-table merge: one RCCL
+all_gather of per-flow summaries over xGMI + device merge/finalize on rank 0.
+Weak scaling: every rank owns a fixed per-GPU shard of one global capture
+(packet-range sharding with global packet indices).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5u]
   torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
@@ -73,12 +75,17 @@ def main():
     kernel_ms, pass_ms = [], []
 
     def step():
-        s, lo, hi = fdist.export_summaries(ctx)
+        if world == 1:
+            # parse + key + aggregate + finalize; the records stay in HBM
+            st = ctx.run()
+        else:
+            # per-shard aggregation, then the flow-table merge: RCCL all_gather
+            # of per-flow summaries + device merge/finalize on rank 0
+            s, lo, hi = fdist.export_summaries(ctx)
+            st = fdist.gather_and_merge(ctx, s, lo, hi)
         kernel_ms.append(ctx.last_kernel_ms())
         pass_ms.append(ctx.last_pass_ms())
-        if world > 1:
-            return fdist.gather_and_merge(ctx, s, lo, hi)
-        return fdist.merge_summaries(ctx, s, lo, hi)
+        return st
 
     def barrier():
         torch.cuda.synchronize()
@@ -129,7 +136,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (counter-based generator, device-resident)",
             "config": {"workload": C["workload"], "packets_total": n_total, "flows": C["flows"],
-                       "parallelism": f"packet-range shards x{world}, RCCL all_gather merge",
+                       "parallelism": (f"dp{world}: packet-range shards, RCCL all_gather flow-table merge"
+                                       if world > 1 else "single GPU"),
                        "use_mac": C["use_mac"]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

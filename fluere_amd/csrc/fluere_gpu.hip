@@ -49,7 +49,11 @@ static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
 namespace {
 
 constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
-constexpr int WIN_ITERS = 32;    // flush LDS every 32 x 1024 packets (u32 byte sums cannot wrap)
+// LDS aggregates are flushed every WIN_ITERS steps of BLOCK packets: a window
+// holds at most 61440 packets, so the 16-bit per-direction packet and flag
+// counts and the u32 per-direction byte sums (<= 65535 B per packet) cannot wrap.
+// A multiple of 3 (the hot loop is unrolled by three).
+constexpr int WIN_ITERS = 60;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
 constexpr uint64_t IDX_MASK = (1ull << 40) - 1;
@@ -85,6 +89,7 @@ struct Glob {
     unsigned long long n_keys, n_heads;
     unsigned long long generic_used;
     unsigned long long n_slow;
+    unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
     unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
     unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
@@ -578,26 +583,37 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         win++;
     };
     const uint64_t lastp = n - 1;  // prefetches past the end re-read the last packet (in bounds)
+    // Triple-buffered software pipeline, unrolled by three so no window is ever
+    // copied (a copy would wait on its load).  At step s the windows of s+1
+    // and s+2 are in flight: step s issues the offset of s+3, then the window
+    // of s+2 (whose offset came one step earlier -- waiting for it retires the
+    // window of s, issued two steps earlier), then processes window s.
     uint64_t li = beg + tid;
     uint32_t oA = B.offs[min(li, lastp)];
     uint32_t oB = B.offs[min(li + BLOCK, lastp)];
-    Win WA, WB;
+    uint32_t oC = B.offs[min(li + 2 * BLOCK, lastp)];
+    Win WA, WB, WC;
     load_win(B, oA, WA);
-    for (uint64_t st = 0; st < nsteps; st += 2) {
-        // software pipeline, unrolled by two so the in-flight window is never
-        // copied (a copy would wait on the load)
+    load_win(B, oB, WB);
+    for (uint64_t st = 0; st < nsteps; st += 3) {
         const uint32_t curA = oA;
-        oA = B.offs[min(li + 2 * BLOCK, lastp)];
-        load_win(B, oB, WB);
+        oA = B.offs[min(li + 3 * BLOCK, lastp)];
+        load_win(B, oC, WC);
         if (li < end) process(WA, curA, li);
         li += BLOCK;
         if (st + 1 == nsteps) break;
         const uint32_t curB = oB;
-        oB = B.offs[min(li + 2 * BLOCK, lastp)];
+        oB = B.offs[min(li + 3 * BLOCK, lastp)];
         load_win(B, oA, WA);
         if (li < end) process(WB, curB, li);
         li += BLOCK;
-        if ((st + 2) % WIN_ITERS == 0 && st + 2 < nsteps) flush();
+        if (st + 2 == nsteps) break;
+        const uint32_t curC = oC;
+        oC = B.offs[min(li + 3 * BLOCK, lastp)];
+        load_win(B, oB, WB);
+        if (li < end) process(WC, curC, li);
+        li += BLOCK;
+        if ((st + 3) % WIN_ITERS == 0 && st + 3 < nsteps) flush();
     }
     flush();
     // sets of windows this workgroup did not have: empty segments
@@ -959,7 +975,16 @@ struct FinArgs {
     fluere_record* out;
     uint8_t* complex;
     int macs;
+    uint64_t out_cap;
 };
+
+// Append one record (Mode A paths): position, updates and ended counters.
+__device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {
+    const unsigned long long pos = atomicAdd(&g->n_rec, 1ull);
+    if (pos < cap) out[pos] = r;
+    atomicAdd(&g->n_updates, (unsigned long long)r.d_pkts);
+    if (r.order_key != NONE64) atomicAdd(&g->n_ended, 1ull);
+}
 
 __device__ void fill_seed(fluere_record& r, const Parsed& P) {
     const PktInfo& pi = P.pi;
@@ -984,10 +1009,7 @@ __device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t g
     parse_record(bs[b], gi - bs[b].first, macs, 0, P);
 }
 
-__global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
-    uint32_t nf = *a.T.n_flows;
-    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= nf || d >= a.T.fmax) return;
+__device__ __forceinline__ void finalize_one(const FinArgs& a, uint32_t d) {
     const Acc& A = a.A;
     unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
     if (fc == NONE64) return;  // TCP flow without any SYN: every packet is dropped (:101-113)
@@ -1018,8 +1040,13 @@ __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
     r.cnt[8] = 0;
     r.last = Q.t;
     r.order_key = (fr == la) ? la : NONE64;
-    unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
-    a.out[pos] = r;
+    emit_record(a.g, a.out, a.out_cap, r);
+}
+
+// one thread per flow, grid-stride over the device-side flow count
+__global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
+    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) finalize_one(a, d);
 }
 
 // ---------------------------------------------------------------------------
@@ -1109,15 +1136,13 @@ __global__ void __launch_bounds__(64) k_fsm_flows(FsmArgs a) {
         update_flow(r, rev, P.pi, P.t);
         if (P.pi.tflags & 5) {  // is_finished: fin or rst (types/flags.rs:27-30)
             r.order_key = gi;
-            unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
-            if (pos < a.out_cap) a.out[pos] = r;
+            emit_record(a.g, a.out, a.out_cap, r);
             active = false;
         }
     }
     if (active) {
         r.order_key = NONE64;
-        unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
-        if (pos < a.out_cap) a.out[pos] = r;
+        emit_record(a.g, a.out, a.out_cap, r);
     }
 }
 
@@ -1401,6 +1426,7 @@ struct MergeArgs {
     Glob* g;
     fluere_record* out;
     uint8_t* complex;
+    uint64_t out_cap;
 };
 
 __global__ void __launch_bounds__(256) k_merge_insert(MergeArgs a) {
@@ -1475,8 +1501,7 @@ __device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t 
     r.first = p.t_first;
     r.last = p.t_last;
     r.order_key = (fr == la) ? la : NONE64;
-    unsigned long long pos = atomicAdd(&a.g->n_rec, 1ull);
-    a.out[pos] = r;
+    emit_record(a.g, a.out, a.out_cap, r);
 }
 
 // grid-stride over the flows counted on the device (no host round trip)
@@ -1543,10 +1568,39 @@ struct fluere_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the last k_parse_agg launch
     // results
-    std::vector<fluere_record> recs;
+    std::vector<fluere_record> recs;  // host copy of the records (made on demand)
     uint64_t n_ended = 0;
     bool have_results = false;
+    bool host_recs = false;          // recs holds the last results
+    uint64_t dev_n_rec = 0;          // records of the last results in d_recs (Mode A / merge order: by order_key)
 };
+
+static void reset_record_counters(fluere_ctx* c) {
+    char* g = (char*)c->d_glob;
+    for (size_t off : {offsetof(Glob, n_rec), offsetof(Glob, n_complex), offsetof(Glob, n_complex_pkts),
+                       offsetof(Glob, n_heads), offsetof(Glob, n_updates), offsetof(Glob, n_ended)})
+        hipMemsetAsync(g + off, 0, 8, c->stream);
+}
+
+// Host copy of device-resident records, ended prefix first in emission order
+// (order_key: global index of the closing packet), then active flows.
+static int fetch_records(fluere_ctx* c) {
+    if (c->host_recs) return FLUERE_OK;
+    hipStream_t s = c->stream;
+    c->recs.resize(c->dev_n_rec);
+    if (c->dev_n_rec)
+        HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, c->dev_n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    std::stable_sort(c->recs.begin(), c->recs.end(), [](const fluere_record& x, const fluere_record& y) {
+        if (x.order_key != y.order_key) return x.order_key < y.order_key;
+        return x.first < y.first;
+    });
+    uint64_t ne = 0;
+    for (auto& r : c->recs) if (r.order_key != NONE64) ne++;
+    c->n_ended = ne;
+    c->host_recs = true;
+    return FLUERE_OK;
+}
 
 static TableSet tables_of(fluere_ctx* c) {
     TableSet T;
@@ -1963,6 +2017,16 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     HIPCHECK(hipEventRecord(c->ev0, s));
     if ((rc = launch_parse_agg(c))) return rc;
     HIPCHECK(hipEventRecord(c->ev1, s));
+    const TableSet T = tables_of(c);
+    const int nb = (int)c->batches.size();
+    const uint64_t timeout_us = c->timeout_ms * 1000ull;
+    // Speculative Mode A finalize over the device-side flow count: in the
+    // common case the whole run needs one host round trip.
+    if ((rc = ensure_recs(c, std::max<uint64_t>(c->d_recs_cap, std::min<uint64_t>(c->fmax, 1u << 16))))) return rc;
+    FinArgs fa{c->d_batches, nb, T, c->acc, c->d_glob, c->d_recs, c->d_complex, c->use_mac, c->d_recs_cap};
+    k_finalize<<<flow_grid(c), 256, 0, s>>>(fa);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventRecord(c->ev2, s));
     Glob g;
     uint32_t nf_err[2];
     HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
@@ -1970,21 +2034,23 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     HIPCHECK(hipStreamSynchronize(s));
     if (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) return FLUERE_E_TABLE_FULL;
     if (nf_err[1] & ERR_FLOWS_FULL) return FLUERE_E_TABLE_FULL;
-    uint32_t nf = nf_err[0];
-    const TableSet T = tables_of(c);
-    const int nb = (int)c->batches.size();
-    const uint64_t timeout_us = c->timeout_ms * 1000ull;
+    uint32_t nf = std::min(nf_err[0], c->fmax);
     // Mode B if any flow could expire inside the capture (offline_fluereflows.rs:161-175)
     bool modeB = g.valid && (g.tmax - g.tmin) >= timeout_us;
-    uint64_t n_ended = 0, n_rec = 0;
+    uint64_t n_ended = 0, n_rec = 0, updates = 0;
     fluere_stats out{};
     if (!modeB) {
-        if ((rc = ensure_recs(c, std::max<uint64_t>(nf, 1)))) return rc;
-        FinArgs fa{c->d_batches, nb, T, c->acc, c->d_glob, c->d_recs, c->d_complex, c->use_mac};
-        if (nf) k_finalize<<<grid_for(nf, 256), 256, 0, s>>>(fa);
-        HIPCHECK(hipGetLastError());
-        HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        if (g.n_rec > c->d_recs_cap) {  // more flows than the record buffer: grow and finalize again
+            reset_record_counters(c);
+            if ((rc = ensure_recs(c, nf))) return rc;
+            fa.out = c->d_recs;
+            fa.out_cap = c->d_recs_cap;
+            k_finalize<<<flow_grid(c), 256, 0, s>>>(fa);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipEventRecord(c->ev2, s));
+            HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+        }
         if (g.n_complex) {
             uint64_t nk = g.n_complex_pkts;
             unsigned long long *keys = nullptr, *keys2 = nullptr, *heads = nullptr;
@@ -2023,25 +2089,21 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             FsmArgs fs{c->d_batches, nb, T, c->d_glob, keys2, nk, heads, c->d_recs, c->d_recs_cap, c->use_mac};
             k_fsm_flows<<<grid_for(g.n_complex, 64), 64, 0, s>>>(fs);
             HIPCHECK(hipGetLastError());
+            HIPCHECK(hipEventRecord(c->ev2, s));
             HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
             HIPCHECK(hipStreamSynchronize(s));
             hipFree(tmp); hipFree(keys); hipFree(keys2); hipFree(heads);
         }
+        // records stay on the device; fluere_get_records copies and orders them
         n_rec = g.n_rec;
-        c->recs.resize(n_rec);
-        if (n_rec)
-            HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipEventRecord(c->ev2, s));
-        HIPCHECK(hipStreamSynchronize(s));
-        // ended prefix in emission order (packet index of the closing packet), then active
-        std::stable_sort(c->recs.begin(), c->recs.end(), [](const fluere_record& x, const fluere_record& y) {
-            if (x.order_key != y.order_key) return x.order_key < y.order_key;
-            return x.first < y.first;
-        });
-        for (auto& r : c->recs) if (r.order_key != NONE64) n_ended++;
+        n_ended = g.n_ended;
+        updates = g.n_updates;
+        c->dev_n_rec = n_rec;
+        c->host_recs = false;
         out.complex_flows = g.n_complex;
     } else {
-        // exact global state machine
+        // exact global state machine (the speculative Mode A results are discarded)
+        reset_record_counters(c);
         uint64_t N = c->n_total;
         SeqMeta* meta = nullptr;
         HeapEnt* heap = nullptr;
@@ -2077,6 +2139,9 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         HIPCHECK(hipStreamSynchronize(s));
         for (uint64_t i = n_ended; i < n_rec; i++) c->recs[i].order_key = NONE64;
         hipFree(meta); hipFree(heap); hipFree(cur); hipFree(cdir);
+        for (auto& r : c->recs) updates += r.d_pkts;
+        c->host_recs = true;
+        c->dev_n_rec = n_rec;
         out.sequential_mode = 1;
     }
     c->n_ended = n_ended;
@@ -2093,9 +2158,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     out.ended = n_ended;
     out.parse_ms = ms_parse;
     out.total_ms = ms_total;
-    uint64_t upd = 0;
-    for (auto& r : c->recs) upd += r.d_pkts;
-    out.updates = upd;
+    out.updates = updates;
     if (st) *st = out;
     return g.raw ? FLUERE_E_UNSUPPORTED : FLUERE_OK;
 }
@@ -2103,6 +2166,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
 extern "C" int fluere_get_records(fluere_ctx* c, fluere_record** out, uint64_t* n, uint64_t* n_ended) {
     if (!c || !out || !n) return FLUERE_E_ARG;
     if (!c->have_results) return FLUERE_E_STATE;
+    int rc = fetch_records(c);
+    if (rc) return rc;
     *n = c->recs.size();
     if (n_ended) *n_ended = c->n_ended;
     *out = (fluere_record*)malloc(std::max<size_t>(1, c->recs.size()) * sizeof(fluere_record));
@@ -2202,24 +2267,6 @@ extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out
     return FLUERE_OK;
 }
 
-static int collect_records(fluere_ctx* c, uint64_t n_rec) {
-    hipStream_t s = c->stream;
-    c->recs.resize(n_rec);
-    if (n_rec)
-        HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipEventRecord(c->ev2, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    std::stable_sort(c->recs.begin(), c->recs.end(), [](const fluere_record& x, const fluere_record& y) {
-        if (x.order_key != y.order_key) return x.order_key < y.order_key;
-        return x.first < y.first;
-    });
-    uint64_t ne = 0;
-    for (auto& r : c->recs) if (r.order_key != NONE64) ne++;
-    c->n_ended = ne;
-    c->have_results = true;
-    return FLUERE_OK;
-}
-
 extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
                                       uint64_t tmax, fluere_stats* st) {
     if (!c || (!d_in && n)) return FLUERE_E_ARG;
@@ -2238,7 +2285,8 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     }
     if ((rc = ensure_recs(c, std::max<uint64_t>(n, 1)))) return rc;
     HIPCHECK(hipEventRecord(c->ev0, s));
-    MergeArgs ma{tables_of(c), c->acc, d_in, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex};
+    MergeArgs ma{tables_of(c), c->acc, d_in, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
+                 c->d_recs_cap};
     if (n) {
         k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
         k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
@@ -2253,18 +2301,21 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     HIPCHECK(hipStreamSynchronize(s));
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
     const uint32_t nf = std::min(nf_err[0], c->fmax);
-    if ((rc = collect_records(c, g.n_rec))) return rc;
+    HIPCHECK(hipEventRecord(c->ev2, s));
+    c->dev_n_rec = g.n_rec;
+    c->host_recs = false;
+    c->have_results = true;
     fluere_stats out{};
     float ms_parse = 0, ms_total = 0;
     hipEventElapsedTime(&ms_parse, c->ev0, c->ev1);
     hipEventElapsedTime(&ms_total, c->ev0, c->ev2);
     out.flows = nf;
-    out.records = c->recs.size();
-    out.ended = c->n_ended;
+    out.records = g.n_rec;
+    out.ended = g.n_ended;
     out.complex_flows = g.n_complex;
     out.parse_ms = ms_parse;
     out.total_ms = ms_total;
-    for (auto& r : c->recs) out.updates += r.d_pkts;
+    out.updates = g.n_updates;
     if (st) *st = out;
     // expiries or order-dependent flows across shards need the per-packet
     // state machine, which the sharded path does not run yet

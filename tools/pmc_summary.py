@@ -30,11 +30,19 @@ def kernel_stats(d):
             for r in rows}
 
 
+def _match(name, kern):
+    """kern: a kernel name prefix inside the (demangled) name, matched up to a
+    template/argument list -- 'k_parse_agg' matches 'k_parse_agg<0, false>(...)'
+    but not 'k_parse_agg_slow(...)'."""
+    i = name.find(kern)
+    return i >= 0 and (i + len(kern) == len(name) or name[i + len(kern)] in "<(")
+
+
 def counters(d, sub, kern):
     rows = _rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
     acc = defaultdict(list)
     for r in rows:
-        if kern in r["Kernel_Name"]:
+        if _match(r["Kernel_Name"], kern):
             # one row per (dispatch, counter); sum over dimension instances happens in rocprofv3
             acc[(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
     per = defaultdict(list)
@@ -52,6 +60,7 @@ def main():
             c = counters(d, sub, kern)
             if c:
                 out["passes"][sub] = c
+    out["kernel"] = kern
     f = out["passes"].get("fetch", {}).get("FETCH_SIZE")
     w = out["passes"].get("write", {}).get("WRITE_SIZE")
     if f is not None:
