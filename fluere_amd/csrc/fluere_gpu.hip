@@ -128,6 +128,16 @@ __device__ __forceinline__ void load_win(const Batch& B, uint32_t off, Win& W) {
     }
 }
 
+// Pins a loaded window at this point: every word is "used" here, so the
+// compiler cannot sink the five loads into the parser's branches (which turns
+// one memory round trip per packet into three dependent ones).
+__device__ __forceinline__ void pin_win(const Win& W) {
+    asm volatile("" ::"v"(W.w[0]), "v"(W.w[1]), "v"(W.w[2]), "v"(W.w[3]), "v"(W.w[4]), "v"(W.w[5]), "v"(W.w[6]),
+                 "v"(W.w[7]), "v"(W.w[8]), "v"(W.w[9]));
+    asm volatile("" ::"v"(W.w[10]), "v"(W.w[11]), "v"(W.w[12]), "v"(W.w[13]), "v"(W.w[14]), "v"(W.w[15]),
+                 "v"(W.w[16]), "v"(W.w[17]), "v"(W.w[18]), "v"(W.w[19]));
+}
+
 __device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
     uint64_t m = 0;
     for (int k = 0; k < 6; k++) m = (m << 8) | p[k];
@@ -297,28 +307,55 @@ struct AggArgs {
     int macs;
 };
 
-// Front end of the hot kernel: the static-offset parser over a record window
-// already in registers (header + first 64 frame bytes).  Returns false when
-// the general parser is needed.
-__device__ __forceinline__ bool parse_fast_window(const Batch& B, uint32_t off, const Win& W, bool macs, Parsed& P) {
-    bool sw = B.flags & 1;
-    uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
-    uint32_t L = min(incl, B.snap);
-    uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
-    if (L > avail) L = (uint32_t)avail;
-    P.L = L;
-    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);
-    if (!parse_fast(W, L, P.pi)) return false;
-    const PktInfo& pi = P.pi;
-    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;  // the fast path never needs the raw parser
-    P.smac = P.dmac = 0;
-    if (macs) {
-        uint64_t d = 0, s = 0;
-        for (int k = 0; k < 6; k++) d = (d << 8) | W.b(16 + k);
-        for (int k = 0; k < 6; k++) s = (s << 8) | W.b(22 + k);
-        P.dmac = d; P.smac = s;
-    }
-    return true;
+// Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
+// from the record window in registers, with selects instead of branches.
+// Everything else (other ethertypes and IP protocols, IPv4 options, VXLAN,
+// short or truncated frames) is left to the general parser (k_parse_agg_slow),
+// which computes the same result for these packets too; this is only the
+// common case of parse_keys + parse_fluereflow (keys.rs:98-343,
+// fluereflows.rs:30-199, ports.rs:7-58, flags.rs:13-38) written out for it.
+// Record bytes (16-B pcap header + frame) used, as window words w[k] = bytes
+// [4k, 4k+4) little-endian: 0-11 header, 28-29 ethertype, 30 version/ihl,
+// 32-33 total length, 38 ttl, 39 protocol, 42-49 addresses, 50-53 ports,
+// 58-65 the VXLAN probe (keys.rs:188), 63 TCP flags.
+struct Hot {
+    uint64_t t;                   // parse_microseconds (time.rs:5-7)
+    uint32_t sip, dip, ports;     // big-endian addresses; src_port << 16 | dst_port
+    uint32_t proto, doct, pkt, ttl, tf;
+};
+enum : uint32_t { HOT_OK = 0, HOT_DROP = 1, HOT_SLOW = 2 };
+
+__device__ __forceinline__ uint32_t hot_parse(const Batch& B, uint32_t off, const Win& W, Hot& h) {
+    const bool sw = B.flags & 1;
+    const uint32_t sec = sw ? bswap32(W.w[0]) : W.w[0];
+    uint32_t frac = sw ? bswap32(W.w[1]) : W.w[1];
+    const uint32_t incl = sw ? bswap32(W.w[2]) : W.w[2];
+    if (B.flags & 2) frac /= 1000u;  // nanosecond capture (wave-uniform)
+    h.t = (uint64_t)sec * 1000000ull + frac;
+    const uint32_t L = min(incl, B.snap);
+    const uint32_t w7 = W.w[7], w8 = W.w[8], w9 = W.w[9];
+    const uint32_t tl = __builtin_amdgcn_perm(0u, w8, 0x0C0C0001u);
+    const uint32_t proto = w9 >> 24;
+    // Ipv4Packet::payload() length: min(total_length - 20, caplen - 34)
+    const uint32_t pe = min(tl > 20u ? tl - 20u : 0u, L > 34u ? L - 34u : 0u);
+    // (bitwise, not short-circuit: no branches)
+    const bool vx = (pe >= 16u) & ((W.w[14] >> 16) == 0x0008u) & (W.w[15] == 0u) & ((W.w[16] & 0xFFFFu) == 0x0064u);
+    const bool whole = (uint64_t)off + 16u + L <= B.nbytes;  // else a truncated last record
+    const bool shape = whole & (L >= 34u) & ((w7 & 0x000FFFFFu) == 0x00050008u) & ((proto == 6u) | (proto == 17u)) & !vx;
+    const bool tcp = proto == 6u;
+    // TCP: ports need 20 payload bytes (InvalidPacket); UDP: 8 (InvalidPacket),
+    // and exactly 8 leaves an empty "UDP" payload (EmptyPacket, keys.rs:182-184)
+    const bool ok = pe >= (tcp ? 20u : 9u);
+    h.sip = __builtin_amdgcn_perm(W.w[11], W.w[10], 0x02030405u);
+    h.dip = __builtin_amdgcn_perm(W.w[12], W.w[11], 0x02030405u);
+    h.ports = __builtin_amdgcn_perm(W.w[13], W.w[12], 0x02030405u);
+    h.proto = proto;
+    h.doct = max(tl, 20u);  // Ipv4Packet::packet_size()
+    h.ttl = (w9 >> 16) & 0xFFu;
+    const bool dns = !tcp & (((h.ports >> 16) == 53u) | ((h.ports & 0xFFFFu) == 53u));  // fluereflows.rs:255-291
+    h.pkt = dns ? pe : tl;
+    h.tf = tcp ? W.w[15] >> 24 : 0u;
+    return shape ? (ok ? HOT_OK : HOT_DROP) : HOT_SLOW;
 }
 
 // update_flow's order-free part straight into the global accumulators
@@ -378,136 +415,191 @@ __device__ __forceinline__ uint32_t lt_hash(uint32_t k0, uint32_t k1, uint32_t k
     return h;
 }
 
-// ABL (diagnostics only): 0 full kernel; 1 parse + canonical key only
+// ABL (diagnostics only): 0 full kernel; 1 parse + canonical key only; 2 + LDS key
+// table, no aggregation; 3 aggregation into hashed slots without the key table
 template <int ABL, bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
+    // LDS flow table.  Per slot: packets (low 32) and bytes (high 32) per
+    // canonical direction in one u64 (one ds_add_u64 per packet; a window
+    // holds <= 61440 packets of <= 65535 bytes, so neither half wraps);
+    // {min pkt, min ttl, max pkt, max ttl}; window-relative positions
+    // {first, first create-eligible, first FIN/RST, last + 1}; flag pairs.
     __shared__ uint4 s_key[LK];
+    __shared__ unsigned long long s_pb[2][NS];
+    __shared__ uint4 s_mm[NS], s_pos[NS];
+    __shared__ uint32_t s_fl[4][NS];
     __shared__ uint32_t s_sk[NS];  // key entry of each slot
-    __shared__ uint32_t s_pk[NS];  // packets per canonical direction, 16-bit halves (window <= 32768)
-    __shared__ uint32_t s_by[2][NS], s_mn[2][NS], s_mx[2][NS], s_fl[4][NS];
-    __shared__ uint32_t s_fa[NS], s_fc[NS], s_fr[NS], s_la[NS];
     __shared__ uint32_t s_nslot;
     __shared__ uint32_t s_own[MAX_OWNERS + 1];  // flush: per-owner counts -> segment starts
     __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
     const int tid = threadIdx.x;
     for (int e = tid; e < LK; e += BLOCK) s_key[e] = make_uint4(0, 0, 0, 0);
     for (int e = tid; e < NS; e += BLOCK) {
-        s_pk[e] = s_by[0][e] = s_by[1][e] = 0;
-        s_mn[0][e] = s_mn[1][e] = NONE32;
-        s_mx[0][e] = s_mx[1][e] = 0;
+        s_pb[0][e] = s_pb[1][e] = 0;
+        s_mm[e] = make_uint4(NONE32, NONE32, 0, 0);
+        s_pos[e] = make_uint4(NONE32, NONE32, NONE32, 0);
         s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
-        s_fa[e] = s_fc[e] = s_fr[e] = NONE32;
-        s_la[e] = 0;
     }
     if (tid < 3) s_cnt[tid] = 0;
     if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; }
     __syncthreads();
 
     const Batch& B = a.B;
-    constexpr bool macs = MACS;  // key family fixed per instantiation (IPv4 fast path: 5-tuple or MAC pair)
     const uint64_t n = B.n;
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t beg = per * blockIdx.x;
     const uint64_t end = min(n, beg + per);
     unsigned long long c_valid = 0, c_drop = 0, c_miss = 0, tmin = NONE64, tmax = 0;
-
-    // The packet loop is uniform over the workgroup (nsteps steps of BLOCK
-    // packets); every WIN_ITERS steps the LDS aggregates are flushed.  Loads
-    // are issued in the order the loop consumes them -- the offset of packet
-    // li+2*BLOCK before the window of li+BLOCK -- so that with in-order vmcnt
-    // accounting a wait for one never drains the other, and the prefetch runs
-    // straight through the flushes.
     const uint64_t nsteps = end > beg ? (end - beg + BLOCK - 1) / BLOCK : 0;
     uint64_t wbase = beg;
-    auto process = [&](const Win& W, const uint32_t off, const uint64_t li) {
-        Parsed P;
-        if (!parse_fast_window(B, off, W, macs, P)) {
-            a.slow[atomicAdd(a.slow_n, 1ull)] = (uint32_t)li;
-            return;
+
+    // One packet per lane per step; the step is uniform over the workgroup.
+    // Packets the hot parser declines, and packets of keys that find no LDS
+    // slot, are appended to the slow list: k_parse_agg_slow runs the general
+    // parser and the global path for them (nothing rare is inlined here).
+    auto process = [&](const Win& W, const uint32_t off, const uint64_t li, const bool live) {
+        Hot h;
+        const uint32_t cls = live ? hot_parse(B, off, W, h) : HOT_DROP;
+        c_drop += (live & (cls == HOT_DROP)) ? 1 : 0;
+        bool valid = live & (cls == HOT_OK);
+        bool slow = live & (cls == HOT_SLOW);
+        // canonical key: lower endpoint (ip, port[, mac]) first (flow_table.h)
+        const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
+        bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
+        uint64_t smac = 0, dmac = 0;
+        if (MACS) {
+            const uint32_t d_hi = __builtin_amdgcn_perm(W.w[5], W.w[4], 0x00010203u);  // frame bytes 0..3 (record 16..19)
+            const uint32_t d_lo = __builtin_amdgcn_perm(W.w[5], W.w[4], 0x0C0C0405u);  // frame bytes 4..5
+            const uint32_t s_hi = __builtin_amdgcn_perm(W.w[6], W.w[5], 0x02030405u);  // frame bytes 6..9
+            const uint32_t s_lo = __builtin_amdgcn_perm(W.w[6], W.w[5], 0x0C0C0607u);  // frame bytes 10..11
+            dmac = ((uint64_t)d_hi << 16) | d_lo;
+            smac = ((uint64_t)s_hi << 16) | s_lo;
+            if ((h.sip == h.dip) & (sp == dp)) gt = smac > dmac;
         }
-        if (P.cls) { c_drop++; return; }
-        c_valid++;
-        tmin = min(tmin, (unsigned long long)P.t);
-        tmax = max(tmax, (unsigned long long)P.t);
-        uint8_t dir;
-        CKey k;
-        canon_key(P, macs, k, dir);
+        const uint32_t dir = gt ? 1u : 0u;
+        const uint32_t lo_ip = gt ? h.dip : h.sip, hi_ip = gt ? h.sip : h.dip;
+        const uint32_t kports = gt ? __builtin_amdgcn_alignbit(h.ports, h.ports, 16) : h.ports;
         if (ABL == 1) {
-            uint32_t x = k.w[0] ^ k.w[4] ^ k.w[8] ^ k.w[9] ^ P.pi.doctets ^ P.pi.rpkt ^ P.pi.rttl ^ dir;
-            asm volatile("" ::"v"(x));
+            if (valid) asm volatile("" ::"v"(lo_ip ^ hi_ip ^ kports ^ h.proto ^ h.doct ^ h.pkt ^ h.ttl ^ dir));
             return;
         }
-        const PktInfo& pi = P.pi;
-        uint32_t d = FAIL;
-        uint32_t k0 = k.w[0], k1 = k.w[4], k2 = k.w[8], tag = (k.w[9] & 0xFF) << 24;
-        if (macs) {  // MAC pairs: dictionary first, the table is keyed by the dense id
-            d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
-            if (d == FAIL || d >= a.T.fmax) return;  // error flag already set
+        uint32_t k0 = lo_ip, k1 = hi_ip, k2 = kports, tag = h.proto << 24;
+        if (MACS && valid) {  // MAC pairs: dictionary first, the table is keyed by the dense id
+            CKey k;
+#pragma unroll
+            for (int j = 0; j < 14; j++) k.w[j] = 0;
+            k.w[0] = lo_ip;
+            k.w[4] = hi_ip;
+            k.w[8] = kports;
+            k.w[9] = (2u << 8) | h.proto;
+            const uint64_t lom = gt ? dmac : smac, him = gt ? smac : dmac;
+            k.w[10] = (uint32_t)(lom >> 16); k.w[11] = (uint32_t)(lom & 0xFFFF) << 16;
+            k.w[12] = (uint32_t)(him >> 16); k.w[13] = (uint32_t)(him & 0xFFFF) << 16;
+            const uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+            if (d == FAIL || d >= a.T.fmax) valid = false;  // error flag already set
             k0 = d; k1 = 0; k2 = 0; tag = 0xFFu << 24;
         }
-        // find or claim the key entry: wave-uniform retry loop (a lane that lost
-        // a claim, or saw an entry being written, reads the pair again next step)
+        // find or claim the key entry.  First probe inline (the common case:
+        // a published entry in the first pair); the wave-uniform retry loop
+        // runs only while some lane still searches (a lane that lost a claim,
+        // or saw an entry being written, reads the pair again next step).
         uint32_t e = lt_hash(k0, k1, k2, tag) & (LK - 2);  // even: entries e, e+1 per step
         uint32_t slot = NS;
-        int state = 0, steps = 0;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 gave up
-        for (int it = 0; it < 2 * LK_STEPS; it++) {
-            if (state == 0) {
-                const uint4 ka = s_key[e], kb = s_key[e + 1];
-                const bool ma = (ka.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && ka.x == k0 && ka.y == k1 &&
-                                ka.z == k2;
-                const bool mb = (kb.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && kb.x == k0 && kb.y == k1 &&
-                                kb.z == k2;
-                if (ma || mb) {
-                    slot = (ma ? ka.w : kb.w) & LT_SLOT;
-                    state = 1;
-                } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
-                    if (++steps == LK_STEPS) state = 2;
-                    else e = (e + 2) & (LK - 1);
-                } else {
-                    // first free entry of the pair; an entry being written (CLAIM) is re-read next step
-                    const uint32_t f = (ka.w == 0) ? e : ((ka.w & LT_READY) && kb.w == 0 ? e + 1 : LK);
-                    if (f < LK && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
-                        slot = atomicAdd(&s_nslot, 1u);
-                        if (slot >= NS) slot = NS;  // no slot left: the key is kept, its packets go global
-                        s_key[f].x = k0;
-                        s_key[f].y = k1;
-                        s_key[f].z = k2;
-                        if (slot < NS) s_sk[slot] = f;
-                        __threadfence_block();
-                        atomicExch(&s_key[f].w, tag | LT_READY | (slot < NS ? slot : LT_SLOT));
+        int steps = 0;
+        int state = valid ? 0 : 2;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 gave up / not valid
+        if (valid) {  // home entry only; its pair partner is read by the loop
+            const uint4 ka = s_key[e];
+            const bool ma = ((ka.w & (0xFF000000u | LT_READY)) == (tag | LT_READY)) & (ka.x == k0) & (ka.y == k1) & (ka.z == k2);
+            slot = ka.w & LT_SLOT;
+            state = ma ? 1 : 0;
+        }
+        if (ABL == 3) {  // diagnostics: aggregation without the key table (wrong slots)
+            slot = lt_hash(k0, k1, k2, tag) % 1000u;
+            state = valid ? 1 : 2;
+        }
+        if (ABL != 3 && __ballot(state == 0)) {
+            for (int it = 0; it < 2 * LK_STEPS; it++) {
+                if (state == 0) {
+                    const uint4 ka = s_key[e], kb = s_key[e + 1];
+                    const bool ma = (ka.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && ka.x == k0 &&
+                                    ka.y == k1 && ka.z == k2;
+                    const bool mb = (kb.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && kb.x == k0 &&
+                                    kb.y == k1 && kb.z == k2;
+                    if (ma || mb) {
+                        slot = (ma ? ka.w : kb.w) & LT_SLOT;
                         state = 1;
+                    } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
+                        if (++steps == LK_STEPS) state = 2;
+                        else e = (e + 2) & (LK - 1);
+                    } else {
+                        // first free entry of the pair; an entry being written (CLAIM) is re-read next step
+                        const uint32_t f = (ka.w == 0) ? e : ((ka.w & LT_READY) && kb.w == 0 ? e + 1 : LK);
+                        if (f < LK && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
+                            slot = atomicAdd(&s_nslot, 1u);
+                            if (slot >= NS) slot = NS;  // no slot left: the key is kept, its packets go slow
+                            s_key[f].x = k0;
+                            s_key[f].y = k1;
+                            s_key[f].z = k2;
+                            if (slot < NS) s_sk[slot] = f;
+                            __threadfence_block();
+                            atomicExch(&s_key[f].w, tag | LT_READY | (slot < NS ? slot : LT_SLOT));
+                            state = 1;
+                        }
                     }
                 }
+                if (__ballot(state == 0) == 0) break;
             }
-            if (__ballot(state == 0) == 0) break;
         }
-        if (slot >= NS) slot = NS;
-        if (state == 1 && slot < NS) {
-            const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
-            const uint32_t loc = (uint32_t)(li - wbase);
-            atomicAdd(&s_pk[slot], 1u << (16 * dir));
-            atomicAdd(&s_by[dir][slot], pi.doctets);
-            if (pkt < s_mn[0][slot]) atomicMin(&s_mn[0][slot], pkt);
-            if (pkt > s_mx[0][slot]) atomicMax(&s_mx[0][slot], pkt);
-            if (ttl < s_mn[1][slot]) atomicMin(&s_mn[1][slot], ttl);
-            if (ttl > s_mx[1][slot]) atomicMax(&s_mx[1][slot], ttl);
-            if (tf) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
-                    if (w) atomicAdd(&s_fl[q][slot], w);
-                }
-                if (tf & 5) atomicMin(&s_fr[slot], loc);
+        const bool agg = valid & (state == 1) & (slot < NS);
+        const bool miss = valid & !agg;
+        c_miss += miss ? 1 : 0;
+        slow |= miss;
+        // slow list: wave-aggregated append (one global atomic per wave)
+        const uint64_t sm = __ballot(slow);
+        if (sm) {
+            const uint32_t lead = __builtin_ctzll(sm);
+            unsigned long long b0 = 0;
+            if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(a.slow_n, (unsigned long long)__popcll(sm));
+            b0 = __shfl(b0, lead, 64);
+            if (slow) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                a.slow[b0 + r] = (uint32_t)li;
             }
-            if (loc < s_fa[slot]) atomicMin(&s_fa[slot], loc);
-            if ((pi.rprot != 6 || (tf & 2)) && loc < s_fc[slot]) atomicMin(&s_fc[slot], loc);
-            atomicMax(&s_la[slot], loc + 1);
+        }
+        if (!agg) return;
+        if (ABL == 2) {  // diagnostics: key table only
+            asm volatile("" ::"v"(slot));
             return;
         }
-        c_miss++;  // no slot: this packet goes to the global accumulators
-        if (!macs) d = dense_of_key(a.T, k, true, a.A.slots, nullptr);
-        if (d == FAIL || d >= a.T.fmax) return;
-        agg_global(a.A, d, dir, pi, B.first + li);
+        c_valid++;
+        tmin = min(tmin, (unsigned long long)h.t);
+        tmax = max(tmax, (unsigned long long)h.t);
+        // update_flow (flows.rs:11-42), order-free part, as fire-and-forget LDS
+        // atomics (no return value: nothing waits on them)
+        const uint32_t tf = h.tf;
+        const uint32_t loc = (uint32_t)(li - wbase);
+        atomicAdd(&s_pb[dir][slot], ((unsigned long long)h.doct << 32) | 1ull);
+        atomicMax(&s_pos[slot].w, loc + 1);
+        // min / max and first positions change rarely: one 16-B read each, and
+        // an atomic only where the packet moves the value (a stale read can
+        // only cost a redundant atomic, never skip a needed one: the values
+        // move monotonically)
+        const uint4 mm = s_mm[slot], ps = s_pos[slot];
+        if (h.pkt < mm.x) atomicMin(&s_mm[slot].x, h.pkt);
+        if (h.ttl < mm.y) atomicMin(&s_mm[slot].y, h.ttl);
+        if (h.pkt > mm.z) atomicMax(&s_mm[slot].z, h.pkt);
+        if (h.ttl > mm.w) atomicMax(&s_mm[slot].w, h.ttl);
+        if (loc < ps.x) atomicMin(&s_pos[slot].x, loc);
+        // a flow is created by any non-TCP packet or a SYN (offline_fluereflows.rs:101-113)
+        if (((h.proto != 6u) | ((tf & 2u) != 0)) & (loc < ps.y)) atomicMin(&s_pos[slot].y, loc);
+        if (tf) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
+                if (w) atomicAdd(&s_fl[q][slot], w);
+            }
+            if (tf & 5) atomicMin(&s_pos[slot].z, loc);  // FIN or RST
+        }
     };
     unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_start = clock64();
     uint32_t win = 0;
@@ -523,7 +615,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         for (uint32_t o = tid; o <= O; o += BLOCK) s_own[o] = 0;
         lds_barrier();
         for (uint32_t e = tid; e < ns; e += BLOCK) {
-            if (s_pk[e] == 0) continue;
+            if ((s_pb[0][e] | s_pb[1][e]) == 0) continue;
             const uint4 kk = s_key[s_sk[e]];
             atomicAdd(&s_own[owner_of(lt_hash(kk.x, kk.y, kk.z, kk.w & 0xFF000000u), O)], 1u);
         }
@@ -556,24 +648,24 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         if (tid == 0) S.base[set] = B.first + wbase;
         lds_barrier();
         for (uint32_t e = tid; e < ns; e += BLOCK) {
-            const uint32_t pk = s_pk[e];
-            if (pk == 0) continue;
+            const unsigned long long p0 = s_pb[0][e], p1 = s_pb[1][e];
+            if ((p0 | p1) == 0) continue;
             const uint4 kk = s_key[s_sk[e]];
             const uint32_t tag = kk.w & 0xFF000000u;
             const uint32_t h = lt_hash(kk.x, kk.y, kk.z, tag);
             const size_t o = (size_t)set * NS + atomicAdd(&s_own[owner_of(h, O)], 1u);
             uint4* dst = reinterpret_cast<uint4*>(S.part + o);
             dst[0] = make_uint4(kk.x, kk.y, kk.z, tag);
-            dst[1] = make_uint4(h, pk, s_by[0][e], s_by[1][e]);
-            dst[2] = make_uint4(s_mn[0][e], s_mn[1][e], s_mx[0][e], s_mx[1][e]);
+            dst[1] = make_uint4(h, (uint32_t)(p0 & 0xFFFF) | ((uint32_t)(p1 & 0xFFFF) << 16), (uint32_t)(p0 >> 32),
+                                (uint32_t)(p1 >> 32));
+            const uint4 mm = s_mm[e];
+            dst[2] = make_uint4(mm.x, mm.y, mm.z, mm.w);
             dst[3] = make_uint4(s_fl[0][e], s_fl[1][e], s_fl[2][e], s_fl[3][e]);
-            dst[4] = make_uint4(s_fa[e], s_fc[e], s_fr[e], s_la[e]);
-            s_pk[e] = s_by[0][e] = s_by[1][e] = 0;
-            s_mn[0][e] = s_mn[1][e] = NONE32;
-            s_mx[0][e] = s_mx[1][e] = 0;
+            dst[4] = s_pos[e];
+            s_pb[0][e] = s_pb[1][e] = 0;
+            s_mm[e] = make_uint4(NONE32, NONE32, 0, 0);
+            s_pos[e] = make_uint4(NONE32, NONE32, NONE32, 0);
             s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
-            s_fa[e] = s_fc[e] = s_fr[e] = NONE32;
-            s_la[e] = 0;
         }
         lds_barrier();
         const unsigned long long f1 = clock64() - f0;
@@ -582,43 +674,58 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         wbase += (uint64_t)BLOCK * WIN_ITERS;
         win++;
     };
-    const uint64_t lastp = n - 1;  // prefetches past the end re-read the last packet (in bounds)
-    // Triple-buffered software pipeline, unrolled by three so no window is ever
-    // copied (a copy would wait on its load).  At step s the windows of s+1
-    // and s+2 are in flight: step s issues the offset of s+3, then the window
-    // of s+2 (whose offset came one step earlier -- waiting for it retires the
-    // window of s, issued two steps earlier), then processes window s.
-    uint64_t li = beg + tid;
-    uint32_t oA = B.offs[min(li, lastp)];
-    uint32_t oB = B.offs[min(li + BLOCK, lastp)];
-    uint32_t oC = B.offs[min(li + 2 * BLOCK, lastp)];
-    Win WA, WB, WC;
-    load_win(B, oA, WA);
-    load_win(B, oB, WB);
-    for (uint64_t st = 0; st < nsteps; st += 3) {
-        const uint32_t curA = oA;
-        oA = B.offs[min(li + 3 * BLOCK, lastp)];
-        load_win(B, oC, WC);
-        if (li < end) process(WA, curA, li);
-        li += BLOCK;
-        if (st + 1 == nsteps) break;
-        const uint32_t curB = oB;
-        oB = B.offs[min(li + 3 * BLOCK, lastp)];
-        load_win(B, oA, WA);
-        if (li < end) process(WB, curB, li);
-        li += BLOCK;
-        if (st + 2 == nsteps) break;
-        const uint32_t curC = oC;
-        oC = B.offs[min(li + 3 * BLOCK, lastp)];
-        load_win(B, oB, WB);
-        if (li < end) process(WC, curC, li);
-        li += BLOCK;
-        if ((st + 3) % WIN_ITERS == 0 && st + 3 < nsteps) flush();
+    const uint64_t lastp = n - 1;  // loads past the end re-read the last packet (in bounds)
+#ifndef FLUERE_HOT_PIPE
+#define FLUERE_HOT_PIPE 1
+#endif
+    if (FLUERE_HOT_PIPE == 1) {
+        // One step per iteration: the offset of the next step is prefetched (a
+        // one-register carry), the window is loaded and consumed in the same
+        // step and pinned (pin_win) so its five loads form one round trip;
+        // latency is hidden by the other waves of the CU.
+        uint64_t li = beg + tid;
+        uint32_t o = B.offs[min(li, lastp)];
+        for (uint64_t st = 0; st < nsteps; st++) {
+            const uint32_t on = B.offs[min(li + BLOCK, lastp)];
+            Win W;
+            load_win(B, o, W);
+            pin_win(W);
+            process(W, o, li, li < end);
+            li += BLOCK;
+            o = on;
+            if ((st + 1) % WIN_ITERS == 0 && st + 1 < nsteps) flush();
+        }
+    } else {
+        // Two steps per iteration, two windows in registers: the window of the
+        // next step is in flight while this one is processed.  Each window is
+        // pinned just before its processing, and the loop carries every window
+        // in its own registers (no copies: a copy would wait for the load).
+        uint64_t li = beg + tid;
+        uint32_t o0 = B.offs[min(li, lastp)], o1 = B.offs[min(li + BLOCK, lastp)];
+        Win WA, WB;
+        load_win(B, o0, WA);
+        uint32_t o2 = B.offs[min(li + 2 * BLOCK, lastp)];
+        for (uint64_t st = 0; st < nsteps; st += 2) {
+            load_win(B, o1, WB);
+            const uint32_t o3 = B.offs[min(li + 3 * BLOCK, lastp)];
+            pin_win(WA);
+            process(WA, o0, li, li < end);
+            li += BLOCK;
+            load_win(B, o2, WA);
+            const uint32_t o4 = B.offs[min(li + 3 * BLOCK, lastp)];
+            pin_win(WB);
+            process(WB, o1, li, (li < end) & (st + 1 < nsteps));
+            li += BLOCK;
+            o0 = o2;
+            o1 = o3;
+            o2 = o4;
+            if ((st + 2) % WIN_ITERS == 0 && st + 2 < nsteps) flush();
+        }
     }
     flush();
     // sets of windows this workgroup did not have: empty segments
     for (uint32_t w = win; w < a.S.W; w++)
-        for (uint32_t o = tid; o <= a.S.O; o += BLOCK) a.S.off[(size_t)o * a.S.n_sets + blockIdx.x * a.S.W + w] = 0;
+        for (uint32_t oo = tid; oo <= a.S.O; oo += BLOCK) a.S.off[(size_t)oo * a.S.n_sets + blockIdx.x * a.S.W + w] = 0;
     // statistics: one global atomic per workgroup
     atomicAdd(&s_cnt[0], c_valid);
     atomicAdd(&s_cnt[1], c_drop);
@@ -1934,6 +2041,8 @@ static int launch_parse_agg(fluere_ctx* c) {
         HIPCHECK(hipEventRecord(c->evk0, c->stream));
         if (a.macs) k_parse_agg<0, true><<<grid, BLOCK, 0, c->stream>>>(a);
         else if (abl == 1) k_parse_agg<1, false><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 2) k_parse_agg<2, false><<<grid, BLOCK, 0, c->stream>>>(a);
+        else if (abl == 3) k_parse_agg<3, false><<<grid, BLOCK, 0, c->stream>>>(a);
         else k_parse_agg<0, false><<<grid, BLOCK, 0, c->stream>>>(a);
         HIPCHECK(hipEventRecord(c->evk1, c->stream));
         if (abl != 1) k_merge_partials<<<O, MB, 0, c->stream>>>(a);
