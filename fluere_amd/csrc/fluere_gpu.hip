@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -93,12 +94,24 @@ struct Glob {
     unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
     unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
+    unsigned long long clean_done;                        // k_cleanup: workgroups finished
+};
+// One device allocation holds Glob and the dictionary counters right after it
+// (n_flows, err), so a run ends with ONE small device->host copy.
+struct Ctl {
+    Glob g;
+    uint32_t n_flows, err;
+    uint32_t pad[14];
 };
 
-#define HIPCHECK(x)                                  \
-    do {                                             \
-        hipError_t e_ = (x);                         \
-        if (e_ != hipSuccess) return FLUERE_E_HIP;   \
+#define HIPCHECK(x)                                                                                  \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            if (getenv("FLUERE_HIP_VERBOSE"))                                                        \
+                fprintf(stderr, "[fluere] %s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            return FLUERE_E_HIP;                                                                     \
+        }                                                                                            \
     } while (0)
 
 // ---------------------------------------------------------------------------
@@ -310,7 +323,7 @@ struct AggArgs {
 // Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
 // from the record window in registers, with selects instead of branches.
 // Everything else (other ethertypes and IP protocols, IPv4 options, VXLAN,
-// short or truncated frames) is left to the general parser (k_parse_agg_slow),
+// short or truncated frames) is left to the general parser (slow_packets, in k_merge_partials),
 // which computes the same result for these packets too; this is only the
 // common case of parse_keys + parse_fluereflow (keys.rs:98-343,
 // fluereflows.rs:30-199, ports.rs:7-58, flags.rs:13-38) written out for it.
@@ -455,7 +468,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 
     // One packet per lane per step; the step is uniform over the workgroup.
     // Packets the hot parser declines, and packets of keys that find no LDS
-    // slot, are appended to the slow list: k_parse_agg_slow runs the general
+    // slot, are appended to the slow list: slow_packets runs the general
     // parser and the global path for them (nothing rare is inlined here).
     auto process = [&](const Win& W, const uint32_t off, const uint64_t li, const bool live) {
         Hot h;
@@ -840,6 +853,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     __syncthreads();
     return scratch[wv] + incl - v;
 }
+__device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned long long stride);
 __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint4 m_key[MT];
     __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
@@ -1041,17 +1055,19 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         atomicAdd(&a.g->cyc_m_scan, c1 - c0);
         atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
     }
+    slow_packets(a, (unsigned long long)blockIdx.x * blockDim.x + tid, (unsigned long long)gridDim.x * blockDim.x);
 }
 
-// The packets parse_fast declined (IPv6, IPv4 options, ARP, VXLAN, VLAN,
-// short frames ...): general parser + direct global aggregation.  Grid-stride
-// over the device-side count, so no host round trip between the two kernels.
-__global__ void __launch_bounds__(256) k_parse_agg_slow(AggArgs a) {
+// The packets the hot kernel left to the general parser (IPv6, IPv4 options,
+// ARP, VXLAN, VLAN, other IP protocols, short frames, keys without an LDS
+// slot ...): general parser + direct global aggregation.  Grid-stride over
+// the device-side count, so no host round trip; runs in the tail of
+// k_merge_partials (one launch fewer per batch).
+__device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned long long stride) {
     const unsigned long long n = *a.slow_n;
     const bool macs = a.macs != 0;
     unsigned long long c_valid = 0, c_drop = 0, c_raw = 0, tmin = NONE64, tmax = 0;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (unsigned long long)gridDim.x * blockDim.x) {
+    for (unsigned long long i = i0; i < n; i += stride) {
         const uint64_t li = a.slow[i];
         Parsed P;
         parse_record(a.B, li, macs, 1, P);
@@ -1116,22 +1132,52 @@ __device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t g
     parse_record(bs[b], gi - bs[b].first, macs, 0, P);
 }
 
-__device__ __forceinline__ void finalize_one(const FinArgs& a, uint32_t d) {
+// Wave-aggregated emit_record: one atomic per counter per wave (a thread-per-
+// flow kernel that hits the three run counters per flow serialises on them).
+// All lanes of the wave must call it (want = this lane has a record).
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void emit_record_wave(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r,
+                                                 bool want) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const uint64_t em = __ballot(want && r.order_key != NONE64);
+    const unsigned long long upd = wave_sum(want ? (unsigned long long)r.d_pkts : 0ull);
+    const uint32_t lead = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if ((uint32_t)(threadIdx.x & 63) == lead) {
+        base = atomicAdd(&g->n_rec, (unsigned long long)__popcll(m));
+        atomicAdd(&g->n_updates, upd);
+        if (em) atomicAdd(&g->n_ended, (unsigned long long)__popcll(em));
+    }
+    base = __shfl(base, lead, 64);
+    if (want) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (base + rank < cap) out[base + rank] = r;
+    }
+}
+
+// Certified flow d -> its record; false when d has no record here (TCP flow
+// without a SYN: dropped; complex: marked for the per-flow state machine).
+__device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluere_record& r, bool& cplx,
+                                             unsigned long long& cplx_pkts) {
     const Acc& A = a.A;
     unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
-    if (fc == NONE64) return;  // TCP flow without any SYN: every packet is dropped (:101-113)
+    if (fc == NONE64) return false;  // TCP flow without any SYN: every packet is dropped (:101-113)
     bool certified = fc == fa && (fr == NONE64 || fr == la);
     if (!certified) {
         a.complex[d] = 1;
-        atomicAdd(&a.g->n_complex, 1ull);
-        atomicAdd(&a.g->n_complex_pkts, (unsigned long long)(A.pk[0][d] + A.pk[1][d]));
-        return;
+        cplx = true;
+        cplx_pkts = A.pk[0][d] + A.pk[1][d];
+        return false;
     }
     const bool macs = a.macs != 0;
     Parsed P;
     parse_global(a.bs, a.nb, fc, macs, P);
     const uint8_t cd = canon_dir(P, macs);
-    fluere_record r;
     fill_seed(r, P);
     Parsed Q;
     parse_global(a.bs, a.nb, la, macs, Q);
@@ -1147,13 +1193,29 @@ __device__ __forceinline__ void finalize_one(const FinArgs& a, uint32_t d) {
     r.cnt[8] = 0;
     r.last = Q.t;
     r.order_key = (fr == la) ? la : NONE64;
-    emit_record(a.g, a.out, a.out_cap, r);
+    return true;
 }
 
-// one thread per flow, grid-stride over the device-side flow count
+// one thread per flow, grid-stride (uniform per workgroup) over the
+// device-side flow count
 __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
     const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) finalize_one(a, d);
+    for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
+        const uint32_t d = d0 + threadIdx.x;
+        fluere_record r;
+        bool cplx = false;
+        unsigned long long cplx_pkts = 0;
+        const bool want = d < nf && finalize_one(a, d, r, cplx, cplx_pkts);
+        emit_record_wave(a.g, a.out, a.out_cap, r, want);
+        const uint64_t cm = __ballot(cplx);
+        if (cm) {
+            const unsigned long long pk = wave_sum(cplx_pkts);
+            if ((uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm)) {
+                atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
+                atomicAdd(&a.g->n_complex_pkts, pk);
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1388,6 +1450,7 @@ struct CleanArgs {
     Acc A;
     uint8_t* complex;
     uint8_t* active;
+    Glob* g;
 };
 
 __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool tables) {
@@ -1410,6 +1473,9 @@ __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool
 // Reset the flows of the last run, grid-stride over the device-side count.
 // After a failed run (error word set) some table slots may have no dense id,
 // so every table word is cleared instead of the recorded chains.
+// The workgroup that finishes last re-initialises the run counters (Glob,
+// n_flows, err): every other workgroup has read n_flows / err before it
+// counted itself done, so nobody can see the reset early.
 __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words) {
     const bool failed = (*a.T.err & (ERR_TABLE_FULL | ERR_SPIN)) != 0;
     const uint32_t nf = failed ? a.T.fmax : min(*a.T.n_flows, a.T.fmax);
@@ -1417,6 +1483,18 @@ __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words) 
     for (size_t d = t0; d < nf; d += stride) cleanup_one(a, (uint32_t)d, !failed);
     if (failed)
         for (size_t w = t0; w < tab_words; w += stride) a.T.tab[0][w] = EMPTY;  // tables are contiguous
+    __shared__ unsigned long long s_rank;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_rank = atomicAdd(&a.g->clean_done, 1ull);
+    }
+    __syncthreads();
+    if (s_rank != gridDim.x - 1) return;
+    __threadfence();
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(a.g);
+    const size_t nw = sizeof(Ctl) / 8;  // Glob + counters (+ padding)
+    for (size_t i = threadIdx.x; i < nw; i += blockDim.x) w[i] = i == offsetof(Glob, tmin) / 8 ? NONE64 : 0ull;
 }
 
 __global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v) {
@@ -1655,8 +1733,10 @@ struct fluere_ctx {
     unsigned long long* d_tab = nullptr;
     void* d_acc = nullptr;
     Acc acc{};
-    uint32_t* d_nflows = nullptr;  // [0] n_flows, [1] err
-    Glob* d_glob = nullptr;
+    uint32_t* d_nflows = nullptr;  // [0] n_flows, [1] err (inside the d_glob allocation: Ctl)
+    Glob* d_glob = nullptr;        // Ctl
+    Ctl* h_ctl = nullptr;          // pinned host copy
+    bool batches_dirty = true;
     uint8_t* d_flow_key = nullptr;
     uint8_t* d_complex = nullptr;
     uint8_t* d_active = nullptr;
@@ -1674,6 +1754,15 @@ struct fluere_ctx {
     bool generic_dirty = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the last k_parse_agg launch
+    hipEvent_t evk_first = nullptr;             // before the first k_parse_agg launch of the pass
+    bool pass_in_run = false;
+    int plan_nb = 0;                            // batches of the last pass
+    double last_run_ms = 0;                     // host wall time of the last fluere_run
+    // hipGraph of the last fluere_run pass, replayed while the plan is unchanged
+    hipGraphExec_t graph = nullptr;
+    void* graph_plan = nullptr;                 // PassPlan the graph was captured from
+    int graph_off = 0;                          // 1: graphs disabled (env or a failed capture)
+    uint64_t prev_nf = ~0ull;                   // flows of the last fetched run (cleanup grid); ~0: unknown
     // results
     std::vector<fluere_record> recs;  // host copy of the records (made on demand)
     uint64_t n_ended = 0;
@@ -1765,13 +1854,14 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     for (int q = 0; q < 2; q++) c->acc.mx[q] = (uint32_t*)take(F * 4);
     for (int q = 0; q < 8; q++) c->acc.fl[q] = (uint32_t*)take(F * 4);
     c->acc.slots = (uint32_t*)take(F * 4 * N_TABLES);
-    if (hipMalloc(&c->d_nflows, 64) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    if (hipMalloc(&c->d_glob, sizeof(Glob)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_glob, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    c->d_nflows = &reinterpret_cast<Ctl*>(c->d_glob)->n_flows;
+    if (hipHostMalloc(&c->h_ctl, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
-        hipEventCreate(&c->evk1) != hipSuccess)
+        hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess)
         return fail(FLUERE_E_HIP);
     // initial state: every table EMPTY, accumulators at their identities
     hipStream_t s = c->stream;
@@ -1785,7 +1875,11 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     k_fill_u32<<<grid_for(8 * F, 256), 256, 0, s>>>(c->acc.fl[0], 8 * F, 0);
     k_fill_u32<<<grid_for(F * N_TABLES, 256), 256, 0, s>>>(c->acc.slots, F * N_TABLES, NONE32);
     if (hipMemsetAsync(c->d_complex, 0, F, s) != hipSuccess) return fail(FLUERE_E_HIP);
-    if (hipMemsetAsync(c->d_nflows, 0, 64, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    {
+        Ctl z{};
+        z.g.tmin = NONE64;
+        if (hipMemcpyAsync(c->d_glob, &z, sizeof z, hipMemcpyHostToDevice, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    }
     if (hipStreamSynchronize(s) != hipSuccess) return fail(FLUERE_E_HIP);
     (void)rc;
     *out = c;
@@ -1799,6 +1893,7 @@ static void free_batches(fluere_ctx* c) {
     }
     c->batches.clear();
     c->n_total = 0;
+    c->batches_dirty = true;
 }
 
 extern "C" int fluere_close(fluere_ctx* c) {
@@ -1807,7 +1902,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     free_batches(c);
     hipFree(c->d_tab);
     hipFree(c->d_acc);
-    hipFree(c->d_nflows);
+    if (c->h_ctl) hipHostFree(c->h_ctl);
     hipFree(c->d_glob);
     hipFree(c->d_flow_key);
     hipFree(c->d_complex);
@@ -1823,6 +1918,9 @@ extern "C" int fluere_close(fluere_ctx* c) {
     if (c->ev2) hipEventDestroy(c->ev2);
     if (c->evk0) hipEventDestroy(c->evk0);
     if (c->evk1) hipEventDestroy(c->evk1);
+    if (c->evk_first) hipEventDestroy(c->evk_first);
+    if (c->graph) hipGraphExecDestroy(c->graph);
+    free(c->graph_plan);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
     return FLUERE_OK;
@@ -1835,12 +1933,31 @@ static unsigned flow_grid(fluere_ctx* c) {
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(c->fmax, 256), (uint64_t)c->n_cu * 16));
 }
 
+// Clears the flows of the last run and re-initialises every run counter
+// (one launch; see k_cleanup).
 static int clear_flows(fluere_ctx* c) {
     hipStream_t s = c->stream;
-    CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active};
-    k_cleanup<<<flow_grid(c), 256, 0, s>>>(a, (size_t)N_TABLES * 2 * (c->C + 1));
+    (void)hipGetLastError();
+    CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
+    // grid: the last fetched run's flow count when known (k_cleanup is
+    // grid-stride over the device count, so any grid is correct)
+    const unsigned g = c->prev_nf == ~0ull ? flow_grid(c)
+                                           : (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(1, grid_for(c->prev_nf, 256)));
+    k_cleanup<<<g, 256, 0, s>>>(a, (size_t)N_TABLES * 2 * (c->C + 1));
+    c->prev_nf = ~0ull;
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipMemsetAsync(c->d_nflows, 0, 64, s));
+    return FLUERE_OK;
+}
+
+// Glob + n_flows + err of the stream's last results: one pinned copy.
+static int fetch_ctl(fluere_ctx* c, Glob& g, uint32_t (&nf_err)[2]) {
+    HIPCHECK(hipMemcpyAsync(c->h_ctl, c->d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    g = c->h_ctl->g;
+    nf_err[0] = c->h_ctl->n_flows;
+    nf_err[1] = c->h_ctl->err;
+    // a failed run clears every table word: keep the full cleanup grid then
+    c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
     return FLUERE_OK;
 }
 
@@ -1869,6 +1986,7 @@ extern "C" int fluere_add_device_batch(fluere_ctx* c, const uint8_t* d_bytes, ui
     hb.b.snap = snaplen ? snaplen : 262144;
     hb.b.flags = (swapped ? 1u : 0u) | (nsec_ts ? 2u : 0u);
     c->batches.push_back(hb);
+    c->batches_dirty = true;
     c->n_total += n;
     c->have_results = false;
     return FLUERE_OK;
@@ -1955,6 +2073,7 @@ extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t
         hb.b.snap = snap;
         hb.b.flags = (sw ? 1u : 0u) | (ns ? 2u : 0u);
         c->batches.push_back(hb);
+    c->batches_dirty = true;
         c->n_total += hb.b.n;
         i = j;
     }
@@ -1963,6 +2082,8 @@ extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t
 }
 
 static int upload_batches(fluere_ctx* c) {
+    if (!c->batches_dirty) return FLUERE_OK;
+    c->batches_dirty = false;
     int nb = (int)c->batches.size();
     if (nb > c->d_batches_cap) {
         hipFree(c->d_batches);
@@ -1991,8 +2112,32 @@ extern "C" int fluere_parse_batch(fluere_ctx* c, fluere_pkt_meta* d_out, uint64_
     return FLUERE_OK;
 }
 
-static int launch_parse_agg(fluere_ctx* c) {
+// A pass = k_cleanup -> per batch (k_parse_agg, k_merge_partials) -> k_finalize
+// -> one device->host copy of the run counters.  plan_pass does every
+// allocation and computes every launch argument; enqueue_pass only launches,
+// so a pass can be captured into a hipGraph and replayed while its plan is
+// unchanged (byte-equal).
+constexpr int PLAN_BATCHES = 8;
+static int ensure_recs(fluere_ctx* c, uint64_t need);
+struct PassPlan {
+    CleanArgs ca;
+    unsigned clean_grid;
+    size_t tab_words;
+    int nb;
+    AggArgs agg[PLAN_BATCHES];
+    unsigned agg_grid[PLAN_BATCHES];
+    uint32_t owners[PLAN_BATCHES];
+    int macs, abl;
+    int finalize;  // fluere_run: k_finalize + counters copy
+    FinArgs fa;
+    unsigned fin_grid;
+    Ctl* h_ctl;
+    Glob* d_glob;
+};
+
+static int plan_batches(fluere_ctx* c, PassPlan& P) {
     AggArgs a;
+    memset(&a, 0, sizeof a);
     a.T = tables_of(c);
     a.A = c->acc;
     a.g = c->d_glob;
@@ -2007,10 +2152,31 @@ static int launch_parse_agg(fluere_ctx* c) {
     }
     a.slow = c->d_slow;
     a.slow_n = &c->d_glob->n_slow;
+    // staging for the largest batch (every batch reuses it, in stream order)
+    size_t need_max = 0;
+    for (auto& hb : c->batches) {
+        if (!hb.b.n) continue;
+        uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
+        unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
+        const uint64_t per = (hb.b.n + grid - 1) / grid;
+        const uint64_t steps = (per + BLOCK - 1) / BLOCK;
+        const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
+        const size_t sets = (size_t)grid * W, cells = sets * NS;
+        const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
+        need_max = std::max(need_max, cells * sizeof(Part) + sets * sizeof(unsigned long long) +
+                                          (size_t)(O + 1) * sets * sizeof(uint32_t) + 64);
+    }
+    if (need_max > c->d_stage_bytes) {
+        hipFree(c->d_stage);
+        c->d_stage = nullptr;
+        c->d_stage_bytes = 0;
+        if (hipMalloc(&c->d_stage, need_max) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_stage_bytes = need_max;
+    }
+    P.nb = 0;
     for (auto& hb : c->batches) {
         if (!hb.b.n) continue;
         a.B = hb.b;
-        HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 8, c->stream));
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
         unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
         // staging: one set per (workgroup, window) -- k_parse_agg's loop bounds
@@ -2019,47 +2185,165 @@ static int launch_parse_agg(fluere_ctx* c) {
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
-        const size_t need = cells * sizeof(Part) + sets * sizeof(unsigned long long) +
-                            (size_t)(O + 1) * sets * sizeof(uint32_t) + 64;
-        if (need > c->d_stage_bytes) {
-            hipFree(c->d_stage);
-            c->d_stage = nullptr;
-            c->d_stage_bytes = 0;
-            if (hipMalloc(&c->d_stage, need) != hipSuccess) return FLUERE_E_NOMEM;
-            c->d_stage_bytes = need;
+        Stage& S = a.S;
+        S.part = (Part*)c->d_stage;
+        S.base = (unsigned long long*)(S.part + cells);
+        S.off = (uint32_t*)(S.base + sets);
+        S.W = W;
+        S.O = O;
+        S.n_sets = (uint32_t)sets;
+        if (P.nb < PLAN_BATCHES) {
+            P.agg[P.nb] = a;
+            P.agg_grid[P.nb] = grid;
+            P.owners[P.nb] = O;
         }
-        {
-            Stage& S = a.S;
-            S.part = (Part*)c->d_stage;
-            S.base = (unsigned long long*)(S.part + cells);
-            S.off = (uint32_t*)(S.base + sets);
-            S.W = W;
-            S.O = O;
-            S.n_sets = (uint32_t)sets;
-        }
-        static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
-        HIPCHECK(hipEventRecord(c->evk0, c->stream));
-        if (a.macs) k_parse_agg<0, true><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 1) k_parse_agg<1, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 2) k_parse_agg<2, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else if (abl == 3) k_parse_agg<3, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        else k_parse_agg<0, false><<<grid, BLOCK, 0, c->stream>>>(a);
-        HIPCHECK(hipEventRecord(c->evk1, c->stream));
-        if (abl != 1) k_merge_partials<<<O, MB, 0, c->stream>>>(a);
-        k_parse_agg_slow<<<(unsigned)std::max(1, c->n_cu * 4), 256, 0, c->stream>>>(a);
-    }
-    HIPCHECK(hipGetLastError());
-    if (getenv("FLUERE_DEBUG")) {  // diagnostics only: synchronises the stream
-        Glob g;
-        HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, c->stream));
-        HIPCHECK(hipStreamSynchronize(c->stream));
-        fprintf(stderr, "[fluere] valid %llu dropped %llu slow %llu LDS-table overflow packets %llu\n", g.valid, g.dropped,
-                g.n_slow, g.n_kc_miss);
-        fprintf(stderr, "[fluere] per-WG clock: total %.0f flush %.0f first flush %.0f | merge scan %.0f ids %.0f\n",
-                g.cyc_total / 256.0, g.cyc_flush / 256.0, g.cyc_flush0 / 256.0, g.cyc_m_scan / 256.0,
-                g.cyc_m_ids / 256.0);
+        P.nb++;
     }
     return FLUERE_OK;
+}
+
+static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
+    memset(&P, 0, sizeof P);  // byte-comparable (padding included)
+    int rc;
+    if ((rc = upload_batches(c))) return rc;  // host -> device, only when the batches changed
+    P.ca = CleanArgs{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
+    // cleanup grid: the last fetched run's flow count when known (k_cleanup is
+    // grid-stride over the device count, so any grid is correct)
+    P.clean_grid = c->prev_nf == ~0ull
+                       ? flow_grid(c)
+                       : (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(1, grid_for(c->prev_nf, 256)));
+    P.tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
+    if ((rc = plan_batches(c, P))) return rc;
+    static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
+    P.macs = c->use_mac;
+    P.abl = abl;
+    P.finalize = finalize ? 1 : 0;
+    P.h_ctl = c->h_ctl;
+    P.d_glob = c->d_glob;
+    if (finalize) {
+        // speculative Mode A finalize over the device-side flow count
+        if ((rc = ensure_recs(c, std::max<uint64_t>(c->d_recs_cap, std::min<uint64_t>(c->fmax, 1u << 16))))) return rc;
+        P.fa = FinArgs{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob,
+                       c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
+        P.fin_grid = flow_grid(c);
+    }
+    return FLUERE_OK;
+}
+
+static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
+    hipStream_t s = c->stream;
+    for (int i = 0; i < P.nb; i++) {
+        const AggArgs& a = P.agg[i];
+        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 8, s));  // run start: k_cleanup zeroed it
+        if (i == 0 && P.nb > 1) HIPCHECK(hipEventRecord(c->evk_first, s));
+        HIPCHECK(hipEventRecord(c->evk0, s));
+        const unsigned grid = P.agg_grid[i];
+        if (P.macs) k_parse_agg<0, true><<<grid, BLOCK, 0, s>>>(a);
+        else if (P.abl == 1) k_parse_agg<1, false><<<grid, BLOCK, 0, s>>>(a);
+        else if (P.abl == 2) k_parse_agg<2, false><<<grid, BLOCK, 0, s>>>(a);
+        else if (P.abl == 3) k_parse_agg<3, false><<<grid, BLOCK, 0, s>>>(a);
+        else k_parse_agg<0, false><<<grid, BLOCK, 0, s>>>(a);
+        HIPCHECK(hipEventRecord(c->evk1, s));
+        k_merge_partials<<<P.owners[i], MB, 0, s>>>(a);  // + the slow list
+    }
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+static int enqueue_pass(fluere_ctx* c, const PassPlan& P) {
+    hipStream_t s = c->stream;
+    k_cleanup<<<P.clean_grid, 256, 0, s>>>(P.ca, P.tab_words);
+    int rc;
+    if ((rc = enqueue_batches(c, P))) return rc;
+    if (P.finalize) {
+        k_finalize<<<P.fin_grid, 256, 0, s>>>(P.fa);
+        HIPCHECK(hipMemcpyAsync(P.h_ctl, P.d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+// The same pass as an explicit hipGraph (linear chain of nodes).  Built node by
+// node rather than by stream capture: a captured hipEventRecord yields no
+// timestamps on this runtime, explicit event-record nodes do.  `P` must stay
+// alive and unchanged while the graph exists (kernel nodes point at its args).
+static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
+    hipGraph_t g = nullptr;
+    HIPCHECK(hipGraphCreate(&g, 0));
+    hipGraphNode_t prev = nullptr, n = nullptr;
+    bool ok = true;
+    auto dep = [&]() { return prev ? 1 : 0; };
+    auto kernel = [&](const void* fn, unsigned grid, unsigned block, void** args) {
+        if (!ok) return;
+        hipKernelNodeParams kp{};
+        kp.func = const_cast<void*>(fn);
+        kp.gridDim = dim3(grid);
+        kp.blockDim = dim3(block);
+        kp.sharedMemBytes = 0;
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        ok = hipGraphAddKernelNode(&n, g, prev ? &prev : nullptr, dep(), &kp) == hipSuccess;
+        prev = n;
+    };
+    auto event = [&](hipEvent_t e) {
+        if (!ok) return;
+        ok = hipGraphAddEventRecordNode(&n, g, prev ? &prev : nullptr, dep(), e) == hipSuccess;
+        prev = n;
+    };
+    void* a_clean[] = {&P.ca, &P.tab_words};
+    kernel((const void*)k_cleanup, P.clean_grid, 256, a_clean);
+    void* a_agg[PLAN_BATCHES][1];
+    for (int i = 0; i < P.nb && ok; i++) {
+        if (i > 0) {
+            hipMemsetParams mp{};
+            mp.dst = &c->d_glob->n_slow;
+            mp.elementSize = 4;
+            mp.width = 2;
+            mp.height = 1;
+            mp.pitch = 8;
+            mp.value = 0;
+            ok = hipGraphAddMemsetNode(&n, g, &prev, 1, &mp) == hipSuccess;
+            prev = n;
+        }
+        if (i == 0 && P.nb > 1) event(c->evk_first);
+        event(c->evk0);
+        a_agg[i][0] = &P.agg[i];
+        const void* fn = P.macs ? (const void*)k_parse_agg<0, true>
+                                : P.abl == 1 ? (const void*)k_parse_agg<1, false>
+                                : P.abl == 2 ? (const void*)k_parse_agg<2, false>
+                                : P.abl == 3 ? (const void*)k_parse_agg<3, false>
+                                             : (const void*)k_parse_agg<0, false>;
+        kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
+        event(c->evk1);
+        kernel((const void*)k_merge_partials, P.owners[i], MB, a_agg[i]);
+    }
+    void* a_fin[] = {&P.fa};
+    if (P.finalize) {
+        kernel((const void*)k_finalize, P.fin_grid, 256, a_fin);
+        if (ok) {
+            ok = hipGraphAddMemcpyNode1D(&n, g, &prev, 1, P.h_ctl, P.d_glob, sizeof(Ctl), hipMemcpyDeviceToHost) ==
+                 hipSuccess;
+            prev = n;
+        }
+    }
+    if (ok) ok = hipGraphInstantiate(out, g, nullptr, nullptr, 0) == hipSuccess;
+    hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return ok ? FLUERE_OK : FLUERE_E_HIP;
+}
+
+// First-batch start event of the last pass (evk0 itself for one batch).
+static hipEvent_t pass_start_event(fluere_ctx* c) { return c->plan_nb > 1 ? c->evk_first : c->evk0; }
+
+static void debug_counters(fluere_ctx* c) {
+    if (!getenv("FLUERE_DEBUG")) return;  // diagnostics only: synchronises the stream
+    Glob g;
+    if (hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return;
+    fprintf(stderr, "[fluere] valid %llu dropped %llu slow %llu LDS-table overflow packets %llu\n", g.valid, g.dropped,
+            g.n_slow, g.n_kc_miss);
+    fprintf(stderr, "[fluere] per-WG clock: total %.0f flush %.0f first flush %.0f | merge scan %.0f ids %.0f\n",
+            g.cyc_total / 256.0, g.cyc_flush / 256.0, g.cyc_flush0 / 256.0, g.cyc_m_scan / 256.0, g.cyc_m_ids / 256.0);
 }
 
 static int init_glob(fluere_ctx* c) {
@@ -2076,13 +2360,23 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     // key-cache misses become read-only dictionary hits (results accumulate)
     static const bool keep = getenv("FLUERE_KEEP_DICT") != nullptr;
     static int runs = 0;
-    int rc = (keep && runs++ > 0) ? 0 : clear_flows(c);
+    const bool kept = keep && runs++ > 0;
+    int rc = kept ? init_glob(c) : clear_flows(c);  // clear_flows re-initialises the counters too
     if (rc) return rc;
-    rc = init_glob(c);
-    if (rc) return rc;
+    c->pass_in_run = false;
+    PassPlan P;
+    memset(&P, 0, sizeof P);
+    if ((rc = upload_batches(c))) return rc;
+    if ((rc = plan_batches(c, P))) return rc;
+    if (P.nb > PLAN_BATCHES) return FLUERE_E_ARG;
+    static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
+    P.macs = c->use_mac;
+    P.abl = abl;
+    c->plan_nb = P.nb;
     HIPCHECK(hipEventRecord(c->ev0, c->stream));
-    rc = launch_parse_agg(c);
+    rc = enqueue_batches(c, P);
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
+    debug_counters(c);
     return rc;
 }
 
@@ -2095,13 +2389,16 @@ extern "C" double fluere_last_kernel_ms(fluere_ctx* c) {
     return ms;
 }
 
-// Duration of the last parse_aggregate pass: k_parse_agg, k_merge_partials and
-// the slow-path kernel (HIP events on the context stream).
+// Duration of the last pass: after fluere_run, its host wall time (submission
+// to results); after fluere_parse_aggregate, the device time of the hot kernel
+// and the merge (HIP events on the context stream).
 extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
     if (!c) return -1.0;
     float ms = -1.0f;
-    if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0;
-    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0;
+    if (c->pass_in_run) return c->last_run_ms;
+    hipEvent_t e0 = c->ev0, e1 = c->ev1;
+    if (hipEventSynchronize(e1) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.0;
     return ms;
 }
 
@@ -2118,29 +2415,74 @@ static int ensure_recs(fluere_ctx* c, uint64_t need) {
 extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     if (!c) return FLUERE_E_ARG;
     HIPCHECK(hipSetDevice(c->device));
+    (void)hipGetLastError();  // launch checks below see only this run's errors
     hipStream_t s = c->stream;
     int rc;
     if ((rc = clear_flows(c))) return rc;
-    if ((rc = init_glob(c))) return rc;
     if ((rc = upload_batches(c))) return rc;
-    HIPCHECK(hipEventRecord(c->ev0, s));
-    if ((rc = launch_parse_agg(c))) return rc;
-    HIPCHECK(hipEventRecord(c->ev1, s));
+    // device timing: evk0 / evk1 around the hot kernel only (each event marker
+    // costs a gap on the stream); the run's total is host wall time
+    c->pass_in_run = true;
+    const auto t_run0 = std::chrono::steady_clock::now();
     const TableSet T = tables_of(c);
     const int nb = (int)c->batches.size();
     const uint64_t timeout_us = c->timeout_ms * 1000ull;
-    // Speculative Mode A finalize over the device-side flow count: in the
-    // common case the whole run needs one host round trip.
-    if ((rc = ensure_recs(c, std::max<uint64_t>(c->d_recs_cap, std::min<uint64_t>(c->fmax, 1u << 16))))) return rc;
-    FinArgs fa{c->d_batches, nb, T, c->acc, c->d_glob, c->d_recs, c->d_complex, c->use_mac, c->d_recs_cap};
-    k_finalize<<<flow_grid(c), 256, 0, s>>>(fa);
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipEventRecord(c->ev2, s));
+    // One pass: cleanup, hot kernel + merge per batch, speculative Mode A
+    // finalize over the device-side flow count, counters to the host.  In the
+    // common case the whole run is this one submission and one host round
+    // trip; it is replayed from a hipGraph while its plan is unchanged.
+    PassPlan P;
+    if ((rc = plan_pass(c, P, true))) return rc;
+    c->plan_nb = P.nb;
+    // hipGraph replay is opt-in (FLUERE_GRAPH=1): measured on MI355X / ROCm 7.2
+    // it is slower than these few direct launches (C2 step 0.264 vs 0.257 ms)
+    static const bool want_graph = getenv("FLUERE_GRAPH") != nullptr && getenv("FLUERE_DEBUG") == nullptr;
+    const bool use_graph = want_graph && !c->graph_off && P.nb <= PLAN_BATCHES;
+    if (P.nb > PLAN_BATCHES) {  // more batches than a plan holds: direct launches, in chunks
+        k_cleanup<<<P.clean_grid, 256, 0, s>>>(P.ca, P.tab_words);
+        std::vector<HostBatch> all = c->batches;
+        for (size_t i = 0; i < all.size(); i += PLAN_BATCHES) {
+            c->batches.assign(all.begin() + i, all.begin() + std::min(all.size(), i + PLAN_BATCHES));
+            PassPlan Q;
+            memset(&Q, 0, sizeof Q);
+            Q.macs = P.macs;
+            Q.abl = P.abl;
+            rc = plan_batches(c, Q);
+            if (!rc) rc = enqueue_batches(c, Q);
+            if (rc) break;
+        }
+        c->batches = all;
+        c->batches_dirty = true;
+        if (rc) return rc;
+        c->plan_nb = 1;  // device timing covers the last chunk only
+        k_finalize<<<P.fin_grid, 256, 0, s>>>(P.fa);
+        HIPCHECK(hipMemcpyAsync(c->h_ctl, c->d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+    } else if (use_graph) {
+        if (!c->graph || !c->graph_plan || memcmp(c->graph_plan, &P, sizeof P) != 0) {
+            if (c->graph) hipGraphExecDestroy(c->graph);
+            c->graph = nullptr;
+            if (!c->graph_plan) c->graph_plan = malloc(sizeof(PassPlan));
+            memcpy(c->graph_plan, &P, sizeof P);  // the graph's kernel nodes read their args from here
+            if (build_pass_graph(c, *reinterpret_cast<PassPlan*>(c->graph_plan), &c->graph) != FLUERE_OK) {
+                c->graph = nullptr;  // no graphs on this runtime: direct launches from now on
+                c->graph_off = 1;
+            }
+        }
+        if (c->graph) HIPCHECK(hipGraphLaunch(c->graph, s));
+        else if ((rc = enqueue_pass(c, P))) return rc;
+    } else {
+        if ((rc = enqueue_pass(c, P))) return rc;
+    }
+    c->prev_nf = ~0ull;  // the pass cleared the flows: unknown until the fetch below
     Glob g;
     uint32_t nf_err[2];
-    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
+    g = c->h_ctl->g;
+    nf_err[0] = c->h_ctl->n_flows;
+    nf_err[1] = c->h_ctl->err;
+    c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
+    debug_counters(c);
+    FinArgs fa = P.fa;
     if (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) return FLUERE_E_TABLE_FULL;
     if (nf_err[1] & ERR_FLOWS_FULL) return FLUERE_E_TABLE_FULL;
     uint32_t nf = std::min(nf_err[0], c->fmax);
@@ -2255,9 +2597,16 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     }
     c->n_ended = n_ended;
     c->have_results = true;
-    float ms_parse = 0, ms_total = 0;
-    hipEventElapsedTime(&ms_parse, c->ev0, c->ev1);
-    hipEventElapsedTime(&ms_total, c->ev0, c->ev2);
+    float ms_parse = 0;
+    {
+        const hipError_t e = hipEventElapsedTime(&ms_parse, pass_start_event(c), c->evk1);
+        if (e != hipSuccess && getenv("FLUERE_HIP_VERBOSE"))
+            fprintf(stderr, "[fluere] parse timing events: %s\n", hipGetErrorString(e));
+        (void)hipGetLastError();  // a timing failure is not a run failure
+    }
+    const double ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_run0).count();
+    c->last_run_ms = ms_total;
     out.packets = c->n_total;
     out.valid = g.valid;
     out.dropped_parse = g.dropped;
@@ -2383,7 +2732,6 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     hipStream_t s = c->stream;
     int rc;
     if ((rc = clear_flows(c))) return rc;
-    if ((rc = init_glob(c))) return rc;
     if (!c->d_pay && hipMalloc(&c->d_pay, (size_t)c->fmax * sizeof(FirstPay)) != hipSuccess) return FLUERE_E_NOMEM;
     if (std::max<uint64_t>(n, 1) > c->d_sd_cap) {
         hipFree(c->d_sd);

@@ -112,7 +112,7 @@ typedef struct fluere_stats {
     uint32_t sequential_mode;  /* 1 if expiries fired (global sequential state machine) */
     uint32_t pad;
     double parse_ms;           /* device time of the fused parse+key+aggregate kernel */
-    double total_ms;           /* device time of the whole run */
+    double total_ms;           /* wall time of the whole run (fluere_run: host clock, submission to results) */
 } fluere_stats;
 
 typedef struct fluere_ctx fluere_ctx;
