@@ -17,7 +17,9 @@ except Exception:  # pragma: no cover - torch is optional for the C ABI itself
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfluere_gpu.so")
+# FLUERE_LIB (diagnostics only): an alternative in-tree build of the same
+# library, e.g. a kernel variant built by tools/variants.sh
+LIB_PATH = os.environ.get("FLUERE_LIB") or os.path.join(_HERE, "libfluere_gpu.so")
 CLI_PATH = os.path.join(_HERE, "fluere")
 
 # enum fluere_status

@@ -415,6 +415,17 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int LK = 4096;                // key entries (64 KiB)
 constexpr int NS = 1280;                // aggregate slots (68 B each, 85 KiB)
 constexpr int LK_STEPS = 16;            // probe steps of two entries
+#ifndef FLUERE_HOT_PK
+#define FLUERE_HOT_PK 1
+#endif
+#ifndef FLUERE_PROBE_PAIR
+#define FLUERE_PROBE_PAIR 1  // 1: the inline probe reads both entries of the home pair
+#endif
+#ifndef FLUERE_AGG_UNCOND
+#define FLUERE_AGG_UNCOND 2  // bit 0: min/max, bit 1: first positions as unconditional atomics
+#endif
+constexpr int PK = FLUERE_HOT_PK;       // packets per lane per hot-loop iteration
+static_assert(WIN_ITERS % PK == 0, "a window holds whole iterations");
 constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
 constexpr int MAX_OWNERS = 256;
 
@@ -459,159 +470,243 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 
     const Batch& B = a.B;
     const uint64_t n = B.n;
-    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const uint64_t beg = per * blockIdx.x;
-    const uint64_t end = min(n, beg + per);
+#ifndef FLUERE_HOT_ORDER
+#define FLUERE_HOT_ORDER 1
+#endif
+    // Packet order.  Step st of workgroup b covers BLOCK consecutive packets:
+    //   ORDER 1 (interleaved): packets (st * G + b) * BLOCK + [0, BLOCK) -- all
+    //     workgroups stream one moving region of the capture together;
+    //   ORDER 0 (contiguous): workgroup b owns the range [b * per, (b+1) * per).
+    // Positions inside a window are relative to the window's first packet
+    // (at most WIN_ITERS * G * BLOCK apart: they fit u32).
+    const uint64_t G = gridDim.x;
+    const uint64_t per = (n + G - 1) / G;
+    const uint64_t stride = FLUERE_HOT_ORDER ? G * BLOCK : BLOCK;
+    const uint64_t beg = FLUERE_HOT_ORDER ? (uint64_t)blockIdx.x * BLOCK : per * blockIdx.x;
+    const uint64_t end = FLUERE_HOT_ORDER ? n : min(n, beg + per);
     unsigned long long c_valid = 0, c_drop = 0, c_miss = 0, tmin = NONE64, tmax = 0;
-    const uint64_t nsteps = end > beg ? (end - beg + BLOCK - 1) / BLOCK : 0;
+    const uint64_t nsteps = end > beg ? (end - beg + stride - 1) / stride : 0;
     uint64_t wbase = beg;
 
-    // One packet per lane per step; the step is uniform over the workgroup.
+    // PK packets per lane per iteration (steps st .. st+PK-1), processed
+    // phase by phase so that the LDS round trips of the PK packets overlap
+    // (every phase issues its reads for all PK packets before using any).
     // Packets the hot parser declines, and packets of keys that find no LDS
     // slot, are appended to the slow list: slow_packets runs the general
     // parser and the global path for them (nothing rare is inlined here).
-    auto process = [&](const Win& W, const uint32_t off, const uint64_t li, const bool live) {
+    struct PS {
         Hot h;
-        const uint32_t cls = live ? hot_parse(B, off, W, h) : HOT_DROP;
-        c_drop += (live & (cls == HOT_DROP)) ? 1 : 0;
-        bool valid = live & (cls == HOT_OK);
-        bool slow = live & (cls == HOT_SLOW);
-        // canonical key: lower endpoint (ip, port[, mac]) first (flow_table.h)
-        const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
-        bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
-        uint64_t smac = 0, dmac = 0;
-        if (MACS) {
-            const uint32_t d_hi = __builtin_amdgcn_perm(W.w[5], W.w[4], 0x00010203u);  // frame bytes 0..3 (record 16..19)
-            const uint32_t d_lo = __builtin_amdgcn_perm(W.w[5], W.w[4], 0x0C0C0405u);  // frame bytes 4..5
-            const uint32_t s_hi = __builtin_amdgcn_perm(W.w[6], W.w[5], 0x02030405u);  // frame bytes 6..9
-            const uint32_t s_lo = __builtin_amdgcn_perm(W.w[6], W.w[5], 0x0C0C0607u);  // frame bytes 10..11
-            dmac = ((uint64_t)d_hi << 16) | d_lo;
-            smac = ((uint64_t)s_hi << 16) | s_lo;
-            if ((h.sip == h.dip) & (sp == dp)) gt = smac > dmac;
+        uint32_t dir, lo_ip, hi_ip, kports, k0, k1, k2, tag, e, slot;
+        int state, steps;
+        bool valid, slow;
+    };
+    auto process = [&](const Win (&W)[PK], const uint32_t (&off)[PK], const uint64_t (&li)[PK], const bool (&live)[PK]) {
+        PS q[PK];
+#pragma unroll
+        for (int u = 0; u < PK; u++) {
+            Hot& h = q[u].h;
+            const uint32_t cls = live[u] ? hot_parse(B, off[u], W[u], h) : HOT_DROP;
+            c_drop += (live[u] & (cls == HOT_DROP)) ? 1 : 0;
+            q[u].valid = live[u] & (cls == HOT_OK);
+            q[u].slow = live[u] & (cls == HOT_SLOW);
+            // canonical key: lower endpoint (ip, port[, mac]) first (flow_table.h)
+            const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
+            bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
+            uint64_t smac = 0, dmac = 0;
+            if (MACS) {
+                const uint32_t d_hi = __builtin_amdgcn_perm(W[u].w[5], W[u].w[4], 0x00010203u);  // frame bytes 0..3
+                const uint32_t d_lo = __builtin_amdgcn_perm(W[u].w[5], W[u].w[4], 0x0C0C0405u);  // frame bytes 4..5
+                const uint32_t s_hi = __builtin_amdgcn_perm(W[u].w[6], W[u].w[5], 0x02030405u);  // frame bytes 6..9
+                const uint32_t s_lo = __builtin_amdgcn_perm(W[u].w[6], W[u].w[5], 0x0C0C0607u);  // frame bytes 10..11
+                dmac = ((uint64_t)d_hi << 16) | d_lo;
+                smac = ((uint64_t)s_hi << 16) | s_lo;
+                if ((h.sip == h.dip) & (sp == dp)) gt = smac > dmac;
+            }
+            q[u].dir = gt ? 1u : 0u;
+            q[u].lo_ip = gt ? h.dip : h.sip;
+            q[u].hi_ip = gt ? h.sip : h.dip;
+            q[u].kports = gt ? __builtin_amdgcn_alignbit(h.ports, h.ports, 16) : h.ports;
+            q[u].k0 = q[u].lo_ip;
+            q[u].k1 = q[u].hi_ip;
+            q[u].k2 = q[u].kports;
+            q[u].tag = h.proto << 24;
+            if (MACS && q[u].valid) {  // MAC pairs: dictionary first, the table is keyed by the dense id
+                CKey k;
+#pragma unroll
+                for (int j = 0; j < 14; j++) k.w[j] = 0;
+                k.w[0] = q[u].lo_ip;
+                k.w[4] = q[u].hi_ip;
+                k.w[8] = q[u].kports;
+                k.w[9] = (2u << 8) | h.proto;
+                const uint64_t lom = gt ? dmac : smac, him = gt ? smac : dmac;
+                k.w[10] = (uint32_t)(lom >> 16); k.w[11] = (uint32_t)(lom & 0xFFFF) << 16;
+                k.w[12] = (uint32_t)(him >> 16); k.w[13] = (uint32_t)(him & 0xFFFF) << 16;
+                const uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+                if (d == FAIL || d >= a.T.fmax) q[u].valid = false;  // error flag already set
+                q[u].k0 = d; q[u].k1 = 0; q[u].k2 = 0; q[u].tag = 0xFFu << 24;
+            }
         }
-        const uint32_t dir = gt ? 1u : 0u;
-        const uint32_t lo_ip = gt ? h.dip : h.sip, hi_ip = gt ? h.sip : h.dip;
-        const uint32_t kports = gt ? __builtin_amdgcn_alignbit(h.ports, h.ports, 16) : h.ports;
         if (ABL == 1) {
-            if (valid) asm volatile("" ::"v"(lo_ip ^ hi_ip ^ kports ^ h.proto ^ h.doct ^ h.pkt ^ h.ttl ^ dir));
+#pragma unroll
+            for (int u = 0; u < PK; u++)
+                if (q[u].valid)
+                    asm volatile("" ::"v"(q[u].lo_ip ^ q[u].hi_ip ^ q[u].kports ^ q[u].h.proto ^ q[u].h.doct ^
+                                          q[u].h.pkt ^ q[u].h.ttl ^ q[u].dir));
             return;
         }
-        uint32_t k0 = lo_ip, k1 = hi_ip, k2 = kports, tag = h.proto << 24;
-        if (MACS && valid) {  // MAC pairs: dictionary first, the table is keyed by the dense id
-            CKey k;
+        // find or claim the key entries.  First probe of every packet inline
+        // (the common case: a published entry at the home position); the
+        // wave-uniform retry loop runs only while some lane still searches (a
+        // lane that lost a claim, or saw an entry being written, reads the
+        // pair again next step).
+        uint4 kh[PK], kh2[PK];
 #pragma unroll
-            for (int j = 0; j < 14; j++) k.w[j] = 0;
-            k.w[0] = lo_ip;
-            k.w[4] = hi_ip;
-            k.w[8] = kports;
-            k.w[9] = (2u << 8) | h.proto;
-            const uint64_t lom = gt ? dmac : smac, him = gt ? smac : dmac;
-            k.w[10] = (uint32_t)(lom >> 16); k.w[11] = (uint32_t)(lom & 0xFFFF) << 16;
-            k.w[12] = (uint32_t)(him >> 16); k.w[13] = (uint32_t)(him & 0xFFFF) << 16;
-            const uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
-            if (d == FAIL || d >= a.T.fmax) valid = false;  // error flag already set
-            k0 = d; k1 = 0; k2 = 0; tag = 0xFFu << 24;
+        for (int u = 0; u < PK; u++) {
+            q[u].e = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag) & (LK - 2);  // even: entries e, e+1 per step
+            kh[u] = s_key[q[u].e];
+            if (FLUERE_PROBE_PAIR) kh2[u] = s_key[q[u].e + 1];
         }
-        // find or claim the key entry.  First probe inline (the common case:
-        // a published entry in the first pair); the wave-uniform retry loop
-        // runs only while some lane still searches (a lane that lost a claim,
-        // or saw an entry being written, reads the pair again next step).
-        uint32_t e = lt_hash(k0, k1, k2, tag) & (LK - 2);  // even: entries e, e+1 per step
-        uint32_t slot = NS;
-        int steps = 0;
-        int state = valid ? 0 : 2;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 gave up / not valid
-        if (valid) {  // home entry only; its pair partner is read by the loop
-            const uint4 ka = s_key[e];
-            const bool ma = ((ka.w & (0xFF000000u | LT_READY)) == (tag | LT_READY)) & (ka.x == k0) & (ka.y == k1) & (ka.z == k2);
-            slot = ka.w & LT_SLOT;
-            state = ma ? 1 : 0;
+        bool searching = false;
+#pragma unroll
+        for (int u = 0; u < PK; u++) {
+            const uint4 ka = kh[u];
+            const bool ma = ((ka.w & (0xFF000000u | LT_READY)) == (q[u].tag | LT_READY)) & (ka.x == q[u].k0) &
+                            (ka.y == q[u].k1) & (ka.z == q[u].k2);
+            bool mb = false;
+            if (FLUERE_PROBE_PAIR) {
+                const uint4 kb = kh2[u];
+                mb = ((kb.w & (0xFF000000u | LT_READY)) == (q[u].tag | LT_READY)) & (kb.x == q[u].k0) &
+                     (kb.y == q[u].k1) & (kb.z == q[u].k2);
+            }
+            q[u].slot = (ma ? ka.w : kh2[u].w) & LT_SLOT;
+            q[u].state = q[u].valid ? ((ma | mb) ? 1 : 0) : 2;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 none
+            q[u].steps = 0;
+            if (ABL == 3) {  // diagnostics: aggregation without the key table (wrong slots)
+                q[u].slot = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag) % 1000u;
+                q[u].state = q[u].valid ? 1 : 2;
+            }
+            searching |= q[u].state == 0;
         }
-        if (ABL == 3) {  // diagnostics: aggregation without the key table (wrong slots)
-            slot = lt_hash(k0, k1, k2, tag) % 1000u;
-            state = valid ? 1 : 2;
-        }
-        if (ABL != 3 && __ballot(state == 0)) {
+        if (ABL != 3 && __ballot(searching)) {
             for (int it = 0; it < 2 * LK_STEPS; it++) {
-                if (state == 0) {
-                    const uint4 ka = s_key[e], kb = s_key[e + 1];
-                    const bool ma = (ka.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && ka.x == k0 &&
-                                    ka.y == k1 && ka.z == k2;
-                    const bool mb = (kb.w & (0xFF000000u | LT_READY)) == (tag | LT_READY) && kb.x == k0 &&
-                                    kb.y == k1 && kb.z == k2;
-                    if (ma || mb) {
-                        slot = (ma ? ka.w : kb.w) & LT_SLOT;
-                        state = 1;
-                    } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
-                        if (++steps == LK_STEPS) state = 2;
-                        else e = (e + 2) & (LK - 1);
-                    } else {
-                        // first free entry of the pair; an entry being written (CLAIM) is re-read next step
-                        const uint32_t f = (ka.w == 0) ? e : ((ka.w & LT_READY) && kb.w == 0 ? e + 1 : LK);
-                        if (f < LK && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
-                            slot = atomicAdd(&s_nslot, 1u);
-                            if (slot >= NS) slot = NS;  // no slot left: the key is kept, its packets go slow
-                            s_key[f].x = k0;
-                            s_key[f].y = k1;
-                            s_key[f].z = k2;
-                            if (slot < NS) s_sk[slot] = f;
-                            __threadfence_block();
-                            atomicExch(&s_key[f].w, tag | LT_READY | (slot < NS ? slot : LT_SLOT));
-                            state = 1;
+                bool more = false;
+#pragma unroll
+                for (int u = 0; u < PK; u++) {
+                    PS& r = q[u];
+                    if (r.state == 0) {
+                        const uint4 ka = s_key[r.e], kb = s_key[r.e + 1];
+                        const bool ma = (ka.w & (0xFF000000u | LT_READY)) == (r.tag | LT_READY) && ka.x == r.k0 &&
+                                        ka.y == r.k1 && ka.z == r.k2;
+                        const bool mb = (kb.w & (0xFF000000u | LT_READY)) == (r.tag | LT_READY) && kb.x == r.k0 &&
+                                        kb.y == r.k1 && kb.z == r.k2;
+                        if (ma || mb) {
+                            r.slot = (ma ? ka.w : kb.w) & LT_SLOT;
+                            r.state = 1;
+                        } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
+                            if (++r.steps == LK_STEPS) r.state = 2;
+                            else r.e = (r.e + 2) & (LK - 1);
+                        } else {
+                            // first free entry of the pair; an entry being written (CLAIM) is re-read next step
+                            const uint32_t f = (ka.w == 0) ? r.e : ((ka.w & LT_READY) && kb.w == 0 ? r.e + 1 : LK);
+                            if (f < LK && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
+                                uint32_t sl = atomicAdd(&s_nslot, 1u);
+                                if (sl >= NS) sl = NS;  // no slot left: the key is kept, its packets go slow
+                                s_key[f].x = r.k0;
+                                s_key[f].y = r.k1;
+                                s_key[f].z = r.k2;
+                                if (sl < NS) s_sk[sl] = f;
+                                __threadfence_block();
+                                atomicExch(&s_key[f].w, r.tag | LT_READY | (sl < NS ? sl : LT_SLOT));
+                                r.slot = sl;
+                                r.state = 1;
+                            }
                         }
                     }
+                    more |= r.state == 0;
                 }
-                if (__ballot(state == 0) == 0) break;
+                if (__ballot(more) == 0) break;
             }
         }
-        const bool agg = valid & (state == 1) & (slot < NS);
-        const bool miss = valid & !agg;
-        c_miss += miss ? 1 : 0;
-        slow |= miss;
-        // slow list: wave-aggregated append (one global atomic per wave)
-        const uint64_t sm = __ballot(slow);
-        if (sm) {
-            const uint32_t lead = __builtin_ctzll(sm);
-            unsigned long long b0 = 0;
-            if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(a.slow_n, (unsigned long long)__popcll(sm));
-            b0 = __shfl(b0, lead, 64);
-            if (slow) {
-                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                a.slow[b0 + r] = (uint32_t)li;
+        bool agg[PK];
+#pragma unroll
+        for (int u = 0; u < PK; u++) {
+            agg[u] = q[u].valid & (q[u].state == 1) & (q[u].slot < NS);
+            const bool miss = q[u].valid & !agg[u];
+            c_miss += miss ? 1 : 0;
+            const bool slow = q[u].slow | miss;
+            // slow list: wave-aggregated append (one global atomic per wave)
+            const uint64_t sm = __ballot(slow);
+            if (sm) {
+                const uint32_t lead = __builtin_ctzll(sm);
+                unsigned long long b0 = 0;
+                if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(a.slow_n, (unsigned long long)__popcll(sm));
+                b0 = __shfl(b0, lead, 64);
+                if (slow) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                    a.slow[b0 + r] = (uint32_t)li[u];
+                }
             }
         }
-        if (!agg) return;
         if (ABL == 2) {  // diagnostics: key table only
-            asm volatile("" ::"v"(slot));
+#pragma unroll
+            for (int u = 0; u < PK; u++) asm volatile("" ::"v"(q[u].slot));
             return;
         }
-        c_valid++;
-        tmin = min(tmin, (unsigned long long)h.t);
-        tmax = max(tmax, (unsigned long long)h.t);
-        // update_flow (flows.rs:11-42), order-free part, as fire-and-forget LDS
-        // atomics (no return value: nothing waits on them)
-        const uint32_t tf = h.tf;
-        const uint32_t loc = (uint32_t)(li - wbase);
-        atomicAdd(&s_pb[dir][slot], ((unsigned long long)h.doct << 32) | 1ull);
-        atomicMax(&s_pos[slot].w, loc + 1);
-        // min / max and first positions change rarely: one 16-B read each, and
-        // an atomic only where the packet moves the value (a stale read can
-        // only cost a redundant atomic, never skip a needed one: the values
-        // move monotonically)
-        const uint4 mm = s_mm[slot], ps = s_pos[slot];
-        if (h.pkt < mm.x) atomicMin(&s_mm[slot].x, h.pkt);
-        if (h.ttl < mm.y) atomicMin(&s_mm[slot].y, h.ttl);
-        if (h.pkt > mm.z) atomicMax(&s_mm[slot].z, h.pkt);
-        if (h.ttl > mm.w) atomicMax(&s_mm[slot].w, h.ttl);
-        if (loc < ps.x) atomicMin(&s_pos[slot].x, loc);
-        // a flow is created by any non-TCP packet or a SYN (offline_fluereflows.rs:101-113)
-        if (((h.proto != 6u) | ((tf & 2u) != 0)) & (loc < ps.y)) atomicMin(&s_pos[slot].y, loc);
-        if (tf) {
+        // update_flow (flows.rs:11-42), order-free part.  Guard reads of every
+        // packet first (a slot index of 0 for lanes without an update keeps
+        // them unconditional), then the atomics: min / max and first
+        // positions change rarely, so they are written only where the packet
+        // moves the value (a stale guard can only cost a redundant atomic,
+        // never skip a needed one: the values move monotonically).
+        uint4 mm[PK];
+        uint2 ps[PK];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t w = ((tf >> (2 * q)) & 1) | (((tf >> (2 * q + 1)) & 1) << 16);
-                if (w) atomicAdd(&s_fl[q][slot], w);
+        for (int u = 0; u < PK; u++) {
+            const uint32_t sl = agg[u] ? q[u].slot : 0u;
+            if (!(FLUERE_AGG_UNCOND & 1)) mm[u] = s_mm[sl];
+            if (!(FLUERE_AGG_UNCOND & 2)) ps[u] = *reinterpret_cast<const uint2*>(&s_pos[sl]);
+        }
+#pragma unroll
+        for (int u = 0; u < PK; u++) {
+            if (!agg[u]) continue;
+            const Hot& h = q[u].h;
+            const uint32_t slot = q[u].slot;
+            c_valid++;
+            tmin = min(tmin, (unsigned long long)h.t);
+            tmax = max(tmax, (unsigned long long)h.t);
+            const uint32_t tf = h.tf;
+            const uint32_t loc = (uint32_t)(li[u] - wbase);
+            atomicAdd(&s_pb[q[u].dir][slot], ((unsigned long long)h.doct << 32) | 1ull);
+            atomicMax(&s_pos[slot].w, loc + 1);
+            if (FLUERE_AGG_UNCOND & 1) {
+                atomicMin(&s_mm[slot].x, h.pkt);
+                atomicMin(&s_mm[slot].y, h.ttl);
+                atomicMax(&s_mm[slot].z, h.pkt);
+                atomicMax(&s_mm[slot].w, h.ttl);
+            } else {
+                if (h.pkt < mm[u].x) atomicMin(&s_mm[slot].x, h.pkt);
+                if (h.ttl < mm[u].y) atomicMin(&s_mm[slot].y, h.ttl);
+                if (h.pkt > mm[u].z) atomicMax(&s_mm[slot].z, h.pkt);
+                if (h.ttl > mm[u].w) atomicMax(&s_mm[slot].w, h.ttl);
             }
-            if (tf & 5) atomicMin(&s_pos[slot].z, loc);  // FIN or RST
+            // a flow is created by any non-TCP packet or a SYN (offline_fluereflows.rs:101-113)
+            const bool elig = (h.proto != 6u) | ((tf & 2u) != 0);
+            if (FLUERE_AGG_UNCOND & 2) {
+                atomicMin(&s_pos[slot].x, loc);
+                atomicMin(&s_pos[slot].y, elig ? loc : NONE32);
+            } else {
+                if (loc < ps[u].x) atomicMin(&s_pos[slot].x, loc);
+                if (elig & (loc < ps[u].y)) atomicMin(&s_pos[slot].y, loc);
+            }
+            if (tf) {
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const uint32_t w = ((tf >> (2 * qq)) & 1) | (((tf >> (2 * qq + 1)) & 1) << 16);
+                    if (w) atomicAdd(&s_fl[qq][slot], w);
+                }
+                if (tf & 5) atomicMin(&s_pos[slot].z, loc);  // FIN or RST
+            }
         }
     };
     unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_start = clock64();
@@ -684,56 +779,38 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         const unsigned long long f1 = clock64() - f0;
         if (win == 0) cyc_flush0 = f1;
         cyc_flush += f1;
-        wbase += (uint64_t)BLOCK * WIN_ITERS;
+        wbase += stride * WIN_ITERS;
         win++;
     };
     const uint64_t lastp = n - 1;  // loads past the end re-read the last packet (in bounds)
-#ifndef FLUERE_HOT_PIPE
-#define FLUERE_HOT_PIPE 1
-#endif
-    if (FLUERE_HOT_PIPE == 1) {
-        // One step per iteration: the offset of the next step is prefetched (a
-        // one-register carry), the window is loaded and consumed in the same
-        // step and pinned (pin_win) so its five loads form one round trip;
-        // latency is hidden by the other waves of the CU.
-        uint64_t li = beg + tid;
-        uint32_t o = B.offs[min(li, lastp)];
-        for (uint64_t st = 0; st < nsteps; st++) {
-            const uint32_t on = B.offs[min(li + BLOCK, lastp)];
-            Win W;
-            load_win(B, o, W);
-            pin_win(W);
-            process(W, o, li, li < end);
-            li += BLOCK;
-            o = on;
-            if ((st + 1) % WIN_ITERS == 0 && st + 1 < nsteps) flush();
+    // PK steps per iteration: the offsets of the next iteration are prefetched
+    // (PK registers of carry), the PK windows are loaded and consumed in the
+    // same iteration and pinned (pin_win) so their loads form one round trip;
+    // only offsets cross the back edge, so no register copy drains a load.
+    uint64_t li = beg + tid;
+    uint32_t o[PK];
+#pragma unroll
+    for (int u = 0; u < PK; u++) o[u] = B.offs[min(li + (uint64_t)u * stride, lastp)];
+    for (uint64_t st = 0; st < nsteps; st += PK) {
+        uint32_t on[PK];
+#pragma unroll
+        for (int u = 0; u < PK; u++) on[u] = B.offs[min(li + (uint64_t)(PK + u) * stride, lastp)];
+        Win W[PK];
+        uint64_t lis[PK];
+        bool live[PK];
+#pragma unroll
+        for (int u = 0; u < PK; u++) load_win(B, o[u], W[u]);
+#pragma unroll
+        for (int u = 0; u < PK; u++) {
+            pin_win(W[u]);
+            lis[u] = li + (uint64_t)u * stride;
+            live[u] = lis[u] < end;
         }
-    } else {
-        // Two steps per iteration, two windows in registers: the window of the
-        // next step is in flight while this one is processed.  Each window is
-        // pinned just before its processing, and the loop carries every window
-        // in its own registers (no copies: a copy would wait for the load).
-        uint64_t li = beg + tid;
-        uint32_t o0 = B.offs[min(li, lastp)], o1 = B.offs[min(li + BLOCK, lastp)];
-        Win WA, WB;
-        load_win(B, o0, WA);
-        uint32_t o2 = B.offs[min(li + 2 * BLOCK, lastp)];
-        for (uint64_t st = 0; st < nsteps; st += 2) {
-            load_win(B, o1, WB);
-            const uint32_t o3 = B.offs[min(li + 3 * BLOCK, lastp)];
-            pin_win(WA);
-            process(WA, o0, li, li < end);
-            li += BLOCK;
-            load_win(B, o2, WA);
-            const uint32_t o4 = B.offs[min(li + 3 * BLOCK, lastp)];
-            pin_win(WB);
-            process(WB, o1, li, (li < end) & (st + 1 < nsteps));
-            li += BLOCK;
-            o0 = o2;
-            o1 = o3;
-            o2 = o4;
-            if ((st + 2) % WIN_ITERS == 0 && st + 2 < nsteps) flush();
-        }
+        process(W, o, lis, live);
+        li += (uint64_t)PK * stride;
+#pragma unroll
+        for (int u = 0; u < PK; u++) o[u] = on[u];
+        if ((st + PK) % WIN_ITERS == 0 && st + PK < nsteps) flush();
     }
     flush();
     // sets of windows this workgroup did not have: empty segments
