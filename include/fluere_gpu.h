@@ -39,8 +39,8 @@ extern "C" {
 enum fluere_status {
     FLUERE_OK = 0,
     FLUERE_E_ARG = -1,         /* bad argument */
-    FLUERE_E_IO = -2,          /* file open/read/write failed (FluereError::Io) */
-    FLUERE_E_PCAP = -3,        /* not a classic pcap file (FluereError::Pcap) */
+    FLUERE_E_IO = -2,          /* file open/read/write failed (FluereError::IoError) */
+    FLUERE_E_PCAP = -3,        /* not a classic pcap file (FluereError::PcapError) */
     FLUERE_E_HIP = -4,         /* HIP runtime error / no device */
     FLUERE_E_NOMEM = -5,       /* device or host allocation failed */
     FLUERE_E_TABLE_FULL = -6,  /* flow dictionary capacity exceeded: reopen with larger max_flows */
@@ -155,13 +155,14 @@ int fluere_parse_batch(fluere_ctx* ctx, fluere_pkt_meta* d_out, uint64_t cap);
 int fluere_run(fluere_ctx* ctx, fluere_stats* stats);
 
 /* Only the parse+key+aggregate pass over the attached batches (k_parse_agg,
- * the partial merge and the slow-path kernel); leaves the flow table
- * populated. Asynchronous. */
+ * then k_merge_partials, which also runs the general parser over the packets
+ * the hot kernel left to it); leaves the flow table populated. Asynchronous. */
 int fluere_parse_aggregate(fluere_ctx* ctx);
 /* Device time (HIP events on the ctx stream) of the last k_parse_agg launch
  * (the roofline kernel) of the last fluere_run / fluere_parse_aggregate, ms. */
 double fluere_last_kernel_ms(fluere_ctx* ctx);
-/* Device time of the whole last parse+key+aggregate pass, ms. */
+/* After fluere_run: its host wall time (submission to results), ms.  After
+ * fluere_parse_aggregate: device time of the hot kernel + merge, ms. */
 double fluere_last_pass_ms(fluere_ctx* ctx);
 
 /* Records of the last fluere_run, host memory, ended prefix first (in the
