@@ -56,10 +56,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU; "nccl" is RCCL on ROCm.  FLUERE_DIST_BACKEND=gloo
+        # rehearses the sharded path with several ranks on one GPU (tests only).
+        backend = os.environ.get("FLUERE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     C = CONFIGS[args.config]
     n_total = C["per_gpu"] * world
     cfg = fluere_amd.synth_cfg(C["kind"], n_total, C["flows"], C["seed"])

@@ -2450,9 +2450,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     P.macs = c->use_mac;
     P.abl = abl;
     c->plan_nb = P.nb;
-    HIPCHECK(hipEventRecord(c->ev0, c->stream));
     rc = enqueue_batches(c, P);
-    HIPCHECK(hipEventRecord(c->ev1, c->stream));
     debug_counters(c);
     return rc;
 }
@@ -2467,15 +2465,14 @@ extern "C" double fluere_last_kernel_ms(fluere_ctx* c) {
 }
 
 // Duration of the last pass: after fluere_run, its host wall time (submission
-// to results); after fluere_parse_aggregate, the device time of the hot kernel
-// and the merge (HIP events on the context stream).
+// to results); after fluere_parse_aggregate, the device time of its hot
+// kernel launches (HIP events on the context stream; no other markers).
 extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
     if (!c) return -1.0;
     float ms = -1.0f;
     if (c->pass_in_run) return c->last_run_ms;
-    hipEvent_t e0 = c->ev0, e1 = c->ev1;
-    if (hipEventSynchronize(e1) != hipSuccess) return -1.0;
-    if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.0;
+    if (hipEventSynchronize(c->evk1) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, pass_start_event(c), c->evk1) != hipSuccess) return -1.0;
     return ms;
 }
 
@@ -2785,9 +2782,7 @@ extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out
     HIPCHECK(hipGetLastError());
     Glob g;
     uint32_t nf_err[2];
-    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    if ((rc = fetch_ctl(c, g, nf_err))) return rc;
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
     if (g.raw) return FLUERE_E_UNSUPPORTED;
     uint32_t nf = std::min(nf_err[0], c->fmax);
@@ -2830,9 +2825,7 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     HIPCHECK(hipGetLastError());
     Glob g;
     uint32_t nf_err[2];
-    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    if ((rc = fetch_ctl(c, g, nf_err))) return rc;
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
     const uint32_t nf = std::min(nf_err[0], c->fmax);
     HIPCHECK(hipEventRecord(c->ev2, s));

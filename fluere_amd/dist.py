@@ -77,16 +77,21 @@ def gather_summaries(summaries, tmin: int, tmax: int, group=None, dst: int = 0):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    out_dev = summaries.device
+    # RCCL moves device tensors over xGMI; gloo (CPU tests, rehearsals) moves host copies
+    if dist.get_backend(group) == "gloo" and summaries.is_cuda:
+        summaries = summaries.cpu()
     dev = summaries.device
     # timestamps are microseconds (< 2^63); an empty shard travels as -1
     meta = torch.tensor([summaries.numel() // SUMMARY_BYTES, tmin if tmin < (1 << 63) else -1, tmax],
                         dtype=torch.int64, device=dev)
-    metas = [torch.empty_like(meta) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group)
-    counts = [int(m[0]) for m in metas]
-    lows = [int(m[1]) for m in metas if int(m[1]) >= 0]
+    metas = torch.empty(world * 3, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(metas, meta, group=group)
+    m = metas.view(world, 3).cpu().tolist()  # one device->host copy
+    counts = [int(r[0]) for r in m]
+    lows = [int(r[1]) for r in m if int(r[1]) >= 0]
     gmin = min(lows) if lows else NONE64
-    gmax = max(int(m[2]) for m in metas)
+    gmax = max(int(r[2]) for r in m)
     cap = max(max(counts), 1) * SUMMARY_BYTES
     send = torch.zeros(cap, dtype=torch.uint8, device=dev)
     send[: summaries.numel()] = summaries
@@ -95,7 +100,7 @@ def gather_summaries(summaries, tmin: int, tmax: int, group=None, dst: int = 0):
     if rank != dst:
         return None
     parts = [recv[r * cap: r * cap + counts[r] * SUMMARY_BYTES] for r in range(world)]
-    return torch.cat(parts), gmin, gmax
+    return torch.cat(parts).to(out_dev), gmin, gmax
 
 
 def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int = 0):

@@ -1,0 +1,88 @@
+"""Host-inclusive rate of the offline path (DESIGN.md "Host-inclusive rate").
+
+The path starts and ends in host memory: a pcap file in the page cache ->
+host indexing -> H2D -> kernels -> D2H records -> CSV.  This times the whole
+`fluere offline` call (fluere_offline_file) on a synthetic capture, and the
+same work split into phases through the FlowContext API:
+  read     file -> host memory
+  ingest   fluere_add_host_pcap: record index on the host + H2D copy
+  run      fluere_run (device-resident pass, one host round trip)
+  records  fluere_get_records (D2H + ordering)
+  csv      fluere_write_csv
+
+  python tools/host_inclusive.py [--config c2|c3] [--packets N] [--reps R]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {"c2": (0, 1000, 0xF10E0002), "c3": (1, 100_000, 0xF10E0003)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--packets", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    import fluere_amd
+    from fluere_amd import offline
+
+    kind, flows, seed = CONFIGS[args.config]
+    cfg = fluere_amd.synth_cfg(kind, args.packets, flows, seed)
+    data = fluere_amd.synth_pcap(cfg)
+    tmp = tempfile.mkdtemp(prefix="fluere_hi_")
+    path = os.path.join(tmp, f"{args.config}.pcap")
+    with open(path, "wb") as f:
+        f.write(data)
+    del data
+    out_dir = os.path.join(tmp, "output")
+    res = {"config": args.config, "packets": args.packets, "file_bytes": os.path.getsize(path)}
+    # whole call, file in the page cache (the first call also warms the runtime)
+    walls = []
+    for _ in range(args.reps + 1):
+        t0 = time.perf_counter()
+        st = offline.fluereflow_fileparse(offline.Args(offline.Files(file=path)), out_dir=out_dir)
+        walls.append(time.perf_counter() - t0)
+    best = min(walls[1:])
+    res["offline_file_s"] = round(best, 4)
+    res["offline_file_mpps"] = round(args.packets / best / 1e6, 2)
+    res["records"] = st["records"]
+    # phases
+    ph = {k: [] for k in ("read", "ingest", "run", "records", "csv")}
+    for _ in range(args.reps):
+        t = time.perf_counter()
+        with open(path, "rb") as f:
+            buf = f.read()
+        ph["read"].append(time.perf_counter() - t)
+        with fluere_amd.FlowContext(max_flows=max(1 << 16, 2 * flows)) as ctx:
+            t = time.perf_counter()
+            ctx.add_host_pcap(buf)
+            ph["ingest"].append(time.perf_counter() - t)
+            t = time.perf_counter()
+            ctx.run()
+            ph["run"].append(time.perf_counter() - t)
+            t = time.perf_counter()
+            recs, _ = ctx.records()
+            ph["records"].append(time.perf_counter() - t)
+        t = time.perf_counter()
+        fluere_amd.fluere_exporter(recs, os.path.join(tmp, "phase.csv"))
+        ph["csv"].append(time.perf_counter() - t)
+        del buf
+    res["phases_s"] = {k: round(min(v), 4) for k, v in ph.items()}
+    tot = sum(res["phases_s"].values())
+    res["phases_total_s"] = round(tot, 4)
+    res["phases_total_mpps"] = round(args.packets / tot / 1e6, 2)
+    res["h2d_gbs"] = round(res["file_bytes"] / res["phases_s"]["ingest"] / 1e9, 2)
+    os.remove(path)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
