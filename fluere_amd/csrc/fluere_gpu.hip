@@ -429,7 +429,10 @@ static_assert(WIN_ITERS % PK == 0, "a window holds whole iterations");
 constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
 constexpr int MAX_OWNERS = 256;
 
-__device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) { return (h >> 8) % O; }
+// merge owner of a flow: the top 24 hash bits scaled to [0, O) (multiply-shift)
+__device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) {
+    return (uint32_t)(((uint64_t)(h >> 8) * O) >> 24);
+}
 
 __device__ __forceinline__ uint32_t lt_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag) {
     uint32_t h = (k0 * 0x9E3779B1u) ^ (k1 * 0x85EBCA77u) ^ (k2 * 0xC2B2AE3Du) ^ tag;
@@ -453,7 +456,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint4 s_mm[NS], s_pos[NS];
     __shared__ uint32_t s_fl[4][NS];
     __shared__ uint32_t s_sk[NS];  // key entry of each slot
-    __shared__ uint32_t s_nslot;
+    __shared__ uint32_t s_nslot, s_chunk;
     __shared__ uint32_t s_own[MAX_OWNERS + 1];  // flush: per-owner counts -> segment starts
     __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
     const int tid = threadIdx.x;
@@ -465,7 +468,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
     }
     if (tid < 3) s_cnt[tid] = 0;
-    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; }
+    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; s_chunk = 0; }
     __syncthreads();
 
     const Batch& B = a.B;
@@ -709,23 +712,34 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             }
         }
     };
-    unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_start = clock64();
+    unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_wait = 0, cyc_start = clock64();
     uint32_t win = 0;
     auto flush = [&]() {
         // the window's partial aggregates -> this workgroup's staging set
         // (plain coalesced stores, lane per slot); k_merge_partials merges them
-        const unsigned long long f0 = clock64();
+        const unsigned long long fw = clock64();
         lds_barrier();
+        const unsigned long long f0 = clock64();  // flush proper (fw..f0: waiting for the slowest wave)
+        cyc_wait += f0 - fw;
         const Stage& S = a.S;
         const uint32_t set = blockIdx.x * S.W + win;
         const uint32_t ns = min(s_nslot, (uint32_t)NS), O = S.O;
-        // counting sort of this window's flows by merge owner
+        if (tid == 0) s_chunk = 0;  // every wave has drawn its last chunk of the window
+        // counting sort of this window's flows by merge owner; a thread keeps
+        // its slots' (at most two) owners and hashes in registers
+        static_assert(NS <= 2 * BLOCK, "two slots per thread");
         for (uint32_t o = tid; o <= O; o += BLOCK) s_own[o] = 0;
         lds_barrier();
-        for (uint32_t e = tid; e < ns; e += BLOCK) {
-            if ((s_pb[0][e] | s_pb[1][e]) == 0) continue;
-            const uint4 kk = s_key[s_sk[e]];
-            atomicAdd(&s_own[owner_of(lt_hash(kk.x, kk.y, kk.z, kk.w & 0xFF000000u), O)], 1u);
+        uint32_t own[2] = {NONE32, NONE32}, hh[2] = {0, 0};
+        uint4 kks[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t e = tid + k * BLOCK;
+            if (e >= ns || (s_pb[0][e] | s_pb[1][e]) == 0) continue;
+            kks[k] = s_key[s_sk[e]];
+            hh[k] = lt_hash(kks[k].x, kks[k].y, kks[k].z, kks[k].w & 0xFF000000u);
+            own[k] = owner_of(hh[k], O);
+            atomicAdd(&s_own[own[k]], 1u);
         }
         lds_barrier();
         if (tid < 64) {  // exclusive scan over the owners (one wave, 4 per lane)
@@ -755,13 +769,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         for (uint32_t o = tid; o <= O; o += BLOCK) S.off[(size_t)o * S.n_sets + set] = s_own[o];
         if (tid == 0) S.base[set] = B.first + wbase;
         lds_barrier();
-        for (uint32_t e = tid; e < ns; e += BLOCK) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t e = tid + k * BLOCK;
+            if (own[k] == NONE32) continue;
             const unsigned long long p0 = s_pb[0][e], p1 = s_pb[1][e];
-            if ((p0 | p1) == 0) continue;
-            const uint4 kk = s_key[s_sk[e]];
+            const uint4 kk = kks[k];
             const uint32_t tag = kk.w & 0xFF000000u;
-            const uint32_t h = lt_hash(kk.x, kk.y, kk.z, tag);
-            const size_t o = (size_t)set * NS + atomicAdd(&s_own[owner_of(h, O)], 1u);
+            const uint32_t h = hh[k];
+            const size_t o = (size_t)set * NS + atomicAdd(&s_own[own[k]], 1u);
             uint4* dst = reinterpret_cast<uint4*>(S.part + o);
             dst[0] = make_uint4(kk.x, kk.y, kk.z, tag);
             dst[1] = make_uint4(h, (uint32_t)(p0 & 0xFFFF) | ((uint32_t)(p1 & 0xFFFF) << 16), (uint32_t)(p0 >> 32),
@@ -783,36 +799,43 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         win++;
     };
     const uint64_t lastp = n - 1;  // loads past the end re-read the last packet (in bounds)
-    // PK steps per iteration: the offsets of the next iteration are prefetched
-    // (PK registers of carry), the PK windows are loaded and consumed in the
-    // same iteration and pinned (pin_win) so their loads form one round trip;
-    // only offsets cross the back edge, so no register copy drains a load.
-    uint64_t li = beg + tid;
-    uint32_t o[PK];
-#pragma unroll
-    for (int u = 0; u < PK; u++) o[u] = B.offs[min(li + (uint64_t)u * stride, lastp)];
-    for (uint64_t st = 0; st < nsteps; st += PK) {
-        uint32_t on[PK];
-#pragma unroll
-        for (int u = 0; u < PK; u++) on[u] = B.offs[min(li + (uint64_t)(PK + u) * stride, lastp)];
-        Win W[PK];
-        uint64_t lis[PK];
-        bool live[PK];
-#pragma unroll
-        for (int u = 0; u < PK; u++) load_win(B, o[u], W[u]);
-#pragma unroll
-        for (int u = 0; u < PK; u++) {
-            pin_win(W[u]);
-            lis[u] = li + (uint64_t)u * stride;
-            live[u] = lis[u] < end;
+    // Window by window.  A window is WIN_ITERS steps of this workgroup, i.e.
+    // WIN_ITERS * WAVES wave-chunks of 64 packets; the chunks are dealt to the
+    // waves dynamically (an LDS counter) so the waves of a workgroup finish a
+    // window together (static assignment left waves idle for ~10% of the
+    // kernel while the slowest one finished).  Per chunk the offset of the
+    // wave's next chunk is prefetched (one register of carry), the window is
+    // loaded and consumed in the same iteration and pinned (pin_win) so its
+    // loads form one round trip; only offsets cross the back edge.
+    static_assert(PK == 1, "dynamic chunks: one packet per lane per iteration");
+    constexpr uint32_t WAVES = BLOCK / 64;
+    const uint32_t lane = tid & 63;
+    auto grab = [&]() {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(&s_chunk, 1u);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    for (uint64_t ws = 0; ws < nsteps; ws += WIN_ITERS) {
+        const uint32_t nch = (uint32_t)min<uint64_t>(WIN_ITERS, nsteps - ws) * WAVES;
+        auto li_of = [&](uint32_t c) -> uint64_t {
+            return beg + (ws + c / WAVES) * stride + (uint64_t)(c % WAVES) * 64 + lane;
+        };
+        uint32_t c = grab();
+        uint32_t o1[1] = {B.offs[min(li_of(c), lastp)]};
+        while (c < nch) {
+            const uint32_t cn = grab();
+            const uint32_t on = B.offs[min(li_of(cn), lastp)];
+            Win W[1];
+            load_win(B, o1[0], W[0]);
+            pin_win(W[0]);
+            const uint64_t lis[1] = {li_of(c)};
+            const bool live[1] = {lis[0] < end};
+            process(W, o1, lis, live);
+            c = cn;
+            o1[0] = on;
         }
-        process(W, o, lis, live);
-        li += (uint64_t)PK * stride;
-#pragma unroll
-        for (int u = 0; u < PK; u++) o[u] = on[u];
-        if ((st + PK) % WIN_ITERS == 0 && st + PK < nsteps) flush();
+        flush();
     }
-    flush();
     // sets of windows this workgroup did not have: empty segments
     for (uint32_t w = win; w < a.S.W; w++)
         for (uint32_t oo = tid; oo <= a.S.O; oo += BLOCK) a.S.off[(size_t)oo * a.S.n_sets + blockIdx.x * a.S.W + w] = 0;
@@ -828,7 +851,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         if (s_cnt[2]) atomicAdd(&a.g->n_kc_miss, s_cnt[2]);
         atomicAdd(&a.g->cyc_total, clock64() - cyc_start);
         atomicAdd(&a.g->cyc_flush, cyc_flush);
-        atomicAdd(&a.g->cyc_flush0, cyc_flush0);
+        atomicAdd(&a.g->cyc_flush0, cyc_wait);
         if (s_cnt[0]) { atomicMin(&a.g->tmin, s_tmin); atomicMax(&a.g->tmax, s_tmax); }
     }
 }
@@ -2419,7 +2442,7 @@ static void debug_counters(fluere_ctx* c) {
     if (hipStreamSynchronize(c->stream) != hipSuccess) return;
     fprintf(stderr, "[fluere] valid %llu dropped %llu slow %llu LDS-table overflow packets %llu\n", g.valid, g.dropped,
             g.n_slow, g.n_kc_miss);
-    fprintf(stderr, "[fluere] per-WG clock: total %.0f flush %.0f first flush %.0f | merge scan %.0f ids %.0f\n",
+    fprintf(stderr, "[fluere] per-WG clock: total %.0f flush %.0f wait-for-waves %.0f | merge scan %.0f ids %.0f\n",
             g.cyc_total / 256.0, g.cyc_flush / 256.0, g.cyc_flush0 / 256.0, g.cyc_m_scan / 256.0, g.cyc_m_ids / 256.0);
 }
 
@@ -2492,8 +2515,6 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     (void)hipGetLastError();  // launch checks below see only this run's errors
     hipStream_t s = c->stream;
     int rc;
-    if ((rc = clear_flows(c))) return rc;
-    if ((rc = upload_batches(c))) return rc;
     // device timing: evk0 / evk1 around the hot kernel only (each event marker
     // costs a gap on the stream); the run's total is host wall time
     c->pass_in_run = true;
