@@ -90,12 +90,14 @@ struct Glob {
     unsigned long long n_keys, n_heads;
     unsigned long long generic_used;
     unsigned long long n_slow;
+    unsigned long long n_spill;  // k_parse_agg: spilled packets of the batch (sorted area cursor); next to n_slow
     unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
     unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
     unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
     unsigned long long clean_done;                        // k_cleanup: workgroups finished
 };
+static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8, "n_slow, n_spill are reset together");
 // One device allocation holds Glob and the dictionary counters right after it
 // (n_flows, err), so a run ends with ONE small device->host copy.
 struct Ctl {
@@ -300,10 +302,24 @@ struct alignas(16) Part {
 };
 static_assert(sizeof(Part) == 80, "Part layout");
 
+// A spilled packet: a valid hot-path packet whose key found no LDS slot (more
+// flows in a workgroup's window than the table holds).  32 bytes; written
+// raw per workgroup during the window, grouped by merge owner at the flush,
+// merged by its owner like a one-packet partial.
+struct alignas(16) Spill {
+    uint32_t k0, k1, k2, tag;     // LDS key words (tag = proto << 24)
+    uint32_t doct, pt, loc, fl;   // pt = pkt | ttl << 16 | elig << 24; fl = tf | dir << 8
+};
+static_assert(sizeof(Spill) == 32, "Spill layout");
+
 struct Stage {
     Part* part;                   // [set * NS + cell]
     uint32_t* off;                // [(O + 1) * n_sets]: off[o * n_sets + set] = first cell of owner o's flows
     unsigned long long* base;     // [set] global index of the window's first packet
+    Spill* spill_raw;             // [workgroup][WIN_ITERS * BLOCK] this window's spills, arrival order
+    Spill* spill;                 // owner-grouped spills of every set (n_spill cursor)
+    uint32_t* soff;               // [(O + 1) * n_sets]: owner o's spills of set s = spill[sbase[s] + soff[o][s] ..)
+    unsigned long long* sbase;    // [set] first spill of the set
     uint32_t W;                   // sets per workgroup
     uint32_t O;                   // merge owners (k_merge_partials workgroups)
     uint32_t n_sets;
@@ -428,6 +444,7 @@ constexpr int PK = FLUERE_HOT_PK;       // packets per lane per hot-loop iterati
 static_assert(WIN_ITERS % PK == 0, "a window holds whole iterations");
 constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
 constexpr int MAX_OWNERS = 256;
+constexpr int SPILL_WG = WIN_ITERS * BLOCK;  // raw spill records per workgroup (one window)
 
 // merge owner of a flow: the top 24 hash bits scaled to [0, O) (multiply-shift)
 __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) {
@@ -456,8 +473,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint4 s_mm[NS], s_pos[NS];
     __shared__ uint32_t s_fl[4][NS];
     __shared__ uint32_t s_sk[NS];  // key entry of each slot
-    __shared__ uint32_t s_nslot, s_chunk;
-    __shared__ uint32_t s_own[MAX_OWNERS + 1];  // flush: per-owner counts -> segment starts
+    __shared__ uint32_t s_nslot, s_chunk, s_nspill;
+    __shared__ uint32_t s_own[MAX_OWNERS + 1];   // flush: per-owner counts -> segment starts
+    __shared__ uint32_t s_scnt[MAX_OWNERS + 1];  // spilled packets per owner (this window) -> segment starts
+    __shared__ unsigned long long s_sbase;
     __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
     const int tid = threadIdx.x;
     for (int e = tid; e < LK; e += BLOCK) s_key[e] = make_uint4(0, 0, 0, 0);
@@ -468,7 +487,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
     }
     if (tid < 3) s_cnt[tid] = 0;
-    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; s_chunk = 0; }
+    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; s_chunk = 0; s_nspill = 0; }
+    for (int o = tid; o <= MAX_OWNERS; o += BLOCK) s_scnt[o] = 0;
     __syncthreads();
 
     const Batch& B = a.B;
@@ -563,9 +583,11 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         // lane that lost a claim, or saw an entry being written, reads the
         // pair again next step).
         uint4 kh[PK], kh2[PK];
+        uint32_t hk[PK];
 #pragma unroll
         for (int u = 0; u < PK; u++) {
-            q[u].e = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag) & (LK - 2);  // even: entries e, e+1 per step
+            hk[u] = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag);
+            q[u].e = hk[u] & (LK - 2);  // even: entries e, e+1 per step
             kh[u] = s_key[q[u].e];
             if (FLUERE_PROBE_PAIR) kh2[u] = s_key[q[u].e + 1];
         }
@@ -634,9 +656,34 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 #pragma unroll
         for (int u = 0; u < PK; u++) {
             agg[u] = q[u].valid & (q[u].state == 1) & (q[u].slot < NS);
+            // a valid packet whose key has no LDS slot spills: a 32-byte record
+            // for its merge owner (wave-aggregated append to this workgroup's
+            // raw spill buffer; grouped by owner at the flush)
             const bool miss = q[u].valid & !agg[u];
             c_miss += miss ? 1 : 0;
-            const bool slow = q[u].slow | miss;
+            const uint64_t mm_ = __ballot(miss);
+            if (mm_) {
+                const uint32_t lead = __builtin_ctzll(mm_);
+                uint32_t b0 = 0;
+                if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(&s_nspill, (uint32_t)__popcll(mm_));
+                b0 = __shfl(b0, lead, 64);
+                if (miss) {
+                    const Hot& h = q[u].h;
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm_ >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mm_, 0u));
+                    const uint32_t loc = (uint32_t)(li[u] - wbase);
+                    const bool elig = (h.proto != 6u) | ((h.tf & 2u) != 0);
+                    uint4* dst = reinterpret_cast<uint4*>(a.S.spill_raw + (size_t)blockIdx.x * SPILL_WG + b0 + r);
+                    dst[0] = make_uint4(q[u].k0, q[u].k1, q[u].k2, q[u].tag);
+                    dst[1] = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), loc,
+                                        h.tf | (q[u].dir << 8));
+                    atomicAdd(&s_scnt[owner_of(hk[u], a.S.O)], 1u);
+                    c_valid++;
+                    tmin = min(tmin, (unsigned long long)h.t);
+                    tmax = max(tmax, (unsigned long long)h.t);
+                }
+            }
+            const bool slow = q[u].slow;
             // slow list: wave-aggregated append (one global atomic per wave)
             const uint64_t sm = __ballot(slow);
             if (sm) {
@@ -718,7 +765,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         // the window's partial aggregates -> this workgroup's staging set
         // (plain coalesced stores, lane per slot); k_merge_partials merges them
         const unsigned long long fw = clock64();
-        lds_barrier();
+        // every wave's spill stores have completed (vmcnt) before the barrier
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const unsigned long long f0 = clock64();  // flush proper (fw..f0: waiting for the slowest wave)
         cyc_wait += f0 - fw;
         const Stage& S = a.S;
@@ -742,33 +790,63 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             atomicAdd(&s_own[own[k]], 1u);
         }
         lds_barrier();
-        if (tid < 64) {  // exclusive scan over the owners (one wave, 4 per lane)
+        // exclusive scans over the owners (one wave each, 4 owners per lane):
+        // wave 0 the slot counts, wave 1 the spill counts
+        static_assert(MAX_OWNERS <= 256, "4 owners per lane");
+        if (tid < 128) {
+            uint32_t* arr = tid < 64 ? s_own : s_scnt;
+            const uint32_t l = tid & 63;
             uint32_t v[4], sum = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const uint32_t o = tid * 4 + q;
-                v[q] = o < O ? s_own[o] : 0;
+                const uint32_t o = l * 4 + q;
+                v[q] = o < O ? arr[o] : 0;
                 sum += v[q];
             }
             uint32_t incl = sum;
 #pragma unroll
             for (int dlt = 1; dlt < 64; dlt <<= 1) {
                 const uint32_t y = __shfl_up(incl, dlt, 64);
-                if (tid >= dlt) incl += y;
+                if (l >= dlt) incl += y;
             }
             uint32_t run = incl - sum;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const uint32_t o = tid * 4 + q;
-                if (o < O) s_own[o] = run;
+                const uint32_t o = l * 4 + q;
+                if (o < O) arr[o] = run;
                 run += v[q];
             }
-            if (tid == 63) s_own[O] = incl;
+            if (l == 63) arr[O] = incl;
+        }
+        const uint32_t nsp = s_nspill;
+        if (tid == 128) s_sbase = nsp ? atomicAdd(&a.g->n_spill, (unsigned long long)nsp) : 0ull;
+        lds_barrier();
+        for (uint32_t o = tid; o <= O; o += BLOCK) {
+            S.off[(size_t)o * S.n_sets + set] = s_own[o];
+            S.soff[(size_t)o * S.n_sets + set] = s_scnt[o];
+        }
+        if (tid == 0) {
+            S.base[set] = B.first + wbase;
+            S.sbase[set] = s_sbase;
         }
         lds_barrier();
-        for (uint32_t o = tid; o <= O; o += BLOCK) S.off[(size_t)o * S.n_sets + set] = s_own[o];
-        if (tid == 0) S.base[set] = B.first + wbase;
-        lds_barrier();
+        // spilled packets -> owner-grouped segments of this set (the raw
+        // records were written by other waves of this workgroup: nontemporal
+        // loads, which bypass the CU's L1)
+        {
+            const Spill* raw = S.spill_raw + (size_t)blockIdx.x * SPILL_WG;
+            const unsigned long long sb = s_sbase;
+            for (uint32_t i = tid; i < nsp; i += BLOCK) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4* src = reinterpret_cast<const u32x4*>(raw + i);
+                const u32x4 a0 = __builtin_nontemporal_load(src), a1 = __builtin_nontemporal_load(src + 1);
+                const uint4 v0 = make_uint4(a0.x, a0.y, a0.z, a0.w), v1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
+                const uint32_t pos = atomicAdd(&s_scnt[owner_of(lt_hash(v0.x, v0.y, v0.z, v0.w), O)], 1u);
+                uint4* dst = reinterpret_cast<uint4*>(S.spill + sb + pos);
+                dst[0] = v0;
+                dst[1] = v1;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const uint32_t e = tid + k * BLOCK;
@@ -791,6 +869,9 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             s_pos[e] = make_uint4(NONE32, NONE32, NONE32, 0);
             s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
         }
+        lds_barrier();
+        for (uint32_t o = tid; o <= MAX_OWNERS; o += BLOCK) s_scnt[o] = 0;
+        if (tid == 0) s_nspill = 0;
         lds_barrier();
         const unsigned long long f1 = clock64() - f0;
         if (win == 0) cyc_flush0 = f1;
@@ -837,8 +918,14 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         flush();
     }
     // sets of windows this workgroup did not have: empty segments
-    for (uint32_t w = win; w < a.S.W; w++)
-        for (uint32_t oo = tid; oo <= a.S.O; oo += BLOCK) a.S.off[(size_t)oo * a.S.n_sets + blockIdx.x * a.S.W + w] = 0;
+    for (uint32_t w = win; w < a.S.W; w++) {
+        const uint32_t set = blockIdx.x * a.S.W + w;
+        for (uint32_t oo = tid; oo <= a.S.O; oo += BLOCK) {
+            a.S.off[(size_t)oo * a.S.n_sets + set] = 0;
+            a.S.soff[(size_t)oo * a.S.n_sets + set] = 0;
+        }
+        if (tid == 0) a.S.sbase[set] = 0;
+    }
     // statistics: one global atomic per workgroup
     atomicAdd(&s_cnt[0], c_valid);
     atomicAdd(&s_cnt[1], c_drop);
@@ -903,6 +990,27 @@ __device__ __forceinline__ void part_of_stage(const Part& p, unsigned long long 
     f.fc = p.pos[1] == NONE32 ? NONE64 : base + p.pos[1];
     f.fr = p.pos[2] == NONE32 ? NONE64 : base + p.pos[2];
     f.la = p.pos[3] ? base + p.pos[3] : 0;
+}
+
+// A spilled packet as a one-packet partial (update_flow of one packet,
+// flows.rs:11-42, with positions as global packet indices).
+__device__ __forceinline__ void spill_to_part(uint32_t doct, uint32_t pt, uint32_t loc, uint32_t fl,
+                                              unsigned long long base, FlowPart& f) {
+    const uint32_t dir = (fl >> 8) & 1, tf = fl & 0xFF;
+    const uint32_t pkt = pt & 0xFFFF, ttl = (pt >> 16) & 0xFF;
+    const unsigned long long gi = base + loc;
+    f.pk[0] = dir ? 0 : 1;
+    f.pk[1] = dir ? 1 : 0;
+    f.by[0] = dir ? 0 : doct;
+    f.by[1] = dir ? doct : 0;
+    f.mn[0] = f.mx[0] = pkt;
+    f.mn[1] = f.mx[1] = ttl;
+#pragma unroll
+    for (int q = 0; q < 8; q++) f.fl[q] = (tf >> q) & 1;
+    f.fa = gi;
+    f.fc = ((pt >> 24) & 1) ? gi : NONE64;
+    f.fr = (tf & 5) ? gi : NONE64;
+    f.la = gi + 1;
 }
 
 // Dense id of a staged key (flow_table.h dictionary; tag 0xFF: the key is the id).
@@ -980,16 +1088,20 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // exclusive scan of the segment lengths; threads then take partials from
     // the flattened index space (binary search for the set), so every thread
     // has about (partials / MB) of them with all their loads in flight.
+    // Pass 0 takes the staged partials, pass 1 the spilled packets (each a
+    // one-packet partial), through the same per-owner segment machinery.
+    for (int pass = 0; pass < 2; pass++)
     for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
         const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
+        const uint32_t* offs = pass ? S.soff : S.off;
         uint32_t len[MCH / MB], tot = 0;
 #pragma unroll
         for (int q = 0; q < MCH / MB; q++) {
             const uint32_t set = c0s + tid * (MCH / MB) + q;
             uint32_t lo = 0, hi = 0;
             if (set < c0s + nset) {
-                lo = S.off[(size_t)me * S.n_sets + set];
-                hi = S.off[(size_t)(me + 1) * S.n_sets + set];
+                lo = offs[(size_t)me * S.n_sets + set];
+                hi = offs[(size_t)(me + 1) * S.n_sets + set];
             }
             m_lo[tid * (MCH / MB) + q] = lo;
             len[q] = hi - lo;
@@ -1012,18 +1124,26 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             }
             const uint32_t set = c0s + lo_i;
             const unsigned long long base = S.base[set];
-            const size_t o = (size_t)set * NS + m_lo[lo_i] + (idx - m_start[lo_i]);
-            Part p;
-            {
+            uint32_t h, k0, k1, k2, tag;
+            FlowPart f;
+            if (pass == 0) {
+                const size_t o = (size_t)set * NS + m_lo[lo_i] + (idx - m_start[lo_i]);
+                Part p;
                 const uint4* src = reinterpret_cast<const uint4*>(S.part + o);
                 uint4 v[5];
 #pragma unroll
                 for (int q = 0; q < 5; q++) v[q] = src[q];
                 __builtin_memcpy(&p, v, sizeof p);
+                h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
+                part_of_stage(p, base, f);
+            } else {
+                const size_t o = S.sbase[set] + m_lo[lo_i] + (idx - m_start[lo_i]);
+                const uint4* src = reinterpret_cast<const uint4*>(S.spill + o);
+                const uint4 v0 = src[0], v1 = src[1];
+                k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
+                h = lt_hash(k0, k1, k2, tag);
+                spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
             }
-            const uint32_t h = p.h, k0 = p.k0, k1 = p.k1, k2 = p.k2, tag = p.tag;
-            FlowPart f;
-            part_of_stage(p, base, f);
             // find or claim the merge entry (same protocol as the hot kernel)
             uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
             int state = 0, probes = 0;
@@ -2235,6 +2355,12 @@ struct PassPlan {
     Glob* d_glob;
 };
 
+// Bytes of the hot kernel's staging area for one batch (Stage layout).
+static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n) {
+    return cells * sizeof(Part) + ((size_t)grid * SPILL_WG + n) * sizeof(Spill) +
+           2 * sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) + 64;
+}
+
 static int plan_batches(fluere_ctx* c, PassPlan& P) {
     AggArgs a;
     memset(&a, 0, sizeof a);
@@ -2263,8 +2389,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
-        need_max = std::max(need_max, cells * sizeof(Part) + sets * sizeof(unsigned long long) +
-                                          (size_t)(O + 1) * sets * sizeof(uint32_t) + 64);
+        need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n));
     }
     if (need_max > c->d_stage_bytes) {
         hipFree(c->d_stage);
@@ -2286,9 +2411,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
         Stage& S = a.S;
+        // layout (16-byte aligned pieces): parts | spill_raw | spill | sbase | base | off | soff
         S.part = (Part*)c->d_stage;
-        S.base = (unsigned long long*)(S.part + cells);
+        S.spill_raw = (Spill*)(S.part + cells);
+        S.spill = S.spill_raw + (size_t)grid * SPILL_WG;
+        S.sbase = (unsigned long long*)(S.spill + hb.b.n);
+        S.base = S.sbase + sets;
         S.off = (uint32_t*)(S.base + sets);
+        S.soff = S.off + (size_t)(O + 1) * sets;
         S.W = W;
         S.O = O;
         S.n_sets = (uint32_t)sets;
@@ -2334,7 +2464,7 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
     hipStream_t s = c->stream;
     for (int i = 0; i < P.nb; i++) {
         const AggArgs& a = P.agg[i];
-        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 8, s));  // run start: k_cleanup zeroed it
+        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 16, s));  // n_slow, n_spill (k_cleanup zeroed them for batch 0)
         if (i == 0 && P.nb > 1) HIPCHECK(hipEventRecord(c->evk_first, s));
         HIPCHECK(hipEventRecord(c->evk0, s));
         const unsigned grid = P.agg_grid[i];
@@ -2398,9 +2528,9 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
             hipMemsetParams mp{};
             mp.dst = &c->d_glob->n_slow;
             mp.elementSize = 4;
-            mp.width = 2;
+            mp.width = 4;  // n_slow, n_spill
             mp.height = 1;
-            mp.pitch = 8;
+            mp.pitch = 16;
             mp.value = 0;
             ok = hipGraphAddMemsetNode(&n, g, &prev, 1, &mp) == hipSuccess;
             prev = n;

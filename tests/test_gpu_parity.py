@@ -36,8 +36,8 @@ def _check_meta(got, want, what):
                     assert np.array_equal(g[f], w[f]), f"{what}[{i}].{f}: {g[f]} != {w[f]}"
 
 
-def _gpu_csv(data, timeout_ms=600000, use_mac=False):
-    with fluere_amd.FlowContext(timeout_ms=timeout_ms, use_mac=use_mac, max_flows=1 << 16) as ctx:
+def _gpu_csv(data, timeout_ms=600000, use_mac=False, max_flows=1 << 16):
+    with fluere_amd.FlowContext(timeout_ms=timeout_ms, use_mac=use_mac, max_flows=max_flows) as ctx:
         ctx.add_host_pcap(data)
         st = ctx.run()
         recs, ne = ctx.records()
@@ -74,6 +74,9 @@ SYNTH = {
     "c5_vlan_small": (_lib.SYNTH_VLAN64, 100_000, 2000, 0xF10E0005, True),
     "c5u_mac_small": (_lib.SYNTH_MAC64, 100_000, 5000, 0xF10E0005, True),
     "many_flows": (_lib.SYNTH_UDP64, 200_000, 50_000, 0xF10E0006, False),
+    # BASELINE configs[2] recipe at 1/5 size: 100k flows overflow every
+    # workgroup's LDS table, so most packets take the spill path
+    "c3_imix_2m": (_lib.SYNTH_IMIX, 2_000_000, 100_000, 0xF10E0003, False),
 }
 
 
@@ -82,7 +85,7 @@ def test_synthetic_csv_matches_oracle(gpu, name):
     kind, n, f, seed, use_mac = SYNTH[name]
     data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
     want = pyoracle.offline(data, use_mac=use_mac)
-    csv, ne, st = _gpu_csv(data, use_mac=use_mac)
+    csv, ne, st = _gpu_csv(data, use_mac=use_mac, max_flows=max(1 << 16, 2 * f))
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
     assert st["packets"] == n
 
