@@ -1739,7 +1739,7 @@ __global__ void __launch_bounds__(256) k_parse_batch(Batch B, fluere_pkt_meta* o
     memset(&m, 0, sizeof m);
     m.k_status = pi.kst;
     m.f_status = pi.fst;
-    m.raw_used = (pi.kst == ST_RAW || pi.fst == ST_RAW) ? 1 : 0;
+    m.raw_used = (pi.raw || pi.kst == ST_RAW || pi.fst == ST_RAW) ? 1 : 0;
     const uint8_t* fr = B.bytes + B.offs[li] + 16;
     if (pi.kst == ST_OK) {
         m.key_v6 = pi.v6; m.key_proto = pi.kproto; m.key_sport = pi.ksp; m.key_dport = pi.kdp;

@@ -37,6 +37,7 @@ struct PktInfo {
     uint32_t rsip[4], rdip[4];  // FluereRecord source / destination
     uint32_t rpkt;          // FluereRecord min_pkt (= max_pkt)
     uint32_t doctets;       // packet_size() of the L3 view
+    uint8_t raw;            // the src/net/parser/raw fallback produced key or record fields
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -85,6 +86,7 @@ __device__ __forceinline__ bool parse_fast(const Win& W, uint32_t L, PktInfo& o)
     for (int k = 0; k < 4; k++) { o.rsip[k] = o.sip[k]; o.rdip[k] = o.dip[k]; }
     o.kst = ST_OK;
     o.fst = ST_OK;
+    o.raw = 0;
     // keys.rs:182-184: "UDP" payload (ip payload[8..]) empty -> EmptyPacket
     if (pe == 8) o.kst = ST_EMPTY;
     // parse_ports (ports.rs:7-58)
@@ -204,6 +206,154 @@ __device__ __forceinline__ bool ipv6_keys(const G& g, Span i, PktInfo& o) {
     if (o.kproto == 58 && pl.len >= 4) { o.ksp = (uint16_t)g.b(pl.off); o.kdp = (uint16_t)g.b(pl.off + 1); }
     return true;
 }
+// ---------------------------------------------------------------------------
+// Raw fallback (src/net/parser/raw): the header the reference derives when
+// pnet's typed views do not apply.  Byte reads from global memory; only
+// packets outside the hot path get here.
+// ---------------------------------------------------------------------------
+struct RawHdr {
+    bool has_src, has_dst, v6;
+    uint32_t src[4], dst[4];
+    uint16_t sport, dport;
+    uint8_t proto;
+    uint16_t length;  // u16 in RawProtocolHeader (raw/mod.rs)
+};
+
+__device__ __forceinline__ void raw_new(RawHdr& h, uint32_t sp, uint32_t dp, uint32_t proto, uint32_t len) {
+    h.has_src = h.has_dst = h.v6 = false;
+    for (int k = 0; k < 4; k++) h.src[k] = h.dst[k] = 0;
+    h.sport = (uint16_t)sp; h.dport = (uint16_t)dp; h.proto = (uint8_t)proto; h.length = (uint16_t)len;
+}
+
+// protocols/icmp.rs:95-131
+__device__ __forceinline__ bool raw_icmp(const G& g, Span p, RawHdr& h) {
+    if (p.len < 4) return false;
+    raw_new(h, g.b(p.off), g.b(p.off + 1), 1, p.len);
+    return true;
+}
+
+// protocols/openvpn.rs:155-220 (control packets :31-72, data packets :85-128)
+__device__ __forceinline__ bool raw_openvpn(const G& g, Span p, RawHdr& h) {
+    if (p.len < 9) return false;
+    const uint32_t t = g.b(p.off);
+    if (!((t >= 1 && t <= 9) || t == 0x40 || t == 0x41)) return false;
+    raw_new(h, t, 0, 0x9B, p.len);
+    if (t == 6 || t == 9) {
+        const Span ip = {p.off + 9, p.len - 9};
+        if (ip.len >= 16 && ((g.b(ip.off) >> 4) & 0x0F) == 4) {
+            h.has_src = h.has_dst = true;
+            ip4_words(g, ip.off + 4, h.src); ip4_words(g, ip.off + 8, h.dst);
+            h.sport = (uint16_t)g.be16(ip.off + 12); h.dport = (uint16_t)g.be16(ip.off + 14);
+        }
+    } else if (p.len >= 21 && (t == 0x40 || t == 0x41)) {
+        h.has_src = h.has_dst = true;
+        ip4_words(g, p.off + 9, h.src); ip4_words(g, p.off + 13, h.dst);
+        h.sport = (uint16_t)g.be16(p.off + 17); h.dport = (uint16_t)g.be16(p.off + 19);
+    }
+    return true;
+}
+
+// protocols/mod.rs:48-84
+__device__ __forceinline__ bool raw_parse_protocol(const G& g, Span p, uint32_t proto, RawHdr& h) {
+    if (proto == 1 && raw_icmp(g, p, h)) return true;
+    if (proto >= 170 && proto <= 172 && raw_openvpn(g, p, h)) return true;
+    return raw_openvpn(g, p, h);
+}
+
+// raw/mod.rs:152-328 RawProtocolHeader::from_raw_packet
+__device__ __attribute__((noinline)) bool raw_from_raw_packet(const G& g, Span p, uint32_t hint, RawHdr& h) {
+    bool outer = false;
+    uint32_t os = 0, od = 0, osp = 0, odp = 0, oproto = 0;
+    if (p.len >= 20 && (g.b(p.off) >> 4) == 4) {
+        const uint32_t hl = (g.b(p.off) & 0x0F) * 4;
+        if (hl >= 20 && hl <= p.len) {
+            outer = true;
+            os = g.be32(p.off + 12); od = g.be32(p.off + 16);
+            oproto = g.b(p.off + 9);
+            if (hl + 4 <= p.len) { osp = g.be16(p.off + hl); odp = g.be16(p.off + hl + 2); }
+        }
+    }
+    if (raw_parse_protocol(g, p, hint, h)) {
+        if (outer) {  // fill what the protocol parser left unset from the outer IPv4 header
+            if (!h.has_src) { h.has_src = true; h.src[0] = os; h.src[1] = h.src[2] = h.src[3] = 0; }
+            if (!h.has_dst) { h.has_dst = true; h.dst[0] = od; h.dst[1] = h.dst[2] = h.dst[3] = 0; }
+            if (h.sport == 0) h.sport = (uint16_t)osp;
+            if (h.dport == 0) h.dport = (uint16_t)odp;
+        }
+        return true;
+    }
+    if (outer) {
+        raw_new(h, osp, odp, oproto, p.len);
+        h.has_src = h.has_dst = true;
+        h.src[0] = os; h.dst[0] = od;
+        return true;
+    }
+    if (p.len < 4) return false;
+    if (hint == 0x36) raw_new(h, g.b(p.off), g.b(p.off + 1), hint, p.len);
+    else raw_new(h, g.be16(p.off), g.be16(p.off + 2), hint, p.len);  // 0xb9 and generic: same ports
+    return true;
+}
+
+// ethertypes/vpn.rs:133-186 extract_ip_addresses
+__device__ __forceinline__ void raw_extract_ips(const G& g, Span q, RawHdr& h) {
+    if (q.len < 20) return;
+    const uint32_t ver = g.b(q.off) >> 4;
+    if (ver == 4) {
+        h.has_src = h.has_dst = true; h.v6 = false;
+        ip4_words(g, q.off + 12, h.src); ip4_words(g, q.off + 16, h.dst);
+    } else if (ver == 6 && q.len >= 40) {
+        h.has_src = h.has_dst = true; h.v6 = true;
+        ip6_words(g, q.off + 8, h.src); ip6_words(g, q.off + 24, h.dst);
+    }
+}
+
+// ethertypes/mod.rs:20-61 parse_ethertype (its 0x0806 arm is unreachable from
+// parse_fluereflow, which handles ARP itself)
+__device__ __forceinline__ bool raw_parse_ethertype(const G& g, Span p, uint32_t et, RawHdr& h) {
+    if (et == 0x0A08 || et == 0x4B65) {  // vpn.rs:15-56, :58-99
+        if (p.len < 4) return false;
+        raw_new(h, et == 0x0A08 ? 2186 : 19301, g.be16(p.off + 2), et == 0x0A08 ? 21 : 22, p.len);
+        raw_extract_ips(g, {p.off + 4, p.len - 4}, h);
+        return true;
+    }
+    if (et == 0x8847 || et == 0x8848) {  // mpls.rs:3-40
+        if (p.len < 4) return false;
+        const uint32_t label = (g.b(p.off) << 12) | (g.b(p.off + 1) << 4) | (g.b(p.off + 2) >> 4);
+        raw_new(h, label & 0xFFFF, (g.b(p.off + 2) >> 1) & 7, 137, p.len);
+        return true;
+    }
+    if (et == 0x12B5) {  // vxlan.rs:8-48
+        if (p.len < 8 || !(g.be32(p.off) == 0x08000000u && g.be32(p.off + 4) == 0x00006400u)) return false;
+        const uint32_t vni = (g.b(p.off + 4) << 16) | (g.b(p.off + 5) << 8) | g.b(p.off + 6);
+        raw_new(h, 4789, vni & 0xFFFF, 0x12, p.len);
+        return true;
+    }
+    if (et == 0x88B8) {  // wireguard.rs:12-80
+        if (p.len < 4) return false;
+        const uint32_t t = g.b(p.off);
+        if (t == 1 && p.len != 148) return false;
+        if (t == 2 && p.len != 92) return false;
+        if (t == 3 && p.len != 64) return false;
+        if (t == 4 && p.len < 16) return false;
+        if (t < 1 || t > 4) return false;
+        raw_new(h, 0, 51820, t, p.len);
+        return true;
+    }
+    if ((et >= 0xB800 && et <= 0xBFFF) || (et >= 0x3600 && et <= 0x36FF)) {  // mod.rs:110-137
+        if (p.len < 4) return false;
+        raw_new(h, g.be16(p.off), g.be16(p.off + 2), g.b(p.off), p.len);
+        return true;
+    }
+    return false;
+}
+
+// raw/mod.rs:330-349 RawProtocolHeader::from_ethertype
+__device__ __forceinline__ bool raw_from_ethertype(const G& g, Span p, uint32_t et, RawHdr& h) {
+    if (raw_parse_ethertype(g, p, et, h)) return true;
+    if (et == 0x0800 && p.len >= 20) return raw_from_raw_packet(g, p, g.b(p.off + 9), h);
+    return raw_from_raw_packet(g, p, et & 0xFF, h);
+}
+
 // arp_keys (keys.rs:345-359)
 __device__ __forceinline__ void arp_keys(const G& g, Span a, PktInfo& o) {
     o.v6 = 0;
@@ -229,6 +379,7 @@ __device__ __attribute__((noinline)) void parse_general(const uint8_t* d, uint32
     o.frame_off = 0;
     o.rprot = o.rtos = o.rttl = o.tflags = 0;
     o.rsp = o.rdp = 0; o.rpkt = 0; o.doctets = 0;
+    o.raw = 0;
     // ---------------- parse_keys (keys.rs:98-343)
     if (L == 0) o.kst = ST_EMPTY;
     else if (L < 14) o.kst = ST_INVALID;
@@ -279,10 +430,28 @@ __device__ __attribute__((noinline)) void parse_general(const uint8_t* d, uint32
             if (P2.len < 4) o.kst = ST_EMPTY;
             else o.kst = vlan_keys(g, P2, o);
         } else {
-            // keys.rs:252-313: the eager chain.  With |P2| >= 4 some member
-            // (at the latest the raw generic parser) returns Ok; below that
-            // every member fails -> UnknownEtherType.
-            o.kst = P2.len >= 4 ? ST_RAW : ST_UNKNOWN_ETHER;
+            // keys.rs:252-313: the eager chain over the payload; the first Ok
+            // wins: ipv4_keys, ipv6_keys, arp_keys, vlan_keys, then the raw
+            // fallback (RawProtocolHeader::from_raw_packet with the low byte of
+            // the ethertype as the protocol hint)
+            uint8_t e = ST_INVALID;
+            if (P2.len >= 20) e = ipv4_keys(g, P2, o) ? ST_OK : ST_INVALID;
+            if (e != ST_OK && P2.len >= 40) e = ipv6_keys(g, P2, o) ? ST_OK : ST_INVALID;
+            if (e != ST_OK && P2.len >= 28) { arp_keys(g, P2, o); e = ST_OK; }
+            if (e != ST_OK && P2.len >= 4) e = vlan_keys(g, P2, o);
+            if (e != ST_OK) {
+                RawHdr h;
+                o.raw = 1;
+                if (raw_from_raw_packet(g, P2, et2 & 0xFF, h)) {
+                    o.v6 = 0;  // from_raw_packet yields IPv4 addresses or none (0.0.0.0)
+                    for (int k = 0; k < 4; k++) { o.sip[k] = h.src[k]; o.dip[k] = h.dst[k]; }
+                    o.ksp = h.sport; o.kdp = h.dport; o.kproto = h.proto;
+                    e = ST_OK;
+                } else {
+                    e = ST_UNKNOWN_ETHER;
+                }
+            }
+            o.kst = e;
         }
     }
     // ---------------- parse_fluereflow (fluereflows.rs:30-199)
@@ -328,7 +497,16 @@ __device__ __attribute__((noinline)) void parse_general(const uint8_t* d, uint32
         o.doctets = 28; o.rpkt = 28; o.rprot = 4;
         ip4_words(g, P2.off + 14, o.rsip); ip4_words(g, P2.off + 24, o.rdip);
     } else {
-        o.fst = ST_RAW;  // RawProtocolHeader::from_ethertype (fluereflows.rs:148-195)
+        // fluereflows.rs:148-195: RawProtocolHeader::from_ethertype over the
+        // whole frame; ttl None -> 0, tos 0, flags of an empty slice
+        RawHdr h;
+        o.raw = 1;
+        if (!raw_from_ethertype(g, fframe, et2, h)) { o.fst = ST_UNKNOWN_ETHER; return; }
+        o.rv6 = h.v6 ? 1 : 0;
+        for (int k = 0; k < 4; k++) { o.rsip[k] = h.src[k]; o.rdip[k] = h.dst[k]; }
+        o.doctets = h.length;
+        o.rsp = h.sport; o.rdp = h.dport;
+        o.rpkt = h.length; o.rttl = 0; o.rprot = h.proto; o.rtos = 0; o.tflags = 0;
     }
 }
 

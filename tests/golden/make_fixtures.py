@@ -147,6 +147,29 @@ def fixtures():
         U(0, 3, eth(et=0x88CC) + b"\x01\x02"),                                 # < 4 bytes payload
         U(0, 4, eth(et=0x8847) + bytes([0, 1, 0x41, 64]) + b"\x00" * 30),      # MPLS
     ]
+    # every sub-parser of the raw fallback (src/net/parser/raw): VPN, VXLAN,
+    # WireGuard and generic ethertype ranges, the eager key chain over an
+    # unknown ethertype, OpenVPN shapes, short L4 payloads of unusual protocols
+    F["raw_more"] = [
+        U(0, 0, eth(et=0x0A08) + bytes([0, 0, 0x12, 0x34]) + ipv4("172.16.0.1", "172.16.0.2", 17, udp(5, 6, b"\x01" * 8))),
+        U(0, 1, eth(et=0x4B65) + bytes([0, 0, 0x56, 0x78]) + ipv6("fd00::1", "fd00::2", 17, udp(7, 8, b"\x02" * 8))),
+        U(0, 2, eth(et=0x12B5) + VXLAN + b"\x03" * 16),
+        U(0, 3, eth(et=0x12B5) + bytes([0x09, 0, 0, 0, 0, 0, 0x64, 0]) + b"\x03" * 16),
+        U(0, 4, eth(et=0x88B8) + bytes([1]) + b"\x00" * 147),
+        U(0, 5, eth(et=0x88B8) + bytes([2]) + b"\x00" * 50),
+        U(0, 6, eth(et=0x88B8) + bytes([4]) + b"\x00" * 31),
+        U(0, 7, eth(et=0xB812) + bytes([0x11, 0x22, 0x33, 0x44, 0x55])),
+        U(0, 8, eth(et=0x3655) + bytes([0x66, 0x77, 0x88, 0x99])),
+        U(0, 9, eth(et=0x88B5) + ipv4("10.9.0.1", "10.9.0.2", 1, b"\x08\x00\x00\x00" + b"\x00" * 12)),
+        U(0, 10, eth(et=0x9000) + bytes([0x40]) + b"\x00" * 8 + bytes([10, 1, 1, 1, 10, 1, 1, 2, 0x04, 0xD2, 0x16, 0x2E])
+          + b"\x00" * 4),
+        U(0, 11, eth(et=0x9000) + bytes([0x06]) + b"\x00" * 8 + ipv4("10.2.2.1", "10.2.2.2", 17, udp(1000, 2000, b"")[:4])),
+        U(0, 12, eth() + ipv4("10.0.0.5", "10.0.0.6", 0x36, b"\xAB\xCD\xEF\x01\x02\x03")),
+        U(0, 13, eth() + ipv4("10.0.0.5", "10.0.0.6", 171, bytes([6]) + b"\x00" * 5)),
+        U(0, 14, eth() + ipv4("10.0.0.5", "10.0.0.6", 99, b"\x12\x34\x56")),
+        U(0, 15, eth(et=0x86DD) + ipv6("fd00::5", "fd00::6", 0x36, b"\xAB\xCD\xEF")),
+        U(0, 16, eth(et=0x8848) + bytes([0xFF, 0xFF, 0xF3, 0x40]) + b"\x00" * 20),
+    ]
     # symmetric key, MAC-keyed flows, timestamp order, expiry
     F["edge_keys"] = [
         U(0, 0, eth() + ipv4(A, A, 17, udp(7, 7, b"\x51" * 10))),               # Key == reverse key
