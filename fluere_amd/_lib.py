@@ -116,6 +116,7 @@ def lib() -> ctypes.CDLL:
         "fluere_pcap_index": (I64, [P, U64, P, U64]),
         "fluere_add_device_batch": (I, [P, P, U64, P, U64, ctypes.c_uint32, I, I]),
         "fluere_add_host_pcap": (I, [P, P, U64]),
+        "fluere_add_pcap_file": (I, [P, ctypes.c_char_p]),
         "fluere_parse_batch": (I, [P, P, U64]),
         "fluere_run": (I, [P, ctypes.POINTER(Stats)]),
         "fluere_parse_aggregate": (I, [P]),
@@ -130,6 +131,7 @@ def lib() -> ctypes.CDLL:
         "fluere_synth_device": (I, [ctypes.POINTER(SynthCfg), U64, U64, P, P, P]),
         "fluere_set_index_base": (I, [P, U64]),
         "fluere_capacity": (U64, [P]),
+        "fluere_total_packets": (U64, [P]),
         "fluere_last_kernel_ms": (ctypes.c_double, [P]),
         "fluere_last_pass_ms": (ctypes.c_double, [P]),
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),

@@ -27,6 +27,10 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -2248,57 +2252,202 @@ extern "C" int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint6
     return pcap_walk(file, nbytes, offsets, cap, nullptr, nullptr, nullptr);
 }
 
+// ---------------------------------------------------------------------------
+// Host ingress.  The capture streams to the device in order through two
+// pinned staging chunks (the copy of one chunk overlaps filling the next),
+// and the record index is built on the host from the staged bytes while they
+// are still in cache: one pass over the headers, libpcap offline semantics
+// (stop at the first bad or truncated record).  The whole capture lands in
+// one device allocation; batches (< 4 GiB each, u32 offsets) are sub-ranges.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kIngestChunk = 32ull << 20;
+constexpr uint32_t kSnapMax = 262144;
+constexpr uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
+
+struct Ingest {
+    fluere_ctx* c;
+    uint64_t size = 0;
+    uint8_t* d = nullptr;
+    uint8_t* pin[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    int sw = 0, ns = 0;
+    uint32_t snap = kSnapMax;
+    uint64_t pos = 24;
+    bool stopped = false;
+    uint8_t tail[16];
+    std::vector<uint64_t> offs;      // absolute record offsets
+    std::vector<size_t> cut;         // first record of each batch
+    std::vector<uint64_t> cut_base;  // byte offset of each batch
+
+    explicit Ingest(fluere_ctx* cc) : c(cc) {}
+    ~Ingest() {
+        for (int i = 0; i < 2; i++)
+            if (busy[i]) hipEventSynchronize(ev[i]);  // no copy may read a freed staging chunk
+        for (int i = 0; i < 2; i++) {
+            if (ev[i]) hipEventDestroy(ev[i]);
+            if (pin[i]) hipHostFree(pin[i]);
+        }
+        if (d) hipFree(d);  // still owned here unless finish() handed it over
+    }
+    int begin(uint64_t nbytes) {
+        if (nbytes < 24) return FLUERE_E_PCAP;
+        size = nbytes;
+        if (hipMalloc(&d, nbytes + 256) != hipSuccess) return FLUERE_E_NOMEM;
+        for (int i = 0; i < 2; i++) {
+            if (hipHostMalloc(&pin[i], kIngestChunk, hipHostMallocDefault) != hipSuccess) return FLUERE_E_NOMEM;
+            if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return FLUERE_E_HIP;
+        }
+        return FLUERE_OK;
+    }
+    // staging slot for chunk k, free once its previous copy has completed
+    uint8_t* slot(uint64_t k) {
+        const int i = (int)(k & 1);
+        if (busy[i]) {
+            hipEventSynchronize(ev[i]);
+            busy[i] = false;
+        }
+        return pin[i];
+    }
+    uint32_t rd32(const uint8_t* p) const {
+        uint32_t v;
+        memcpy(&v, p, 4);
+        return sw ? __builtin_bswap32(v) : v;
+    }
+    // chunk k = bytes [cs, cs + len) of the capture, already in slot(k)
+    int feed(uint64_t k, uint64_t cs, uint64_t len) {
+        const uint8_t* b = pin[k & 1];
+        if (cs == 0) {  // pcap global header (libpcap offline)
+            uint32_t magic;
+            memcpy(&magic, b, 4);
+            if (magic == 0xa1b2c3d4u) {
+            } else if (magic == 0xd4c3b2a1u) sw = 1;
+            else if (magic == 0xa1b23c4du) ns = 1;
+            else if (magic == 0x4d3cb2a1u) { sw = 1; ns = 1; }
+            else return FLUERE_E_PCAP;
+            snap = rd32(b + 16);
+            if (snap == 0 || snap > kSnapMax) snap = kSnapMax;
+            cut.push_back(0);
+            cut_base.push_back(24);
+        }
+        const uint64_t ce = cs + len;
+        uint8_t h[16];
+        while (!stopped && pos + 16 <= ce) {
+            const uint8_t* hp;
+            if (pos >= cs) {
+                hp = b + (pos - cs);
+            } else {  // header straddles the previous chunk (its last 16 bytes are in tail)
+                for (int j = 0; j < 16; j++) h[j] = pos + j >= cs ? b[pos + j - cs] : tail[16 - (cs - (pos + j))];
+                hp = h;
+            }
+            const uint32_t incl = rd32(hp + 8);
+            if (incl > kSnapMax || pos + 16 + (uint64_t)incl > size) {
+                stopped = true;
+                break;
+            }
+            if (pos + 16 + incl - cut_base.back() > kMaxBatch) {
+                cut.push_back(offs.size());
+                cut_base.push_back(pos);
+            }
+            offs.push_back(pos);
+            pos += 16 + (uint64_t)incl;
+        }
+        if (pos + 16 > size) stopped = true;
+        if (len >= 16) memcpy(tail, b + len - 16, 16);
+        else {  // short final chunk: shift it into the tail
+            memmove(tail, tail + len, 16 - len);
+            memcpy(tail + 16 - len, b, len);
+        }
+        const int i = (int)(k & 1);
+        HIPCHECK(hipMemcpyAsync(d + cs, b, len, hipMemcpyHostToDevice, c->stream));
+        HIPCHECK(hipEventRecord(ev[i], c->stream));
+        busy[i] = true;
+        return FLUERE_OK;
+    }
+    // the index as batches of the context (device bytes handed over)
+    int finish() {
+        HIPCHECK(hipMemsetAsync(d + size, 0, 256, c->stream));
+        const size_t n = offs.size();
+        uint32_t* d_offs = nullptr;
+        if (hipMalloc(&d_offs, std::max<size_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        std::vector<uint32_t> rel(std::max<size_t>(n, 1));
+        for (size_t q = 0; q < cut.size(); q++) {
+            const size_t i0 = cut[q], i1 = q + 1 < cut.size() ? cut[q + 1] : n;
+            for (size_t k = i0; k < i1; k++) rel[k] = (uint32_t)(offs[k] - cut_base[q]);
+        }
+        if (n) HIPCHECK(hipMemcpyAsync(d_offs, rel.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHECK(hipStreamSynchronize(c->stream));  // rel is pageable; staging slots free
+        for (int i = 0; i < 2; i++) busy[i] = false;
+        bool first = true;
+        for (size_t q = 0; q < cut.size(); q++) {
+            const size_t i0 = cut[q], i1 = q + 1 < cut.size() ? cut[q + 1] : n;
+            if (i1 == i0) continue;
+            const uint64_t base = cut_base[q];
+            const uint64_t endb = q + 1 < cut.size() ? cut_base[q + 1] : size;
+            HostBatch hb;
+            hb.own_bytes = first ? d : nullptr;  // one allocation for every batch
+            hb.own_offs = first ? d_offs : nullptr;
+            first = false;
+            hb.b.bytes = d + base;
+            hb.b.offs = d_offs + i0;
+            hb.b.nbytes = endb - base;
+            hb.b.n = i1 - i0;
+            hb.b.first = c->index_base + c->n_total;
+            hb.b.snap = snap;
+            hb.b.flags = (sw ? 1u : 0u) | (ns ? 2u : 0u);
+            c->batches.push_back(hb);
+            c->batches_dirty = true;
+            c->n_total += hb.b.n;
+        }
+        if (first) {  // no records: nothing attached
+            hipFree(d_offs);
+        } else {
+            d = nullptr;  // owned by the first batch now
+        }
+        c->have_results = false;
+        return FLUERE_OK;
+    }
+};
+
 extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t nbytes) {
     if (!c || !file) return FLUERE_E_ARG;
     HIPCHECK(hipSetDevice(c->device));
-    uint32_t snap;
-    int sw, ns;
-    int64_t n = pcap_walk(file, nbytes, nullptr, 0, &snap, &sw, &ns);
-    if (n < 0) return (int)n;
-    std::vector<uint64_t> offs((size_t)n);
-    pcap_walk(file, nbytes, offs.data(), (uint64_t)n, nullptr, nullptr, nullptr);
-    // split into batches of < 4 GiB (u32 offsets relative to the batch start)
-    size_t i = 0;
-    const uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
-    while (i < (size_t)n || (n == 0 && i == 0)) {
-        if (n == 0) break;
-        uint64_t base = offs[i];
-        size_t j = i;
-        while (j < (size_t)n) {
-            uint32_t incl;
-            memcpy(&incl, file + offs[j] + 8, 4);
-            if (sw) incl = __builtin_bswap32(incl);
-            if (offs[j] + 16 + incl - base > kMaxBatch) break;
-            j++;
-        }
-        uint64_t endb = (j < (size_t)n) ? offs[j] : nbytes;
-        uint64_t nb = endb - base;
-        std::vector<uint32_t> rel(j - i);
-        for (size_t k = i; k < j; k++) rel[k - i] = (uint32_t)(offs[k] - base);
-        HostBatch hb;
-        if (hipMalloc(&hb.own_bytes, nb + 256) != hipSuccess) return FLUERE_E_NOMEM;
-        if (hipMalloc(&hb.own_offs, std::max<size_t>(rel.size(), 1) * 4) != hipSuccess) {
-            hipFree(hb.own_bytes);
-            return FLUERE_E_NOMEM;
-        }
-        HIPCHECK(hipMemcpyAsync(hb.own_bytes, file + base, nb, hipMemcpyHostToDevice, c->stream));
-        HIPCHECK(hipMemsetAsync((uint8_t*)hb.own_bytes + nb, 0, 256, c->stream));
-        HIPCHECK(hipMemcpyAsync(hb.own_offs, rel.data(), rel.size() * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHECK(hipStreamSynchronize(c->stream));
-        hb.b.bytes = (const uint8_t*)hb.own_bytes;
-        hb.b.offs = (const uint32_t*)hb.own_offs;
-        hb.b.nbytes = nb;
-        hb.b.n = j - i;
-        hb.b.first = c->index_base + c->n_total;
-        hb.b.snap = snap;
-        hb.b.flags = (sw ? 1u : 0u) | (ns ? 2u : 0u);
-        c->batches.push_back(hb);
-    c->batches_dirty = true;
-        c->n_total += hb.b.n;
-        i = j;
+    Ingest in(c);
+    int rc = in.begin(nbytes);
+    if (rc) return rc;
+    for (uint64_t k = 0, cs = 0; cs < nbytes; k++, cs += kIngestChunk) {
+        const uint64_t len = std::min(kIngestChunk, nbytes - cs);
+        memcpy(in.slot(k), file + cs, len);
+        if ((rc = in.feed(k, cs, len))) return rc;
     }
-    c->have_results = false;
-    return FLUERE_OK;
+    return in.finish();
+}
+
+// File ingress for fluere_offline_file: read() straight into the pinned
+// staging chunks (no intermediate copy of the capture in host memory).
+extern "C" int fluere_add_pcap_file(fluere_ctx* c, const char* path) {
+    if (!c || !path) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return FLUERE_E_IO;
+    struct stat stt;
+    if (fstat(fd, &stt) != 0) { close(fd); return FLUERE_E_IO; }
+    const uint64_t nbytes = (uint64_t)stt.st_size;
+    Ingest in(c);
+    int rc = in.begin(nbytes);
+    for (uint64_t k = 0, cs = 0; !rc && cs < nbytes; k++, cs += kIngestChunk) {
+        const uint64_t len = std::min(kIngestChunk, nbytes - cs);
+        uint8_t* dst = in.slot(k);
+        uint64_t got = 0;
+        while (got < len) {
+            const ssize_t r = pread(fd, dst + got, len - got, (off_t)(cs + got));
+            if (r <= 0) { rc = FLUERE_E_IO; break; }
+            got += (uint64_t)r;
+        }
+        if (!rc) rc = in.feed(k, cs, len);
+    }
+    close(fd);
+    return rc ? rc : in.finish();
 }
 
 static int upload_batches(fluere_ctx* c) {
@@ -2911,6 +3060,7 @@ extern "C" int fluere_synth_device(const fluere_synth_cfg* cfg, uint64_t first, 
 // multi-GPU merge
 // ---------------------------------------------------------------------------
 extern "C" uint64_t fluere_capacity(fluere_ctx* c) { return c ? c->fmax : 0; }
+extern "C" uint64_t fluere_total_packets(fluere_ctx* c) { return c ? c->n_total : 0; }
 
 extern "C" int fluere_set_index_base(fluere_ctx* c, uint64_t base) {
     if (!c) return FLUERE_E_ARG;

@@ -10,6 +10,7 @@
 //       ./output-style directory, convert, write <stem>_converted.csv.
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -134,28 +135,21 @@ static int mkdir_p(const std::string& dir) {
 extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, int use_mac, const char* out_dir,
                                    fluere_stats* stats) {
     if (!pcap_path) return FLUERE_E_ARG;
-    FILE* f = fopen(pcap_path, "rb");
-    if (!f) return FLUERE_E_IO;
-    std::vector<uint8_t> file;
-    {
-        uint8_t chunk[1 << 16];
-        size_t r;
-        while ((r = fread(chunk, 1, sizeof chunk, f)) > 0) file.insert(file.end(), chunk, chunk + r);
-        fclose(f);
-    }
+    struct stat sb;
+    if (stat(pcap_path, &sb) != 0) return FLUERE_E_IO;
     std::string dir = out_dir ? out_dir : "./output";
     if (mkdir_p(dir) != 0) return FLUERE_E_IO;
     std::string out = dir + "/" + file_stem(pcap_path) + "_converted.csv";
     fluere_opts o{};
     o.timeout_ms = timeout_ms;
     o.use_mac = use_mac;
-    int64_t n = fluere_pcap_index(file.data(), file.size(), nullptr, 0);
-    if (n < 0) return (int)n;
-    o.max_flows = (uint64_t)std::max<int64_t>(1 << 16, std::min<int64_t>(n, 1 << 22));
+    // flow capacity from the file size (a record is at least 16 bytes; flows
+    // rarely exceed one per 64 bytes of capture)
+    o.max_flows = std::max<uint64_t>(1 << 16, std::min<uint64_t>((uint64_t)sb.st_size / 64, 1 << 22));
     fluere_ctx* c = nullptr;
     int rc = fluere_open(&o, &c);
     if (rc) return rc;
-    rc = fluere_add_host_pcap(c, file.data(), file.size());
+    rc = fluere_add_pcap_file(c, pcap_path);
     fluere_stats st{};
     if (!rc) rc = fluere_run(c, &st);
     if (stats) *stats = st;

@@ -65,6 +65,11 @@ class FlowContext:
         n = self._L.fluere_pcap_index(buf, len(data), None, 0)
         self.n_packets += max(int(n), 0)
 
+    def add_pcap_file(self, path: str):
+        """Stream a capture file to the device (pinned chunks, host-side index)."""
+        check(self._L.fluere_add_pcap_file(self._h, os.fsencode(path)), "fluere_add_pcap_file")
+        self.n_packets = int(self._L.fluere_total_packets(self._h))
+
     def add_device_batch(self, d_bytes, nbytes: int, d_offsets, n: int, snaplen: int = 65535, swapped=False,
                          nsec=False, keep=()):
         """Attach device-resident records (pointers or torch tensors)."""

@@ -141,8 +141,13 @@ int fluere_add_device_batch(fluere_ctx* ctx, const uint8_t* d_bytes, uint64_t nb
                             const uint32_t* d_offsets, uint64_t n_packets, uint32_t snaplen, int swapped,
                             int nsec_ts);
 
-/* Copy a host pcap file image to the device (owned by ctx) and attach it. */
+/* Copy a host pcap file image to the device (owned by ctx) and attach it.
+ * The bytes stream through pinned staging chunks (copies overlap the next
+ * chunk) while the record index is built on the host in one pass. */
 int fluere_add_host_pcap(fluere_ctx* ctx, const uint8_t* file, uint64_t nbytes);
+/* The same, reading the capture file straight into the staging chunks
+ * (Capture::from_file, offline_fluereflows.rs:44). */
+int fluere_add_pcap_file(fluere_ctx* ctx, const char* path);
 
 /* ---- compute ------------------------------------------------------------- */
 /* Per-packet parse_keys/parse_fluereflow of every attached packet into a
@@ -194,6 +199,8 @@ typedef struct fluere_flow_summary {
  * summary buffer of this many entries lets fluere_export_summaries run in one
  * pass with a single host round trip. */
 uint64_t fluere_capacity(fluere_ctx* ctx);
+/* Records attached to the context (every batch). */
+uint64_t fluere_total_packets(fluere_ctx* ctx);
 int fluere_set_index_base(fluere_ctx* ctx, uint64_t first_global_index);
 /* Export this context's flows after fluere_parse_aggregate.  tmin/tmax: time
  * range of the valid packets (for the expiry-mode decision). */

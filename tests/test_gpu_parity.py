@@ -199,3 +199,44 @@ def test_flow_dictionary_ids(gpu, n_keys, dup):
     assert np.all(ids_by_key == ids_by_key[:, :1]), "equal keys got different ids"
     uniq = ids_by_key[:, 0]
     assert len(np.unique(uniq)) == n_keys and uniq.max() == n_keys - 1
+
+
+def test_file_ingest_across_chunks(gpu, tmp_path):
+    """fluere_add_pcap_file / fluere_offline_file: a capture larger than the
+    32 MiB staging chunks (headers straddle chunk boundaries), against the
+    oracle on the same bytes, and the in-memory ingest of the same file."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 150_000, 3000, 0xF11E)
+    data = fluere_amd.synth_pcap(cfg)
+    assert len(data) > 40 << 20
+    path = tmp_path / "cap.pcap"
+    path.write_bytes(data)
+    want = pyoracle.offline(data)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_pcap_file(str(path))
+        assert ctx.n_packets == cfg.n_packets
+        ctx.run()
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "file ingest")
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_host_pcap(data)
+        ctx.run()
+        recs2, ne2 = ctx.records()
+    assert ne2 == ne and np.array_equal(np.sort(recs2, order=["first", "last"]), np.sort(recs, order=["first", "last"]))
+    st = fluere_amd.fluereflow_fileparse(fluere_amd.Args(fluere_amd.Files(file=str(path))), out_dir=str(tmp_path / "out"))
+    got = (tmp_path / "out" / "cap_converted.csv").read_text()
+    assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "fluere_offline_file")
+
+
+def test_truncated_tail_record(gpu, tmp_path):
+    """libpcap stops at a record whose bytes run past the end of the file."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_UDP64, 1000, 10, 0xF12E)
+    data = fluere_amd.synth_pcap(cfg)[:-30]
+    want = pyoracle.offline(data)
+    path = tmp_path / "t.pcap"
+    path.write_bytes(data)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_pcap_file(str(path))
+        assert ctx.n_packets == 999
+        ctx.run()
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "truncated")

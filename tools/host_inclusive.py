@@ -4,8 +4,8 @@ The path starts and ends in host memory: a pcap file in the page cache ->
 host indexing -> H2D -> kernels -> D2H records -> CSV.  This times the whole
 `fluere offline` call (fluere_offline_file) on a synthetic capture, and the
 same work split into phases through the FlowContext API:
-  read     file -> host memory
-  ingest   fluere_add_host_pcap: record index on the host + H2D copy
+  ingest   fluere_add_pcap_file: file -> pinned staging chunks -> HBM, with
+           the record index built on the host from the staged bytes
   run      fluere_run (device-resident pass, one host round trip)
   records  fluere_get_records (D2H + ordering)
   csv      fluere_write_csv
@@ -55,15 +55,11 @@ def main():
     res["offline_file_mpps"] = round(args.packets / best / 1e6, 2)
     res["records"] = st["records"]
     # phases
-    ph = {k: [] for k in ("read", "ingest", "run", "records", "csv")}
+    ph = {k: [] for k in ("ingest", "run", "records", "csv")}
     for _ in range(args.reps):
-        t = time.perf_counter()
-        with open(path, "rb") as f:
-            buf = f.read()
-        ph["read"].append(time.perf_counter() - t)
         with fluere_amd.FlowContext(max_flows=max(1 << 16, 2 * flows)) as ctx:
             t = time.perf_counter()
-            ctx.add_host_pcap(buf)
+            ctx.add_pcap_file(path)  # file -> pinned chunks -> HBM, host-side record index
             ph["ingest"].append(time.perf_counter() - t)
             t = time.perf_counter()
             ctx.run()
@@ -74,7 +70,6 @@ def main():
         t = time.perf_counter()
         fluere_amd.fluere_exporter(recs, os.path.join(tmp, "phase.csv"))
         ph["csv"].append(time.perf_counter() - t)
-        del buf
     res["phases_s"] = {k: round(min(v), 4) for k, v in ph.items()}
     tot = sum(res["phases_s"].values())
     res["phases_total_s"] = round(tot, 4)
