@@ -57,15 +57,22 @@ constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
 // LDS aggregates are flushed every WIN_ITERS steps of BLOCK packets: a window
 // holds at most 61440 packets, so the 16-bit per-direction packet and flag
 // counts and the u32 per-direction byte sums (<= 65535 B per packet) cannot wrap.
-// A multiple of 3 (the hot loop is unrolled by three).
 constexpr int WIN_ITERS = 60;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
 constexpr uint64_t IDX_MASK = (1ull << 40) - 1;
 
+// Chunk descriptor (one per 64 records, built when a batch is attached, from
+// its offsets): x = offset of the chunk's first record, y = the records'
+// common stride when the 64 records are evenly spaced with a stride of at
+// most 80 B, a multiple of 16 ("dense": the hot kernel reads the chunk's span
+// with five coalesced loads per lane and reads no offsets), else 0 ("sparse":
+// per-record windows at the record offsets).
 struct Batch {
     const uint8_t* bytes;
     const uint32_t* offs;
+    const uint2* desc;    // [n_desc] or null
+    uint64_t n_desc;      // n / 64 (whole chunks)
     uint64_t nbytes;
     uint64_t n;
     uint64_t first;  // global index of packet 0
@@ -324,10 +331,15 @@ struct Stage {
     Spill* spill;                 // owner-grouped spills of every set (n_spill cursor)
     uint32_t* soff;               // [(O + 1) * n_sets]: owner o's spills of set s = spill[sbase[s] + soff[o][s] ..)
     unsigned long long* sbase;    // [set] first spill of the set
+    unsigned long long* wgs;      // [workgroup][WGS_N] run statistics of each hot-kernel workgroup (plain
+                                  // stores; k_merge_partials sums them: no contended atomics at the end)
     uint32_t W;                   // sets per workgroup
     uint32_t O;                   // merge owners (k_merge_partials workgroups)
     uint32_t n_sets;
+    uint32_t n_wg;                // hot-kernel workgroups
 };
+// per-workgroup statistics: valid, dropped, LDS-table misses, tmin, tmax, cycles total / flush / wave wait
+constexpr int WGS_N = 8;
 
 struct AggArgs {
     Batch B;
@@ -338,6 +350,7 @@ struct AggArgs {
     uint32_t* slow;            // packets (batch-local indices) parse_fast did not take
     unsigned long long* slow_n;
     int macs;
+    unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
 };
 
 // Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
@@ -432,14 +445,24 @@ __device__ __forceinline__ void lds_barrier() {
 //   non-MAC kernels: key = (lo_ip, hi_ip, lo_port<<16|hi_port), proto
 //   MAC kernels:     key = (dense id, 0, 0), proto 0xFF (the dictionary is
 //                    walked per packet; the table only pre-aggregates)
-constexpr int LK = 4096;                // key entries (64 KiB)
-constexpr int NS = 1280;                // aggregate slots (68 B each, 85 KiB)
+constexpr int LK_BITS = 11;
+constexpr int LK = 1 << LK_BITS;        // key entries (32 KiB)
+#ifndef FLUERE_NS
+#define FLUERE_NS 1280
+#endif
+constexpr int NS = FLUERE_NS;                // aggregate slots (68 B each, 85 KiB)
 constexpr int LK_STEPS = 16;            // probe steps of two entries
 #ifndef FLUERE_HOT_PK
 #define FLUERE_HOT_PK 1
 #endif
-#ifndef FLUERE_PROBE_PAIR
-#define FLUERE_PROBE_PAIR 1  // 1: the inline probe reads both entries of the home pair
+#ifndef FLUERE_FLUSH_LINEAR
+#define FLUERE_FLUSH_LINEAR 0  // diagnostics only (wrong results): partials in slot order
+#endif
+#ifndef FLUERE_DENSE_POLICY
+#define FLUERE_DENSE_POLICY "nt"  // cache policy of the dense chunk loads (streamed once)
+#endif
+#ifndef FLUERE_PROBE2
+#define FLUERE_PROBE2 1  // 1: two-choice pairs (the inline probe reads both candidate pairs); 0: one pair, linear
 #endif
 #ifndef FLUERE_AGG_UNCOND
 #define FLUERE_AGG_UNCOND 2  // bit 0: min/max, bit 1: first positions as unconditional atomics
@@ -477,11 +500,12 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint4 s_mm[NS], s_pos[NS];
     __shared__ uint32_t s_fl[4][NS];
     __shared__ uint32_t s_sk[NS];  // key entry of each slot
+    __shared__ uint4 s_slab[BLOCK / 64][160];  // per wave: half a dense chunk's span (32 x 80 B)
     __shared__ uint32_t s_nslot, s_chunk, s_nspill;
     __shared__ uint32_t s_own[MAX_OWNERS + 1];   // flush: per-owner counts -> segment starts
     __shared__ uint32_t s_scnt[MAX_OWNERS + 1];  // spilled packets per owner (this window) -> segment starts
     __shared__ unsigned long long s_sbase;
-    __shared__ unsigned long long s_cnt[3], s_tmin, s_tmax;
+    __shared__ unsigned long long s_cnt[5], s_tmin, s_tmax;
     const int tid = threadIdx.x;
     for (int e = tid; e < LK; e += BLOCK) s_key[e] = make_uint4(0, 0, 0, 0);
     for (int e = tid; e < NS; e += BLOCK) {
@@ -490,7 +514,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         s_pos[e] = make_uint4(NONE32, NONE32, NONE32, 0);
         s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
     }
-    if (tid < 3) s_cnt[tid] = 0;
+    if (tid < 5) s_cnt[tid] = 0;
     if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; s_chunk = 0; s_nspill = 0; }
     for (int o = tid; o <= MAX_OWNERS; o += BLOCK) s_scnt[o] = 0;
     __syncthreads();
@@ -512,6 +536,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     const uint64_t beg = FLUERE_HOT_ORDER ? (uint64_t)blockIdx.x * BLOCK : per * blockIdx.x;
     const uint64_t end = FLUERE_HOT_ORDER ? n : min(n, beg + per);
     unsigned long long c_valid = 0, c_drop = 0, c_miss = 0, tmin = NONE64, tmax = 0;
+    uint32_t d_loops = 0, d_iters = 0;  // diagnostics (per wave, uniform)
     const uint64_t nsteps = end > beg ? (end - beg + stride - 1) / stride : 0;
     uint64_t wbase = beg;
 
@@ -523,7 +548,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     // parser and the global path for them (nothing rare is inlined here).
     struct PS {
         Hot h;
-        uint32_t dir, lo_ip, hi_ip, kports, k0, k1, k2, tag, e, slot;
+        uint32_t dir, lo_ip, hi_ip, kports, k0, k1, k2, tag, e, e2, slot;
         int state, steps;
         bool valid, slow;
     };
@@ -586,30 +611,44 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         // wave-uniform retry loop runs only while some lane still searches (a
         // lane that lost a claim, or saw an entry being written, reads the
         // pair again next step).
-        uint4 kh[PK], kh2[PK];
+        // Probe sequence of a key: pair e1, pair e2, then linear from e2 + 2
+        // (write-once table, so lookups and inserts follow one sequence).
+        // Two-choice placement keeps nearly every key in one of its first two
+        // pairs; both are read inline, so the retry loop below runs only for
+        // inserts and for the rare key placed further on.
         uint32_t hk[PK];
+        uint4 kp[PK][4];
 #pragma unroll
         for (int u = 0; u < PK; u++) {
             hk[u] = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag);
-            q[u].e = hk[u] & (LK - 2);  // even: entries e, e+1 per step
-            kh[u] = s_key[q[u].e];
-            if (FLUERE_PROBE_PAIR) kh2[u] = s_key[q[u].e + 1];
+            const uint32_t e1 = hk[u] & (LK - 2);  // even: entries e, e+1 per step
+            uint32_t e2 = (hk[u] >> 12) * 0x9E3779B1u >> (32 - LK_BITS + 1) << 1;
+            e2 = FLUERE_PROBE2 ? (e2 == e1 ? e1 ^ 2u : e2) : (e1 + 2) & (LK - 1);
+            q[u].e = e1;
+            q[u].e2 = e2;
+            kp[u][0] = s_key[e1];
+            kp[u][1] = s_key[e1 + 1];
+            kp[u][2] = FLUERE_PROBE2 ? s_key[e2] : make_uint4(0, 0, 0, 0);
+            kp[u][3] = FLUERE_PROBE2 ? s_key[e2 + 1] : make_uint4(0, 0, 0, 0);
         }
         bool searching = false;
 #pragma unroll
         for (int u = 0; u < PK; u++) {
-            const uint4 ka = kh[u];
-            const bool ma = ((ka.w & (0xFF000000u | LT_READY)) == (q[u].tag | LT_READY)) & (ka.x == q[u].k0) &
-                            (ka.y == q[u].k1) & (ka.z == q[u].k2);
-            bool mb = false;
-            if (FLUERE_PROBE_PAIR) {
-                const uint4 kb = kh2[u];
-                mb = ((kb.w & (0xFF000000u | LT_READY)) == (q[u].tag | LT_READY)) & (kb.x == q[u].k0) &
-                     (kb.y == q[u].k1) & (kb.z == q[u].k2);
-            }
-            q[u].slot = (ma ? ka.w : kh2[u].w) & LT_SLOT;
-            q[u].state = q[u].valid ? ((ma | mb) ? 1 : 0) : 2;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 none
-            q[u].steps = 0;
+            bool m[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                m[k] = ((kp[u][k].w & (0xFF000000u | LT_READY)) == (q[u].tag | LT_READY)) & (kp[u][k].x == q[u].k0) &
+                       (kp[u][k].y == q[u].k1) & (kp[u][k].z == q[u].k2);
+            const uint32_t sw = m[0] ? kp[u][0].w : m[1] ? kp[u][1].w : m[2] ? kp[u][2].w : kp[u][3].w;
+            q[u].slot = sw & LT_SLOT;
+            const bool found = m[0] | m[1] | m[2] | m[3];
+            q[u].state = q[u].valid ? (found ? 1 : 0) : 2;  // 0 searching, 1 found (slot < NS, or NS: no slot), 2 none
+            const bool full1 = (kp[u][0].w & kp[u][1].w & LT_READY) != 0;
+            const bool full2 = (kp[u][2].w & kp[u][3].w & LT_READY) != 0;
+            // where the search goes on: the first pair of the sequence not yet
+            // known to be full of other keys
+            q[u].steps = full1 ? (full2 ? 2 : 1) : 0;
+            q[u].e = full1 ? (full2 ? (q[u].e2 + 2) & (LK - 1) : q[u].e2) : q[u].e;
             if (ABL == 3) {  // diagnostics: aggregation without the key table (wrong slots)
                 q[u].slot = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag) % 1000u;
                 q[u].state = q[u].valid ? 1 : 2;
@@ -617,7 +656,9 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             searching |= q[u].state == 0;
         }
         if (ABL != 3 && __ballot(searching)) {
+            d_loops++;
             for (int it = 0; it < 2 * LK_STEPS; it++) {
+                d_iters++;
                 bool more = false;
 #pragma unroll
                 for (int u = 0; u < PK; u++) {
@@ -633,7 +674,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                             r.state = 1;
                         } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
                             if (++r.steps == LK_STEPS) r.state = 2;
-                            else r.e = (r.e + 2) & (LK - 1);
+                            else r.e = r.steps == 1 ? r.e2 : (r.e + 2) & (LK - 1);
                         } else {
                             // first free entry of the pair; an entry being written (CLAIM) is re-read next step
                             const uint32_t f = (ka.w == 0) ? r.e : ((ka.w & LT_READY) && kb.w == 0 ? r.e + 1 : LK);
@@ -763,12 +804,13 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             }
         }
     };
-    unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_wait = 0, cyc_start = clock64();
+    unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_wait = 0, cyc_start = clock64(), rt_start = wall_clock64();
     uint32_t win = 0;
     auto flush = [&]() {
         // the window's partial aggregates -> this workgroup's staging set
         // (plain coalesced stores, lane per slot); k_merge_partials merges them
         const unsigned long long fw = clock64();
+        if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 1] = wall_clock64();
         // every wave's spill stores have completed (vmcnt) before the barrier
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const unsigned long long f0 = clock64();  // flush proper (fw..f0: waiting for the slowest wave)
@@ -779,13 +821,18 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         if (tid == 0) s_chunk = 0;  // every wave has drawn its last chunk of the window
         // counting sort of this window's flows by merge owner; a thread keeps
         // its slots' (at most two) owners and hashes in registers
-        static_assert(NS <= 2 * BLOCK, "two slots per thread");
+        constexpr int SPT = (NS + BLOCK - 1) / BLOCK;  // slots per thread
         for (uint32_t o = tid; o <= O; o += BLOCK) s_own[o] = 0;
         lds_barrier();
-        uint32_t own[2] = {NONE32, NONE32}, hh[2] = {0, 0};
-        uint4 kks[2];
+        uint32_t own[SPT], hh[SPT];
+        uint4 kks[SPT];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < SPT; k++) {
+            own[k] = NONE32;
+            hh[k] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < SPT; k++) {
             const uint32_t e = tid + k * BLOCK;
             if (e >= ns || (s_pb[0][e] | s_pb[1][e]) == 0) continue;
             kks[k] = s_key[s_sk[e]];
@@ -794,6 +841,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             atomicAdd(&s_own[own[k]], 1u);
         }
         lds_barrier();
+        if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 4] = wall_clock64();
         // exclusive scans over the owners (one wave each, 4 owners per lane):
         // wave 0 the slot counts, wave 1 the spill counts
         static_assert(MAX_OWNERS <= 256, "4 owners per lane");
@@ -834,6 +882,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             S.sbase[set] = s_sbase;
         }
         lds_barrier();
+        if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 5] = wall_clock64();
         // spilled packets -> owner-grouped segments of this set (the raw
         // records were written by other waves of this workgroup: nontemporal
         // loads, which bypass the CU's L1)
@@ -852,15 +901,16 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             }
         }
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < SPT; k++) {
             const uint32_t e = tid + k * BLOCK;
             if (own[k] == NONE32) continue;
             const unsigned long long p0 = s_pb[0][e], p1 = s_pb[1][e];
             const uint4 kk = kks[k];
             const uint32_t tag = kk.w & 0xFF000000u;
             const uint32_t h = hh[k];
-            const size_t o = (size_t)set * NS + atomicAdd(&s_own[own[k]], 1u);
+            const size_t o = (size_t)set * NS + (FLUERE_FLUSH_LINEAR ? e : atomicAdd(&s_own[own[k]], 1u));
             uint4* dst = reinterpret_cast<uint4*>(S.part + o);
+            if (FLUERE_FLUSH_LINEAR == 2 && kk.x != 0x12345678u) continue;  // diagnostics: no stores
             dst[0] = make_uint4(kk.x, kk.y, kk.z, tag);
             dst[1] = make_uint4(h, (uint32_t)(p0 & 0xFFFF) | ((uint32_t)(p1 & 0xFFFF) << 16), (uint32_t)(p0 >> 32),
                                 (uint32_t)(p1 >> 32));
@@ -874,10 +924,12 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
         }
         lds_barrier();
+        if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 6] = wall_clock64();
         for (uint32_t o = tid; o <= MAX_OWNERS; o += BLOCK) s_scnt[o] = 0;
         if (tid == 0) s_nspill = 0;
         lds_barrier();
         const unsigned long long f1 = clock64() - f0;
+        if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 2] = wall_clock64();
         if (win == 0) cyc_flush0 = f1;
         cyc_flush += f1;
         wbase += stride * WIN_ITERS;
@@ -895,30 +947,117 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     static_assert(PK == 1, "dynamic chunks: one packet per lane per iteration");
     constexpr uint32_t WAVES = BLOCK / 64;
     const uint32_t lane = tid & 63;
+    uint4* slab = s_slab[__builtin_amdgcn_readfirstlane(tid >> 6)];
     auto grab = [&]() {
         uint32_t v = 0;
         if (lane == 0) v = atomicAdd(&s_chunk, 1u);
         return __builtin_amdgcn_readfirstlane(v);
     };
+    // a per-lane zero the compiler cannot see through: keeps the (uniform)
+    // descriptor loads on the vector memory path (vmcnt), so they never hold
+    // up the LDS waits (lgkmcnt) of the processing as a scalar load would
+    uint32_t vzero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     for (uint64_t ws = 0; ws < nsteps; ws += WIN_ITERS) {
         const uint32_t nch = (uint32_t)min<uint64_t>(WIN_ITERS, nsteps - ws) * WAVES;
         auto li_of = [&](uint32_t c) -> uint64_t {
             return beg + (ws + c / WAVES) * stride + (uint64_t)(c % WAVES) * 64 + lane;
         };
+        // descriptor of chunk c (Batch::desc): a vector load, every lane the same word
+        auto desc_of = [&](uint32_t c) -> uint2 {
+            const uint64_t ch = (li_of(c) - lane) >> 6;
+            if (c >= nch || ch >= B.n_desc) return make_uint2(0, 0);
+            return B.desc[ch + vzero];
+        };
+        // Software pipeline, one chunk deep: while chunk c is processed the
+        // loads of the wave's next chunk cn are in flight.  Dense chunks: six
+        // coalesced nontemporal 16-byte loads per lane cover the chunk's span
+        // (64 windows at stride <= 80 B); they are transposed to per-lane
+        // windows through the wave's LDS slab.  Sparse chunks: the record
+        // offsets are loaded one chunk ahead, the windows when processed.
+        // The loads are issued unconditionally (inline asm; a chunk that does
+        // not need them points them at one cached line), so no branch merges
+        // registers that are still being loaded: such a merge makes the
+        // compiler copy them, which waits for them and drains the pipeline.
+        // Their completion is waited for explicitly (vmcnt(0) at the top).
+        u32x4 v[5];
+        uint32_t osp;
+        auto issue = [&](uint32_t c, uint2 d) {
+            const bool dense = d.y != 0;
+            const uint64_t li = min(li_of(c), lastp);
+            const uint8_t* g = dense ? B.bytes + d.x : reinterpret_cast<const uint8_t*>(B.offs + (li & ~63ull));
+            const uint32_t np = dense ? (63u * d.y + 80u + 15u) / 16u : 1u;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const uint8_t* p = g + 16u * min(k * 64u + lane, np - 1u);
+                asm volatile("global_load_dwordx4 %0, %1, off " FLUERE_DENSE_POLICY : "=v"(v[k]) : "v"(p) : "memory");
+            }
+            const uint32_t* po = dense ? B.offs : B.offs + li;
+            asm volatile("global_load_dword %0, %1, off" : "=v"(osp) : "v"(po) : "memory");
+        };
         uint32_t c = grab();
-        uint32_t o1[1] = {B.offs[min(li_of(c), lastp)]};
+        uint2 dc = desc_of(c);
+        dc.x = __builtin_amdgcn_readfirstlane(dc.x);
+        dc.y = __builtin_amdgcn_readfirstlane(dc.y);
+        issue(c, dc);
+        uint32_t cn = grab();
+        uint2 dn_v = desc_of(cn);
         while (c < nch) {
-            const uint32_t cn = grab();
-            const uint32_t on = B.offs[min(li_of(cn), lastp)];
+            const uint32_t c2 = grab();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c's loads (issue) and dn_v
+            const uint2 dn = make_uint2(__builtin_amdgcn_readfirstlane(dn_v.x), __builtin_amdgcn_readfirstlane(dn_v.y));
             Win W[1];
-            load_win(B, o1[0], W[0]);
-            pin_win(W[0]);
+            uint32_t o1[1];
             const uint64_t lis[1] = {li_of(c)};
-            const bool live[1] = {lis[0] < end};
+            bool live[1];
+            if (dc.y) {
+                // two halves of 32 records through a 160-piece slab: half h
+                // needs pieces [2hS, 2hS + 160) of the span, record i its
+                // five pieces at slab byte (i & 31) * S (16-byte aligned)
+                uint4 r[2][5];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t p0 = 2u * h * dc.y;
+#pragma unroll
+                    for (int k = 0; k < 5; k++) {
+                        const uint32_t sl = k * 64u + lane - p0;
+                        if (sl < 160u) slab[sl] = make_uint4(v[k].x, v[k].y, v[k].z, v[k].w);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    const uint4* sp = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(slab) + (lane & 31u) * dc.y);
+#pragma unroll
+                    for (int k = 0; k < 5; k++) r[h][k] = sp[k];
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                }
+                const bool hi = lane >= 32u;
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    W[0].w[4 * k + 0] = hi ? r[1][k].x : r[0][k].x;
+                    W[0].w[4 * k + 1] = hi ? r[1][k].y : r[0][k].y;
+                    W[0].w[4 * k + 2] = hi ? r[1][k].z : r[0][k].z;
+                    W[0].w[4 * k + 3] = hi ? r[1][k].w : r[0][k].w;
+                }
+                o1[0] = dc.x + lane * dc.y;
+                live[0] = true;  // dense chunks are whole
+                pin_win(W[0]);
+            } else {
+                o1[0] = osp;
+                load_win(B, osp, W[0]);
+                live[0] = lis[0] < end;
+                pin_win(W[0]);
+            }
+            // pinned in each branch: after the merge no wait covers the window
+            issue(cn < nch ? cn : c, cn < nch ? dn : make_uint2(0, 0));
+            dn_v = desc_of(c2);
             process(W, o1, lis, live);
             c = cn;
-            o1[0] = on;
+            dc = dn;
+            cn = c2;
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) issue
         flush();
     }
     // sets of windows this workgroup did not have: empty segments
@@ -930,20 +1069,48 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         }
         if (tid == 0) a.S.sbase[set] = 0;
     }
-    // statistics: one global atomic per workgroup
-    atomicAdd(&s_cnt[0], c_valid);
-    atomicAdd(&s_cnt[1], c_drop);
-    atomicAdd(&s_cnt[2], c_miss);
-    if (c_valid) { atomicMin(&s_tmin, tmin); atomicMax(&s_tmax, tmax); }
-    __syncthreads();
+    // statistics: one record per workgroup (plain stores), summed by k_merge_partials
+    if ((tid & 63) == 0 && d_loops && a.dbg) {
+        atomicAdd(&s_cnt[3], (unsigned long long)d_loops);
+        atomicAdd(&s_cnt[4], (unsigned long long)d_iters);
+    }
+    // wave reductions (shuffles), then one LDS atomic per wave and counter (a
+    // 64-bit LDS atomic from every lane compiles to a 64-step lane loop)
+    {
+        uint32_t cv = (uint32_t)c_valid, cd = (uint32_t)c_drop, cm = (uint32_t)c_miss;
+        unsigned long long tn = tmin, tx = tmax;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            cv += __shfl_xor(cv, o, 64);
+            cd += __shfl_xor(cd, o, 64);
+            cm += __shfl_xor(cm, o, 64);
+            tn = min(tn, (unsigned long long)__shfl_xor(tn, o, 64));
+            tx = max(tx, (unsigned long long)__shfl_xor(tx, o, 64));
+        }
+        if ((tid & 63) == 0) {
+            if (cv) atomicAdd(&s_cnt[0], (unsigned long long)cv);
+            if (cd) atomicAdd(&s_cnt[1], (unsigned long long)cd);
+            if (cm) atomicAdd(&s_cnt[2], (unsigned long long)cm);
+            if (cv) { atomicMin(&s_tmin, tn); atomicMax(&s_tmax, tx); }
+        }
+    }
+    lds_barrier();  // LDS only: the flush's stores need not have completed here
     if (tid == 0) {
-        if (s_cnt[0]) atomicAdd(&a.g->valid, s_cnt[0]);
-        if (s_cnt[1]) atomicAdd(&a.g->dropped, s_cnt[1]);
-        if (s_cnt[2]) atomicAdd(&a.g->n_kc_miss, s_cnt[2]);
-        atomicAdd(&a.g->cyc_total, clock64() - cyc_start);
-        atomicAdd(&a.g->cyc_flush, cyc_flush);
-        atomicAdd(&a.g->cyc_flush0, cyc_wait);
-        if (s_cnt[0]) { atomicMin(&a.g->tmin, s_tmin); atomicMax(&a.g->tmax, s_tmax); }
+        unsigned long long* st = a.S.wgs + (size_t)blockIdx.x * WGS_N;
+        st[0] = s_cnt[0];
+        st[1] = s_cnt[1];
+        st[2] = s_cnt[2];
+        st[3] = s_cnt[0] ? s_tmin : NONE64;
+        st[4] = s_cnt[0] ? s_tmax : 0;
+        st[5] = clock64() - cyc_start;
+        st[6] = cyc_flush;
+        st[7] = cyc_wait;
+        if (a.dbg) {
+            const unsigned long long rt_end = wall_clock64();
+            a.dbg[blockIdx.x * 8 + 0] = rt_start;
+            a.dbg[blockIdx.x * 8 + 3] = rt_end;
+            a.dbg[blockIdx.x * 8 + 7] = s_cnt[3] | (s_cnt[4] << 32);  // probe loops | iterations
+        }
     }
 }
 
@@ -1088,6 +1255,31 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __syncthreads();
     const Stage& S = a.S;
     const uint32_t me = blockIdx.x;
+    if (me == 0 && tid < 64) {
+        // the hot kernel's per-workgroup statistics -> the run counters (one wave)
+        unsigned long long v[WGS_N] = {0, 0, 0, NONE64, 0, 0, 0, 0};
+        for (uint32_t w = tid; w < S.n_wg; w += 64) {
+            const unsigned long long* st = S.wgs + (size_t)w * WGS_N;
+#pragma unroll
+            for (int k = 0; k < WGS_N; k++) v[k] = k == 3 ? min(v[k], st[k]) : k == 4 ? max(v[k], st[k]) : v[k] + st[k];
+        }
+#pragma unroll
+        for (int k = 0; k < WGS_N; k++)
+            for (int d = 32; d >= 1; d >>= 1) {
+                const unsigned long long o = __shfl_xor(v[k], d, 64);
+                v[k] = k == 3 ? min(v[k], o) : k == 4 ? max(v[k], o) : v[k] + o;
+            }
+        if (tid == 0) {
+            Glob* g = a.g;
+            if (v[0]) atomicAdd(&g->valid, v[0]);
+            if (v[1]) atomicAdd(&g->dropped, v[1]);
+            if (v[2]) atomicAdd(&g->n_kc_miss, v[2]);
+            if (v[0]) { atomicMin(&g->tmin, v[3]); atomicMax(&g->tmax, v[4]); }
+            atomicAdd(&g->cyc_total, v[5]);
+            atomicAdd(&g->cyc_flush, v[6]);
+            atomicAdd(&g->cyc_flush0, v[7]);
+        }
+    }
     // This owner's segment of every set, flattened: per chunk of MCH sets, an
     // exclusive scan of the segment lengths; threads then take partials from
     // the flattened index space (binary search for the set), so every thread
@@ -1718,7 +1910,8 @@ __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words) 
     __threadfence();
     unsigned long long* w = reinterpret_cast<unsigned long long*>(a.g);
     const size_t nw = sizeof(Ctl) / 8;  // Glob + counters (+ padding)
-    for (size_t i = threadIdx.x; i < nw; i += blockDim.x) w[i] = i == offsetof(Glob, tmin) / 8 ? NONE64 : 0ull;
+    for (size_t i = threadIdx.x; i < nw; i += blockDim.x)
+        w[i] = i == offsetof(Glob, tmin) / 8 ? NONE64 : 0ull;
 }
 
 __global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v) {
@@ -1933,13 +2126,35 @@ unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); 
 
 }  // namespace
 
+// Chunk descriptors (Batch::desc): one wave per chunk of 64 records.  Dense
+// when the offsets are base + i * S with S in {16, 32, 48, 64, 80} and the
+// chunk's span, read as 16-byte pieces from base, lies inside the readable
+// buffer (nbytes + 80, the fluere_add_device_batch contract).
+__global__ void __launch_bounds__(256) k_chunk_desc(const uint32_t* offs, uint64_t nbytes, uint64_t nd, uint2* desc) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t ch = t / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (ch >= nd) return;  // whole waves (blockDim is a multiple of 64)
+    const uint32_t o = offs[ch * 64 + lane];
+    const uint32_t base = __shfl(o, 0, 64), o1 = __shfl(o, 1, 64);
+    const uint32_t S = o1 - base;
+    const bool even = o == base + lane * S;
+    const uint32_t npieces = (63u * S + 80u + 15u) / 16u;
+    const bool dense = __all(even) && S >= 16u && S <= 80u && (S & 15u) == 0 &&
+                       (uint64_t)base + 16ull * npieces <= nbytes + 80ull;
+    if (lane == 0) desc[ch] = make_uint2(base, dense ? S : 0u);
+}
+
 // ===========================================================================
 // host side
 // ===========================================================================
+static unsigned long long* g_hot_dbg = nullptr;  // FLUERE_DEBUG: per-workgroup hot-kernel timestamps
+
 struct HostBatch {
-    Batch b;
+    Batch b{};
     void* own_bytes = nullptr;
     void* own_offs = nullptr;
+    uint2* own_desc = nullptr;  // chunk descriptors (built by upload_batches)
 };
 
 struct fluere_ctx {
@@ -2114,6 +2329,7 @@ static void free_batches(fluere_ctx* c) {
     for (auto& hb : c->batches) {
         if (hb.own_bytes) hipFree(hb.own_bytes);
         if (hb.own_offs) hipFree(hb.own_offs);
+        if (hb.own_desc) hipFree(hb.own_desc);
     }
     c->batches.clear();
     c->n_total = 0;
@@ -2454,6 +2670,17 @@ static int upload_batches(fluere_ctx* c) {
     if (!c->batches_dirty) return FLUERE_OK;
     c->batches_dirty = false;
     int nb = (int)c->batches.size();
+    // chunk descriptors of batches attached since the last pass (index data,
+    // like the offsets: built once per attached batch, from the offsets)
+    for (auto& hb : c->batches) {
+        const uint64_t nd = hb.b.n / 64;
+        if (hb.b.desc || !nd) continue;
+        if (hipMalloc(&hb.own_desc, nd * sizeof(uint2)) != hipSuccess) return FLUERE_E_NOMEM;
+        k_chunk_desc<<<grid_for(nd * 64, 256), 256, 0, c->stream>>>(hb.b.offs, hb.b.nbytes, nd, hb.own_desc);
+        HIPCHECK(hipGetLastError());
+        hb.b.desc = hb.own_desc;
+        hb.b.n_desc = nd;
+    }
     if (nb > c->d_batches_cap) {
         hipFree(c->d_batches);
         c->d_batches = nullptr;
@@ -2507,7 +2734,8 @@ struct PassPlan {
 // Bytes of the hot kernel's staging area for one batch (Stage layout).
 static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n) {
     return cells * sizeof(Part) + ((size_t)grid * SPILL_WG + n) * sizeof(Spill) +
-           2 * sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) + 64;
+           2 * sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) +
+           (size_t)grid * WGS_N * sizeof(unsigned long long) + 64;
 }
 
 static int plan_batches(fluere_ctx* c, PassPlan& P) {
@@ -2527,6 +2755,10 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     }
     a.slow = c->d_slow;
     a.slow_n = &c->d_glob->n_slow;
+    if (getenv("FLUERE_DEBUG")) {
+        if (!g_hot_dbg && hipMalloc(&g_hot_dbg, 4096 * 8 * 8) != hipSuccess) g_hot_dbg = nullptr;
+        a.dbg = g_hot_dbg;
+    }
     // staging for the largest batch (every batch reuses it, in stream order)
     size_t need_max = 0;
     for (auto& hb : c->batches) {
@@ -2568,6 +2800,8 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         S.base = S.sbase + sets;
         S.off = (uint32_t*)(S.base + sets);
         S.soff = S.off + (size_t)(O + 1) * sets;
+        S.wgs = (unsigned long long*)(((uintptr_t)(S.soff + (size_t)(O + 1) * sets) + 7) & ~(uintptr_t)7);
+        S.n_wg = grid;
         S.W = W;
         S.O = O;
         S.n_sets = (uint32_t)sets;
@@ -2723,6 +2957,39 @@ static void debug_counters(fluere_ctx* c) {
             g.n_slow, g.n_kc_miss);
     fprintf(stderr, "[fluere] per-WG clock: total %.0f flush %.0f wait-for-waves %.0f | merge scan %.0f ids %.0f\n",
             g.cyc_total / 256.0, g.cyc_flush / 256.0, g.cyc_flush0 / 256.0, g.cyc_m_scan / 256.0, g.cyc_m_ids / 256.0);
+    if (g_hot_dbg) {
+        // per XCD (workgroup b runs on XCD b % 8): mean / max workgroup time, mean flush, mean end
+        std::vector<unsigned long long> w(256 * 8);
+        if (hipMemcpy(w.data(), g_hot_dbg, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            unsigned long long t0 = ~0ull;
+            for (int b = 0; b < 256; b++) t0 = std::min(t0, w[b * 8]);
+            unsigned long long t1 = 0, smax = 0, loops = 0, iters = 0;
+            for (int b = 0; b < 256; b++) {
+                t1 = std::max(t1, w[b * 8 + 3]);
+                smax = std::max(smax, w[b * 8]);
+                loops += w[b * 8 + 7] & 0xFFFFFFFFull;
+                iters += w[b * 8 + 7] >> 32;
+            }
+            fprintf(stderr, "[fluere] WG starts spread %.1f us, first start -> last end %.1f us; probe loop %llu wave-chunks, %llu iterations\n",
+                    (smax - t0) / 100.0, (t1 - t0) / 100.0, loops, iters);
+            for (int x = 0; x < 8; x++) {
+                double sd = 0, md = 0, sf = 0, se = 0, p1 = 0, p2 = 0, p3 = 0;
+                for (int b = x; b < 256; b += 8) {
+                    const unsigned long long* q = &w[b * 8];
+                    const double d = (q[3] - q[0]) / 100.0;
+                    sd += d; md = std::max(md, d);
+                    sf += (q[2] - q[1]) / 100.0;
+                    se += (q[1] - t0) / 100.0;
+                    p1 += (q[4] - q[1]) / 100.0;
+                    p2 += (q[5] - q[4]) / 100.0;
+                    p3 += (q[6] - q[5]) / 100.0;
+                }
+                fprintf(stderr, "[fluere]   XCD %d: sort %.1f offs %.1f parts %.1f | ", x, p1 / 32, p2 / 32, p3 / 32);
+                fprintf(stderr, "[fluere]   XCD %d: WG mean %.1f max %.1f us, loop end mean %.1f us, flush mean %.1f us\n", x,
+                        sd / 32, md, se / 32, sf / 32);
+            }
+        }
+    }
 }
 
 static int init_glob(fluere_ctx* c) {

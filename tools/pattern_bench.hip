@@ -262,6 +262,134 @@ __global__ void __launch_bounds__(1024) k_interleave(const uint8_t* buf, const u
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+
+// nontemporal variants (global_load ... nt): V0nt streaming ceiling, V1nt lane windows
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(1024) k_stream_nt(const u32x4_t* buf, uint64_t n16, uint32_t* sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        const u32x4_t v = __builtin_nontemporal_load(buf + i);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+// V8: wave per 64 dense records (C2: stride 80, no offsets): five coalesced
+// 1-KiB nt loads, staged through a wave-private LDS slab, lane windows read back
+template <bool NT, int INFL>
+__global__ void __launch_bounds__(1024) k_dense(const uint8_t* buf, uint32_t* sink) {
+    __shared__ uint4 slab[16][320];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nchunk = (N_REC + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * 16;
+    uint32_t acc = 0;
+    for (uint64_t ch = (uint64_t)blockIdx.x * 16 + wv; ch < nchunk; ch += wstride * INFL) {
+        u32x4_t v[INFL][5];
+#pragma unroll
+        for (int j = 0; j < INFL; j++) {
+            const uint64_t cj = min(ch + j * wstride, nchunk - 1);
+            const u32x4_t* g = reinterpret_cast<const u32x4_t*>(buf + HDR + cj * 64 * REC);
+#pragma unroll
+            for (int c = 0; c < 5; c++) v[j][c] = NT ? __builtin_nontemporal_load(g + c * 64 + lane) : g[c * 64 + lane];
+        }
+#pragma unroll
+        for (int j = 0; j < INFL; j++) {
+#pragma unroll
+            for (int c = 0; c < 5; c++) slab[wv][c * 64 + lane] = make_uint4(v[j][c].x, v[j][c].y, v[j][c].z, v[j][c].w);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int c = 0; c < 5; c++) {
+                const uint4 x = slab[wv][lane * 5 + c];
+                acc ^= x.x ^ x.y ^ x.z ^ x.w;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// V9: lane windows (V1/V2) with nontemporal loads; OFFS: offsets read per record
+template <bool OFFS>
+__global__ void __launch_bounds__(1024) k_window_nt(const uint8_t* buf, const uint32_t* offs, uint32_t* sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N_REC; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* p = buf + (OFFS ? __builtin_nontemporal_load(offs + i) : HDR + i * REC);
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            u32x4_t v;
+            // 8-byte aligned record starts: two 8-B nt loads per 16 B
+            typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+            const u32x2_t a0 = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p + 16 * c));
+            const u32x2_t a1 = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p + 16 * c + 8));
+            v.x = a0.x; v.y = a0.y; v.z = a1.x; v.w = a1.y;
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+// V10: lane windows, nt 16-B loads via inline asm (unaligned dwordx4 is legal on gfx950)
+__device__ __forceinline__ uint4 ld_nt16(const void* p) {
+    uint4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+template <bool OFFS>
+__global__ void __launch_bounds__(1024) k_window_nta(const uint8_t* buf, const uint32_t* offs, uint32_t* sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N_REC; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* p = buf + (OFFS ? offs[i] : HDR + i * REC);
+        uint4 v[5];
+#pragma unroll
+        for (int c = 0; c < 5; c++) v[c] = ld_nt16(p + 16 * c);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 5; c++) acc ^= v[c].x ^ v[c].y ^ v[c].z ^ v[c].w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// V11: the hot kernel's intended front end: NW waves per CU, wave per 64 dense
+// records, six coalesced 16-B nt loads per lane (5136-B span incl. the 8-B
+// misalignment of pcap records), the next chunk's loads in flight while the
+// current chunk is transposed through a wave-private LDS slab and processed
+template <int NW, int WORK>
+__global__ void __launch_bounds__(NW * 64) k_dense2(const uint8_t* buf, uint32_t* sink) {
+    __shared__ uint4 slab[NW][321];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nchunk = N_REC / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * NW;
+    uint32_t acc = 0;
+    uint64_t ch = (uint64_t)blockIdx.x * NW + wv;
+    u32x4_t v[6];
+    auto issue = [&](uint64_t c) {
+        const uint64_t off = HDR + min(c, nchunk - 1) * 64 * REC;
+        const u32x4_t* g = reinterpret_cast<const u32x4_t*>(buf + (off & ~15ull));
+#pragma unroll
+        for (int k = 0; k < 5; k++) v[k] = __builtin_nontemporal_load(g + k * 64 + lane);
+        if (lane == 0) v[5] = __builtin_nontemporal_load(g + 320);
+    };
+    issue(ch);
+    for (; ch < nchunk; ch += wstride) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 5; k++) slab[wv][k * 64 + lane] = make_uint4(v[k].x, v[k].y, v[k].z, v[k].w);
+        if (lane == 0) slab[wv][320] = make_uint4(v[5].x, v[5].y, v[5].z, v[5].w);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t rel = (uint32_t)((HDR + ch * 64 * REC) & 15) + lane * REC;
+        const uint2* sp = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(&slab[wv][0]) + rel);
+        uint32_t w[20];
+#pragma unroll
+        for (int c = 0; c < 10; c++) { const uint2 x = sp[c]; w[2 * c] = x.x; w[2 * c + 1] = x.y; }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(ch + wstride);
+        uint32_t x = 0;
+#pragma unroll
+        for (int c = 0; c < 20; c++) x ^= w[c];
+        acc += work<WORK>(x);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 __global__ void k_fill(uint32_t* w, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         w[i] = (uint32_t)(i * 2654435761u) | 1u;
@@ -332,6 +460,48 @@ int main() {
         run(nm, [&] { k_window_work<0><<<g, 1024>>>(buf, offs, sink); });
         snprintf(nm, sizeof nm, "V2w64 g=%d", g);
         run(nm, [&] { k_window_work<64><<<g, 1024>>>(buf, offs, sink); });
+    }
+    for (int g : {256, 512, 1024, 2048}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "V0nt stream g=%d", g);
+        run(nm, [&] { k_stream_nt<<<g, 1024>>>((const u32x4_t*)(buf + 32), N_REC * REC / 16, sink); });
+    }
+    for (int g : {256}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "V8 dense g=%d", g);
+        run(nm, [&] { k_dense<false, 1><<<g, 1024>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V8 dense nt g=%d", g);
+        run(nm, [&] { k_dense<true, 1><<<g, 1024>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V8 dense nt x2 g=%d", g);
+        run(nm, [&] { k_dense<true, 2><<<g, 1024>>>(buf, sink); });
+    }
+    for (int g : {256, 512}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "V9 window nt8 g=%d", g);
+        run(nm, [&] { k_window_nt<false><<<g, 1024>>>(buf, offs, sink); });
+        snprintf(nm, sizeof nm, "V9 window+offs nt8 g=%d", g);
+        run(nm, [&] { k_window_nt<true><<<g, 1024>>>(buf, offs, sink); });
+        snprintf(nm, sizeof nm, "V10 window nt16 g=%d", g);
+        run(nm, [&] { k_window_nta<false><<<g, 1024>>>(buf, offs, sink); });
+        snprintf(nm, sizeof nm, "V10 window+offs nt16 g=%d", g);
+        run(nm, [&] { k_window_nta<true><<<g, 1024>>>(buf, offs, sink); });
+    }
+    for (int g : {256}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "V11 dense2 nw8 w0 g=%d", g);
+        run(nm, [&] { k_dense2<8, 0><<<g, 512>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V11 dense2 nw8 w64 g=%d", g);
+        run(nm, [&] { k_dense2<8, 64><<<g, 512>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V11 dense2 nw8 w128 g=%d", g);
+        run(nm, [&] { k_dense2<8, 128><<<g, 512>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V11 dense2 nw16 w0 g=%d", g);
+        run(nm, [&] { k_dense2<16, 0><<<g, 1024>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V11 dense2 nw16 w64 g=%d", g);
+        run(nm, [&] { k_dense2<16, 64><<<g, 1024>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V11 dense2 nw16 w128 g=%d", g);
+        run(nm, [&] { k_dense2<16, 128><<<g, 1024>>>(buf, sink); });
+        snprintf(nm, sizeof nm, "V11 dense2 nw4 w0 g=%d", g);
+        run(nm, [&] { k_dense2<4, 0><<<g, 256>>>(buf, sink); });
     }
     return 0;
 }
