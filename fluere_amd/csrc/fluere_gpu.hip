@@ -1867,7 +1867,19 @@ struct CleanArgs {
     uint8_t* complex;
     uint8_t* active;
     Glob* g;
+    // speculative cleanup (enqueued right behind a run's counter copy): clear
+    // only if the run needs no further device work -- no table error, no
+    // complex flow, no expiry inside the capture (Mode B), records fitted.
+    // fluere_run takes the same decision on the host from the copied counters.
+    int spec;
+    unsigned long long timeout_us, recs_cap;
 };
+
+__device__ __host__ __forceinline__ bool run_complete(const Glob& g, uint32_t err, unsigned long long timeout_us,
+                                                      unsigned long long recs_cap) {
+    const bool modeB = g.valid && (g.tmax - g.tmin) >= timeout_us;
+    return !(err & (ERR_TABLE_FULL | ERR_SPIN | ERR_FLOWS_FULL)) && !modeB && g.n_complex == 0 && g.n_rec <= recs_cap;
+}
 
 __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool tables) {
     for (int t = 0; t < N_TABLES; t++) {
@@ -1893,6 +1905,7 @@ __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool
 // n_flows, err): every other workgroup has read n_flows / err before it
 // counted itself done, so nobody can see the reset early.
 __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words) {
+    if (a.spec && !run_complete(*a.g, *a.T.err, a.timeout_us, a.recs_cap)) return;  // every workgroup decides alike
     const bool failed = (*a.T.err & (ERR_TABLE_FULL | ERR_SPIN)) != 0;
     const uint32_t nf = failed ? a.T.fmax : min(*a.T.n_flows, a.T.fmax);
     const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2194,7 +2207,10 @@ struct fluere_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the last k_parse_agg launch
     hipEvent_t evk_first = nullptr;             // before the first k_parse_agg launch of the pass
+    hipEvent_t ev_ctl = nullptr;                // after a run's counter copy (the speculative cleanup follows)
+    uint64_t last_nf = 0;                       // flows of the last completed run (sizing only)
     bool pass_in_run = false;
+    bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
     int plan_nb = 0;                            // batches of the last pass
     double last_run_ms = 0;                     // host wall time of the last fluere_run
     // hipGraph of the last fluere_run pass, replayed while the plan is unchanged
@@ -2300,7 +2316,8 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
-        hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess)
+        hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess ||
+        hipEventCreate(&c->ev_ctl) != hipSuccess)
         return fail(FLUERE_E_HIP);
     // initial state: every table EMPTY, accumulators at their identities
     hipStream_t s = c->stream;
@@ -2359,6 +2376,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     if (c->evk0) hipEventDestroy(c->evk0);
     if (c->evk1) hipEventDestroy(c->evk1);
     if (c->evk_first) hipEventDestroy(c->evk_first);
+    if (c->ev_ctl) hipEventDestroy(c->ev_ctl);
     if (c->graph) hipGraphExecDestroy(c->graph);
     free(c->graph_plan);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -2724,6 +2742,10 @@ struct PassPlan {
     unsigned agg_grid[PLAN_BATCHES];
     uint32_t owners[PLAN_BATCHES];
     int macs, abl;
+    int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
+    int spec;      // 1: a speculative k_cleanup follows the counter copy (ev_ctl marks the copy)
+    CleanArgs spec_ca;
+    unsigned spec_grid;
     int finalize;  // fluere_run: k_finalize + counters copy
     FinArgs fa;
     unsigned fin_grid;
@@ -2826,6 +2848,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
                        ? flow_grid(c)
                        : (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(1, grid_for(c->prev_nf, 256)));
     P.tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
+    P.clean = c->precleaned ? 0 : 1;
     if ((rc = plan_batches(c, P))) return rc;
     static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
     P.macs = c->use_mac;
@@ -2839,6 +2862,14 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
         P.fa = FinArgs{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob,
                        c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
         P.fin_grid = flow_grid(c);
+        P.spec_ca = P.ca;
+        P.spec_ca.spec = 1;
+        P.spec_ca.timeout_us = c->timeout_ms * 1000ull;
+        P.spec_ca.recs_cap = c->d_recs_cap;
+        // grid-stride over the device flow count: any grid is correct; size it
+        // for the last known flow count
+        const uint64_t guess = c->last_nf ? c->last_nf : c->fmax;
+        P.spec_grid = (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(8, grid_for(guess, 256)));
     }
     return FLUERE_OK;
 }
@@ -2865,12 +2896,17 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
 
 static int enqueue_pass(fluere_ctx* c, const PassPlan& P) {
     hipStream_t s = c->stream;
-    k_cleanup<<<P.clean_grid, 256, 0, s>>>(P.ca, P.tab_words);
+    if (P.clean) k_cleanup<<<P.clean_grid, 256, 0, s>>>(P.ca, P.tab_words);
+    c->precleaned = false;
     int rc;
     if ((rc = enqueue_batches(c, P))) return rc;
     if (P.finalize) {
         k_finalize<<<P.fin_grid, 256, 0, s>>>(P.fa);
         HIPCHECK(hipMemcpyAsync(P.h_ctl, P.d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+        if (P.spec) {
+            HIPCHECK(hipEventRecord(c->ev_ctl, s));
+            k_cleanup<<<P.spec_grid, 256, 0, s>>>(P.spec_ca, P.tab_words);
+        }
     }
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
@@ -2904,7 +2940,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
         prev = n;
     };
     void* a_clean[] = {&P.ca, &P.tab_words};
-    kernel((const void*)k_cleanup, P.clean_grid, 256, a_clean);
+    if (P.clean) kernel((const void*)k_cleanup, P.clean_grid, 256, a_clean);
     void* a_agg[PLAN_BATCHES][1];
     for (int i = 0; i < P.nb && ok; i++) {
         if (i > 0) {
@@ -2948,10 +2984,11 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
 // First-batch start event of the last pass (evk0 itself for one batch).
 static hipEvent_t pass_start_event(fluere_ctx* c) { return c->plan_nb > 1 ? c->evk_first : c->evk0; }
 
-static void debug_counters(fluere_ctx* c) {
+static void debug_counters(fluere_ctx* c, const Glob* have = nullptr) {
     if (!getenv("FLUERE_DEBUG")) return;  // diagnostics only: synchronises the stream
     Glob g;
-    if (hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return;
+    if (have) g = *have;
+    else if (hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return;
     fprintf(stderr, "[fluere] valid %llu dropped %llu slow %llu LDS-table overflow packets %llu\n", g.valid, g.dropped,
             g.n_slow, g.n_kc_miss);
@@ -3019,6 +3056,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     P.macs = c->use_mac;
     P.abl = abl;
     c->plan_nb = P.nb;
+    c->precleaned = false;
     rc = enqueue_batches(c, P);
     debug_counters(c);
     return rc;
@@ -3080,7 +3118,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     static const bool want_graph = getenv("FLUERE_GRAPH") != nullptr && getenv("FLUERE_DEBUG") == nullptr;
     const bool use_graph = want_graph && !c->graph_off && P.nb <= PLAN_BATCHES;
     if (P.nb > PLAN_BATCHES) {  // more batches than a plan holds: direct launches, in chunks
-        k_cleanup<<<P.clean_grid, 256, 0, s>>>(P.ca, P.tab_words);
+        if (P.clean) k_cleanup<<<P.clean_grid, 256, 0, s>>>(P.ca, P.tab_words);
+        c->precleaned = false;
         std::vector<HostBatch> all = c->batches;
         for (size_t i = 0; i < all.size(); i += PLAN_BATCHES) {
             c->batches.assign(all.begin() + i, all.begin() + std::min(all.size(), i + PLAN_BATCHES));
@@ -3109,20 +3148,42 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
                 c->graph_off = 1;
             }
         }
-        if (c->graph) HIPCHECK(hipGraphLaunch(c->graph, s));
-        else if ((rc = enqueue_pass(c, P))) return rc;
+        if (c->graph) {
+            HIPCHECK(hipGraphLaunch(c->graph, s));
+            c->precleaned = false;
+        } else if ((rc = enqueue_pass(c, P))) return rc;
     } else {
+        P.spec = 1;
         if ((rc = enqueue_pass(c, P))) return rc;
     }
     c->prev_nf = ~0ull;  // the pass cleared the flows: unknown until the fetch below
     Glob g;
     uint32_t nf_err[2];
-    HIPCHECK(hipStreamSynchronize(s));
+    const auto t_enq = std::chrono::steady_clock::now();
+    if (P.spec) {
+        // poll the copy's event: a blocking wait adds ~15 us of wake-up
+        // latency to every run (FLUERE_BLOCKING_WAIT=1 restores it)
+        static const bool blocking = getenv("FLUERE_BLOCKING_WAIT") != nullptr;
+        if (blocking) HIPCHECK(hipEventSynchronize(c->ev_ctl));
+        else {
+            hipError_t q;
+            while ((q = hipEventQuery(c->ev_ctl)) == hipErrorNotReady) {
+            }
+            HIPCHECK(q);
+        }
+    } else {
+        HIPCHECK(hipStreamSynchronize(s));
+    }
+    const auto t_sync = std::chrono::steady_clock::now();
     g = c->h_ctl->g;
     nf_err[0] = c->h_ctl->n_flows;
     nf_err[1] = c->h_ctl->err;
     c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
-    debug_counters(c);
+    // the speculative cleanup behind the copy clears the flows exactly when
+    // the run needs no more device work (the same test, on the same counters)
+    const bool spec_cleared = P.spec && run_complete(g, nf_err[1], P.spec_ca.timeout_us, P.spec_ca.recs_cap);
+    if (spec_cleared) c->last_nf = nf_err[0];
+    debug_counters(c, &g);
     FinArgs fa = P.fa;
     if (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) return FLUERE_E_TABLE_FULL;
     if (nf_err[1] & ERR_FLOWS_FULL) return FLUERE_E_TABLE_FULL;
@@ -3259,6 +3320,22 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     out.total_ms = ms_total;
     out.updates = updates;
     if (st) *st = out;
+    // The run's per-flow state is not needed any more (records are kept in
+    // d_recs): clear it now, asynchronously, so the next pass starts with the
+    // hot kernel and the cleanup overlaps the caller's turnaround.
+    if (spec_cleared || clear_flows(c) == FLUERE_OK) {
+        c->precleaned = true;
+        c->prev_nf = 0;
+    }
+    static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
+    if (hostprof) {
+        static auto t_prev_exit = std::chrono::steady_clock::now();
+        const auto t_exit = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[fluere] host: since last exit %.1f | plan+enqueue %.1f | sync wait %.1f | after sync %.1f us\n",
+                us(t_prev_exit, t_run0), us(t_run0, t_enq), us(t_enq, t_sync), us(t_sync, t_exit));
+        t_prev_exit = t_exit;
+    }
     return g.raw ? FLUERE_E_UNSUPPORTED : FLUERE_OK;
 }
 
@@ -3372,6 +3449,7 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     hipStream_t s = c->stream;
     int rc;
     if ((rc = clear_flows(c))) return rc;
+    c->precleaned = false;
     if (!c->d_pay && hipMalloc(&c->d_pay, (size_t)c->fmax * sizeof(FirstPay)) != hipSuccess) return FLUERE_E_NOMEM;
     if (std::max<uint64_t>(n, 1) > c->d_sd_cap) {
         hipFree(c->d_sd);
