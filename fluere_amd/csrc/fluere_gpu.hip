@@ -25,6 +25,7 @@
 // / tos / first taken from the first packet and `last` from the last one
 // (offline_fluereflows.rs:97-157, flows.rs:11-42).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <fcntl.h>
@@ -1286,7 +1287,8 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // has about (partials / MB) of them with all their loads in flight.
     // Pass 0 takes the staged partials, pass 1 the spilled packets (each a
     // one-packet partial), through the same per-owner segment machinery.
-    for (int pass = 0; pass < 2; pass++)
+    const int passes = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 2 : 1;  // no spills: one pass
+    for (int pass = 0; pass < passes; pass++)
     for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
         const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
         const uint32_t* offs = pass ? S.soff : S.off;
@@ -1467,7 +1469,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         f.la = m_la[e];
         part_to_global(a.A, d, f);
     }
-    if (tid == 0) {
+    if (tid == 0 && a.dbg) {  // diagnostics: contended atomics, debug runs only
         atomicAdd(&a.g->cyc_m_scan, c1 - c0);
         atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
     }
@@ -2879,15 +2881,18 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
     for (int i = 0; i < P.nb; i++) {
         const AggArgs& a = P.agg[i];
         if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 16, s));  // n_slow, n_spill (k_cleanup zeroed them for batch 0)
-        if (i == 0 && P.nb > 1) HIPCHECK(hipEventRecord(c->evk_first, s));
-        HIPCHECK(hipEventRecord(c->evk0, s));
         const unsigned grid = P.agg_grid[i];
-        if (P.macs) k_parse_agg<0, true><<<grid, BLOCK, 0, s>>>(a);
-        else if (P.abl == 1) k_parse_agg<1, false><<<grid, BLOCK, 0, s>>>(a);
-        else if (P.abl == 2) k_parse_agg<2, false><<<grid, BLOCK, 0, s>>>(a);
-        else if (P.abl == 3) k_parse_agg<3, false><<<grid, BLOCK, 0, s>>>(a);
-        else k_parse_agg<0, false><<<grid, BLOCK, 0, s>>>(a);
-        HIPCHECK(hipEventRecord(c->evk1, s));
+        const void* fn = P.macs ? (const void*)k_parse_agg<0, true>
+                         : P.abl == 1 ? (const void*)k_parse_agg<1, false>
+                         : P.abl == 2 ? (const void*)k_parse_agg<2, false>
+                         : P.abl == 3 ? (const void*)k_parse_agg<3, false>
+                                      : (const void*)k_parse_agg<0, false>;
+        // HIP events carried by the dispatch itself (start / stop timestamps of
+        // the hot kernel): separate event markers would each add a gap to the
+        // stream.  The first batch of a multi-batch pass starts evk_first.
+        void* args[] = {const_cast<AggArgs*>(&a)};
+        HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, (i == 0 && P.nb > 1) ? c->evk_first : c->evk0,
+                                    c->evk1, 0));
         k_merge_partials<<<P.owners[i], MB, 0, s>>>(a);  // + the slow list
     }
     HIPCHECK(hipGetLastError());
