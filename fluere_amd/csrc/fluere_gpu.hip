@@ -1242,6 +1242,20 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint32_t m_lo[MCH], m_start[MCH], m_scan[MB / 64 + 1];
     const int tid = threadIdx.x;
     const unsigned long long c0 = clock64();
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 0] = wall_clock64();
+    // loads issued before the LDS initialisation (their latency overlaps it):
+    // this owner's segment bounds of the first set chunk, and the run counters
+    const uint32_t me = blockIdx.x;
+    uint32_t pre_lo[MCH / MB], pre_hi[MCH / MB];
+#pragma unroll
+    for (int q = 0; q < MCH / MB; q++) {
+        const uint32_t set = tid * (MCH / MB) + q;
+        const bool in = set < a.S.n_sets;
+        pre_lo[q] = in ? a.S.off[(size_t)me * a.S.n_sets + set] : 0;
+        pre_hi[q] = in ? a.S.off[(size_t)(me + 1) * a.S.n_sets + set] : 0;
+    }
+    const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int e = tid; e < MT; e += MB) {
         m_key[e] = make_uint4(0, 0, 0, 0);
         m_pk[0][e] = m_pk[1][e] = 0;
@@ -1254,9 +1268,9 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         m_la[e] = 0;
     }
     __syncthreads();
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 1] = wall_clock64();
     const Stage& S = a.S;
-    const uint32_t me = blockIdx.x;
-    if (me == 0 && tid < 64) {
+    auto reduce_stats = [&]() {
         // the hot kernel's per-workgroup statistics -> the run counters (one wave)
         unsigned long long v[WGS_N] = {0, 0, 0, NONE64, 0, 0, 0, 0};
         for (uint32_t w = tid; w < S.n_wg; w += 64) {
@@ -1280,14 +1294,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             atomicAdd(&g->cyc_flush, v[6]);
             atomicAdd(&g->cyc_flush0, v[7]);
         }
-    }
+    };
     // This owner's segment of every set, flattened: per chunk of MCH sets, an
     // exclusive scan of the segment lengths; threads then take partials from
     // the flattened index space (binary search for the set), so every thread
     // has about (partials / MB) of them with all their loads in flight.
     // Pass 0 takes the staged partials, pass 1 the spilled packets (each a
     // one-packet partial), through the same per-owner segment machinery.
-    const int passes = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 2 : 1;  // no spills: one pass
+    const int passes = n_spill_all ? 2 : 1;  // no spills: one pass
     for (int pass = 0; pass < passes; pass++)
     for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
         const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
@@ -1297,7 +1311,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         for (int q = 0; q < MCH / MB; q++) {
             const uint32_t set = c0s + tid * (MCH / MB) + q;
             uint32_t lo = 0, hi = 0;
-            if (set < c0s + nset) {
+            if (pass == 0 && c0s == 0) {  // prefetched
+                lo = pre_lo[q];
+                hi = pre_hi[q];
+            } else if (set < c0s + nset) {
                 lo = offs[(size_t)me * S.n_sets + set];
                 hi = offs[(size_t)(me + 1) * S.n_sets + set];
             }
@@ -1313,6 +1330,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         }
         __syncthreads();
         const uint32_t total = m_scan[MB / 64];
+        if (a.dbg && tid == 0 && c0s == 0 && pass == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 2] = wall_clock64();
         for (uint32_t idx = tid; idx < total; idx += MB) {
             uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
             while (lo_i < hi_i) {
@@ -1391,6 +1409,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // of its keys, so a claim (EMPTY -> PENDING) normally succeeds at once;
     // the new ids of the whole workgroup come from ONE atomicAdd on the flow
     // counter (a single hot address: per-flow increments would serialise).
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 3] = wall_clock64();
     static_assert(MT == MB, "one merge entry per thread");
     if (tid == 0) m_nclaim = 0;
     __syncthreads();
@@ -1424,8 +1443,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         }
     }
     __syncthreads();
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 7] = wall_clock64();
     if (tid == 0) m_base = m_nclaim ? atomicAdd(a.T.n_flows, m_nclaim) : 0;
     __syncthreads();
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 6] = wall_clock64();
     if (claimed) {
         d = m_base + rank;
         if (d >= a.T.fmax) {
@@ -1452,6 +1473,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(16);
     }
     if (wait) atomicOr(a.T.err, ERR_SPIN);
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 4] = wall_clock64();
     if (have && d != FAIL && d < a.T.fmax) {
         FlowPart f;
 #pragma unroll
@@ -1469,11 +1491,16 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         f.la = m_la[e];
         part_to_global(a.A, d, f);
     }
+    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 5] = wall_clock64();
     if (tid == 0 && a.dbg) {  // diagnostics: contended atomics, debug runs only
         atomicAdd(&a.g->cyc_m_scan, c1 - c0);
         atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
     }
-    slow_packets(a, (unsigned long long)blockIdx.x * blockDim.x + tid, (unsigned long long)gridDim.x * blockDim.x);
+    // the hot kernel's per-workgroup statistics -> the run counters (one wave
+    // of the last workgroup, off the other owners' critical path)
+    if (me == gridDim.x - 1 && tid < 64) reduce_stats();
+    if (n_slow_all)
+        slow_packets(a, (unsigned long long)blockIdx.x * blockDim.x + tid, (unsigned long long)gridDim.x * blockDim.x);
 }
 
 // The packets the hot kernel left to the general parser (IPv6, IPv4 options,
@@ -3014,6 +3041,23 @@ static void debug_counters(fluere_ctx* c, const Glob* have = nullptr) {
             }
             fprintf(stderr, "[fluere] WG starts spread %.1f us, first start -> last end %.1f us; probe loop %llu wave-chunks, %llu iterations\n",
                     (smax - t0) / 100.0, (t1 - t0) / 100.0, loops, iters);
+            {
+                // merge kernel phases (owner workgroups 0..255), mean us from its first start
+                std::vector<unsigned long long> m(256 * 8);
+                if (hipMemcpy(m.data(), g_hot_dbg + 4096 * 8 - 2048, m.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                    unsigned long long m0 = ~0ull;
+                    for (int b = 0; b < 256; b++) m0 = std::min(m0, m[b * 8]);
+                    double ph[8] = {0}, mx[8] = {0};
+                    for (int b = 0; b < 256; b++)
+                        for (int k = 0; k < 8; k++) {
+                            ph[k] += (m[b * 8 + k] - m0) / 100.0 / 256;
+                            mx[k] = std::max(mx[k], (m[b * 8 + k] - m0) / 100.0);
+                        }
+                    fprintf(stderr, "[fluere] merge phases (mean/max us): init %.1f/%.1f offs+scan %.1f/%.1f parts %.1f/%.1f "
+                            "claims %.1f/%.1f n_flows %.1f/%.1f ids %.1f/%.1f global %.1f/%.1f\n",
+                            ph[1], mx[1], ph[2], mx[2], ph[3], mx[3], ph[7], mx[7], ph[6], mx[6], ph[4], mx[4], ph[5], mx[5]);
+                }
+            }
             for (int x = 0; x < 8; x++) {
                 double sd = 0, md = 0, sf = 0, se = 0, p1 = 0, p2 = 0, p3 = 0;
                 for (int b = x; b < 256; b += 8) {
