@@ -108,6 +108,7 @@ struct Glob {
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
     unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
     unsigned long long clean_done;                        // k_cleanup: workgroups finished
+    unsigned long long fin_done;                          // k_finalize: workgroups finished
 };
 static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8, "n_slow, n_spill are reset together");
 // One device allocation holds Glob and the dictionary counters right after it
@@ -115,7 +116,8 @@ static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8, "n_slow, n_
 struct Ctl {
     Glob g;
     uint32_t n_flows, err;
-    uint32_t pad[14];
+    uint32_t seq;  // host copy only: k_finalize's last workgroup writes the run's number here last
+    uint32_t pad[13];
 };
 
 #define HIPCHECK(x)                                                                                  \
@@ -1544,6 +1546,8 @@ struct FinArgs {
     uint8_t* complex;
     int macs;
     uint64_t out_cap;
+    Ctl* host_ctl;   // non-null: the last workgroup writes the run counters to this pinned host copy,
+    uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
 };
 
 // Append one record (Mode A paths): position, updates and ended counters.
@@ -1660,6 +1664,29 @@ __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
                 atomicAdd(&a.g->n_complex_pkts, pk);
             }
         }
+    }
+    if (!a.host_ctl) return;
+    // the last workgroup to finish copies the run counters (Glob, n_flows,
+    // err) to the pinned host copy and then publishes the run's number
+    __shared__ unsigned long long f_rank;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        f_rank = atomicAdd(&a.g->fin_done, 1ull);
+    }
+    __syncthreads();
+    if (f_rank != gridDim.x - 1) return;
+    __threadfence();
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.g);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.host_ctl);
+    constexpr uint32_t nw = offsetof(Ctl, seq) / 4;
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x)
+        __hip_atomic_store(dst + i, __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&a.host_ctl->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2240,6 +2267,7 @@ struct fluere_ctx {
     uint64_t last_nf = 0;                       // flows of the last completed run (sizing only)
     bool pass_in_run = false;
     bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
+    uint32_t run_seq = 0;                       // number of the last run that publishes its counters (Ctl::seq)
     int plan_nb = 0;                            // batches of the last pass
     double last_run_ms = 0;                     // host wall time of the last fluere_run
     // hipGraph of the last fluere_run pass, replayed while the plan is unchanged
@@ -2341,6 +2369,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     if (hipMalloc(&c->d_glob, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     c->d_nflows = &reinterpret_cast<Ctl*>(c->d_glob)->n_flows;
     if (hipHostMalloc(&c->h_ctl, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    memset(c->h_ctl, 0, sizeof(Ctl));
     if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -2772,7 +2801,7 @@ struct PassPlan {
     uint32_t owners[PLAN_BATCHES];
     int macs, abl;
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
-    int spec;      // 1: a speculative k_cleanup follows the counter copy (ev_ctl marks the copy)
+    int spec;      // 1: k_finalize publishes the counters to the host itself, a speculative k_cleanup follows
     CleanArgs spec_ca;
     unsigned spec_grid;
     int finalize;  // fluere_run: k_finalize + counters copy
@@ -2934,10 +2963,12 @@ static int enqueue_pass(fluere_ctx* c, const PassPlan& P) {
     if ((rc = enqueue_batches(c, P))) return rc;
     if (P.finalize) {
         k_finalize<<<P.fin_grid, 256, 0, s>>>(P.fa);
-        HIPCHECK(hipMemcpyAsync(P.h_ctl, P.d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, s));
         if (P.spec) {
-            HIPCHECK(hipEventRecord(c->ev_ctl, s));
+            // k_finalize's last workgroup writes the counters to the pinned
+            // host copy and publishes P.fa.seq; the speculative cleanup follows
             k_cleanup<<<P.spec_grid, 256, 0, s>>>(P.spec_ca, P.tab_words);
+        } else {
+            HIPCHECK(hipMemcpyAsync(P.h_ctl, P.d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, s));
         }
     }
     HIPCHECK(hipGetLastError());
@@ -3203,6 +3234,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         } else if ((rc = enqueue_pass(c, P))) return rc;
     } else {
         P.spec = 1;
+        P.fa.host_ctl = c->h_ctl;
+        P.fa.seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
         if ((rc = enqueue_pass(c, P))) return rc;
     }
     c->prev_nf = ~0ull;  // the pass cleared the flows: unknown until the fetch below
@@ -3210,15 +3243,19 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     uint32_t nf_err[2];
     const auto t_enq = std::chrono::steady_clock::now();
     if (P.spec) {
-        // poll the copy's event: a blocking wait adds ~15 us of wake-up
-        // latency to every run (FLUERE_BLOCKING_WAIT=1 restores it)
-        static const bool blocking = getenv("FLUERE_BLOCKING_WAIT") != nullptr;
-        if (blocking) HIPCHECK(hipEventSynchronize(c->ev_ctl));
-        else {
-            hipError_t q;
-            while ((q = hipEventQuery(c->ev_ctl)) == hipErrorNotReady) {
+        // poll the run number k_finalize publishes in the pinned host copy
+        // (a blocking wait would add ~15 us of wake-up latency to every run);
+        // now and then ask whether the stream failed instead
+        volatile uint32_t* seqp = &c->h_ctl->seq;
+        for (uint32_t spin = 1;; spin++) {
+            if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == P.fa.seq) break;
+            if ((spin & 1023) == 0) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q == hipErrorNotReady) continue;
+                if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == P.fa.seq) break;
+                HIPCHECK(q);
+                return FLUERE_E_HIP;  // the stream finished without publishing: cannot happen
             }
-            HIPCHECK(q);
         }
     } else {
         HIPCHECK(hipStreamSynchronize(s));
@@ -3234,6 +3271,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     if (spec_cleared) c->last_nf = nf_err[0];
     debug_counters(c, &g);
     FinArgs fa = P.fa;
+    fa.host_ctl = nullptr;  // re-launches below read the counters back with copies
     if (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) return FLUERE_E_TABLE_FULL;
     if (nf_err[1] & ERR_FLOWS_FULL) return FLUERE_E_TABLE_FULL;
     uint32_t nf = std::min(nf_err[0], c->fmax);
