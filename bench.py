@@ -74,7 +74,11 @@ def main():
     # synthetic capture generated directly in HBM (untimed)
     b, o, nbytes = fluere_amd.synth_device(cfg, first, n)
     torch.cuda.synchronize()
-    ctx = fluere_amd.FlowContext(use_mac=C["use_mac"], max_flows=max(1 << 16, 2 * C["flows"]), device=local)
+    # N > 1: the context runs on torch's stream, so the collective of the
+    # shard exchange is ordered after the export without a host wait
+    ctx = fluere_amd.FlowContext(use_mac=C["use_mac"], max_flows=max(1 << 16, 2 * C["flows"]), device=local,
+                                 stream=torch.cuda.current_stream().cuda_stream if world > 1 else None)
+    exchange = fdist.ShardExchange(ctx) if world > 1 else None
     fdist.set_index_base(ctx, first)
     ctx.add_device_batch(b, nbytes, o, n)
 
@@ -85,10 +89,9 @@ def main():
             # parse + key + aggregate + finalize; the records stay in HBM
             st = ctx.run()
         else:
-            # per-shard aggregation, then the flow-table merge: RCCL all_gather
-            # of per-flow summaries + device merge/finalize on rank 0
-            s, lo, hi = fdist.export_summaries(ctx)
-            st = fdist.gather_and_merge(ctx, s, lo, hi)
+            # per-shard aggregation, then the flow-table merge: one RCCL
+            # all_gather of the shard blocks + device merge/finalize on rank 0
+            st = exchange.step()
         # HIP events around k_parse_agg on the context stream (fluere_stats.parse_ms)
         kernel_ms.append(st["parse_ms"] if world == 1 else ctx.last_kernel_ms())
         pass_ms.append(st["total_ms"] if world == 1 else ctx.last_pass_ms())

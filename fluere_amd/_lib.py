@@ -89,6 +89,7 @@ SUMMARY_DTYPE = np.dtype([
     ("first_dport", "<u2"), ("first_dir", "u1"), ("first_prot", "u1"), ("first_tos", "u1"), ("pad0", "u1"),
     ("pad1", "<u4"), ("pad2", "<u4"),
 ])
+SHARD_HEADER_BYTES = 64  # fluere_shard_header
 SUMMARY_BYTES = SUMMARY_DTYPE.itemsize  # struct fluere_flow_summary
 assert SUMMARY_BYTES == 192
 
@@ -137,6 +138,9 @@ def lib() -> ctypes.CDLL:
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),
         "fluere_export_summaries": (I, [P, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "fluere_merge_summaries": (I, [P, P, U64, U64, U64, ctypes.POINTER(Stats)]),
+        "fluere_shard_block_bytes": (U64, [U64]),
+        "fluere_export_device": (I, [P, P, U64]),
+        "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, ctypes.POINTER(Stats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -32,7 +32,7 @@ constexpr int N_TABLES = 14;        // 0,1: IPv4 fast chain; 2..13: generic leve
 constexpr int MAX_PROBE = 4096;
 constexpr uint32_t FAIL = 0xFFFFFFFFu;
 
-enum : uint32_t { ERR_TABLE_FULL = 1, ERR_FLOWS_FULL = 2, ERR_SPIN = 4 };
+enum : uint32_t { ERR_TABLE_FULL = 1, ERR_FLOWS_FULL = 2, ERR_SPIN = 4, ERR_CAPACITY = 8 };
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

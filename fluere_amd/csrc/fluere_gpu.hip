@@ -51,6 +51,7 @@ using namespace fl;
 static_assert(sizeof(fluere_record) == 152, "fluere_record ABI");
 static_assert(sizeof(fluere_pkt_meta) == 128, "fluere_pkt_meta ABI");
 static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
+static_assert(sizeof(fluere_shard_header) == 64, "fluere_shard_header ABI");
 
 namespace {
 
@@ -1647,6 +1648,32 @@ __device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluer
 
 // one thread per flow, grid-stride (uniform per workgroup) over the
 // device-side flow count
+// The last workgroup to finish (counter *done) copies the run counters (Glob,
+// n_flows, err) to the pinned host copy, then publishes seq there (the host
+// polls it: no copy kernel, no event on the way back).
+__device__ void publish_ctl(Glob* g, unsigned long long* done, Ctl* host_ctl, uint32_t seq) {
+    __shared__ unsigned long long p_rank;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        p_rank = atomicAdd(done, 1ull);
+    }
+    __syncthreads();
+    if (p_rank != gridDim.x - 1) return;
+    __threadfence();
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(host_ctl);
+    constexpr uint32_t nw = offsetof(Ctl, seq) / 4;
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x)
+        __hip_atomic_store(dst + i, __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&host_ctl->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
     const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
@@ -1665,29 +1692,7 @@ __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
             }
         }
     }
-    if (!a.host_ctl) return;
-    // the last workgroup to finish copies the run counters (Glob, n_flows,
-    // err) to the pinned host copy and then publishes the run's number
-    __shared__ unsigned long long f_rank;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        f_rank = atomicAdd(&a.g->fin_done, 1ull);
-    }
-    __syncthreads();
-    if (f_rank != gridDim.x - 1) return;
-    __threadfence();
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.g);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(a.host_ctl);
-    constexpr uint32_t nw = offsetof(Ctl, seq) / 4;
-    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x)
-        __hip_atomic_store(dst + i, __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        __hip_atomic_store(&a.host_ctl->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -2087,6 +2092,25 @@ __global__ void __launch_bounds__(256) k_export(FinArgs a, fluere_flow_summary* 
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) export_one(a, out, d);
 }
 
+// Shard block export (fluere_export_device): header + min(n_flows, cap) summaries.
+__global__ void __launch_bounds__(256) k_export_block(FinArgs a, uint8_t* blk, uint64_t cap) {
+    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    fluere_flow_summary* out = reinterpret_cast<fluere_flow_summary*>(blk + sizeof(fluere_shard_header));
+    const uint32_t ne = (uint32_t)min<uint64_t>(nf, cap);
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ne; d += gridDim.x * blockDim.x) export_one(a, out, d);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        fluere_shard_header h{};
+        h.n_flows = nf;
+        h.tmin = a.g->tmin;
+        h.tmax = a.g->tmax;
+        h.valid = a.g->valid;
+        h.dropped = a.g->dropped;
+        h.raw = a.g->raw;
+        h.err = *a.T.err;
+        *reinterpret_cast<fluere_shard_header*>(blk) = h;
+    }
+}
+
 struct MergeArgs {
     TableSet T;
     Acc A;
@@ -2098,12 +2122,45 @@ struct MergeArgs {
     fluere_record* out;
     uint8_t* complex;
     uint64_t out_cap;
+    // gathered blocks (fluere_merge_gathered): summary i is entry i % cap of
+    // block i / cap; entries past the block's n_flows are skipped
+    const uint8_t* blocks;
+    unsigned long long cap, block_bytes;
+    Ctl* host_ctl;   // non-null: k_merge_finalize publishes the counters (publish_ctl)
+    uint32_t seq;
 };
+
+// summary i of a merge (flat array, or gathered blocks); null when absent
+__device__ __forceinline__ const fluere_flow_summary* merge_input(const MergeArgs& a, unsigned long long i) {
+    if (i >= a.n) return nullptr;
+    if (!a.blocks) return a.in + i;
+    const uint8_t* blk = a.blocks + (i / a.cap) * a.block_bytes;
+    const fluere_shard_header* h = reinterpret_cast<const fluere_shard_header*>(blk);
+    const unsigned long long j = i % a.cap;
+    if (j >= h->n_flows) return nullptr;
+    return reinterpret_cast<const fluere_flow_summary*>(blk + sizeof(fluere_shard_header)) + j;
+}
 
 __global__ void __launch_bounds__(256) k_merge_insert(MergeArgs a) {
     unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const fluere_flow_summary& s = a.in[i];
+    if (a.blocks && i < a.n && i % a.cap == 0) {  // the block's run counters
+        const fluere_shard_header* h = reinterpret_cast<const fluere_shard_header*>(a.blocks + (i / a.cap) * a.block_bytes);
+        if (h->valid) {
+            atomicAdd(&a.g->valid, (unsigned long long)h->valid);
+            atomicMin(&a.g->tmin, (unsigned long long)h->tmin);
+            atomicMax(&a.g->tmax, (unsigned long long)h->tmax);
+        }
+        if (h->dropped) atomicAdd(&a.g->dropped, (unsigned long long)h->dropped);
+        if (h->raw) atomicAdd(&a.g->raw, (unsigned long long)h->raw);
+        if (h->err) atomicOr(a.T.err, h->err);
+        if (h->n_flows > a.cap) atomicOr(a.T.err, ERR_CAPACITY);  // the block was cut short
+    }
+    const fluere_flow_summary* sp = merge_input(a, i);
+    if (!sp) {
+        if (i < a.n) a.sd[i] = FAIL;
+        return;
+    }
+    const fluere_flow_summary& s = *sp;
     CKey k;
     for (int j = 0; j < 14; j++) k.w[j] = s.key[j];
     uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
@@ -2127,7 +2184,7 @@ __global__ void __launch_bounds__(256) k_merge_payload(MergeArgs a) {
     if (i >= a.n) return;
     uint32_t d = a.sd[i];
     if (d == FAIL || d >= a.T.fmax) return;
-    const fluere_flow_summary& s = a.in[i];
+    const fluere_flow_summary& s = *merge_input(a, i);
     // packet indices are global and unique: exactly one shard holds each
     if (s.first_create != NONE64 && s.first_create == a.A.fc[d]) {
         a.pay[d].t_first = s.first_time;
@@ -2179,6 +2236,7 @@ __device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t 
 __global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
     const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) merge_finalize_one(a, d);
+    if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
 }
 
 // test seam: insert canonical keys, return dense ids (flow dictionary checks)
@@ -2473,6 +2531,27 @@ static int fetch_ctl(fluere_ctx* c, Glob& g, uint32_t (&nf_err)[2]) {
     nf_err[0] = c->h_ctl->n_flows;
     nf_err[1] = c->h_ctl->err;
     // a failed run clears every table word: keep the full cleanup grid then
+    c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
+    return FLUERE_OK;
+}
+
+// Poll the pinned host copy until the last kernel has published run seq
+// (publish_ctl); now and then ask whether the stream failed instead.
+static int wait_published(fluere_ctx* c, uint32_t seq, Glob& g, uint32_t (&nf_err)[2]) {
+    volatile uint32_t* seqp = &c->h_ctl->seq;
+    for (uint32_t spin = 1;; spin++) {
+        if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == seq) break;
+        if ((spin & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == seq) break;
+            HIPCHECK(q);
+            return FLUERE_E_HIP;  // the stream finished without publishing: cannot happen
+        }
+    }
+    g = c->h_ctl->g;
+    nf_err[0] = c->h_ctl->n_flows;
+    nf_err[1] = c->h_ctl->err;
     c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
     return FLUERE_OK;
 }
@@ -3243,28 +3322,17 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     uint32_t nf_err[2];
     const auto t_enq = std::chrono::steady_clock::now();
     if (P.spec) {
-        // poll the run number k_finalize publishes in the pinned host copy
-        // (a blocking wait would add ~15 us of wake-up latency to every run);
-        // now and then ask whether the stream failed instead
-        volatile uint32_t* seqp = &c->h_ctl->seq;
-        for (uint32_t spin = 1;; spin++) {
-            if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == P.fa.seq) break;
-            if ((spin & 1023) == 0) {
-                const hipError_t q = hipStreamQuery(s);
-                if (q == hipErrorNotReady) continue;
-                if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == P.fa.seq) break;
-                HIPCHECK(q);
-                return FLUERE_E_HIP;  // the stream finished without publishing: cannot happen
-            }
-        }
+        // k_finalize publishes the counters in the pinned host copy; poll it
+        // (a blocking wait would add ~15 us of wake-up latency to every run)
+        if ((rc = wait_published(c, P.fa.seq, g, nf_err))) return rc;
     } else {
         HIPCHECK(hipStreamSynchronize(s));
+        g = c->h_ctl->g;
+        nf_err[0] = c->h_ctl->n_flows;
+        nf_err[1] = c->h_ctl->err;
+        c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
     }
     const auto t_sync = std::chrono::steady_clock::now();
-    g = c->h_ctl->g;
-    nf_err[0] = c->h_ctl->n_flows;
-    nf_err[1] = c->h_ctl->err;
-    c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
     // the speculative cleanup behind the copy clears the flows exactly when
     // the run needs no more device work (the same test, on the same counters)
     const bool spec_cleared = P.spec && run_complete(g, nf_err[1], P.spec_ca.timeout_us, P.spec_ca.recs_cap);
@@ -3529,9 +3597,10 @@ extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out
     return FLUERE_OK;
 }
 
-extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
-                                      uint64_t tmax, fluere_stats* st) {
-    if (!c || (!d_in && n)) return FLUERE_E_ARG;
+// Merge of shard summaries: a flat array (d_in, n) or gathered shard blocks
+// (blocks, n_shards * cap entries; tmin / tmax then come from the headers).
+static int merge_common(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, const uint8_t* blocks, uint64_t cap,
+                        uint64_t tmin, uint64_t tmax, fluere_stats* st) {
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
@@ -3545,30 +3614,37 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
         if (hipMalloc(&c->d_sd, std::max<uint64_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
         c->d_sd_cap = std::max<uint64_t>(n, 1);
     }
-    if ((rc = ensure_recs(c, std::max<uint64_t>(n, 1)))) return rc;
-    HIPCHECK(hipEventRecord(c->ev0, s));
+    if ((rc = ensure_recs(c, std::min<uint64_t>(std::max<uint64_t>(n, 1), std::max<uint64_t>(c->fmax, 1))))) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
     MergeArgs ma{tables_of(c), c->acc, d_in, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
-                 c->d_recs_cap};
+                 c->d_recs_cap, blocks, cap, fluere_shard_block_bytes(cap), c->h_ctl, seq};
+    // (no event markers: each adds a gap to the stream; timing is host wall)
     if (n) {
         k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
         k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
     }
-    HIPCHECK(hipEventRecord(c->ev1, s));
     k_merge_finalize<<<flow_grid(c), 256, 0, s>>>(ma);
     HIPCHECK(hipGetLastError());
     Glob g;
     uint32_t nf_err[2];
-    if ((rc = fetch_ctl(c, g, nf_err))) return rc;
+    if ((rc = wait_published(c, seq, g, nf_err))) return rc;
+    if (nf_err[1] & ERR_CAPACITY) return FLUERE_E_ARG;  // a shard had more flows than its block holds
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
     const uint32_t nf = std::min(nf_err[0], c->fmax);
-    HIPCHECK(hipEventRecord(c->ev2, s));
     c->dev_n_rec = g.n_rec;
     c->host_recs = false;
     c->have_results = true;
     fluere_stats out{};
-    float ms_parse = 0, ms_total = 0;
-    hipEventElapsedTime(&ms_parse, c->ev0, c->ev1);
-    hipEventElapsedTime(&ms_total, c->ev0, c->ev2);
+    const double ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double ms_parse = 0;
+    if (blocks) {
+        tmin = g.tmin;
+        tmax = g.tmax;
+        out.valid = g.valid;
+        out.dropped_parse = g.dropped;
+        out.unsupported = g.raw;
+    }
     out.flows = nf;
     out.records = g.n_rec;
     out.ended = g.n_ended;
@@ -3580,7 +3656,36 @@ extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* 
     // expiries or order-dependent flows across shards need the per-packet
     // state machine, which the sharded path does not run yet
     if (g.n_complex || (tmax >= tmin && tmax - tmin >= c->timeout_ms * 1000ull)) return FLUERE_E_UNSUPPORTED;
+    if (blocks && g.raw) return FLUERE_E_UNSUPPORTED;
     return FLUERE_OK;
+}
+
+extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
+                                      uint64_t tmax, fluere_stats* st) {
+    if (!c || (!d_in && n)) return FLUERE_E_ARG;
+    return merge_common(c, d_in, n, nullptr, 0, tmin, tmax, st);
+}
+
+extern "C" uint64_t fluere_shard_block_bytes(uint64_t cap) {
+    return sizeof(fluere_shard_header) + cap * sizeof(fluere_flow_summary);
+}
+
+extern "C" int fluere_export_device(fluere_ctx* c, void* d_block, uint64_t cap) {
+    if (!c || !d_block) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    int rc;
+    if ((rc = upload_batches(c))) return rc;
+    FinArgs fa{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(std::max<uint64_t>(cap, 1), 256), flow_grid(c)));
+    k_export_block<<<grid, 256, 0, c->stream>>>(fa, (uint8_t*)d_block, cap);
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap,
+                                     fluere_stats* st) {
+    if (!c || (!d_blocks && n_shards) || (n_shards && !cap)) return FLUERE_E_ARG;
+    return merge_common(c, nullptr, (uint64_t)n_shards * cap, (const uint8_t*)d_blocks, cap, 0, 0, st);
 }
 
 extern "C" int fluere_debug_dense_ids(fluere_ctx* c, const uint32_t* d_keys, uint64_t n, uint32_t* d_out) {

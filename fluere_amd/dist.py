@@ -12,7 +12,7 @@ from __future__ import annotations
 import ctypes
 
 from . import _lib
-from ._lib import SUMMARY_BYTES, Stats, check
+from ._lib import SHARD_HEADER_BYTES, SUMMARY_BYTES, Stats, check
 
 
 def shard_range(n_packets: int, rank: int, world: int):
@@ -114,3 +114,67 @@ def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int 
     allsum, gmin, gmax = got
     torch.cuda.current_stream().synchronize()  # the collective ran on torch's stream, the merge runs on ctx's
     return merge_summaries(ctx, allsum, gmin, gmax)
+
+
+class ShardExchange:
+    """The multi-GPU step without host round trips in the middle: every rank
+    runs parse+key+aggregate over its shard and exports its flows into one
+    shard block (fluere_shard_header + `cap` summaries) on the device; one
+    all_gather moves the blocks (RCCL over xGMI); rank `dst` merges them on the
+    device (fluere_merge_gathered).  The only host reads are the gathered
+    headers (every rank checks that no shard had more than `cap` flows, and
+    grows `cap` and exchanges again if one had) and the merge's counters.
+
+    The context must run on torch's current stream (FlowContext(stream=
+    torch.cuda.current_stream().cuda_stream)) so the collective is ordered
+    after the export; otherwise the context stream is synchronised first."""
+
+    def __init__(self, ctx, cap: int = 1024, group=None, dst: int = 0):
+        self.ctx, self.cap, self.group, self.dst = ctx, max(1, int(cap)), group, dst
+        self._send = self._recv = None
+
+    def _buffers(self, world, device):
+        import torch
+        blk = int(_lib.lib().fluere_shard_block_bytes(self.cap))
+        if self._send is None or self._send.numel() != blk or self._send.device != device:
+            self._send = torch.empty(blk, dtype=torch.uint8, device=device)
+            self._recv = torch.empty(world * blk, dtype=torch.uint8, device=device)
+        return blk
+
+    def step(self):
+        """One sharded pass; the merge stats on rank dst, None elsewhere."""
+        import torch
+        import torch.distributed as dist
+        L = _lib.lib()
+        ctx = self.ctx
+        world = dist.get_world_size(self.group)
+        rank = dist.get_rank(self.group)
+        gloo = dist.get_backend(self.group) == "gloo"
+        ctx.parse_aggregate()
+        while True:
+            blk = self._buffers(world, torch.device("cuda", torch.cuda.current_device()))
+            check(L.fluere_export_device(ctx._h, self._send.data_ptr(), self.cap), "fluere_export_device")
+            if ctx.stream is None or ctx.stream != torch.cuda.current_stream().cuda_stream:
+                torch.cuda.synchronize()  # the export ran on the context's own stream
+            if gloo:  # CPU rehearsal: host copies
+                recv_h = torch.empty(world * blk, dtype=torch.uint8)
+                dist.all_gather_into_tensor(recv_h, self._send.cpu(), group=self.group)
+                self._recv.copy_(recv_h)
+            else:
+                dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+            # the headers' flow counts (one small device->host copy)
+            n = self._recv.view(world, blk)[:, :8].contiguous().view(torch.int64).cpu().tolist()
+            need = max(int(v[0]) for v in n)
+            if need <= self.cap:
+                break
+            while self.cap < need:  # a shard had more flows: grow the blocks, exchange again
+                self.cap *= 2
+        if rank != self.dst:
+            return None
+        st = Stats()
+        rc = L.fluere_merge_gathered(ctx._h, self._recv.data_ptr(), world, self.cap, ctypes.byref(st))
+        if rc != _lib.E_UNSUPPORTED:
+            check(rc, "fluere_merge_gathered")
+        d = st.as_dict()
+        d["rc"] = rc
+        return d

@@ -33,6 +33,7 @@ class FlowContext:
         h = ctypes.c_void_p()
         check(L.fluere_open(ctypes.byref(o), ctypes.byref(h)), "fluere_open")
         self._h = h
+        self.stream = stream  # HIP stream handle the context runs on (None: its own)
         self._keep = []  # device buffers the batches point into
         self.n_packets = 0
 

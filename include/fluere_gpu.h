@@ -211,6 +211,25 @@ int fluere_export_summaries(fluere_ctx* ctx, fluere_flow_summary* d_out, uint64_
 int fluere_merge_summaries(fluere_ctx* ctx, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
                            uint64_t tmax, fluere_stats* stats);
 
+/* Shard exchange without host round trips (the multi-GPU step): a shard
+ * block is a 64-byte fluere_shard_header followed by cap summaries.
+ * fluere_export_device enqueues (asynchronously, on the context stream) the
+ * export of this context's flows after fluere_parse_aggregate into one block:
+ * min(n_flows, cap) summaries; the header holds the true n_flows, so a reader
+ * sees when cap was too small.  fluere_merge_gathered merges n_shards
+ * consecutive blocks (as an all-gather leaves them) like
+ * fluere_merge_summaries; FLUERE_E_ARG if a block holds more than cap flows.
+ * No reference counterpart (the reference is single-threaded). */
+typedef struct {
+    uint64_t n_flows, tmin, tmax, valid, dropped, raw;
+    uint32_t err, pad;
+    uint64_t reserved;
+} fluere_shard_header;          /* 64 bytes */
+uint64_t fluere_shard_block_bytes(uint64_t cap);
+int fluere_export_device(fluere_ctx* ctx, void* d_block, uint64_t cap);
+int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
+                          fluere_stats* stats);
+
 /* Test seam: insert n canonical keys (14 u32 words each, device memory) into
  * the flow dictionary and write each key's dense flow id. */
 int fluere_debug_dense_ids(fluere_ctx* ctx, const uint32_t* d_keys, uint64_t n, uint32_t* d_out);

@@ -2,6 +2,8 @@
 committed goldens.  Bit-exact (integer / byte work): per-packet
 parse_keys/parse_fluereflow views and the flow CSV (header equal, ended
 prefix equal in order, active suffix equal as a multiset)."""
+import ctypes
+
 import numpy as np
 import pyoracle
 import pytest
@@ -154,6 +156,46 @@ def test_sharded_merge_equals_single(gpu):
         fluere_amd.dist.merge_summaries(ctx, allsum, tmin, tmax)
         recs, ne = ctx.records()
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "sharded")
+
+
+def test_gathered_blocks_merge_equals_single(gpu):
+    """The multi-GPU exchange format: every shard exports one device block
+    (fluere_export_device: header + cap summaries) into consecutive slots of
+    one buffer, as an all_gather leaves them; fluere_merge_gathered merges
+    them.  Also: a block cut short (more flows than cap) is an error."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    L = _lib.lib()
+    G = 4
+    per = cfg.n_packets // G
+    for cap, ok in ((4096, True), (1024, False)):
+        blk = int(L.fluere_shard_block_bytes(cap))
+        buf = torch.zeros(G * blk, dtype=torch.uint8, device="cuda")
+        ctxs = []
+        for r in range(G):
+            ctx = fluere_amd.FlowContext(max_flows=1 << 16)
+            b, o, nbytes = fluere_amd.synth_device(cfg, r * per, per)
+            _lib.check(L.fluere_set_index_base(ctx._h, r * per), "base")
+            ctx.add_device_batch(b, nbytes, o, per)
+            torch.cuda.synchronize()
+            ctx.parse_aggregate()
+            _lib.check(L.fluere_export_device(ctx._h, buf.data_ptr() + r * blk, cap), "export_device")
+            ctxs.append(ctx)
+        torch.cuda.synchronize()
+        hdr = buf.view(G, blk)[:, :8].contiguous().view(torch.int64).cpu().tolist()
+        assert sum(int(h[0]) for h in hdr) >= 4000
+        with fluere_amd.FlowContext(max_flows=1 << 16) as m:
+            st = _lib.Stats()
+            rc = L.fluere_merge_gathered(m._h, buf.data_ptr(), G, cap, ctypes.byref(st))
+            if ok:
+                _lib.check(rc, "merge_gathered")
+                recs, ne = m.records()
+                assert st.valid == cfg.n_packets
+                assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "gathered")
+            else:
+                assert rc == _lib.E_ARG
+        for ctx in ctxs:
+            ctx.close()
 
 
 def test_c2_full_size_parity(gpu):
