@@ -659,6 +659,16 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             }
             searching |= q[u].state == 0;
         }
+        // every aggregate slot taken (more flows in this window than NS): a
+        // key not in its two inline pairs spills at once -- inserting it
+        // would gain nothing, and the search through a full table costs a
+        // dozen LDS round trips per chunk
+        if (searching && s_nslot >= NS) {
+#pragma unroll
+            for (int u = 0; u < PK; u++)
+                if (q[u].state == 0) q[u].state = 2;
+            searching = false;
+        }
         if (ABL != 3 && __ballot(searching)) {
             d_loops++;
             for (int it = 0; it < 2 * LK_STEPS; it++) {
@@ -893,15 +903,31 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         {
             const Spill* raw = S.spill_raw + (size_t)blockIdx.x * SPILL_WG;
             const unsigned long long sb = s_sbase;
-            for (uint32_t i = tid; i < nsp; i += BLOCK) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4* src = reinterpret_cast<const u32x4*>(raw + i);
-                const u32x4 a0 = __builtin_nontemporal_load(src), a1 = __builtin_nontemporal_load(src + 1);
-                const uint4 v0 = make_uint4(a0.x, a0.y, a0.z, a0.w), v1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
-                const uint32_t pos = atomicAdd(&s_scnt[owner_of(lt_hash(v0.x, v0.y, v0.z, v0.w), O)], 1u);
-                uint4* dst = reinterpret_cast<uint4*>(S.spill + sb + pos);
-                dst[0] = v0;
-                dst[1] = v1;
+            // SU records per thread per round, all loads issued first (one
+            // round trip per round instead of one per record)
+            constexpr int SU = 4;
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const uint32_t last = nsp ? nsp - 1 : 0;  // (loads stay inside the buffer even if hoisted)
+            for (uint32_t i0 = 0; i0 < nsp; i0 += SU * BLOCK) {
+                u32x4 a0[SU], a1[SU];
+#pragma unroll
+                for (int u = 0; u < SU; u++) {
+                    const uint32_t i = i0 + u * BLOCK + tid;
+                    const u32x4* src = reinterpret_cast<const u32x4*>(raw + min(i, last));
+                    a0[u] = __builtin_nontemporal_load(src);
+                    a1[u] = __builtin_nontemporal_load(src + 1);
+                }
+#pragma unroll
+                for (int u = 0; u < SU; u++) {
+                    const uint32_t i = i0 + u * BLOCK + tid;
+                    if (i >= nsp) continue;
+                    const uint4 v0 = make_uint4(a0[u].x, a0[u].y, a0[u].z, a0[u].w);
+                    const uint4 v1 = make_uint4(a1[u].x, a1[u].y, a1[u].z, a1[u].w);
+                    const uint32_t pos = atomicAdd(&s_scnt[owner_of(lt_hash(v0.x, v0.y, v0.z, v0.w), O)], 1u);
+                    uint4* dst = reinterpret_cast<uint4*>(S.spill + sb + pos);
+                    dst[0] = v0;
+                    dst[1] = v1;
+                }
             }
         }
 #pragma unroll
