@@ -175,10 +175,15 @@ __device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
 }
 
 // mode: 0 production (fast path first), 1 general parser only
+__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P);
 __device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool macs, int mode, Parsed& P) {
     uint32_t off = B.offs[li];
     Win W;
     load_win(B, off, W);
+    parse_loaded(B, off, W, macs, mode, P);
+}
+// The record at batch offset off, its window W already loaded.
+__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P) {
     bool sw = B.flags & 1;
     uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
     uint32_t L = min(incl, B.snap);
@@ -1651,12 +1656,22 @@ __device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluer
         return false;
     }
     const bool macs = a.macs != 0;
+    // the first and the last packet: both offsets, then both windows, in flight together
+    const int bp = find_batch(a.bs, a.nb, fc), bq = find_batch(a.bs, a.nb, la);
+    const Batch& BP = a.bs[bp];
+    const Batch& BQ = a.bs[bq];
+    const uint32_t op = BP.offs[fc - BP.first], oq = BQ.offs[la - BQ.first];
+    Win WP, WQ;
+    load_win(BP, op, WP);
+    load_win(BQ, oq, WQ);
+    pin_win(WP);
+    pin_win(WQ);
     Parsed P;
-    parse_global(a.bs, a.nb, fc, macs, P);
+    parse_loaded(BP, op, WP, macs, 0, P);
     const uint8_t cd = canon_dir(P, macs);
     fill_seed(r, P);
     Parsed Q;
-    parse_global(a.bs, a.nb, la, macs, Q);
+    parse_loaded(BQ, oq, WQ, macs, 0, Q);
     uint32_t p0 = A.pk[0][d], p1 = A.pk[1][d];
     unsigned long long b0 = A.by[0][d], b1 = A.by[1][d];
     r.d_pkts = p0 + p1;
