@@ -7,7 +7,9 @@ reference's offline-mode seams.  See DESIGN.md.
 from . import dist  # noqa: F401
 from ._lib import FluereError, available  # noqa: F401
 from .offline import (Args, Files, FlowContext, FluereRecord, Parameters, fluere_exporter,  # noqa: F401
-                      fluereflow_fileparse, format_csv, synth_cfg, synth_device, synth_pcap)
+                      fluereflow_fileparse, format_csv, synth_cfg, synth_device, synth_device_batches,
+                      synth_pcap)
 
 __all__ = ["Args", "Files", "Parameters", "FlowContext", "FluereRecord", "FluereError", "available",
-           "fluere_exporter", "fluereflow_fileparse", "format_csv", "synth_cfg", "synth_device", "synth_pcap"]
+           "fluere_exporter", "fluereflow_fileparse", "format_csv", "synth_cfg", "synth_device",
+           "synth_device_batches", "synth_pcap"]

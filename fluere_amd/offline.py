@@ -250,3 +250,22 @@ def synth_device(cfg: SynthCfg, first: int, n: int, stream: Optional[int] = None
     check(L.fluere_synth_device(ctypes.byref(cfg), first, n, b.data_ptr(), o.data_ptr(), stream),
           "fluere_synth_device")
     return b, o, nbytes
+
+
+def synth_device_batches(cfg: SynthCfg, first: int, n: int, max_bytes: int = 3 << 30,
+                         stream: Optional[int] = None):
+    """Packets [first, first+n) generated in HBM as consecutive batches of at
+    most max_bytes each (a batch's record offsets are u32, so one batch stays
+    below 4 GiB; IMIX shards of C4 are larger) -> [(bytes, offsets, nbytes, n_i)]."""
+    L = _lib.lib()
+    if max_bytes >= 1 << 32:
+        raise ValueError("a batch holds less than 4 GiB")
+    out, p, end = [], first, first + n
+    while p < end or not out:
+        m = end - p
+        while m > 1 and L.fluere_synth_range_bytes(ctypes.byref(cfg), p, m) > max_bytes:
+            m = (m + 1) // 2
+        b, o, nb = synth_device(cfg, p, m, stream)
+        out.append((b, o, nb, m))
+        p += m
+    return out
