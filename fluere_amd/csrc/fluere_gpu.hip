@@ -331,15 +331,22 @@ struct alignas(16) Spill {
     uint32_t doct, pt, loc, fl;   // pt = pkt | ttl << 16 | elig << 24; fl = tf | dir << 8
 };
 static_assert(sizeof(Spill) == 32, "Spill layout");
+// MAC kernels: a spilled packet takes two records: {k0, k1, k2, tag},
+// {m0, m1, m2, key hash}, {doct, pt, loc, fl}, padding.
+__host__ __device__ constexpr int spill_units(bool macs) { return macs ? 2 : 1; }
 
 struct Stage {
     Part* part;                   // [set * NS + cell]
     uint32_t* off;                // [(O + 1) * n_sets]: off[o * n_sets + set] = first cell of owner o's flows
     unsigned long long* base;     // [set] global index of the window's first packet
-    Spill* spill_raw;             // [workgroup][WIN_ITERS * BLOCK] this window's spills, arrival order
-    Spill* spill;                 // owner-grouped spills of every set (n_spill cursor)
+    // Spilled packets are stored as planes of 16-byte words (word w of every
+    // record together), so a wave's loads and stores of one word are contiguous.
+    Spill* spill_raw;             // [workgroup][word][WIN_ITERS * BLOCK] this window's spills, arrival order
+    Spill* spill;                 // [word][spill_cap] owner-grouped spills of every set (n_spill cursor)
+    unsigned long long spill_cap; // records per plane of spill (the batch's packet count)
     uint32_t* soff;               // [(O + 1) * n_sets]: owner o's spills of set s = spill[sbase[s] + soff[o][s] ..)
     unsigned long long* sbase;    // [set] first spill of the set
+    uint4* partx;                 // MAC runs: [set * NS + cell] the partial's MAC words and key hash
     unsigned long long* wgs;      // [workgroup][WGS_N] run statistics of each hot-kernel workgroup (plain
                                   // stores; k_merge_partials sums them: no contended atomics at the end)
     uint32_t W;                   // sets per workgroup
@@ -480,7 +487,8 @@ constexpr int PK = FLUERE_HOT_PK;       // packets per lane per hot-loop iterati
 static_assert(WIN_ITERS % PK == 0, "a window holds whole iterations");
 constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
 constexpr int MAX_OWNERS = 256;
-constexpr int SPILL_WG = WIN_ITERS * BLOCK;  // raw spill records per workgroup (one window)
+constexpr int SPILL_WG = WIN_ITERS * BLOCK;  // raw spilled packets per workgroup (one window)
+constexpr int NS_MAC = 768;             // MAC kernels: slots (the key table holds LK / 2 keys + sidecars)
 
 // merge owner of a flow: the top 24 hash bits scaled to [0, O) (multiply-shift)
 __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) {
@@ -493,6 +501,29 @@ __device__ __forceinline__ uint32_t lt_hash(uint32_t k0, uint32_t k1, uint32_t k
     h *= 0x7FEB352Du;
     h ^= h >> 15;
     return h;
+}
+
+// MAC kernels (-M): the flow key is the 5-tuple words plus the canonical MAC
+// pair packed in three words, m0 = lo MAC bytes 0..3, m1 = lo MAC bytes 4..5
+// << 16 | hi MAC bytes 4..5, m2 = hi MAC bytes 0..3 (dictionary words 10..13
+// of the canonical key, flow_table.h).  Key tables keep the MAC words in a
+// sidecar entry whose w = 1 marks it written.
+__device__ __forceinline__ uint32_t mac_hash(uint32_t h, uint32_t m0, uint32_t m1, uint32_t m2) {
+    return h ^ lt_hash(m0, m1, m2, 0x5BD1E995u);
+}
+// The dictionary key of a MAC-kernel key (same words as flow_of with macs).
+__device__ __forceinline__ void mac_ckey(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag, uint32_t m0,
+                                         uint32_t m1, uint32_t m2, CKey& k) {
+#pragma unroll
+    for (int j = 0; j < 14; j++) k.w[j] = 0;
+    k.w[0] = k0;
+    k.w[4] = k1;
+    k.w[8] = k2;
+    k.w[9] = (2u << 8) | (tag >> 24);
+    k.w[10] = m0;
+    k.w[11] = m1 & 0xFFFF0000u;
+    k.w[12] = m2;
+    k.w[13] = m1 << 16;
 }
 
 // ABL (diagnostics only): 0 full kernel; 1 parse + canonical key only; 2 + LDS key
@@ -516,6 +547,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ unsigned long long s_sbase;
     __shared__ unsigned long long s_cnt[5], s_tmin, s_tmax;
     const int tid = threadIdx.x;
+    // MAC kernels: LK / 2 key entries, each with its MAC sidecar at + LK / 2
+    constexpr int LKL = MACS ? LK / 2 : LK, LKL_BITS = MACS ? LK_BITS - 1 : LK_BITS;
+    constexpr uint32_t NSL = MACS ? NS_MAC : NS;
+    constexpr int SPU = spill_units(MACS);
     for (int e = tid; e < LK; e += BLOCK) s_key[e] = make_uint4(0, 0, 0, 0);
     for (int e = tid; e < NS; e += BLOCK) {
         s_pb[0][e] = s_pb[1][e] = 0;
@@ -558,6 +593,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     struct PS {
         Hot h;
         uint32_t dir, lo_ip, hi_ip, kports, k0, k1, k2, tag, e, e2, slot;
+        uint32_t m0, m1, m2;  // MAC kernels: the canonical MAC pair (mac_ckey)
         int state, steps;
         bool valid, slow;
     };
@@ -591,20 +627,12 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             q[u].k1 = q[u].hi_ip;
             q[u].k2 = q[u].kports;
             q[u].tag = h.proto << 24;
-            if (MACS && q[u].valid) {  // MAC pairs: dictionary first, the table is keyed by the dense id
-                CKey k;
-#pragma unroll
-                for (int j = 0; j < 14; j++) k.w[j] = 0;
-                k.w[0] = q[u].lo_ip;
-                k.w[4] = q[u].hi_ip;
-                k.w[8] = q[u].kports;
-                k.w[9] = (2u << 8) | h.proto;
+            q[u].m0 = q[u].m1 = q[u].m2 = 0;
+            if (MACS) {  // the MAC pair joins the key (the dictionary is walked once per slot, at the flush)
                 const uint64_t lom = gt ? dmac : smac, him = gt ? smac : dmac;
-                k.w[10] = (uint32_t)(lom >> 16); k.w[11] = (uint32_t)(lom & 0xFFFF) << 16;
-                k.w[12] = (uint32_t)(him >> 16); k.w[13] = (uint32_t)(him & 0xFFFF) << 16;
-                const uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
-                if (d == FAIL || d >= a.T.fmax) q[u].valid = false;  // error flag already set
-                q[u].k0 = d; q[u].k1 = 0; q[u].k2 = 0; q[u].tag = 0xFFu << 24;
+                q[u].m0 = (uint32_t)(lom >> 16);
+                q[u].m1 = ((uint32_t)(lom & 0xFFFF) << 16) | (uint32_t)(him & 0xFFFF);
+                q[u].m2 = (uint32_t)(him >> 16);
             }
         }
         if (ABL == 1) {
@@ -630,9 +658,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 #pragma unroll
         for (int u = 0; u < PK; u++) {
             hk[u] = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag);
-            const uint32_t e1 = hk[u] & (LK - 2);  // even: entries e, e+1 per step
-            uint32_t e2 = (hk[u] >> 12) * 0x9E3779B1u >> (32 - LK_BITS + 1) << 1;
-            e2 = FLUERE_PROBE2 ? (e2 == e1 ? e1 ^ 2u : e2) : (e1 + 2) & (LK - 1);
+            if (MACS) hk[u] = mac_hash(hk[u], q[u].m0, q[u].m1, q[u].m2);
+            const uint32_t e1 = hk[u] & (LKL - 2);  // even: entries e, e+1 per step
+            uint32_t e2 = (hk[u] >> 12) * 0x9E3779B1u >> (32 - LKL_BITS + 1) << 1;
+            e2 = FLUERE_PROBE2 ? (e2 == e1 ? e1 ^ 2u : e2) : (e1 + 2) & (LKL - 1);
             q[u].e = e1;
             q[u].e2 = e2;
             kp[u][0] = s_key[e1];
@@ -648,6 +677,22 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             for (int k = 0; k < 4; k++)
                 m[k] = ((kp[u][k].w & (0xFF000000u | LT_READY)) == (q[u].tag | LT_READY)) & (kp[u][k].x == q[u].k0) &
                        (kp[u][k].y == q[u].k1) & (kp[u][k].z == q[u].k2);
+            if (MACS) {
+                // the sidecar of an entry whose 5-tuple words match (read after the
+                // entry, so a published entry's sidecar is seen written)
+                bool hit = false;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (m[k] & !hit) {
+                        const uint32_t ek = (k < 2 ? q[u].e : q[u].e2) + (k & 1);
+                        const uint4 xs = s_key[LKL + ek];
+                        m[k] = (xs.w == 1u) & (xs.x == q[u].m0) & (xs.y == q[u].m1) & (xs.z == q[u].m2);
+                        hit = m[k];
+                    } else {
+                        m[k] = false;
+                    }
+                }
+            }
             const uint32_t sw = m[0] ? kp[u][0].w : m[1] ? kp[u][1].w : m[2] ? kp[u][2].w : kp[u][3].w;
             q[u].slot = sw & LT_SLOT;
             const bool found = m[0] | m[1] | m[2] | m[3];
@@ -657,7 +702,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             // where the search goes on: the first pair of the sequence not yet
             // known to be full of other keys
             q[u].steps = full1 ? (full2 ? 2 : 1) : 0;
-            q[u].e = full1 ? (full2 ? (q[u].e2 + 2) & (LK - 1) : q[u].e2) : q[u].e;
+            q[u].e = full1 ? (full2 ? (q[u].e2 + 2) & (LKL - 1) : q[u].e2) : q[u].e;
             if (ABL == 3) {  // diagnostics: aggregation without the key table (wrong slots)
                 q[u].slot = lt_hash(q[u].k0, q[u].k1, q[u].k2, q[u].tag) % 1000u;
                 q[u].state = q[u].valid ? 1 : 2;
@@ -668,7 +713,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         // key not in its two inline pairs spills at once -- inserting it
         // would gain nothing, and the search through a full table costs a
         // dozen LDS round trips per chunk
-        if (searching && s_nslot >= NS) {
+        if (searching && s_nslot >= NSL) {
 #pragma unroll
             for (int u = 0; u < PK; u++)
                 if (q[u].state == 0) q[u].state = 2;
@@ -684,28 +729,34 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     PS& r = q[u];
                     if (r.state == 0) {
                         const uint4 ka = s_key[r.e], kb = s_key[r.e + 1];
-                        const bool ma = (ka.w & (0xFF000000u | LT_READY)) == (r.tag | LT_READY) && ka.x == r.k0 &&
-                                        ka.y == r.k1 && ka.z == r.k2;
-                        const bool mb = (kb.w & (0xFF000000u | LT_READY)) == (r.tag | LT_READY) && kb.x == r.k0 &&
-                                        kb.y == r.k1 && kb.z == r.k2;
+                        bool ma = (ka.w & (0xFF000000u | LT_READY)) == (r.tag | LT_READY) && ka.x == r.k0 &&
+                                  ka.y == r.k1 && ka.z == r.k2;
+                        bool mb = (kb.w & (0xFF000000u | LT_READY)) == (r.tag | LT_READY) && kb.x == r.k0 &&
+                                  kb.y == r.k1 && kb.z == r.k2;
+                        if (MACS) {
+                            const uint4 xa = s_key[LKL + r.e], xb = s_key[LKL + r.e + 1];
+                            ma = ma && xa.w == 1u && xa.x == r.m0 && xa.y == r.m1 && xa.z == r.m2;
+                            mb = mb && xb.w == 1u && xb.x == r.m0 && xb.y == r.m1 && xb.z == r.m2;
+                        }
                         if (ma || mb) {
                             r.slot = (ma ? ka.w : kb.w) & LT_SLOT;
                             r.state = 1;
                         } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
                             if (++r.steps == LK_STEPS) r.state = 2;
-                            else r.e = r.steps == 1 ? r.e2 : (r.e + 2) & (LK - 1);
+                            else r.e = r.steps == 1 ? r.e2 : (r.e + 2) & (LKL - 1);
                         } else {
                             // first free entry of the pair; an entry being written (CLAIM) is re-read next step
-                            const uint32_t f = (ka.w == 0) ? r.e : ((ka.w & LT_READY) && kb.w == 0 ? r.e + 1 : LK);
-                            if (f < LK && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
+                            const uint32_t f = (ka.w == 0) ? r.e : ((ka.w & LT_READY) && kb.w == 0 ? r.e + 1 : LKL);
+                            if (f < LKL && atomicCAS(&s_key[f].w, 0u, LT_CLAIM) == 0u) {
                                 uint32_t sl = atomicAdd(&s_nslot, 1u);
-                                if (sl >= NS) sl = NS;  // no slot left: the key is kept, its packets go slow
+                                if (sl >= NSL) sl = NSL;  // no slot left: the key is kept, its packets spill
                                 s_key[f].x = r.k0;
                                 s_key[f].y = r.k1;
                                 s_key[f].z = r.k2;
-                                if (sl < NS) s_sk[sl] = f;
+                                if (MACS) s_key[LKL + f] = make_uint4(r.m0, r.m1, r.m2, 1u);
+                                if (sl < NSL) s_sk[sl] = f;
                                 __threadfence_block();
-                                atomicExch(&s_key[f].w, r.tag | LT_READY | (sl < NS ? sl : LT_SLOT));
+                                atomicExch(&s_key[f].w, r.tag | LT_READY | (sl < NSL ? sl : LT_SLOT));
                                 r.slot = sl;
                                 r.state = 1;
                             }
@@ -719,7 +770,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         bool agg[PK];
 #pragma unroll
         for (int u = 0; u < PK; u++) {
-            agg[u] = q[u].valid & (q[u].state == 1) & (q[u].slot < NS);
+            agg[u] = q[u].valid & (q[u].state == 1) & (q[u].slot < NSL);
             // a valid packet whose key has no LDS slot spills: a 32-byte record
             // for its merge owner (wave-aggregated append to this workgroup's
             // raw spill buffer; grouped by owner at the flush)
@@ -737,10 +788,11 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mm_, 0u));
                     const uint32_t loc = (uint32_t)(li[u] - wbase);
                     const bool elig = (h.proto != 6u) | ((h.tf & 2u) != 0);
-                    uint4* dst = reinterpret_cast<uint4*>(a.S.spill_raw + (size_t)blockIdx.x * SPILL_WG + b0 + r);
+                    uint4* dst = reinterpret_cast<uint4*>(a.S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2 * SPU + b0 + r;
                     dst[0] = make_uint4(q[u].k0, q[u].k1, q[u].k2, q[u].tag);
-                    dst[1] = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), loc,
-                                        h.tf | (q[u].dir << 8));
+                    if (MACS) dst[SPILL_WG] = make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]);
+                    dst[(MACS ? 2 : 1) * SPILL_WG] = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24),
+                                                                loc, h.tf | (q[u].dir << 8));
                     atomicAdd(&s_scnt[owner_of(hk[u], a.S.O)], 1u);
                     c_valid++;
                     tmin = min(tmin, (unsigned long long)h.t);
@@ -836,7 +888,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         cyc_wait += f0 - fw;
         const Stage& S = a.S;
         const uint32_t set = blockIdx.x * S.W + win;
-        const uint32_t ns = min(s_nslot, (uint32_t)NS), O = S.O;
+        const uint32_t ns = min(s_nslot, NSL), O = S.O;
         if (tid == 0) s_chunk = 0;  // every wave has drawn its last chunk of the window
         // counting sort of this window's flows by merge owner; a thread keeps
         // its slots' (at most two) owners and hashes in registers
@@ -856,6 +908,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             if (e >= ns || (s_pb[0][e] | s_pb[1][e]) == 0) continue;
             kks[k] = s_key[s_sk[e]];
             hh[k] = lt_hash(kks[k].x, kks[k].y, kks[k].z, kks[k].w & 0xFF000000u);
+            if (MACS) {  // the MAC words travel beside the partial (S.partx); same hash as the hot loop's
+                const uint4 xs = s_key[LKL + s_sk[e]];
+                hh[k] = mac_hash(hh[k], xs.x, xs.y, xs.z);
+            }
             own[k] = owner_of(hh[k], O);
             atomicAdd(&s_own[own[k]], 1u);
         }
@@ -906,32 +962,40 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         // records were written by other waves of this workgroup: nontemporal
         // loads, which bypass the CU's L1)
         {
-            const Spill* raw = S.spill_raw + (size_t)blockIdx.x * SPILL_WG;
+            const uint4* raw = reinterpret_cast<const uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2 * SPU;
             const unsigned long long sb = s_sbase;
             // SU records per thread per round, all loads issued first (one
             // round trip per round instead of one per record)
             constexpr int SU = 4;
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
             const uint32_t last = nsp ? nsp - 1 : 0;  // (loads stay inside the buffer even if hoisted)
+            constexpr int SW = MACS ? 3 : 2;  // 16-byte words per spilled packet
             for (uint32_t i0 = 0; i0 < nsp; i0 += SU * BLOCK) {
-                u32x4 a0[SU], a1[SU];
+                u32x4 av[SU][SW];
 #pragma unroll
                 for (int u = 0; u < SU; u++) {
                     const uint32_t i = i0 + u * BLOCK + tid;
                     const u32x4* src = reinterpret_cast<const u32x4*>(raw + min(i, last));
-                    a0[u] = __builtin_nontemporal_load(src);
-                    a1[u] = __builtin_nontemporal_load(src + 1);
+#pragma unroll
+                    for (int w = 0; w < SW; w++) av[u][w] = __builtin_nontemporal_load(src + (size_t)w * SPILL_WG);
                 }
+                // every load of the round issued before the first use (the
+                // compiler would sink a guarded record's loads into its branch)
+#pragma unroll
+                for (int u = 0; u < SU; u++)
+#pragma unroll
+                    for (int w = 0; w < SW; w++) asm volatile("" ::"v"(av[u][w]));
 #pragma unroll
                 for (int u = 0; u < SU; u++) {
                     const uint32_t i = i0 + u * BLOCK + tid;
                     if (i >= nsp) continue;
-                    const uint4 v0 = make_uint4(a0[u].x, a0[u].y, a0[u].z, a0[u].w);
-                    const uint4 v1 = make_uint4(a1[u].x, a1[u].y, a1[u].z, a1[u].w);
-                    const uint32_t pos = atomicAdd(&s_scnt[owner_of(lt_hash(v0.x, v0.y, v0.z, v0.w), O)], 1u);
-                    uint4* dst = reinterpret_cast<uint4*>(S.spill + sb + pos);
-                    dst[0] = v0;
-                    dst[1] = v1;
+                    const u32x4 v0 = av[u][0];
+                    const uint32_t hsp = MACS ? av[u][1].w : lt_hash(v0.x, v0.y, v0.z, v0.w);
+                    const uint32_t pos = atomicAdd(&s_scnt[owner_of(hsp, O)], 1u);
+                    uint4* dst = reinterpret_cast<uint4*>(S.spill) + sb + pos;
+#pragma unroll
+                    for (int w = 0; w < SW; w++)
+                        dst[(size_t)w * S.spill_cap] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
                 }
             }
         }
@@ -953,6 +1017,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             dst[2] = make_uint4(mm.x, mm.y, mm.z, mm.w);
             dst[3] = make_uint4(s_fl[0][e], s_fl[1][e], s_fl[2][e], s_fl[3][e]);
             dst[4] = s_pos[e];
+            if (MACS) {  // (re-read from LDS: registers are scarce across the spill scatter)
+                const uint4 xs = s_key[LKL + s_sk[e]];
+                S.partx[o] = make_uint4(xs.x, xs.y, xs.z, h);
+            }
             s_pb[0][e] = s_pb[1][e] = 0;
             s_mm[e] = make_uint4(NONE32, NONE32, 0, 0);
             s_pos[e] = make_uint4(NONE32, NONE32, NONE32, 0);
@@ -1270,6 +1338,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 __device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned long long stride);
 __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint4 m_key[MT];
+    __shared__ uint4 m_kx[MT];  // MAC runs: the MAC sidecar of each entry (w = 1 once written)
     __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
     __shared__ unsigned long long m_by[2][MT], m_fa[MT], m_fc[MT], m_fr[MT], m_la[MT];
     __shared__ uint32_t m_nclaim, m_base;
@@ -1290,8 +1359,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     }
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool macs = a.macs != 0;
     for (int e = tid; e < MT; e += MB) {
         m_key[e] = make_uint4(0, 0, 0, 0);
+        m_kx[e] = make_uint4(0, 0, 0, 0);
         m_pk[0][e] = m_pk[1][e] = 0;
         m_by[0][e] = m_by[1][e] = 0;
         m_mn[0][e] = m_mn[1][e] = NONE32;
@@ -1374,7 +1445,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             }
             const uint32_t set = c0s + lo_i;
             const unsigned long long base = S.base[set];
-            uint32_t h, k0, k1, k2, tag;
+            uint32_t h, k0, k1, k2, tag, x0 = 0, x1 = 0, x2 = 0;
             FlowPart f;
             if (pass == 0) {
                 const size_t o = (size_t)set * NS + m_lo[lo_i] + (idx - m_start[lo_i]);
@@ -1385,14 +1456,25 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 for (int q = 0; q < 5; q++) v[q] = src[q];
                 __builtin_memcpy(&p, v, sizeof p);
                 h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
+                if (macs) {
+                    const uint4 xx = S.partx[o];
+                    x0 = xx.x; x1 = xx.y; x2 = xx.z;
+                }
                 part_of_stage(p, base, f);
             } else {
                 const size_t o = S.sbase[set] + m_lo[lo_i] + (idx - m_start[lo_i]);
-                const uint4* src = reinterpret_cast<const uint4*>(S.spill + o);
-                const uint4 v0 = src[0], v1 = src[1];
+                const uint4* src = reinterpret_cast<const uint4*>(S.spill) + o;
+                const uint4 v0 = src[0], v1 = src[S.spill_cap];
                 k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
-                h = lt_hash(k0, k1, k2, tag);
-                spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
+                if (macs) {  // {key}, {MAC words, hash}, {payload}
+                    const uint4 v2 = src[2 * S.spill_cap];
+                    x0 = v1.x; x1 = v1.y; x2 = v1.z;
+                    h = v1.w;
+                    spill_to_part(v2.x, v2.y, v2.z, v2.w, base, f);
+                } else {
+                    h = lt_hash(k0, k1, k2, tag);
+                    spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
+                }
             }
             // find or claim the merge entry (same protocol as the hot kernel)
             uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
@@ -1400,14 +1482,20 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             for (int it = 0; it < 128; it++) {
                 if (state == 0) {
                     const uint4 kk = m_key[e];
+                    bool xm = true;
+                    if (macs) {  // MAC words
+                        const uint4 xx = m_kx[e];
+                        xm = xx.w == 1u && xx.x == x0 && xx.y == x1 && xx.z == x2;
+                    }
                     if (kk.w & LT_READY) {
-                        if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2) state = 1;
+                        if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2 && xm) state = 1;
                         else if (++probes == 64) state = 2;
                         else e = (e + 1) & (MT - 1);
                     } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
                         m_key[e].x = k0;
                         m_key[e].y = k1;
                         m_key[e].z = k2;
+                        if (macs) m_kx[e] = make_uint4(x0, x1, x2, 1u);
                         __threadfence_block();
                         atomicExch(&m_key[e].w, tag | LT_READY);
                         state = 1;
@@ -1433,7 +1521,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
                 if (f.la) atomicMax(&m_la[e], f.la);
             } else {
-                const uint32_t d = staged_id(a.T, k0, k1, k2, tag, a.A.slots);
+                uint32_t d;
+                if (macs && tag != 0xFF000000u) {
+                    CKey ck;
+                    mac_ckey(k0, k1, k2, tag, x0, x1, x2, ck);
+                    d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+                } else {
+                    d = staged_id(a.T, k0, k1, k2, tag, a.A.slots);
+                }
                 if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
             }
         }
@@ -1457,7 +1552,12 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     unsigned long long* val = nullptr;
     if (have) {
         if (tag == 0xFF000000u) {
-            d = kk.x;  // MAC kernels stage dense ids
+            d = kk.x;  // MAC kernels' partials carry dense ids
+        } else if (macs) {  // a spilled MAC-kernel key: one dictionary walk per flow and owner
+            const uint4 xx = m_kx[e];
+            CKey ck;
+            mac_ckey(kk.x, kk.y, kk.z, tag, xx.x, xx.y, xx.z, ck);
+            d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
         } else {       // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
             unsigned long long v = EMPTY;
             s0 = tab_slot(a.T, 0, ((uint64_t)kk.x << 32) | kk.y, true);
@@ -2932,10 +3032,10 @@ struct PassPlan {
 };
 
 // Bytes of the hot kernel's staging area for one batch (Stage layout).
-static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n) {
-    return cells * sizeof(Part) + ((size_t)grid * SPILL_WG + n) * sizeof(Spill) +
+static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n, bool macs) {
+    return cells * (sizeof(Part) + (macs ? sizeof(uint4) : 0)) + ((size_t)grid * SPILL_WG + n) * spill_units(macs) * sizeof(Spill) +
            2 * sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) +
-           (size_t)grid * WGS_N * sizeof(unsigned long long) + 64;
+           (size_t)grid * WGS_N * sizeof(unsigned long long) + 64 + (macs ? 16 : 0);
 }
 
 static int plan_batches(fluere_ctx* c, PassPlan& P) {
@@ -2970,7 +3070,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
-        need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n));
+        need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n, c->use_mac));
     }
     if (need_max > c->d_stage_bytes) {
         hipFree(c->d_stage);
@@ -2995,12 +3095,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         // layout (16-byte aligned pieces): parts | spill_raw | spill | sbase | base | off | soff
         S.part = (Part*)c->d_stage;
         S.spill_raw = (Spill*)(S.part + cells);
-        S.spill = S.spill_raw + (size_t)grid * SPILL_WG;
-        S.sbase = (unsigned long long*)(S.spill + hb.b.n);
+        S.spill = S.spill_raw + (size_t)grid * SPILL_WG * spill_units(c->use_mac);
+        S.sbase = (unsigned long long*)(S.spill + hb.b.n * spill_units(c->use_mac));
+        S.spill_cap = hb.b.n;  // planes of 16-byte words: 2 (4 with MACs) per Spill unit
         S.base = S.sbase + sets;
         S.off = (uint32_t*)(S.base + sets);
         S.soff = S.off + (size_t)(O + 1) * sets;
         S.wgs = (unsigned long long*)(((uintptr_t)(S.soff + (size_t)(O + 1) * sets) + 7) & ~(uintptr_t)7);
+        S.partx = c->use_mac ? (uint4*)(((uintptr_t)(S.wgs + (size_t)grid * WGS_N) + 15) & ~(uintptr_t)15) : nullptr;
         S.n_wg = grid;
         S.W = W;
         S.O = O;

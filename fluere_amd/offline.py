@@ -252,7 +252,7 @@ def synth_device(cfg: SynthCfg, first: int, n: int, stream: Optional[int] = None
     return b, o, nbytes
 
 
-def synth_device_batches(cfg: SynthCfg, first: int, n: int, max_bytes: int = 3 << 30,
+def synth_device_batches(cfg: SynthCfg, first: int, n: int, max_bytes: int = (1 << 32) - (1 << 20),
                          stream: Optional[int] = None):
     """Packets [first, first+n) generated in HBM as consecutive batches of at
     most max_bytes each (a batch's record offsets are u32, so one batch stays

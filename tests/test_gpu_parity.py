@@ -282,3 +282,44 @@ def test_truncated_tail_record(gpu, tmp_path):
         ctx.run()
         recs, ne = ctx.records()
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "truncated")
+
+
+# MAC kernels (-M): the LDS key tables carry the MAC pair beside the 5-tuple
+# (sidecar entries); a few flows take the slot path, many flows the wide spill
+# path (merge owners resolve each key once)
+MAC_SYNTH = {
+    "mac_few_flows": (_lib.SYNTH_MAC64, 400_000, 300, 0xF10E0015),
+    "mac_many_flows": (_lib.SYNTH_MAC64, 1_000_000, 50_000, 0xF10E0025),
+}
+
+
+@pytest.mark.parametrize("name", sorted(MAC_SYNTH))
+def test_mac_keys_match_oracle(gpu, name):
+    kind, n, f, seed = MAC_SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=True)
+    csv, ne, st = _gpu_csv(data, use_mac=True, max_flows=max(1 << 16, 2 * f))
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
+    assert st["packets"] == n
+
+
+def test_mac_pairs_sharing_a_5tuple(gpu):
+    """One 5-tuple under many MAC pairs, both directions, interleaved: every
+    (5-tuple, MAC pair) is its own flow (keys.rs:332-340 with -M)."""
+    import random
+    import pktbuild as pb
+    rng = random.Random(7)
+    pkts, t = [], 0
+    for i in range(60_000):
+        m = rng.randrange(3000)
+        a, b = f"02:00:00:{m >> 8:02x}:{m & 255:02x}:01", f"02:00:00:{m >> 8:02x}:{m & 255:02x}:02"
+        if rng.random() < 0.3:
+            frame = pb.eth(dst=a, src=b) + pb.ipv4("10.0.0.2", "10.0.0.1", 17, pb.udp(9000, 40000))
+        else:
+            frame = pb.eth(dst=b, src=a) + pb.ipv4("10.0.0.1", "10.0.0.2", 17, pb.udp(40000, 9000))
+        pkts.append((1_700_000_000 + t // 1_000_000, t % 1_000_000, frame))
+        t += 1
+    data = pb.pcap(pkts)
+    want = pyoracle.offline(data, use_mac=True)
+    csv, ne, st = _gpu_csv(data, use_mac=True)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "mac_pairs_sharing_a_5tuple")
