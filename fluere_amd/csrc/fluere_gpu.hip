@@ -488,7 +488,10 @@ static_assert(WIN_ITERS % PK == 0, "a window holds whole iterations");
 constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
 constexpr int MAX_OWNERS = 256;
 constexpr int SPILL_WG = WIN_ITERS * BLOCK;  // raw spilled packets per workgroup (one window)
-constexpr int NS_MAC = 768;             // MAC kernels: slots (the key table holds LK / 2 keys + sidecars)
+constexpr int NS_MAC = 768;
+#ifndef FLUERE_SPILL_NT
+#define FLUERE_SPILL_NT 0  // bit 0: owner-grouped spill stores nontemporal
+#endif             // MAC kernels: slots (the key table holds LK / 2 keys + sidecars)
 
 // merge owner of a flow: the top 24 hash bits scaled to [0, O) (multiply-shift)
 __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) {
@@ -994,8 +997,12 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     const uint32_t pos = atomicAdd(&s_scnt[owner_of(hsp, O)], 1u);
                     uint4* dst = reinterpret_cast<uint4*>(S.spill) + sb + pos;
 #pragma unroll
-                    for (int w = 0; w < SW; w++)
-                        dst[(size_t)w * S.spill_cap] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
+                    for (int w = 0; w < SW; w++) {
+                        if (FLUERE_SPILL_NT & 1)
+                            __builtin_nontemporal_store(av[u][w], reinterpret_cast<u32x4*>(dst + (size_t)w * S.spill_cap));
+                        else
+                            dst[(size_t)w * S.spill_cap] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
+                    }
                 }
             }
         }
@@ -3038,6 +3045,18 @@ static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, 
            (size_t)grid * WGS_N * sizeof(unsigned long long) + 64 + (macs ? 16 : 0);
 }
 
+// Merge owners (workgroups of k_merge_partials).  FLUERE_MAC_OWNERS caps them
+// for MAC runs (diagnostics): fewer owners mean fewer owner-grouped write
+// streams at the flush (C5u k_parse_agg 0.65 / 0.58 / 0.52 ms at 256 / 128 / 64
+// owners) but a slower merge (step 0.97 / 1.14 / 3.3 ms), so all are used.
+#ifndef FLUERE_MAC_OWNERS
+#define FLUERE_MAC_OWNERS 256
+#endif
+static uint32_t merge_owners(const fluere_ctx* c) {
+    const int cap = c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS;
+    return (uint32_t)std::max(1, std::min(c->n_cu, cap));
+}
+
 static int plan_batches(fluere_ctx* c, PassPlan& P) {
     AggArgs a;
     memset(&a, 0, sizeof a);
@@ -3069,7 +3088,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint64_t steps = (per + BLOCK - 1) / BLOCK;
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
-        const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
+        const uint32_t O = merge_owners(c);
         need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n, c->use_mac));
     }
     if (need_max > c->d_stage_bytes) {
@@ -3090,7 +3109,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint64_t steps = (per + BLOCK - 1) / BLOCK;
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
-        const uint32_t O = (uint32_t)std::max(1, std::min(c->n_cu, MAX_OWNERS));
+        const uint32_t O = merge_owners(c);
         Stage& S = a.S;
         // layout (16-byte aligned pieces): parts | spill_raw | spill | sbase | base | off | soff
         S.part = (Part*)c->d_stage;
