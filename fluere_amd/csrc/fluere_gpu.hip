@@ -1316,7 +1316,7 @@ __device__ __forceinline__ uint32_t staged_id(const TableSet& T, uint32_t k0, ui
 // find no LDS entry merge straight into the global accumulators.
 constexpr int MB = 1024;   // merge kernel block
 constexpr int MT = 1024;   // merge table entries (120 B each)
-constexpr int MCH = 2048;  // sets per scan chunk
+constexpr int MCH = 1024;  // sets per scan chunk
 
 // Exclusive scan of one value per thread over a 1024-thread block; returns
 // this thread's prefix, and leaves the block total in scratch[MB / 64].
@@ -1349,7 +1349,11 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
     __shared__ unsigned long long m_by[2][MT], m_fa[MT], m_fc[MT], m_fr[MT], m_la[MT];
     __shared__ uint32_t m_nclaim, m_base;
-    __shared__ uint32_t m_lo[MCH], m_start[MCH], m_scan[MB / 64 + 1];
+    // per set of the current chunk: this owner's first record (index into the
+    // partials or the spill planes), its start in the flattened index space,
+    // and the window's first packet (relative to the batch): a record's
+    // loads then depend on LDS reads only
+    __shared__ uint32_t m_lo[MCH], m_start[MCH], m_wb[MCH], m_scan[MB / 64 + 1];
     const int tid = threadIdx.x;
     const unsigned long long c0 = clock64();
     if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 0] = wall_clock64();
@@ -1357,12 +1361,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // this owner's segment bounds of the first set chunk, and the run counters
     const uint32_t me = blockIdx.x;
     uint32_t pre_lo[MCH / MB], pre_hi[MCH / MB];
+    unsigned long long pre_wb[MCH / MB];
 #pragma unroll
     for (int q = 0; q < MCH / MB; q++) {
         const uint32_t set = tid * (MCH / MB) + q;
         const bool in = set < a.S.n_sets;
         pre_lo[q] = in ? a.S.off[(size_t)me * a.S.n_sets + set] : 0;
         pre_hi[q] = in ? a.S.off[(size_t)(me + 1) * a.S.n_sets + set] : 0;
+        pre_wb[q] = in ? a.S.base[set] : 0;
     }
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1423,14 +1429,20 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         for (int q = 0; q < MCH / MB; q++) {
             const uint32_t set = c0s + tid * (MCH / MB) + q;
             uint32_t lo = 0, hi = 0;
+            unsigned long long wb = 0, rb = 0;
             if (pass == 0 && c0s == 0) {  // prefetched
                 lo = pre_lo[q];
                 hi = pre_hi[q];
+                wb = pre_wb[q];
             } else if (set < c0s + nset) {
                 lo = offs[(size_t)me * S.n_sets + set];
                 hi = offs[(size_t)(me + 1) * S.n_sets + set];
+                wb = S.base[set];
+                if (pass) rb = S.sbase[set];
             }
-            m_lo[tid * (MCH / MB) + q] = lo;
+            if (pass == 0) rb = (unsigned long long)set * NS;
+            m_lo[tid * (MCH / MB) + q] = (uint32_t)(rb + lo);
+            m_wb[tid * (MCH / MB) + q] = (uint32_t)(wb - a.B.first);
             len[q] = hi - lo;
             tot += len[q];
         }
@@ -1450,12 +1462,11 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 if (m_start[mid] <= idx) lo_i = mid;
                 else hi_i = mid - 1;
             }
-            const uint32_t set = c0s + lo_i;
-            const unsigned long long base = S.base[set];
+            const unsigned long long base = a.B.first + m_wb[lo_i];
             uint32_t h, k0, k1, k2, tag, x0 = 0, x1 = 0, x2 = 0;
             FlowPart f;
             if (pass == 0) {
-                const size_t o = (size_t)set * NS + m_lo[lo_i] + (idx - m_start[lo_i]);
+                const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
                 Part p;
                 const uint4* src = reinterpret_cast<const uint4*>(S.part + o);
                 uint4 v[5];
@@ -1469,7 +1480,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 }
                 part_of_stage(p, base, f);
             } else {
-                const size_t o = S.sbase[set] + m_lo[lo_i] + (idx - m_start[lo_i]);
+                const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
                 const uint4* src = reinterpret_cast<const uint4*>(S.spill) + o;
                 const uint4 v0 = src[0], v1 = src[S.spill_cap];
                 k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
