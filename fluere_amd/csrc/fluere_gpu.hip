@@ -1317,6 +1317,9 @@ __device__ __forceinline__ uint32_t staged_id(const TableSet& T, uint32_t k0, ui
 constexpr int MB = 1024;   // merge kernel block
 constexpr int MT = 1024;   // merge table entries (120 B each)
 constexpr int MCH = 1024;  // sets per scan chunk
+#ifndef FLUERE_MERGE_GUARD
+#define FLUERE_MERGE_GUARD 1  // read-before-atomic for min / max / positions (0: unconditional)
+#endif
 
 // Exclusive scan of one value per thread over a 1024-thread block; returns
 // this thread's prefix, and leaves the block total in scratch[MB / 64].
@@ -1522,22 +1525,35 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 if (__ballot(state == 0) == 0) break;
             }
             if (state == 1) {
+                // Many records land on one entry (a flow's partials from every
+                // set, its spilled packets), and LDS atomics on one address
+                // serialise: min / max and first / last positions are read
+                // first and written only where the record moves them (values
+                // move monotonically, so a stale read costs at most a
+                // redundant atomic).
+#if FLUERE_MERGE_GUARD
+                const uint32_t gmn0 = m_mn[0][e], gmn1 = m_mn[1][e], gmx0 = m_mx[0][e], gmx1 = m_mx[1][e];
+                const unsigned long long gfa = m_fa[e], gfc = m_fc[e], gla = m_la[e];
+#else
+                const uint32_t gmn0 = NONE32, gmn1 = NONE32, gmx0 = 0, gmx1 = 0;
+                const unsigned long long gfa = NONE64, gfc = NONE64, gla = 0;
+#endif
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
                     if (f.pk[q]) {
                         atomicAdd(&m_pk[q][e], f.pk[q]);
                         atomicAdd(&m_by[q][e], f.by[q]);
                     }
-                    atomicMin(&m_mn[q][e], f.mn[q]);
-                    atomicMax(&m_mx[q][e], f.mx[q]);
+                    if (f.mn[q] < (q ? gmn1 : gmn0) || !FLUERE_MERGE_GUARD) atomicMin(&m_mn[q][e], f.mn[q]);
+                    if (f.mx[q] > (q ? gmx1 : gmx0) || !FLUERE_MERGE_GUARD) atomicMax(&m_mx[q][e], f.mx[q]);
                 }
 #pragma unroll
                 for (int q = 0; q < 8; q++)
                     if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
-                if (f.fa != NONE64) atomicMin(&m_fa[e], f.fa);
-                if (f.fc != NONE64) atomicMin(&m_fc[e], f.fc);
+                if (f.fa != NONE64 && f.fa < gfa) atomicMin(&m_fa[e], f.fa);
+                if (f.fc != NONE64 && f.fc < gfc) atomicMin(&m_fc[e], f.fc);
                 if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
-                if (f.la) atomicMax(&m_la[e], f.la);
+                if (f.la && (f.la > gla || !FLUERE_MERGE_GUARD)) atomicMax(&m_la[e], f.la);
             } else {
                 uint32_t d;
                 if (macs && tag != 0xFF000000u) {
