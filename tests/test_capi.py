@@ -102,3 +102,28 @@ def test_synth_vlan_header_only_and_mac_keyed():
     assert pyoracle.offline(fluere_amd.synth_pcap(v), use_mac=True)["n"] == 0
     m = fluere_amd.synth_cfg(_lib.SYNTH_MAC64, 5_000, 50, 0xF10E0005)
     assert pyoracle.offline(fluere_amd.synth_pcap(m), use_mac=True)["n"] == 50
+
+
+def test_device_batches_split_below_4gib(monkeypatch):
+    """bench.py's C4 shard (12.5M IMIX packets, ~4.3 GiB) is attached as
+    consecutive batches that each stay below 4 GiB (u32 record offsets) and
+    together cover the shard exactly (host-side split; generation stubbed)."""
+    from fluere_amd import offline
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 12_500_000, 125_000, 0xF10E0004)
+    L = _lib.lib()
+    total = L.fluere_synth_range_bytes(ctypes.byref(cfg), 0, 12_500_000)
+    assert total >= 1 << 32
+    calls = []
+
+    def fake(cfg_, first, n, stream=None):
+        nb = L.fluere_synth_range_bytes(ctypes.byref(cfg_), first, n)
+        calls.append((first, n, nb))
+        return None, None, nb
+
+    monkeypatch.setattr(offline, "synth_device", fake)
+    out = offline.synth_device_batches(cfg, 0, 12_500_000)
+    assert len(out) >= 2
+    assert all(nb < 1 << 32 for _, _, nb, _ in out)
+    assert sum(n for _, _, _, n in out) == 12_500_000
+    assert [c[0] for c in calls] == [sum(c[1] for c in calls[:i]) for i in range(len(calls))]
+    assert sum(c[2] for c in calls) == total
