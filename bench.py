@@ -10,7 +10,7 @@ all_gather of per-flow summaries over xGMI + device merge/finalize on rank 0.
 Weak scaling: every rank owns a fixed per-GPU shard of one global capture
 (packet-range sharding with global packet indices).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5u]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5u]
   torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
 """
 from __future__ import annotations
@@ -32,6 +32,8 @@ CONFIGS = {
                workload="10M IMIX 64/576/1500 TCP+UDP, 100k flows per GPU (BASELINE configs[2])"),
     "c4": dict(kind=1, per_gpu=12_500_000, flows=125_000, seed=0xF10E0004, use_mac=False,
                workload="IMIX TCP+UDP, 12.5M packets / 125k flows per GPU (BASELINE configs[3] at 8 GPUs)"),
+    "c5": dict(kind=2, per_gpu=10_000_000, flows=50_000, seed=0xF10E0005, use_mac=True,
+               workload="10M x 64B VLAN-tagged, 50k MAC pairs, --useMAC (BASELINE configs[4]; header-only CSV)"),
     "c5u": dict(kind=3, per_gpu=10_000_000, flows=50_000, seed=0xF10E0005, use_mac=True,
                 workload="10M x 64B untagged, 50k MAC pairs, --useMAC (BASELINE configs[4], untagged)"),
 }

@@ -417,7 +417,14 @@ __device__ __forceinline__ uint32_t hot_parse(const Batch& B, uint32_t off, cons
     const bool dns = !tcp & (((h.ports >> 16) == 53u) | ((h.ports & 0xFFFFu) == 53u));  // fluereflows.rs:255-291
     h.pkt = dns ? pe : tl;
     h.tf = tcp ? W.w[15] >> 24 : 0u;
-    return shape ? (ok ? HOT_OK : HOT_DROP) : HOT_SLOW;
+    // 802.1Q frames: vlan_keys (keys.rs:417-435) reads the bytes after the tag
+    // as a whole Ethernet header, so the key parse fails (the packet is
+    // skipped) unless frame bytes 30..31 read 0x0800 / 0x86DD; frames shorter
+    // than 32 bytes fail as well.  Those are dropped here, not listed slow.
+    const uint32_t in_et = W.w[11] >> 16;  // frame bytes 30, 31
+    const bool vlan_drop =
+        whole & ((w7 & 0xFFFFu) == 0x0081u) & ((L < 32u) | ((in_et != 0x0008u) & (in_et != 0xDD86u)));
+    return shape ? (ok ? HOT_OK : HOT_DROP) : (vlan_drop ? HOT_DROP : HOT_SLOW);
 }
 
 // update_flow's order-free part straight into the global accumulators

@@ -323,3 +323,28 @@ def test_mac_pairs_sharing_a_5tuple(gpu):
     want = pyoracle.offline(data, use_mac=True)
     csv, ne, st = _gpu_csv(data, use_mac=True)
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "mac_pairs_sharing_a_5tuple")
+
+
+def test_vlan_frames_drop_or_misparse(gpu):
+    """802.1Q frames: the hot parser drops those whose key parse fails
+    (keys.rs:417-435 reads the bytes after the tag as an Ethernet header);
+    frames whose bytes 30..31 read 0x0800 / 0x86DD (source IP 8.0.x.x /
+    134.221.x.x) and short frames go through the general parser."""
+    import struct
+    import pktbuild as pb
+    pkts, t = [], 0
+    srcs = ["10.0.0.1", "8.0.1.2", "134.221.3.4", "8.0.9.9", "192.168.1.1"]
+    for i in range(4000):
+        src = srcs[i % len(srcs)]
+        tag = struct.pack(">HH", (i % 7) + 1, 0x0800)
+        l3 = pb.ipv4(src, "10.0.0.2", 17, pb.udp(40000 + i % 50, 9000, payload=bytes(range(24))))
+        frame = pb.eth(et=0x8100) + tag + l3
+        if i % 97 == 0:
+            frame = frame[:14 + (i % 5) * 5]  # short frames (14..34 bytes)
+        pkts.append((1_700_000_000, t, frame))
+        t += 1
+    data = pb.pcap(pkts)
+    for use_mac in (False, True):
+        want = pyoracle.offline(data, use_mac=use_mac)
+        csv, ne, st = _gpu_csv(data, use_mac=use_mac)
+        assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"vlan_mac{int(use_mac)}")
