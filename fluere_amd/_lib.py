@@ -82,6 +82,15 @@ PKT_META_DTYPE = np.dtype([
 ])
 assert PKT_META_DTYPE.itemsize == 128
 
+# struct fluere_raw_hdr (64 bytes): fluere_debug_raw output
+RAW_HDR_DTYPE = np.dtype([
+    ("some", "u1"), ("has_src", "u1"), ("has_dst", "u1"), ("ip_v6", "u1"), ("src", "u1", 16), ("dst", "u1", 16),
+    ("src_port", "<u2"), ("dst_port", "<u2"), ("protocol", "u1"), ("has_flags", "u1"), ("flags", "u1"),
+    ("has_version", "u1"), ("version", "u1"), ("has_ethertype", "u1"), ("has_payload", "u1"), ("pad0", "u1"),
+    ("length", "<u2"), ("ethertype", "<u2"), ("payload_off", "<u4"), ("payload_len", "<u4"), ("pad1", "<u4"),
+])
+assert RAW_HDR_DTYPE.itemsize == 64
+
 SUMMARY_DTYPE = np.dtype([
     ("key", "<u4", 14), ("pkts", "<u4", 2), ("bytes", "<u8", 2), ("min_pkt", "<u4"), ("max_pkt", "<u4"),
     ("min_ttl", "<u4"), ("max_ttl", "<u4"), ("flag_cnt", "<u4", 8), ("first_all", "<u8"), ("first_create", "<u8"),
@@ -136,6 +145,7 @@ def lib() -> ctypes.CDLL:
         "fluere_last_kernel_ms": (ctypes.c_double, [P]),
         "fluere_last_pass_ms": (ctypes.c_double, [P]),
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),
+        "fluere_debug_raw": (I, [I, P, P, P, P, U64, P, P]),
         "fluere_export_summaries": (I, [P, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "fluere_merge_summaries": (I, [P, P, U64, U64, U64, ctypes.POINTER(Stats)]),
         "fluere_shard_block_bytes": (U64, [U64]),

@@ -45,10 +45,7 @@ int main(int argc, char** argv) {
         printf("[INFO] Active flows: %llu\n", (unsigned long long)(st.records - st.ended));
         printf("[INFO] Ended flows: %llu\n", (unsigned long long)st.ended);
     }
-    if (rc == FLUERE_E_UNSUPPORTED)
-        fprintf(stderr, "[WARN] %llu packets need parser classes not yet on the GPU\n",
-                (unsigned long long)st.unsupported);
-    else if (rc)
+    if (rc)
         fprintf(stderr, "[ERROR] fluere offline failed: %d\n", rc);
     return rc ? 1 : 0;
 }

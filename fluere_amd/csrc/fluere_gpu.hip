@@ -52,6 +52,7 @@ static_assert(sizeof(fluere_record) == 152, "fluere_record ABI");
 static_assert(sizeof(fluere_pkt_meta) == 128, "fluere_pkt_meta ABI");
 static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
 static_assert(sizeof(fluere_shard_header) == 64, "fluere_shard_header ABI");
+static_assert(sizeof(fluere_raw_hdr) == 64, "fluere_raw_hdr ABI");
 
 namespace {
 
@@ -139,7 +140,7 @@ struct Parsed {
     uint64_t t;
     uint64_t smac, dmac;  // big-endian packed MACs of the keyed frame
     uint32_t L;
-    uint8_t cls;          // 0 valid, 1 dropped (NetError), 2 raw class
+    uint8_t cls;          // 0 valid, 1 dropped (NetError)
 };
 
 __device__ __forceinline__ uint32_t hdr_word(uint32_t w, bool swapped) { return swapped ? bswap32(w) : w; }
@@ -199,9 +200,7 @@ __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const
         P.pi = g;
     }
     const PktInfo& pi = P.pi;
-    bool kbad = pi.kst != ST_OK && pi.kst != ST_RAW;
-    bool fbad = pi.fst != ST_OK && pi.fst != ST_RAW;
-    P.cls = (kbad || fbad) ? 1 : ((pi.kst == ST_RAW || pi.fst == ST_RAW) ? 2 : 0);
+    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;
     P.smac = P.dmac = 0;
     if (macs && P.cls == 0) {
         if (fast) {
@@ -1686,13 +1685,12 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
 __device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned long long stride) {
     const unsigned long long n = *a.slow_n;
     const bool macs = a.macs != 0;
-    unsigned long long c_valid = 0, c_drop = 0, c_raw = 0, tmin = NONE64, tmax = 0;
+    unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
     for (unsigned long long i = i0; i < n; i += stride) {
         const uint64_t li = a.slow[i];
         Parsed P;
         parse_record(a.B, li, macs, 1, P);
-        if (P.cls == 1) { c_drop++; continue; }
-        if (P.cls == 2) { c_raw++; continue; }
+        if (P.cls) { c_drop++; continue; }
         c_valid++;
         tmin = min(tmin, (unsigned long long)P.t);
         tmax = max(tmax, (unsigned long long)P.t);
@@ -1703,7 +1701,6 @@ __device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned l
     }
     if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
     if (c_drop) atomicAdd(&a.g->dropped, c_drop);
-    if (c_raw) atomicAdd(&a.g->raw, c_raw);
 }
 
 // ---------------------------------------------------------------------------
@@ -2192,7 +2189,7 @@ __global__ void __launch_bounds__(256) k_parse_batch(Batch B, fluere_pkt_meta* o
     memset(&m, 0, sizeof m);
     m.k_status = pi.kst;
     m.f_status = pi.fst;
-    m.raw_used = (pi.raw || pi.kst == ST_RAW || pi.fst == ST_RAW) ? 1 : 0;
+    m.raw_used = pi.raw;
     const uint8_t* fr = B.bytes + B.offs[li] + 16;
     if (pi.kst == ST_OK) {
         m.key_v6 = pi.v6; m.key_proto = pi.kproto; m.key_sport = pi.ksp; m.key_dport = pi.kdp;
@@ -2429,6 +2426,44 @@ __global__ void __launch_bounds__(256) k_dense_test(TableSet T, const uint32_t* 
     CKey k;
     for (int j = 0; j < 14; j++) k.w[j] = keys[i * 14 + j];
     out[i] = dense_of_key(T, k, true, slots, nullptr);
+}
+
+// test seam (fluere_debug_raw): one raw-fallback entry point of parse.h per
+// byte string, exactly the device functions the parsers call
+__global__ void __launch_bounds__(256) k_raw_probe(int fn, const uint8_t* bytes, const uint32_t* off, const uint32_t* len,
+                                                   const uint32_t* arg, unsigned long long n, fluere_raw_hdr* out) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const G g{bytes + off[i]};
+    const Span p{0, len[i]};
+    RawHdr h;
+    raw_new(h, 0, 0, 0, 0);
+    bool some = false;
+    switch (fn) {
+    case FLUERE_RAW_FROM_RAW_PACKET: some = raw_from_raw_packet(g, p, arg[i] & 0xFF, h); break;
+    case FLUERE_RAW_FROM_ETHERTYPE: some = raw_from_ethertype(g, p, arg[i] & 0xFFFF, h); break;
+    case FLUERE_RAW_PARSE_ETHERTYPE: some = raw_parse_ethertype(g, p, arg[i] & 0xFFFF, h); break;
+    case FLUERE_RAW_PARSE_PROTOCOL: some = raw_parse_protocol(g, p, arg[i] & 0xFF, h); break;
+    case FLUERE_RAW_OPENVPN: some = raw_openvpn(g, p, h); break;
+    case FLUERE_RAW_ICMP: some = raw_icmp(g, p, h); break;
+    default: break;
+    }
+    fluere_raw_hdr r;
+    memset(&r, 0, sizeof r);
+    r.some = some;
+    if (some) {
+        r.has_src = h.has_src; r.has_dst = h.has_dst; r.ip_v6 = h.v6;
+        for (int k = 0; k < 4; k++)
+            for (int b = 0; b < 4; b++) {
+                r.src[4 * k + b] = (uint8_t)(h.src[k] >> (24 - 8 * b));
+                r.dst[4 * k + b] = (uint8_t)(h.dst[k] >> (24 - 8 * b));
+            }
+        r.src_port = h.sport; r.dst_port = h.dport; r.protocol = h.proto; r.length = h.length;
+        r.has_flags = h.has_flags; r.flags = h.flags; r.has_version = h.has_version; r.version = h.version;
+        r.has_ethertype = h.has_ethertype; r.ethertype = h.ethertype;
+        r.has_payload = h.has_payload; r.payload_off = h.payload_off; r.payload_len = h.payload_len;
+    }
+    out[i] = r;
 }
 
 unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
@@ -2936,7 +2971,10 @@ struct Ingest {
             const size_t i0 = cut[q], i1 = q + 1 < cut.size() ? cut[q + 1] : n;
             if (i1 == i0) continue;
             const uint64_t base = cut_base[q];
-            const uint64_t endb = q + 1 < cut.size() ? cut_base[q + 1] : size;
+            // the last batch ends with its last indexed record (pos), not at the
+            // end of the file: a corrupt tail after a bad record header is not
+            // part of any batch (and cannot push it past the 4 GiB offset range)
+            const uint64_t endb = q + 1 < cut.size() ? cut_base[q + 1] : pos;
             HostBatch hb;
             hb.own_bytes = first ? d : nullptr;  // one allocation for every batch
             hb.own_offs = first ? d_offs : nullptr;
@@ -3663,7 +3701,6 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     out.packets = c->n_total;
     out.valid = g.valid;
     out.dropped_parse = g.dropped;
-    out.unsupported = g.raw;
     out.flows = nf;
     out.records = n_rec;
     out.ended = n_ended;
@@ -3687,7 +3724,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
                 us(t_prev_exit, t_run0), us(t_run0, t_enq), us(t_enq, t_sync), us(t_sync, t_exit));
         t_prev_exit = t_exit;
     }
-    return g.raw ? FLUERE_E_UNSUPPORTED : FLUERE_OK;
+    return FLUERE_OK;
 }
 
 extern "C" int fluere_get_records(fluere_ctx* c, fluere_record** out, uint64_t* n, uint64_t* n_ended) {
@@ -3780,7 +3817,6 @@ extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out
     uint32_t nf_err[2];
     if ((rc = fetch_ctl(c, g, nf_err))) return rc;
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
-    if (g.raw) return FLUERE_E_UNSUPPORTED;
     uint32_t nf = std::min(nf_err[0], c->fmax);
     *n = nf;
     if (tmin) *tmin = g.tmin;
@@ -3839,8 +3875,7 @@ static int merge_common(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t
         tmax = g.tmax;
         out.valid = g.valid;
         out.dropped_parse = g.dropped;
-        out.unsupported = g.raw;
-    }
+        }
     out.flows = nf;
     out.records = g.n_rec;
     out.ended = g.n_ended;
@@ -3852,7 +3887,6 @@ static int merge_common(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t
     // expiries or order-dependent flows across shards need the per-packet
     // state machine, which the sharded path does not run yet
     if (g.n_complex || (tmax >= tmin && tmax - tmin >= c->timeout_ms * 1000ull)) return FLUERE_E_UNSUPPORTED;
-    if (blocks && g.raw) return FLUERE_E_UNSUPPORTED;
     return FLUERE_OK;
 }
 
@@ -3893,4 +3927,15 @@ extern "C" int fluere_debug_dense_ids(fluere_ctx* c, const uint32_t* d_keys, uin
     uint32_t nf_err[2];
     HIPCHECK(hipMemcpy(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost));
     return nf_err[1] ? FLUERE_E_TABLE_FULL : FLUERE_OK;
+}
+
+extern "C" int fluere_debug_raw(int fn, const uint8_t* d_bytes, const uint32_t* d_off, const uint32_t* d_len,
+                                const uint32_t* d_arg, uint64_t n, fluere_raw_hdr* d_out, void* stream) {
+    if (fn < FLUERE_RAW_FROM_RAW_PACKET || fn > FLUERE_RAW_ICMP) return FLUERE_E_ARG;
+    if (n && (!d_bytes || !d_off || !d_len || !d_arg || !d_out)) return FLUERE_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (n) k_raw_probe<<<grid_for(n, 256), 256, 0, s>>>(fn, d_bytes, d_off, d_len, d_arg, n, d_out);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
 }

@@ -144,16 +144,24 @@ extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, i
     o.timeout_ms = timeout_ms;
     o.use_mac = use_mac;
     // flow capacity from the file size (a record is at least 16 bytes; flows
-    // rarely exceed one per 64 bytes of capture)
+    // rarely exceed one per 64 bytes of capture).  The reference's HashMap has
+    // no limit: a capture with more flows reopens with twice the capacity.
     o.max_flows = std::max<uint64_t>(1 << 16, std::min<uint64_t>((uint64_t)sb.st_size / 64, 1 << 22));
     fluere_ctx* c = nullptr;
-    int rc = fluere_open(&o, &c);
-    if (rc) return rc;
-    rc = fluere_add_pcap_file(c, pcap_path);
     fluere_stats st{};
-    if (!rc) rc = fluere_run(c, &st);
+    int rc;
+    for (;;) {
+        rc = fluere_open(&o, &c);
+        if (rc) return rc;
+        rc = fluere_add_pcap_file(c, pcap_path);
+        if (!rc) rc = fluere_run(c, &st);
+        if (rc != FLUERE_E_TABLE_FULL || o.max_flows >= (1ull << 23)) break;
+        fluere_close(c);
+        c = nullptr;
+        o.max_flows *= 2;
+    }
     if (stats) *stats = st;
-    if (rc && rc != FLUERE_E_UNSUPPORTED) { fluere_close(c); return rc; }
+    if (rc) { fluere_close(c); return rc; }
     int run_rc = rc;
     fluere_record* recs = nullptr;
     uint64_t nr = 0, ne = 0;

@@ -13,15 +13,14 @@
 //   * parse_general: everything else the GPU supports (IPv4 options, IPv6,
 //     ARP, VXLAN decapsulation, the 802.1Q misparse, ICMPv6/GRE port
 //     quirks), reading bytes from global memory (L1/L2 hits: the window was
-//     just loaded).  Packets whose parse_fluereflow result comes from
-//     src/net/parser/raw are classified PKT_RAW.
+//     just loaded), including the src/net/parser/raw fallback.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace fl {
 
-enum : uint8_t { ST_OK = 0, ST_EMPTY = 1, ST_INVALID = 2, ST_UNKNOWN_ETHER = 3, ST_RAW = 0xFE };
+enum : uint8_t { ST_OK = 0, ST_EMPTY = 1, ST_INVALID = 2, ST_UNKNOWN_ETHER = 3 };
 
 // Result of both parsers for one packet.
 struct PktInfo {
@@ -217,18 +216,38 @@ struct RawHdr {
     uint16_t sport, dport;
     uint8_t proto;
     uint16_t length;  // u16 in RawProtocolHeader (raw/mod.rs)
+    // Option fields the reference's tests assert (never read by the hot path;
+    // flags only feed parse_flags of an empty slice, fluereflows.rs:151)
+    bool has_flags, has_version, has_ethertype, has_payload;
+    uint8_t flags, version;
+    uint16_t ethertype;
+    uint32_t payload_off, payload_len;  // payload = bytes [payload_off, +payload_len) of the G view
 };
 
+// raw/mod.rs:40-71 RawProtocolHeader::new (Option fields None)
 __device__ __forceinline__ void raw_new(RawHdr& h, uint32_t sp, uint32_t dp, uint32_t proto, uint32_t len) {
     h.has_src = h.has_dst = h.v6 = false;
     for (int k = 0; k < 4; k++) h.src[k] = h.dst[k] = 0;
     h.sport = (uint16_t)sp; h.dport = (uint16_t)dp; h.proto = (uint8_t)proto; h.length = (uint16_t)len;
+    h.has_flags = h.has_version = h.has_ethertype = h.has_payload = false;
+    h.flags = h.version = 0;
+    h.ethertype = 0;
+    h.payload_off = h.payload_len = 0;
+}
+__device__ __forceinline__ void raw_payload(RawHdr& h, Span p, uint32_t off) {
+    off = min(off, p.len);
+    h.has_payload = true;
+    h.payload_off = p.off + off;
+    h.payload_len = p.len - off;
 }
 
-// protocols/icmp.rs:95-131
+// protocols/icmp.rs:10-48
 __device__ __forceinline__ bool raw_icmp(const G& g, Span p, RawHdr& h) {
     if (p.len < 4) return false;
     raw_new(h, g.b(p.off), g.b(p.off + 1), 1, p.len);
+    if (p.len > 4) raw_payload(h, p, 4);
+    h.has_flags = true; h.flags = (uint8_t)g.b(p.off);
+    h.has_version = true; h.version = (uint8_t)g.b(p.off + 1);
     return true;
 }
 
@@ -238,6 +257,7 @@ __device__ __forceinline__ bool raw_openvpn(const G& g, Span p, RawHdr& h) {
     const uint32_t t = g.b(p.off);
     if (!((t >= 1 && t <= 9) || t == 0x40 || t == 0x41)) return false;
     raw_new(h, t, 0, 0x9B, p.len);
+    raw_payload(h, p, 9);
     if (t == 6 || t == 9) {
         const Span ip = {p.off + 9, p.len - 9};
         if (ip.len >= 16 && ((g.b(ip.off) >> 4) & 0x0F) == 4) {
@@ -284,13 +304,14 @@ __device__ __attribute__((noinline)) bool raw_from_raw_packet(const G& g, Span p
     }
     if (outer) {
         raw_new(h, osp, odp, oproto, p.len);
+        raw_payload(h, p, 0);
         h.has_src = h.has_dst = true;
         h.src[0] = os; h.dst[0] = od;
         return true;
     }
     if (p.len < 4) return false;
-    if (hint == 0x36) raw_new(h, g.b(p.off), g.b(p.off + 1), hint, p.len);
-    else raw_new(h, g.be16(p.off), g.be16(p.off + 2), hint, p.len);  // 0xb9 and generic: same ports
+    if (hint == 0x36) { raw_new(h, g.b(p.off), g.b(p.off + 1), hint, p.len); raw_payload(h, p, 2); }  // :271-283
+    else { raw_new(h, g.be16(p.off), g.be16(p.off + 2), hint, p.len); raw_payload(h, p, hint == 0xb9 ? 4 : 0); }  // :249-304
     return true;
 }
 
@@ -307,25 +328,48 @@ __device__ __forceinline__ void raw_extract_ips(const G& g, Span q, RawHdr& h) {
     }
 }
 
-// ethertypes/mod.rs:20-61 parse_ethertype (its 0x0806 arm is unreachable from
-// parse_fluereflow, which handles ARP itself)
+// ethertypes/mod.rs:136-159 analyze_packet_structure -> payload start (len = none)
+__device__ __forceinline__ uint32_t raw_custom_payload_start(const G& g, Span p) {
+    const uint32_t b = g.b(p.off);
+    const uint32_t hs = (b >= 0xB8 && b <= 0xBF) ? 8u : (b == 0x36 || b == 0x37) ? 6u : 4u;
+    const bool has = (b >= 0xB8 && b <= 0xBF) || b == 0x36 || b == 0x37 || b == 0x6C || p.len > 4;
+    return (has && p.len > hs) ? hs : 0xFFFFFFFFu;
+}
+
+// ethertypes/mod.rs:20-61 parse_ethertype.  Its 0x0806 arm (arp.rs:3-44) is
+// unreachable from parse_fluereflow, which handles ARP itself; it is here so
+// the reference's parse_ethertype tests pin this function whole.
 __device__ __forceinline__ bool raw_parse_ethertype(const G& g, Span p, uint32_t et, RawHdr& h) {
     if (et == 0x0A08 || et == 0x4B65) {  // vpn.rs:15-56, :58-99
         if (p.len < 4) return false;
         raw_new(h, et == 0x0A08 ? 2186 : 19301, g.be16(p.off + 2), et == 0x0A08 ? 21 : 22, p.len);
+        raw_payload(h, p, 4);
         raw_extract_ips(g, {p.off + 4, p.len - 4}, h);
+        return true;
+    }
+    if (et == 0x0806) {  // arp.rs:3-44
+        if (p.len < 28) return false;
+        raw_new(h, g.be16(p.off + 6), 0, 0x08, p.len);
+        h.has_src = h.has_dst = true;
+        ip4_words(g, p.off + 14, h.src); ip4_words(g, p.off + 24, h.dst);
+        h.has_ethertype = true; h.ethertype = 0x0806;
         return true;
     }
     if (et == 0x8847 || et == 0x8848) {  // mpls.rs:3-40
         if (p.len < 4) return false;
         const uint32_t label = (g.b(p.off) << 12) | (g.b(p.off + 1) << 4) | (g.b(p.off + 2) >> 4);
         raw_new(h, label & 0xFFFF, (g.b(p.off + 2) >> 1) & 7, 137, p.len);
+        uint32_t off = 4;  // label stack walk (:18-26)
+        if (!(g.b(p.off + 2) & 1))
+            while (off + 4 <= p.len && !(g.b(p.off + off + 2) & 1)) off += 4;
+        raw_payload(h, p, off);
         return true;
     }
     if (et == 0x12B5) {  // vxlan.rs:8-48
         if (p.len < 8 || !(g.be32(p.off) == 0x08000000u && g.be32(p.off + 4) == 0x00006400u)) return false;
         const uint32_t vni = (g.b(p.off + 4) << 16) | (g.b(p.off + 5) << 8) | g.b(p.off + 6);
         raw_new(h, 4789, vni & 0xFFFF, 0x12, p.len);
+        raw_payload(h, p, 8);
         return true;
     }
     if (et == 0x88B8) {  // wireguard.rs:12-80
@@ -337,11 +381,17 @@ __device__ __forceinline__ bool raw_parse_ethertype(const G& g, Span p, uint32_t
         if (t == 4 && p.len < 16) return false;
         if (t < 1 || t > 4) return false;
         raw_new(h, 0, 51820, t, p.len);
+        raw_payload(h, p, 0);
+        h.has_flags = true; h.flags = (uint8_t)t;
+        h.has_version = true; h.version = 1;
+        h.has_ethertype = true; h.ethertype = 0x88B8;
         return true;
     }
-    if ((et >= 0xB800 && et <= 0xBFFF) || (et >= 0x3600 && et <= 0x36FF)) {  // mod.rs:110-137
+    if ((et >= 0xB800 && et <= 0xBFFF) || (et >= 0x3600 && et <= 0x36FF)) {  // mod.rs:107-134
         if (p.len < 4) return false;
         raw_new(h, g.be16(p.off), g.be16(p.off + 2), g.b(p.off), p.len);
+        const uint32_t ps = raw_custom_payload_start(g, p);
+        if (ps != 0xFFFFFFFFu) raw_payload(h, p, ps);
         return true;
     }
     return false;

@@ -141,8 +141,10 @@ class ShardExchange:
             self._recv = torch.empty(world * blk, dtype=torch.uint8, device=device)
         return blk
 
-    def step(self):
-        """One sharded pass; the merge stats on rank dst, None elsewhere."""
+    def step(self, allow_unsupported: bool = False):
+        """One sharded pass; the merge stats on rank dst, None elsewhere.
+        Raises FluereError when the merge cannot give the exact result
+        (FLUERE_E_UNSUPPORTED) unless allow_unsupported."""
         import torch
         import torch.distributed as dist
         L = _lib.lib()
@@ -173,7 +175,7 @@ class ShardExchange:
             return None
         st = Stats()
         rc = L.fluere_merge_gathered(ctx._h, self._recv.data_ptr(), world, self.cap, ctypes.byref(st))
-        if rc != _lib.E_UNSUPPORTED:
+        if rc != _lib.E_UNSUPPORTED or not allow_unsupported:
             check(rc, "fluere_merge_gathered")
         d = st.as_dict()
         d["rc"] = rc

@@ -44,7 +44,7 @@ enum fluere_status {
     FLUERE_E_HIP = -4,         /* HIP runtime error / no device */
     FLUERE_E_NOMEM = -5,       /* device or host allocation failed */
     FLUERE_E_TABLE_FULL = -6,  /* flow dictionary capacity exceeded: reopen with larger max_flows */
-    FLUERE_E_UNSUPPORTED = -7, /* input needs a parser class not yet on the GPU (see stats) */
+    FLUERE_E_UNSUPPORTED = -7, /* the sharded merge cannot give the exact result (expiries inside the capture) */
     FLUERE_E_STATE = -8        /* call order violated */
 };
 
@@ -53,8 +53,7 @@ enum fluere_pkt_status {
     FLUERE_PKT_OK = 0,
     FLUERE_PKT_EMPTY = 1,         /* NetError::EmptyPacket */
     FLUERE_PKT_INVALID = 2,       /* NetError::InvalidPacket */
-    FLUERE_PKT_UNKNOWN_ETHER = 3, /* NetError::UnknownEtherType */
-    FLUERE_PKT_RAW = 0xFE         /* needs src/net/parser/raw (not yet on the GPU) */
+    FLUERE_PKT_UNKNOWN_ETHER = 3  /* NetError::UnknownEtherType */
 };
 
 /* The fluereflow record with a C layout.  IpAddr is {v6 flag, 16 bytes}
@@ -104,7 +103,7 @@ typedef struct fluere_stats {
     uint64_t valid;            /* passed parse_keys and parse_fluereflow */
     uint64_t updates;          /* valid and not dropped by the TCP SYN gate */
     uint64_t dropped_parse;    /* parse_keys or parse_fluereflow returned Err */
-    uint64_t unsupported;      /* packets in FLUERE_PKT_RAW class */
+    uint64_t unsupported;      /* always 0: every parser class runs on the GPU (kept for the ABI layout) */
     uint64_t flows;            /* distinct canonical flow keys */
     uint64_t complex_flows;    /* flows resolved by the exact per-flow state machine */
     uint64_t records;          /* emitted records */
@@ -233,6 +232,41 @@ int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shar
 /* Test seam: insert n canonical keys (14 u32 words each, device memory) into
  * the flow dictionary and write each key's dense flow id. */
 int fluere_debug_dense_ids(fluere_ctx* ctx, const uint32_t* d_keys, uint64_t n, uint32_t* d_out);
+
+/* Test seam (parser probe): run the device restatement of one entry point of
+ * the raw fallback (src/net/parser/raw, reached from parse_ports ports.rs:47,
+ * the parse_keys eager chain keys.rs:279-296 and parse_fluereflow
+ * fluereflows.rs:148-195) over n byte strings, so the reference's own unit
+ * tests of those functions pin the GPU code directly:
+ *   FLUERE_RAW_FROM_RAW_PACKET  RawProtocolHeader::from_raw_packet(p, arg as u8)  raw/mod.rs:152
+ *   FLUERE_RAW_FROM_ETHERTYPE   RawProtocolHeader::from_ethertype(p, arg as u16)  raw/mod.rs:330
+ *   FLUERE_RAW_PARSE_ETHERTYPE  ethertypes::parse_ethertype(p, arg)               raw/ethertypes/mod.rs:20
+ *   FLUERE_RAW_PARSE_PROTOCOL   protocols::parse_protocol(p, arg)                 raw/protocols/mod.rs:48
+ *   FLUERE_RAW_OPENVPN          OpenVpnParser::parse_packet                       raw/protocols/openvpn.rs:155
+ *   FLUERE_RAW_ICMP             IcmpParser::parse_packet                          raw/protocols/icmp.rs:10
+ * String i is d_bytes[d_off[i], d_off[i] + d_len[i]) (device memory); the
+ * result (Some / None and the RawProtocolHeader fields) goes to d_out[i]. */
+enum {
+    FLUERE_RAW_FROM_RAW_PACKET = 0,
+    FLUERE_RAW_FROM_ETHERTYPE = 1,
+    FLUERE_RAW_PARSE_ETHERTYPE = 2,
+    FLUERE_RAW_PARSE_PROTOCOL = 3,
+    FLUERE_RAW_OPENVPN = 4,
+    FLUERE_RAW_ICMP = 5
+};
+typedef struct fluere_raw_hdr {
+    uint8_t some;                      /* Option<RawProtocolHeader>::is_some() */
+    uint8_t has_src, has_dst, ip_v6;   /* src_ip / dst_ip: Some, and IpAddr::V6 */
+    uint8_t src[16], dst[16];          /* IPv4 in the first 4 bytes */
+    uint16_t src_port, dst_port;
+    uint8_t protocol, has_flags, flags, has_version;
+    uint8_t version, has_ethertype, has_payload, pad0;
+    uint16_t length, ethertype;
+    uint32_t payload_off, payload_len; /* payload = the string's bytes [off, off + len) */
+    uint32_t pad1;
+} fluere_raw_hdr;                      /* 64 bytes */
+int fluere_debug_raw(int fn, const uint8_t* d_bytes, const uint32_t* d_off, const uint32_t* d_len,
+                     const uint32_t* d_arg, uint64_t n, fluere_raw_hdr* d_out, void* stream);
 
 /* ---- egress -------------------------------------------------------------- */
 /* Write the CSV exactly as fluere_exporter does (header + one row per record). */

@@ -55,23 +55,29 @@ static span v6_payload(span i) {
 }
 
 /* ---- raw fallback: src/net/parser/raw ---------------------------------- */
-typedef struct {
-    int has_src, has_dst;
-    or_ip src, dst;
-    uint16_t sport, dport;
-    uint8_t proto;
-    uint16_t length;
-} raw_hdr;
+/* RawProtocolHeader (raw/mod.rs:9-37), the fields the reference's own tests
+ * and the hot path read; payload as a slice [payload_off, +payload_len) of
+ * the parsed bytes (Some/None in has_payload). */
+typedef or_raw_hdr raw_hdr;
 
+/* raw/mod.rs:40-71 RawProtocolHeader::new (Option fields None) */
 static void raw_new(raw_hdr* h, uint16_t sp, uint16_t dp, uint8_t proto, uint32_t len) {
     memset(h, 0, sizeof *h);
     h->sport = sp; h->dport = dp; h->proto = proto; h->length = (uint16_t)len;
 }
+static void raw_payload(raw_hdr* h, span p, uint32_t off) {
+    h->has_payload = 1;
+    h->payload_off = off < p.n ? off : p.n;
+    h->payload_len = p.n - h->payload_off;
+}
 
-/* protocols/icmp.rs:95-131 */
+/* protocols/icmp.rs:10-48 IcmpParser::parse_packet */
 static int raw_icmp(span p, raw_hdr* h) {
     if (p.n < 4) return 0;
     raw_new(h, p.p[0], p.p[1], 1, p.n);
+    if (p.n > 4) raw_payload(h, p, 4);
+    h->has_flags = 1; h->flags = p.p[0];     /* with_flags(icmp_type) */
+    h->has_version = 1; h->version = p.p[1]; /* with_version(icmp_code) */
     return 1;
 }
 
@@ -81,6 +87,7 @@ static int raw_openvpn(span p, raw_hdr* h) {
     uint8_t t = p.p[0];
     if (!((t >= 1 && t <= 9) || t == 0x40 || t == 0x41)) return 0;
     raw_new(h, t, 0, 0x9B, p.n);
+    raw_payload(h, p, 9);
     if (t == 6 || t == 9) {
         span ip = sp_from(p, 9);
         if (ip.n >= 16 && ((ip.p[0] >> 4) & 0x0F) == 4) {
@@ -100,7 +107,7 @@ static int raw_openvpn(span p, raw_hdr* h) {
     return 1;
 }
 
-/* protocols/mod.rs:48-84 */
+/* protocols/mod.rs:48-84 parse_protocol */
 static int raw_parse_protocol(span p, uint8_t proto, raw_hdr* h) {
     if (proto == 1 && raw_icmp(p, h)) return 1;
     if (proto >= 170 && proto <= 172 && raw_openvpn(p, h)) return 1;
@@ -136,12 +143,14 @@ static int raw_from_raw_packet(span p, uint8_t hint, raw_hdr* h) {
     }
     if (outer) {
         raw_new(h, osp, odp, oproto, p.n);
+        raw_payload(h, p, 0);
         h->has_src = h->has_dst = 1; h->src = os; h->dst = od;
         return 1;
     }
     if (p.n < 4) return 0;
-    if (hint == 0x36) raw_new(h, p.p[0], p.p[1], hint, p.n);
-    else raw_new(h, be16(p.p), be16(p.p + 2), hint, p.n); /* 0xb9 and generic: same ports */
+    if (hint == 0x36) { raw_new(h, p.p[0], p.p[1], hint, p.n); raw_payload(h, p, 2); }           /* :271-283 */
+    else if (hint == 0xb9) { raw_new(h, be16(p.p), be16(p.p + 2), hint, p.n); raw_payload(h, p, 4); } /* :249-270 */
+    else { raw_new(h, be16(p.p), be16(p.p + 2), hint, p.n); raw_payload(h, p, 0); }             /* :284-304 */
     return 1;
 }
 
@@ -152,25 +161,49 @@ static void raw_extract_ips(span q, raw_hdr* h) {
     if ((q.p[0] >> 4) == 6 && q.n >= 40) { h->has_src = h->has_dst = 1; ip6(&h->src, q.p + 8); ip6(&h->dst, q.p + 24); }
 }
 
-/* ethertypes/mod.rs:20-61 parse_ethertype (0x0806 arm is unreachable from
- * parse_fluereflow, which handles ARP itself). */
+/* ethertypes/mod.rs:136-159 analyze_packet_structure */
+void or_raw_analyze_structure(const uint8_t* p, uint32_t n, uint32_t* header_size, int* has_payload) {
+    uint8_t b = n ? p[0] : 0;
+    if (b >= 0xB8 && b <= 0xBF) { *header_size = 8; *has_payload = 1; }
+    else if (b == 0x36 || b == 0x37) { *header_size = 6; *has_payload = 1; }
+    else if (b == 0x6C) { *header_size = 4; *has_payload = 1; }
+    else { *header_size = 4; *has_payload = n > 4; }
+}
+
+/* ethertypes/mod.rs:20-61 parse_ethertype.  Its 0x0806 arm (arp.rs:3-44) is
+ * unreachable from parse_fluereflow, which handles ARP itself; it is kept so
+ * the reference's parse_ethertype tests pin this function whole. */
 static int raw_parse_ethertype(span p, uint16_t et, raw_hdr* h) {
     if (et == 0x0A08 || et == 0x4B65) { /* vpn.rs:15-56, :58-99 */
         if (p.n < 4) return 0;
         raw_new(h, et == 0x0A08 ? 2186 : 19301, be16(p.p + 2), et == 0x0A08 ? 21 : 22, p.n);
+        raw_payload(h, p, 4);
         raw_extract_ips(sp_from(p, 4), h);
+        return 1;
+    }
+    if (et == 0x0806) { /* arp.rs:3-44 */
+        if (p.n < 28) return 0;
+        raw_new(h, be16(p.p + 6), 0, 0x08, p.n);
+        h->has_src = h->has_dst = 1;
+        ip4(&h->src, p.p + 14); ip4(&h->dst, p.p + 24);
+        h->has_ethertype = 1; h->ethertype = 0x0806;
         return 1;
     }
     if (et == 0x8847 || et == 0x8848) { /* mpls.rs:3-40 */
         if (p.n < 4) return 0;
         uint32_t label = ((uint32_t)p.p[0] << 12) | ((uint32_t)p.p[1] << 4) | ((uint32_t)p.p[2] >> 4);
         raw_new(h, (uint16_t)label, (p.p[2] >> 1) & 7, 137, p.n);
+        uint32_t off = 4;  /* label stack walk (:18-26) */
+        if (!(p.p[2] & 1))
+            while (off + 4 <= p.n && !(p.p[off + 2] & 1)) off += 4;
+        raw_payload(h, p, off);
         return 1;
     }
     if (et == 0x12B5) { /* vxlan.rs:8-48 */
         if (p.n < 8 || memcmp(p.p, VXLAN_HEADER, 8) != 0) return 0;
         uint32_t vni = ((uint32_t)p.p[4] << 16) | ((uint32_t)p.p[5] << 8) | p.p[6];
         raw_new(h, 4789, (uint16_t)vni, 0x12, p.n);
+        raw_payload(h, p, 8);
         return 1;
     }
     if (et == 0x88B8) { /* wireguard.rs:12-80 */
@@ -182,11 +215,18 @@ static int raw_parse_ethertype(span p, uint16_t et, raw_hdr* h) {
         if (t == 4 && p.n < 16) return 0;
         if (t < 1 || t > 4) return 0;
         raw_new(h, 0, 51820, t, p.n);
+        raw_payload(h, p, 0);
+        h->has_flags = 1; h->flags = t;
+        h->has_version = 1; h->version = 1;
+        h->has_ethertype = 1; h->ethertype = 0x88B8;
         return 1;
     }
-    if ((et >= 0xB800 && et <= 0xBFFF) || (et >= 0x3600 && et <= 0x36FF)) { /* mod.rs:110-137 */
+    if ((et >= 0xB800 && et <= 0xBFFF) || (et >= 0x3600 && et <= 0x36FF)) { /* mod.rs:107-134 */
         if (p.n < 4) return 0;
         raw_new(h, be16(p.p), be16(p.p + 2), p.p[0], p.n);
+        uint32_t hs; int hp;
+        or_raw_analyze_structure(p.p, p.n, &hs, &hp);
+        if (hp && p.n > hs) raw_payload(h, p, hs);
         return 1;
     }
     return 0;
@@ -198,6 +238,22 @@ static int raw_from_ethertype(span p, uint16_t et, raw_hdr* h) {
     if (et == 0x0800 && p.n >= 20) return raw_from_raw_packet(p, p.p[9], h);
     return raw_from_raw_packet(p, (uint8_t)et, h);
 }
+
+/* exported for the pinning tests (tests/test_oracle.py) */
+int or_raw_from_raw_packet(const uint8_t* p, uint32_t n, uint8_t hint, or_raw_hdr* h) {
+    return raw_from_raw_packet(sp_make(p, n), hint, h);
+}
+int or_raw_from_ethertype(const uint8_t* p, uint32_t n, uint16_t et, or_raw_hdr* h) {
+    return raw_from_ethertype(sp_make(p, n), et, h);
+}
+int or_raw_parse_ethertype(const uint8_t* p, uint32_t n, uint16_t et, or_raw_hdr* h) {
+    return raw_parse_ethertype(sp_make(p, n), et, h);
+}
+int or_raw_parse_protocol(const uint8_t* p, uint32_t n, uint8_t proto, or_raw_hdr* h) {
+    return raw_parse_protocol(sp_make(p, n), proto, h);
+}
+int or_raw_openvpn(const uint8_t* p, uint32_t n, or_raw_hdr* h) { return raw_openvpn(sp_make(p, n), h); }
+int or_raw_icmp(const uint8_t* p, uint32_t n, or_raw_hdr* h) { return raw_icmp(sp_make(p, n), h); }
 
 /* ---- ports / flags / tos ------------------------------------------------ */
 /* src/net/parser/ports.rs:7-58 */

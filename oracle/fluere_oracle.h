@@ -10,7 +10,10 @@
  * Parity pinning: the reference is Rust and cannot be built here (no
  * cargo/rustc, no libpcap).  This restatement is pinned by
  * the reference's own byte fixtures (src/net/parser/ipv4.rs:74-106,
- * udp.rs:49-89) and the known-answer rows derived from the reference
+ * udp.rs:49-89), by the reference's unit tests of the raw fallback the hot
+ * path reaches (raw/mod.rs:353-673, raw/ethertypes/mod.rs:162-346,
+ * raw/protocols/openvpn.rs:226-334, raw/protocols/icmp.rs:51-74; transcribed
+ * in tests/test_oracle.py) and the known-answer rows derived from the reference
  * source.  Third-party behaviour (pnet 0.35,
  * libpcap via pcap 2.3, csv 1.3, Rust std Display) is restated from
  * their published semantics; see SURVEY.md Appendix C.
@@ -87,6 +90,39 @@ int or_parse_keys(const uint8_t* d, uint32_t len, or_key* key, or_key* rev, int*
 /* parse_fluereflow (src/net/parser/fluereflows.rs:30-199). */
 int or_parse_fluereflow(const uint8_t* d, uint32_t len, uint64_t sec, uint64_t usec,
                         uint64_t* doctets, uint8_t flags[9], or_record* rec, int* raw_used);
+
+/* RawProtocolHeader (src/net/parser/raw/mod.rs:9-37): the fields the
+ * reference's own unit tests and the hot path read.  Option<T> fields carry
+ * a has_ flag; payload is the slice [payload_off, payload_off + payload_len)
+ * of the parsed bytes. */
+typedef struct {
+    uint8_t has_src, has_dst;
+    or_ip src, dst;
+    uint16_t sport, dport;
+    uint8_t proto;
+    uint16_t length;
+    uint8_t has_flags, flags, has_version, version;
+    uint8_t has_ethertype;
+    uint16_t ethertype;
+    uint8_t has_payload;
+    uint32_t payload_off, payload_len;
+} or_raw_hdr;
+
+/* The raw fallback's entry points; 1 = Some(header), 0 = None.
+ *   or_raw_from_raw_packet   raw/mod.rs:152-328
+ *   or_raw_from_ethertype    raw/mod.rs:330-349
+ *   or_raw_parse_ethertype   raw/ethertypes/mod.rs:20-61
+ *   or_raw_parse_protocol    raw/protocols/mod.rs:48-84
+ *   or_raw_openvpn           raw/protocols/openvpn.rs:155-220
+ *   or_raw_icmp              raw/protocols/icmp.rs:10-48
+ *   or_raw_analyze_structure raw/ethertypes/mod.rs:136-159 */
+int or_raw_from_raw_packet(const uint8_t* p, uint32_t n, uint8_t hint, or_raw_hdr* h);
+int or_raw_from_ethertype(const uint8_t* p, uint32_t n, uint16_t et, or_raw_hdr* h);
+int or_raw_parse_ethertype(const uint8_t* p, uint32_t n, uint16_t et, or_raw_hdr* h);
+int or_raw_parse_protocol(const uint8_t* p, uint32_t n, uint8_t proto, or_raw_hdr* h);
+int or_raw_openvpn(const uint8_t* p, uint32_t n, or_raw_hdr* h);
+int or_raw_icmp(const uint8_t* p, uint32_t n, or_raw_hdr* h);
+void or_raw_analyze_structure(const uint8_t* p, uint32_t n, uint32_t* header_size, int* has_payload);
 
 /* Classic pcap record index (libpcap offline semantics). */
 typedef struct {

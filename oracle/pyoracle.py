@@ -29,6 +29,22 @@ class _Result(ctypes.Structure):
                 ("loop_seconds", ctypes.c_double), ("cap", ctypes.c_uint64)]
 
 
+class _OrIp(ctypes.Structure):
+    _fields_ = [("v6", ctypes.c_uint8), ("b", ctypes.c_uint8 * 16)]
+
+
+class _OrRawHdr(ctypes.Structure):
+    _fields_ = [("has_src", ctypes.c_uint8), ("has_dst", ctypes.c_uint8), ("src", _OrIp), ("dst", _OrIp),
+                ("sport", ctypes.c_uint16), ("dport", ctypes.c_uint16), ("proto", ctypes.c_uint8),
+                ("length", ctypes.c_uint16), ("has_flags", ctypes.c_uint8), ("flags", ctypes.c_uint8),
+                ("has_version", ctypes.c_uint8), ("version", ctypes.c_uint8), ("has_ethertype", ctypes.c_uint8),
+                ("ethertype", ctypes.c_uint16), ("has_payload", ctypes.c_uint8), ("payload_off", ctypes.c_uint32),
+                ("payload_len", ctypes.c_uint32)]
+
+
+_RAW_FNS = ["or_raw_from_raw_packet", "or_raw_from_ethertype", "or_raw_parse_ethertype", "or_raw_parse_protocol",
+            "or_raw_openvpn", "or_raw_icmp"]
+
 _lib = None
 
 
@@ -53,6 +69,14 @@ def lib():
         L.or_parse_batch.restype = ctypes.c_int
         L.or_pcap_index.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
         L.or_pcap_index.restype = ctypes.c_int64
+        for i, name in enumerate(_RAW_FNS):
+            fn = getattr(L, name)
+            fn.restype = ctypes.c_int
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32] + ([ctypes.c_uint32] if i < 4 else []) + \
+                [ctypes.POINTER(_OrRawHdr)]
+        L.or_raw_analyze_structure.restype = None
+        L.or_raw_analyze_structure.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                               ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -97,3 +121,33 @@ def time_offline_cli(path: str, timeout_ms: int = 600000, use_mac: bool = False,
         pass
     out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
     return json.loads(out.strip().splitlines()[-1])
+
+
+def _ip(has, ip):
+    if not has:
+        return None
+    return bytes(ip.b) if ip.v6 else bytes(ip.b[:4])
+
+
+def raw_call(fn: int, data: bytes, arg: int = 0) -> dict:
+    """One raw-fallback entry point of the oracle (tests/raw_vectors.py codes)
+    -> the RawProtocolHeader as a dict (see tests/raw_vectors.py)."""
+    L = lib()
+    buf = (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(data + b"\0")
+    h = _OrRawHdr()
+    args = [buf, len(data)] + ([arg] if fn < 4 else []) + [ctypes.byref(h)]
+    some = getattr(L, _RAW_FNS[fn])(*args)
+    if not some:
+        return dict(some=False)
+    return dict(some=True, src=_ip(h.has_src, h.src), dst=_ip(h.has_dst, h.dst), src_port=h.sport, dst_port=h.dport,
+                protocol=h.proto, length=h.length, flags=h.flags if h.has_flags else None,
+                version=h.version if h.has_version else None, ethertype=h.ethertype if h.has_ethertype else None,
+                payload=data[h.payload_off:h.payload_off + h.payload_len] if h.has_payload else None)
+
+
+def analyze_structure(data: bytes):
+    L = lib()
+    buf = (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(data + b"\0")
+    hs, hp = ctypes.c_uint32(), ctypes.c_int()
+    L.or_raw_analyze_structure(buf, len(data), ctypes.byref(hs), ctypes.byref(hp))
+    return hs.value, bool(hp.value)

@@ -6,6 +6,13 @@
   (tv_sec 1672986985, tv_usec 100000; ipv4.rs:58-65).  Its expected CSV row
   (``ref_ipv4_frame.expected.csv``) is derived from the reference source
    -- it pins the oracle, it is not produced by it.
+* ``ref_raw_vectors.pcap``: every byte vector of the reference's unit tests
+  of the raw fallback (tests/raw_vectors.py, transcribed from
+  src/net/parser/raw/**) inside frames that reach the call sites of those
+  parsers on the hot path: the parse_keys eager chain over an unknown
+  ethertype whose low byte is the test's protocol hint (keys.rs:279-296),
+  parse_fluereflow's from_ethertype arm (fluereflows.rs:148-195) and
+  parse_ports for an unknown IP protocol (ports.rs:47).
 * ``edge_*.pcap``: hand-built captures for every edge the hot path has
   (SURVEY.md Appendix B.3).  Their golden CSVs are produced by the C oracle
   (oracle/fluere_oracle.c) and committed, so the GPU box needs neither the
@@ -190,7 +197,35 @@ def fixtures():
         U(0, 2100, eth() + ipv4(B, A, 17, udp(2, 1, b"\x64" * 10))),
         U(0, 4000, eth() + ipv4(A, B, 6, tcp(3, 4, SYN))),
     ]
+    F["ref_raw_vectors"] = raw_vector_frames()
     return F
+
+
+def raw_vector_frames():
+    import raw_vectors as RV
+    out, k = [], 0
+    special = {0, 1, 2, 4, 6, 17, 47, 50, 51, 53, 58}
+    # from_ethertype reads the whole frame from the destination MAC on: a first
+    # byte outside the OpenVPN packet types keeps its heuristic out of the way
+    M = "5e:00:00:00:00:02"
+    for name, where, fn, data, arg, check in RV.VECTORS:
+        frames = []
+        if fn in (RV.FROM_RAW_PACKET, RV.PARSE_PROTOCOL, RV.OPENVPN, RV.ICMP):
+            hint = arg & 0xFF
+            frames.append(eth(M, et=0x9900 | hint) + data)          # eager chain: from_raw_packet(payload, et as u8)
+            if hint not in special and len(data) < 8:           # parse_ports -> from_raw_packet(l4, proto)
+                frames.append(eth(M) + ipv4("10.7.0.1", "10.7.0.2", hint, data))
+        if fn in (RV.FROM_ETHERTYPE, RV.PARSE_ETHERTYPE):
+            frames.append(eth(M, et=arg) + data)                 # parse_fluereflow: from_ethertype(frame, et)
+        if fn == RV.ICMP:
+            frames.append(eth(M) + ipv4("10.7.0.3", "10.7.0.4", 1, data + b"\x00"))
+        for f in frames:
+            out.append(U(0, k, f))
+            k += 1
+    for data, size, has in RV.ANALYZE_STRUCTURE:
+        out.append(U(0, k, eth(M, et=0x3601) + data))
+        k += 1
+    return out
 
 
 # (timeout_ms, use_mac) combinations checked per fixture

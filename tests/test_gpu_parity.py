@@ -348,3 +348,55 @@ def test_vlan_frames_drop_or_misparse(gpu):
         want = pyoracle.offline(data, use_mac=use_mac)
         csv, ne, st = _gpu_csv(data, use_mac=use_mac)
         assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"vlan_mac{int(use_mac)}")
+
+
+# ---- the reference's unit tests of the raw fallback, on the device functions
+import raw_vectors as RV  # noqa: E402
+
+
+def _gpu_raw(calls):
+    """calls: [(fn, bytes, arg)] -> one header dict per call (fluere_debug_raw)."""
+    out = []
+    for fn in sorted({c[0] for c in calls}):
+        idx = [i for i, c in enumerate(calls) if c[0] == fn]
+        blob, offs, lens, args = b"", [], [], []
+        for i in idx:
+            offs.append(len(blob))
+            lens.append(len(calls[i][1]))
+            args.append(calls[i][2])
+            blob += calls[i][1]
+        d_b = torch.tensor(list(blob + bytes(64)), dtype=torch.uint8, device="cuda")
+        d_o = torch.tensor(offs, dtype=torch.int32, device="cuda")
+        d_l = torch.tensor(lens, dtype=torch.int32, device="cuda")
+        d_a = torch.tensor(args, dtype=torch.int32, device="cuda")
+        d_out = torch.zeros(len(idx) * 64, dtype=torch.uint8, device="cuda")
+        _lib.check(_lib.lib().fluere_debug_raw(fn, d_b.data_ptr(), d_o.data_ptr(), d_l.data_ptr(), d_a.data_ptr(),
+                                               len(idx), d_out.data_ptr(), None), "debug_raw")
+        rows = d_out.cpu().numpy().view(_lib.RAW_HDR_DTYPE)
+        for i, r in zip(idx, rows):
+            data = calls[i][1]
+            ipb = (lambda b: bytes(b) if r["ip_v6"] else bytes(b[:4]))
+            h = dict(some=bool(r["some"]))
+            if h["some"]:
+                h.update(src=ipb(r["src"]) if r["has_src"] else None, dst=ipb(r["dst"]) if r["has_dst"] else None,
+                         src_port=int(r["src_port"]), dst_port=int(r["dst_port"]), protocol=int(r["protocol"]),
+                         length=int(r["length"]), flags=int(r["flags"]) if r["has_flags"] else None,
+                         version=int(r["version"]) if r["has_version"] else None,
+                         ethertype=int(r["ethertype"]) if r["has_ethertype"] else None,
+                         payload=data[r["payload_off"]:r["payload_off"] + r["payload_len"]] if r["has_payload"] else None)
+            out.append((i, h))
+    return [h for _, h in sorted(out, key=lambda x: x[0])]
+
+
+def test_reference_raw_vectors_on_device(gpu):
+    """Every transcribed reference assertion (raw/mod.rs, ethertypes/mod.rs,
+    openvpn.rs, icmp.rs tests) holds for the device functions, and every field
+    equals the oracle's."""
+    calls = [(fn, data, arg) for _, _, fn, data, arg, _ in RV.VECTORS]
+    calls += [(RV.PARSE_ETHERTYPE, data, 0x3601) for data, _, _ in RV.ANALYZE_STRUCTURE]
+    got = _gpu_raw(calls)
+    for (name, where, fn, data, arg, check), h in zip(RV.VECTORS, got):
+        check(h)
+        assert h == pyoracle.raw_call(fn, data, arg), f"{name} ({where})"
+    for (data, size, has), h in zip(RV.ANALYZE_STRUCTURE, got[len(RV.VECTORS):]):
+        assert h["some"] and h["payload"] == (data[size:] if has and len(data) > size else None)

@@ -45,3 +45,21 @@ def test_edge_semantics_spot_checks():
     # 8-byte ICMP echo dropped, 9-byte kept (keys.rs:182-184)
     rows = golden_csv("edge_empty_payload.t600000.csv").splitlines()[1:]
     assert len(rows) == 2 and any(",1,1,29," in x for x in rows)
+
+
+# ---- the reference's unit tests of the raw fallback (tests/raw_vectors.py)
+import raw_vectors as RV  # noqa: E402
+
+
+@pytest.mark.parametrize("vec", RV.VECTORS, ids=[v[0] for v in RV.VECTORS])
+def test_reference_raw_vector(vec):
+    name, where, fn, data, arg, check = vec
+    check(pyoracle.raw_call(fn, data, arg))
+
+
+@pytest.mark.parametrize("data,size,has", RV.ANALYZE_STRUCTURE)
+def test_reference_analyze_packet_structure(data, size, has):
+    # ethertypes/mod.rs:321-346, and the payload start parse_custom_protocol takes from it
+    assert pyoracle.analyze_structure(data) == (size, has)
+    h = pyoracle.raw_call(RV.PARSE_ETHERTYPE, data, 0x3601)
+    assert h["some"] and h["payload"] == (data[size:] if has and len(data) > size else None)
