@@ -400,3 +400,23 @@ def test_reference_raw_vectors_on_device(gpu):
         assert h == pyoracle.raw_call(fn, data, arg), f"{name} ({where})"
     for (data, size, has), h in zip(RV.ANALYZE_STRUCTURE, got[len(RV.VECTORS):]):
         assert h["some"] and h["payload"] == (data[size:] if has and len(data) > size else None)
+
+
+def test_offline_file_grows_flow_table(gpu, tmp_path):
+    """fluere_offline_file sizes the flow table from the file size; a capture
+    with more flows than that (59-byte records, one flow each) reopens with a
+    larger table instead of failing (the reference's HashMap has no limit)."""
+    import pktbuild as pb
+    n = 100_000
+    pkts = [(1_700_000_000, i, pb.eth() + pb.ipv4("10.1.0.1", "10.2.0.1", 17, pb.udp(1 + i % 60000, 7 + i // 60000,
+                                                                                     b"z")))
+            for i in range(n)]
+    data = pb.pcap(pkts)
+    assert len(data) // 64 < n
+    path = tmp_path / "many.pcap"
+    path.write_bytes(data)
+    want = pyoracle.offline(data)
+    st = fluere_amd.fluereflow_fileparse(fluere_amd.Args(fluere_amd.Files(file=str(path))), out_dir=str(tmp_path / "o"))
+    got = (tmp_path / "o" / "many_converted.csv").read_text()
+    assert st["records"] == n
+    assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "offline_file many flows")
