@@ -31,7 +31,7 @@ _ERR_NAMES = {
     E_STATE: "call order",
 }
 
-SYNTH_UDP64, SYNTH_IMIX, SYNTH_VLAN64, SYNTH_MAC64 = 0, 1, 2, 3
+SYNTH_UDP64, SYNTH_IMIX, SYNTH_VLAN64, SYNTH_MAC64, SYNTH_TCP = 0, 1, 2, 3, 4
 
 
 class FluereError(RuntimeError):

@@ -1,0 +1,340 @@
+// device.h -- device-side types and helpers shared by the MI355X kernels of
+// fluere_gpu.hip (hot path, finalize, merge) and exact.hip (the exact state
+// machine): batches, per-flow accumulators, run counters, the per-packet
+// front end (parse_keys + parse_fluereflow over a record window), canonical
+// flow keys and the flow dictionary lookup, record building.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/fluere_gpu.h"
+#include "flow_table.h"
+#include "parse.h"
+
+namespace fl {
+
+constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
+// LDS aggregates are flushed every WIN_ITERS steps of BLOCK packets: a window
+// holds at most 61440 packets, so the 16-bit per-direction packet and flag
+// counts and the u32 per-direction byte sums (<= 65535 B per packet) cannot wrap.
+constexpr int WIN_ITERS = 60;
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr unsigned long long NONE64 = ~0ull;
+constexpr uint64_t IDX_MASK = (1ull << 40) - 1;
+
+// Chunk descriptor (one per 64 records, built when a batch is attached, from
+// its offsets): x = offset of the chunk's first record, y = the records'
+// common stride when the 64 records are evenly spaced with a stride of at
+// most 80 B, a multiple of 16 ("dense": the hot kernel reads the chunk's span
+// with five coalesced loads per lane and reads no offsets), else 0 ("sparse":
+// per-record windows at the record offsets).
+struct Batch {
+    const uint8_t* bytes;
+    const uint32_t* offs;
+    const uint2* desc;    // [n_desc] or null
+    uint64_t n_desc;      // n / 64 (whole chunks)
+    uint64_t nbytes;
+    uint64_t n;
+    uint64_t first;  // global index of packet 0
+    uint32_t snap;
+    uint32_t flags;  // bit0 byte-swapped headers, bit1 nanosecond timestamps
+};
+
+struct Acc {
+    uint32_t* pk[2];
+    unsigned long long* by[2];
+    uint32_t* mn[2];  // min pkt, min ttl
+    uint32_t* mx[2];  // max pkt, max ttl
+    uint32_t* fl[8];  // fin syn rst psh ack urg ece cwr
+    unsigned long long* fa;  // first packet (any)
+    unsigned long long* fc;  // first create-eligible packet
+    unsigned long long* fr;  // first FIN/RST packet
+    unsigned long long* la;  // last packet
+    uint32_t* slots;         // [fmax][N_TABLES] chain slots (cleanup)
+};
+
+struct Glob {
+    unsigned long long valid, dropped, raw;
+    unsigned long long tmin, tmax;
+    unsigned long long n_rec;
+    unsigned long long n_complex, n_complex_pkts;
+    unsigned long long n_keys, n_heads;
+    unsigned long long generic_used;
+    unsigned long long n_slow;
+    unsigned long long n_spill;  // k_parse_agg: spilled packets of the batch (sorted area cursor); next to n_slow
+    unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
+    unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
+    unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
+    unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
+    unsigned long long clean_done;                        // k_cleanup: workgroups finished
+    unsigned long long fin_done;                          // k_finalize: workgroups finished
+};
+static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8, "n_slow, n_spill are reset together");
+// One device allocation holds Glob and the dictionary counters right after it
+// (n_flows, err), so a run ends with ONE small device->host copy.
+struct Ctl {
+    Glob g;
+    uint32_t n_flows, err;
+    uint32_t seq;  // host copy only: k_finalize's last workgroup writes the run's number here last
+    uint32_t pad[13];
+};
+
+#define HIPCHECK(x)                                                                                  \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            if (getenv("FLUERE_HIP_VERBOSE"))                                                        \
+                fprintf(stderr, "[fluere] %s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            return FLUERE_E_HIP;                                                                     \
+        }                                                                                            \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// per-packet front end shared by every kernel
+// ---------------------------------------------------------------------------
+struct Parsed {
+    PktInfo pi;
+    uint64_t t;
+    uint64_t smac, dmac;  // big-endian packed MACs of the keyed frame
+    uint32_t L;
+    uint8_t cls;          // 0 valid, 1 dropped (NetError)
+};
+
+__device__ __forceinline__ uint32_t hdr_word(uint32_t w, bool swapped) { return swapped ? bswap32(w) : w; }
+
+// Five unconditional 16-byte loads (unaligned global_load_dwordx4): record
+// header + the first 64 frame bytes.  Unconditional so the compiler can count
+// outstanding loads and keep the next packet's window in flight; batches are
+// readable 80 bytes past their end (fluere_add_device_batch contract).
+__device__ __forceinline__ void load_win(const Batch& B, uint32_t off, Win& W) {
+    const uint8_t* p = B.bytes + off;
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        uint4 v;
+        __builtin_memcpy(&v, p + 16 * c, 16);
+        W.w[4 * c + 0] = v.x; W.w[4 * c + 1] = v.y; W.w[4 * c + 2] = v.z; W.w[4 * c + 3] = v.w;
+    }
+}
+
+// Pins a loaded window at this point: every word is "used" here, so the
+// compiler cannot sink the five loads into the parser's branches (which turns
+// one memory round trip per packet into three dependent ones).
+__device__ __forceinline__ void pin_win(const Win& W) {
+    asm volatile("" ::"v"(W.w[0]), "v"(W.w[1]), "v"(W.w[2]), "v"(W.w[3]), "v"(W.w[4]), "v"(W.w[5]), "v"(W.w[6]),
+                 "v"(W.w[7]), "v"(W.w[8]), "v"(W.w[9]));
+    asm volatile("" ::"v"(W.w[10]), "v"(W.w[11]), "v"(W.w[12]), "v"(W.w[13]), "v"(W.w[14]), "v"(W.w[15]),
+                 "v"(W.w[16]), "v"(W.w[17]), "v"(W.w[18]), "v"(W.w[19]));
+}
+
+__device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
+    uint64_t m = 0;
+    for (int k = 0; k < 6; k++) m = (m << 8) | p[k];
+    return m;
+}
+
+// mode: 0 production (fast path first), 1 general parser only
+__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P);
+__device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool macs, int mode, Parsed& P) {
+    uint32_t off = B.offs[li];
+    Win W;
+    load_win(B, off, W);
+    parse_loaded(B, off, W, macs, mode, P);
+}
+// The record at batch offset off, its window W already loaded.
+__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P) {
+    bool sw = B.flags & 1;
+    uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
+    uint32_t L = min(incl, B.snap);
+    uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
+    if (L > avail) L = (uint32_t)avail;
+    P.L = L;
+    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);  // time.rs:5-7
+    const uint8_t* fr = B.bytes + off + 16;
+    bool fast = (mode == 0) && parse_fast(W, L, P.pi);
+    if (!fast) {
+        PktInfo g;  // only this copy lives on the stack (parse_general is out of line)
+        parse_general(fr, L, g);
+        P.pi = g;
+    }
+    const PktInfo& pi = P.pi;
+    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;
+    P.smac = P.dmac = 0;
+    if (macs && P.cls == 0) {
+        if (fast) {
+            // frame bytes 0..12 = record bytes 16..28
+            uint64_t d = 0, s = 0;
+            for (int k = 0; k < 6; k++) d = (d << 8) | W.b(16 + k);
+            for (int k = 0; k < 6; k++) s = (s << 8) | W.b(22 + k);
+            P.dmac = d; P.smac = s;
+        } else {
+            P.dmac = mac_be(fr + pi.frame_off);
+            P.smac = mac_be(fr + pi.frame_off + 6);
+        }
+    }
+}
+
+__device__ __forceinline__ int find_batch(const Batch* bs, int nb, uint64_t gi) {
+    int b = 0;
+    while (b + 1 < nb && bs[b + 1].first <= gi) b++;
+    return b;
+}
+
+__device__ __forceinline__ uint8_t canon_dir(const Parsed& P, bool macs) {
+    const PktInfo& pi = P.pi;
+    return src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs) ? 1 : 0;
+}
+
+// Canonical key of a parsed packet.  dir = 1 when the packet travels from the
+// higher endpoint to the lower one.
+__device__ __forceinline__ void canon_key(const Parsed& P, bool macs, CKey& k, uint8_t& dir) {
+    const PktInfo& pi = P.pi;
+    bool gt = src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs);
+    dir = gt ? 1 : 0;
+    uint32_t lop = gt ? pi.kdp : pi.ksp, hip = gt ? pi.ksp : pi.kdp;
+    uint64_t lom = gt ? P.dmac : P.smac, him = gt ? P.smac : P.dmac;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // per-word selects keep the IP arrays in registers
+        k.w[j] = gt ? pi.dip[j] : pi.sip[j];
+        k.w[4 + j] = gt ? pi.sip[j] : pi.dip[j];
+    }
+    k.w[8] = (lop << 16) | hip;
+    uint32_t kind = (pi.v6 ? 1u : 0u) | (macs ? 2u : 0u);
+    k.w[9] = (kind << 8) | pi.kproto;
+    k.w[10] = macs ? (uint32_t)(lom >> 16) : 0; k.w[11] = macs ? (uint32_t)(lom & 0xFFFF) << 16 : 0;
+    k.w[12] = macs ? (uint32_t)(him >> 16) : 0; k.w[13] = macs ? (uint32_t)(him & 0xFFFF) << 16 : 0;
+}
+
+// Exact dense flow id of a canonical key (flow_table.h chains).
+__device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& k, bool insert, uint32_t* chain_out,
+                                                 unsigned long long* generic_used) {
+    const uint32_t kind = k.w[9] >> 8;
+    const bool v6 = kind & 1, macs = kind & 2;
+    uint32_t chain[N_TABLES];
+    for (int j = 0; j < N_TABLES; j++) chain[j] = NONE32;
+    uint32_t s;
+    int ft;
+    unsigned long long v = EMPTY;
+    if (!v6 && !macs) {
+        s = tab_slot(T, 0, ((uint64_t)k.w[0] << 32) | k.w[4], insert);
+        if (s == FAIL) return FAIL;
+        chain[0] = s;
+        s = tab_slot(T, 1, ((uint64_t)s << 40) | ((uint64_t)k.w[8] << 8) | (k.w[9] & 0xFF), insert, &v);
+        if (s == FAIL) return FAIL;
+        chain[1] = s;
+        ft = 1;
+    } else {
+        if (generic_used && insert) *generic_used = 1;
+        // 32-bit units: kind|proto, ports, lo_ip, hi_ip, [lo_mac, hi_mac]
+        uint32_t u[13];
+        u[0] = k.w[9];
+        u[1] = k.w[8];
+        const uint32_t m0 = k.w[10], m1 = k.w[11] | (k.w[12] >> 16), m2 = (k.w[12] << 16) | (k.w[13] >> 16);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            u[2 + j] = v6 ? k.w[j] : (j == 0 ? k.w[0] : j == 1 ? k.w[4] : j == 2 ? m0 : m1);
+            u[6 + j] = v6 ? k.w[4 + j] : (j == 0 ? m2 : 0);
+        }
+        u[10] = m0; u[11] = m1; u[12] = m2;
+        const int m = v6 ? (macs ? 13 : 10) : 7;
+        s = tab_slot(T, 2, ((uint64_t)u[0] << 32) | u[1], insert, &v);
+        if (s == FAIL) return FAIL;
+        chain[2] = s;
+        ft = 2;
+#pragma unroll
+        for (int j = 2; j < 13; j++) {
+            if (j < m) {
+                s = tab_slot(T, j + 1, ((uint64_t)s << 32) | u[j], insert, &v);
+                if (s == FAIL) return FAIL;
+                chain[j + 1] = s;
+                ft = j + 1;
+            }
+        }
+    }
+    return dense_id(T, ft, s, insert, k, chain, chain_out, v);
+}
+
+__device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, bool macs, bool insert,
+                                           uint8_t& dir, uint32_t* chain_out, unsigned long long* generic_used) {
+    CKey k;
+    canon_key(P, macs, k, dir);
+    return dense_of_key(T, k, insert, chain_out, generic_used);
+}
+
+// Append one record (Mode A paths): position, updates and ended counters.
+__device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {
+    const unsigned long long pos = atomicAdd(&g->n_rec, 1ull);
+    if (pos < cap) out[pos] = r;
+    atomicAdd(&g->n_updates, (unsigned long long)r.d_pkts);
+    if (r.order_key != NONE64) atomicAdd(&g->n_ended, 1ull);
+}
+
+__device__ inline void fill_seed(fluere_record& r, const Parsed& P) {
+    const PktInfo& pi = P.pi;
+    memset(&r, 0, sizeof r);
+    r.src_v6 = r.dst_v6 = pi.rv6;
+    for (int k = 0; k < 4; k++) {
+        uint32_t s = pi.rsip[k], d = pi.rdip[k];
+        for (int b = 0; b < 4; b++) {
+            r.source[4 * k + b] = (uint8_t)(s >> (24 - 8 * b));
+            r.destination[4 * k + b] = (uint8_t)(d >> (24 - 8 * b));
+        }
+    }
+    r.prot = pi.rprot; r.tos = pi.rtos;
+    r.src_port = pi.rsp; r.dst_port = pi.rdp;
+    r.min_pkt = r.max_pkt = pi.rpkt;
+    r.min_ttl = r.max_ttl = pi.rttl;
+    r.first = r.last = P.t;
+}
+
+__device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t gi, bool macs, Parsed& P) {
+    int b = find_batch(bs, nb, gi);
+    parse_record(bs[b], gi - bs[b].first, macs, 0, P);
+}
+
+// Wave-aggregated emit_record: one atomic per counter per wave (a thread-per-
+// flow kernel that hits the three run counters per flow serialises on them).
+// All lanes of the wave must call it (want = this lane has a record).
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void emit_record_wave(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r,
+                                                 bool want) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const uint64_t em = __ballot(want && r.order_key != NONE64);
+    const unsigned long long upd = wave_sum(want ? (unsigned long long)r.d_pkts : 0ull);
+    const uint32_t lead = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if ((uint32_t)(threadIdx.x & 63) == lead) {
+        base = atomicAdd(&g->n_rec, (unsigned long long)__popcll(m));
+        atomicAdd(&g->n_updates, upd);
+        if (em) atomicAdd(&g->n_ended, (unsigned long long)__popcll(em));
+    }
+    base = __shfl(base, lead, 64);
+    if (want) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (base + rank < cap) out[base + rank] = r;
+    }
+}
+
+__device__ __forceinline__ void update_flow(fluere_record& r, bool rev, const PktInfo& pi, uint64_t t) {
+    // src/net/flows.rs:11-42 (u32 counters wrap like the release build)
+    r.d_pkts += 1;
+    r.d_octets += pi.doctets;
+    r.max_pkt = max(r.max_pkt, pi.rpkt);
+    r.min_pkt = min(r.min_pkt, pi.rpkt);
+    r.max_ttl = max(r.max_ttl, pi.rttl);
+    r.min_ttl = min(r.min_ttl, pi.rttl);
+    for (int q = 0; q < 8; q++) r.cnt[q] += (pi.tflags >> q) & 1;
+    r.last = t;
+    if (rev) { r.in_pkts += 1; r.in_bytes += pi.doctets; }
+    else { r.out_pkts += 1; r.out_bytes += pi.doctets; }
+}
+
+}  // namespace fl

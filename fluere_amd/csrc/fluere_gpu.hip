@@ -11,11 +11,13 @@
 //   k_finalize    one thread per flow: if the order-free aggregate is exactly
 //                 what the reference state machine would produce (certificate
 //                 below) build the FluereRecord, else mark the flow complex.
-//   complex flows (Mode A: no expiry can fire): their packets are gathered,
-//                 radix-sorted by (flow, packet index) and replayed by an exact
-//                 per-flow state machine (SYN gate, FIN/RST split).
-//   Mode B (capture span >= timeout, so expiries can fire): the exact global
-//                 state machine over per-packet metadata (k_seq_*).
+//   complex flows (Mode A: no expiry can fire) and Mode B (capture span >=
+//                 timeout, so expiries can fire): the exact state machine of
+//                 exact.hip -- packets sorted by (flow, index), a per-flow
+//                 pointer chase over flow instances (SYN gate, FIN/RST split,
+//                 hard-timeout sweep), segmented reductions for the records.
+//                 Mode B captures whose timestamps go backwards fall back to
+//                 the sequential kernel (k_seq_*).
 //
 // Certificate (Mode A, per flow): first create-eligible packet == first
 // packet of the flow (TCP: the first packet carries SYN) and no FIN/RST before
@@ -42,8 +44,8 @@
 #include <vector>
 
 #include "../../include/fluere_gpu.h"
-#include "flow_table.h"
-#include "parse.h"
+#include "device.h"
+#include "exact.h"
 #include "synth.h"
 
 using namespace fl;
@@ -55,253 +57,6 @@ static_assert(sizeof(fluere_shard_header) == 64, "fluere_shard_header ABI");
 static_assert(sizeof(fluere_raw_hdr) == 64, "fluere_raw_hdr ABI");
 
 namespace {
-
-constexpr int BLOCK = 1024;      // hot kernel: one 16-wave workgroup per CU
-// LDS aggregates are flushed every WIN_ITERS steps of BLOCK packets: a window
-// holds at most 61440 packets, so the 16-bit per-direction packet and flag
-// counts and the u32 per-direction byte sums (<= 65535 B per packet) cannot wrap.
-constexpr int WIN_ITERS = 60;
-constexpr uint32_t NONE32 = 0xFFFFFFFFu;
-constexpr unsigned long long NONE64 = ~0ull;
-constexpr uint64_t IDX_MASK = (1ull << 40) - 1;
-
-// Chunk descriptor (one per 64 records, built when a batch is attached, from
-// its offsets): x = offset of the chunk's first record, y = the records'
-// common stride when the 64 records are evenly spaced with a stride of at
-// most 80 B, a multiple of 16 ("dense": the hot kernel reads the chunk's span
-// with five coalesced loads per lane and reads no offsets), else 0 ("sparse":
-// per-record windows at the record offsets).
-struct Batch {
-    const uint8_t* bytes;
-    const uint32_t* offs;
-    const uint2* desc;    // [n_desc] or null
-    uint64_t n_desc;      // n / 64 (whole chunks)
-    uint64_t nbytes;
-    uint64_t n;
-    uint64_t first;  // global index of packet 0
-    uint32_t snap;
-    uint32_t flags;  // bit0 byte-swapped headers, bit1 nanosecond timestamps
-};
-
-struct Acc {
-    uint32_t* pk[2];
-    unsigned long long* by[2];
-    uint32_t* mn[2];  // min pkt, min ttl
-    uint32_t* mx[2];  // max pkt, max ttl
-    uint32_t* fl[8];  // fin syn rst psh ack urg ece cwr
-    unsigned long long* fa;  // first packet (any)
-    unsigned long long* fc;  // first create-eligible packet
-    unsigned long long* fr;  // first FIN/RST packet
-    unsigned long long* la;  // last packet
-    uint32_t* slots;         // [fmax][N_TABLES] chain slots (cleanup)
-};
-
-struct Glob {
-    unsigned long long valid, dropped, raw;
-    unsigned long long tmin, tmax;
-    unsigned long long n_rec;
-    unsigned long long n_complex, n_complex_pkts;
-    unsigned long long n_keys, n_heads;
-    unsigned long long generic_used;
-    unsigned long long n_slow;
-    unsigned long long n_spill;  // k_parse_agg: spilled packets of the batch (sorted area cursor); next to n_slow
-    unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
-    unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
-    unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
-    unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
-    unsigned long long clean_done;                        // k_cleanup: workgroups finished
-    unsigned long long fin_done;                          // k_finalize: workgroups finished
-};
-static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8, "n_slow, n_spill are reset together");
-// One device allocation holds Glob and the dictionary counters right after it
-// (n_flows, err), so a run ends with ONE small device->host copy.
-struct Ctl {
-    Glob g;
-    uint32_t n_flows, err;
-    uint32_t seq;  // host copy only: k_finalize's last workgroup writes the run's number here last
-    uint32_t pad[13];
-};
-
-#define HIPCHECK(x)                                                                                  \
-    do {                                                                                             \
-        hipError_t e_ = (x);                                                                         \
-        if (e_ != hipSuccess) {                                                                      \
-            if (getenv("FLUERE_HIP_VERBOSE"))                                                        \
-                fprintf(stderr, "[fluere] %s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
-            return FLUERE_E_HIP;                                                                     \
-        }                                                                                            \
-    } while (0)
-
-// ---------------------------------------------------------------------------
-// per-packet front end shared by every kernel
-// ---------------------------------------------------------------------------
-struct Parsed {
-    PktInfo pi;
-    uint64_t t;
-    uint64_t smac, dmac;  // big-endian packed MACs of the keyed frame
-    uint32_t L;
-    uint8_t cls;          // 0 valid, 1 dropped (NetError)
-};
-
-__device__ __forceinline__ uint32_t hdr_word(uint32_t w, bool swapped) { return swapped ? bswap32(w) : w; }
-
-// Five unconditional 16-byte loads (unaligned global_load_dwordx4): record
-// header + the first 64 frame bytes.  Unconditional so the compiler can count
-// outstanding loads and keep the next packet's window in flight; batches are
-// readable 80 bytes past their end (fluere_add_device_batch contract).
-__device__ __forceinline__ void load_win(const Batch& B, uint32_t off, Win& W) {
-    const uint8_t* p = B.bytes + off;
-#pragma unroll
-    for (int c = 0; c < 5; c++) {
-        uint4 v;
-        __builtin_memcpy(&v, p + 16 * c, 16);
-        W.w[4 * c + 0] = v.x; W.w[4 * c + 1] = v.y; W.w[4 * c + 2] = v.z; W.w[4 * c + 3] = v.w;
-    }
-}
-
-// Pins a loaded window at this point: every word is "used" here, so the
-// compiler cannot sink the five loads into the parser's branches (which turns
-// one memory round trip per packet into three dependent ones).
-__device__ __forceinline__ void pin_win(const Win& W) {
-    asm volatile("" ::"v"(W.w[0]), "v"(W.w[1]), "v"(W.w[2]), "v"(W.w[3]), "v"(W.w[4]), "v"(W.w[5]), "v"(W.w[6]),
-                 "v"(W.w[7]), "v"(W.w[8]), "v"(W.w[9]));
-    asm volatile("" ::"v"(W.w[10]), "v"(W.w[11]), "v"(W.w[12]), "v"(W.w[13]), "v"(W.w[14]), "v"(W.w[15]),
-                 "v"(W.w[16]), "v"(W.w[17]), "v"(W.w[18]), "v"(W.w[19]));
-}
-
-__device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
-    uint64_t m = 0;
-    for (int k = 0; k < 6; k++) m = (m << 8) | p[k];
-    return m;
-}
-
-// mode: 0 production (fast path first), 1 general parser only
-__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P);
-__device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool macs, int mode, Parsed& P) {
-    uint32_t off = B.offs[li];
-    Win W;
-    load_win(B, off, W);
-    parse_loaded(B, off, W, macs, mode, P);
-}
-// The record at batch offset off, its window W already loaded.
-__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P) {
-    bool sw = B.flags & 1;
-    uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
-    uint32_t L = min(incl, B.snap);
-    uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
-    if (L > avail) L = (uint32_t)avail;
-    P.L = L;
-    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);  // time.rs:5-7
-    const uint8_t* fr = B.bytes + off + 16;
-    bool fast = (mode == 0) && parse_fast(W, L, P.pi);
-    if (!fast) {
-        PktInfo g;  // only this copy lives on the stack (parse_general is out of line)
-        parse_general(fr, L, g);
-        P.pi = g;
-    }
-    const PktInfo& pi = P.pi;
-    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;
-    P.smac = P.dmac = 0;
-    if (macs && P.cls == 0) {
-        if (fast) {
-            // frame bytes 0..12 = record bytes 16..28
-            uint64_t d = 0, s = 0;
-            for (int k = 0; k < 6; k++) d = (d << 8) | W.b(16 + k);
-            for (int k = 0; k < 6; k++) s = (s << 8) | W.b(22 + k);
-            P.dmac = d; P.smac = s;
-        } else {
-            P.dmac = mac_be(fr + pi.frame_off);
-            P.smac = mac_be(fr + pi.frame_off + 6);
-        }
-    }
-}
-
-__device__ __forceinline__ int find_batch(const Batch* bs, int nb, uint64_t gi) {
-    int b = 0;
-    while (b + 1 < nb && bs[b + 1].first <= gi) b++;
-    return b;
-}
-
-__device__ __forceinline__ uint8_t canon_dir(const Parsed& P, bool macs) {
-    const PktInfo& pi = P.pi;
-    return src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs) ? 1 : 0;
-}
-
-// Canonical key of a parsed packet.  dir = 1 when the packet travels from the
-// higher endpoint to the lower one.
-__device__ __forceinline__ void canon_key(const Parsed& P, bool macs, CKey& k, uint8_t& dir) {
-    const PktInfo& pi = P.pi;
-    bool gt = src_gt_dst(pi.sip, pi.dip, pi.ksp, pi.kdp, P.smac, P.dmac, pi.v6, macs);
-    dir = gt ? 1 : 0;
-    uint32_t lop = gt ? pi.kdp : pi.ksp, hip = gt ? pi.ksp : pi.kdp;
-    uint64_t lom = gt ? P.dmac : P.smac, him = gt ? P.smac : P.dmac;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {  // per-word selects keep the IP arrays in registers
-        k.w[j] = gt ? pi.dip[j] : pi.sip[j];
-        k.w[4 + j] = gt ? pi.sip[j] : pi.dip[j];
-    }
-    k.w[8] = (lop << 16) | hip;
-    uint32_t kind = (pi.v6 ? 1u : 0u) | (macs ? 2u : 0u);
-    k.w[9] = (kind << 8) | pi.kproto;
-    k.w[10] = macs ? (uint32_t)(lom >> 16) : 0; k.w[11] = macs ? (uint32_t)(lom & 0xFFFF) << 16 : 0;
-    k.w[12] = macs ? (uint32_t)(him >> 16) : 0; k.w[13] = macs ? (uint32_t)(him & 0xFFFF) << 16 : 0;
-}
-
-// Exact dense flow id of a canonical key (flow_table.h chains).
-__device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& k, bool insert, uint32_t* chain_out,
-                                                 unsigned long long* generic_used) {
-    const uint32_t kind = k.w[9] >> 8;
-    const bool v6 = kind & 1, macs = kind & 2;
-    uint32_t chain[N_TABLES];
-    for (int j = 0; j < N_TABLES; j++) chain[j] = NONE32;
-    uint32_t s;
-    int ft;
-    unsigned long long v = EMPTY;
-    if (!v6 && !macs) {
-        s = tab_slot(T, 0, ((uint64_t)k.w[0] << 32) | k.w[4], insert);
-        if (s == FAIL) return FAIL;
-        chain[0] = s;
-        s = tab_slot(T, 1, ((uint64_t)s << 40) | ((uint64_t)k.w[8] << 8) | (k.w[9] & 0xFF), insert, &v);
-        if (s == FAIL) return FAIL;
-        chain[1] = s;
-        ft = 1;
-    } else {
-        if (generic_used && insert) *generic_used = 1;
-        // 32-bit units: kind|proto, ports, lo_ip, hi_ip, [lo_mac, hi_mac]
-        uint32_t u[13];
-        u[0] = k.w[9];
-        u[1] = k.w[8];
-        const uint32_t m0 = k.w[10], m1 = k.w[11] | (k.w[12] >> 16), m2 = (k.w[12] << 16) | (k.w[13] >> 16);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            u[2 + j] = v6 ? k.w[j] : (j == 0 ? k.w[0] : j == 1 ? k.w[4] : j == 2 ? m0 : m1);
-            u[6 + j] = v6 ? k.w[4 + j] : (j == 0 ? m2 : 0);
-        }
-        u[10] = m0; u[11] = m1; u[12] = m2;
-        const int m = v6 ? (macs ? 13 : 10) : 7;
-        s = tab_slot(T, 2, ((uint64_t)u[0] << 32) | u[1], insert, &v);
-        if (s == FAIL) return FAIL;
-        chain[2] = s;
-        ft = 2;
-#pragma unroll
-        for (int j = 2; j < 13; j++) {
-            if (j < m) {
-                s = tab_slot(T, j + 1, ((uint64_t)s << 32) | u[j], insert, &v);
-                if (s == FAIL) return FAIL;
-                chain[j + 1] = s;
-                ft = j + 1;
-            }
-        }
-    }
-    return dense_id(T, ft, s, insert, k, chain, chain_out, v);
-}
-
-__device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, bool macs, bool insert,
-                                           uint8_t& dir, uint32_t* chain_out, unsigned long long* generic_used) {
-    CKey k;
-    canon_key(P, macs, k, dir);
-    return dense_of_key(T, k, insert, chain_out, generic_used);
-}
 
 // ---------------------------------------------------------------------------
 // k_parse_agg: the hot kernel
@@ -1720,65 +1475,6 @@ struct FinArgs {
     uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
 };
 
-// Append one record (Mode A paths): position, updates and ended counters.
-__device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {
-    const unsigned long long pos = atomicAdd(&g->n_rec, 1ull);
-    if (pos < cap) out[pos] = r;
-    atomicAdd(&g->n_updates, (unsigned long long)r.d_pkts);
-    if (r.order_key != NONE64) atomicAdd(&g->n_ended, 1ull);
-}
-
-__device__ void fill_seed(fluere_record& r, const Parsed& P) {
-    const PktInfo& pi = P.pi;
-    memset(&r, 0, sizeof r);
-    r.src_v6 = r.dst_v6 = pi.rv6;
-    for (int k = 0; k < 4; k++) {
-        uint32_t s = pi.rsip[k], d = pi.rdip[k];
-        for (int b = 0; b < 4; b++) {
-            r.source[4 * k + b] = (uint8_t)(s >> (24 - 8 * b));
-            r.destination[4 * k + b] = (uint8_t)(d >> (24 - 8 * b));
-        }
-    }
-    r.prot = pi.rprot; r.tos = pi.rtos;
-    r.src_port = pi.rsp; r.dst_port = pi.rdp;
-    r.min_pkt = r.max_pkt = pi.rpkt;
-    r.min_ttl = r.max_ttl = pi.rttl;
-    r.first = r.last = P.t;
-}
-
-__device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t gi, bool macs, Parsed& P) {
-    int b = find_batch(bs, nb, gi);
-    parse_record(bs[b], gi - bs[b].first, macs, 0, P);
-}
-
-// Wave-aggregated emit_record: one atomic per counter per wave (a thread-per-
-// flow kernel that hits the three run counters per flow serialises on them).
-// All lanes of the wave must call it (want = this lane has a record).
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ void emit_record_wave(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r,
-                                                 bool want) {
-    const uint64_t m = __ballot(want);
-    if (!m) return;
-    const uint64_t em = __ballot(want && r.order_key != NONE64);
-    const unsigned long long upd = wave_sum(want ? (unsigned long long)r.d_pkts : 0ull);
-    const uint32_t lead = __builtin_ctzll(m);
-    unsigned long long base = 0;
-    if ((uint32_t)(threadIdx.x & 63) == lead) {
-        base = atomicAdd(&g->n_rec, (unsigned long long)__popcll(m));
-        atomicAdd(&g->n_updates, upd);
-        if (em) atomicAdd(&g->n_ended, (unsigned long long)__popcll(em));
-    }
-    base = __shfl(base, lead, 64);
-    if (want) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (base + rank < cap) out[base + rank] = r;
-    }
-}
-
 // Certified flow d -> its record; false when d has no record here (TCP flow
 // without a SYN: dropped; complex: marked for the per-flow state machine).
 __device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluere_record& r, bool& cplx,
@@ -1875,104 +1571,8 @@ __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// complex flows, Mode A: gather -> sort by (flow, index) -> per-flow replay
-// ---------------------------------------------------------------------------
-struct CollectArgs {
-    Batch B;
-    TableSet T;
-    Glob* g;
-    const uint8_t* complex;
-    unsigned long long* keys;
-    unsigned long long cap;
-    int macs;
-};
-
-__global__ void __launch_bounds__(256) k_collect(CollectArgs a) {
-    uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= a.B.n) return;
-    const bool macs = a.macs != 0;
-    Parsed P;
-    parse_record(a.B, li, macs, 0, P);
-    if (P.cls != 0) return;
-    uint8_t dir;
-    uint32_t d = flow_of(a.T, P, macs, false, dir, nullptr, nullptr);
-    if (d == FAIL || !a.complex[d]) return;
-    unsigned long long pos = atomicAdd(&a.g->n_keys, 1ull);
-    if (pos < a.cap) a.keys[pos] = ((unsigned long long)d << 40) | (a.B.first + li);
-}
-
-__global__ void k_heads(const unsigned long long* keys, unsigned long long n, unsigned long long* heads, Glob* g) {
-    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (i == 0 || (keys[i] >> 40) != (keys[i - 1] >> 40)) heads[atomicAdd(&g->n_heads, 1ull)] = i;
-}
-
-__device__ __forceinline__ void update_flow(fluere_record& r, bool rev, const PktInfo& pi, uint64_t t) {
-    // src/net/flows.rs:11-42 (u32 counters wrap like the release build)
-    r.d_pkts += 1;
-    r.d_octets += pi.doctets;
-    r.max_pkt = max(r.max_pkt, pi.rpkt);
-    r.min_pkt = min(r.min_pkt, pi.rpkt);
-    r.max_ttl = max(r.max_ttl, pi.rttl);
-    r.min_ttl = min(r.min_ttl, pi.rttl);
-    for (int q = 0; q < 8; q++) r.cnt[q] += (pi.tflags >> q) & 1;
-    r.last = t;
-    if (rev) { r.in_pkts += 1; r.in_bytes += pi.doctets; }
-    else { r.out_pkts += 1; r.out_bytes += pi.doctets; }
-}
-
-struct FsmArgs {
-    const Batch* bs;
-    int nb;
-    TableSet T;
-    Glob* g;
-    const unsigned long long* keys;
-    unsigned long long n_keys;
-    const unsigned long long* heads;
-    fluere_record* out;
-    unsigned long long out_cap;
-    int macs;
-};
-
-__global__ void __launch_bounds__(64) k_fsm_flows(FsmArgs a) {
-    unsigned long long h = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= a.g->n_heads) return;
-    const bool macs = a.macs != 0;
-    unsigned long long i = a.heads[h];
-    const unsigned long long d = a.keys[i] >> 40;
-    bool active = false;
-    uint8_t cdir = 0;
-    fluere_record r;
-    for (; i < a.n_keys && (a.keys[i] >> 40) == d; i++) {
-        uint64_t gi = a.keys[i] & IDX_MASK;
-        Parsed P;
-        parse_global(a.bs, a.nb, gi, macs, P);
-        const uint8_t dir = canon_dir(P, macs);
-        bool rev;
-        if (active) {
-            rev = dir != cdir;
-        } else {
-            if (P.pi.rprot == 6 && !(P.pi.tflags & 2)) continue;  // offline_fluereflows.rs:101-113
-            active = true;
-            cdir = dir;
-            fill_seed(r, P);
-            rev = false;
-        }
-        update_flow(r, rev, P.pi, P.t);
-        if (P.pi.tflags & 5) {  // is_finished: fin or rst (types/flags.rs:27-30)
-            r.order_key = gi;
-            emit_record(a.g, a.out, a.out_cap, r);
-            active = false;
-        }
-    }
-    if (active) {
-        r.order_key = NONE64;
-        emit_record(a.g, a.out, a.out_cap, r);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Mode B: exact global state machine (expiries can fire)
+// Mode B, sequential fallback (timestamps not non-decreasing): the exact
+// global state machine on one thread (expiries can fire)
 // ---------------------------------------------------------------------------
 struct SeqMeta {
     uint32_t d;       // dense flow id, NONE32 = not a valid packet
@@ -2533,6 +2133,8 @@ struct fluere_ctx {
     uint32_t* d_sd = nullptr;   // merge scratch (summary -> dense id)
     uint64_t d_sd_cap = 0;
     void* d_stage = nullptr;    // hot-kernel partial aggregates (Stage)
+    void* d_exact = nullptr;    // exact state machine scratch (exact.hip)
+    size_t d_exact_bytes = 0;
     size_t d_stage_bytes = 0;
     bool generic_dirty = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
@@ -2702,6 +2304,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_pay);
     hipFree(c->d_slow);
     hipFree(c->d_stage);
+    hipFree(c->d_exact);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -3594,47 +3197,16 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             HIPCHECK(hipStreamSynchronize(s));
         }
         if (g.n_complex) {
-            uint64_t nk = g.n_complex_pkts;
-            unsigned long long *keys = nullptr, *keys2 = nullptr, *heads = nullptr;
-            void* tmp = nullptr;
-            size_t tmp_bytes = 0;
-            if (hipMalloc(&keys, nk * 8) != hipSuccess || hipMalloc(&keys2, nk * 8) != hipSuccess ||
-                hipMalloc(&heads, nk * 8) != hipSuccess) {
-                hipFree(keys); hipFree(keys2); hipFree(heads);
-                return FLUERE_E_NOMEM;
-            }
-            for (auto& hb : c->batches) {
-                if (!hb.b.n) continue;
-                CollectArgs ca{hb.b, T, c->d_glob, c->d_complex, keys, nk, c->use_mac};
-                k_collect<<<grid_for(hb.b.n, 256), 256, 0, s>>>(ca);
-            }
-            hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys2, (int)nk, 0, 64, s);
-            if (hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)) != hipSuccess) {
-                hipFree(keys); hipFree(keys2); hipFree(heads);
-                return FLUERE_E_NOMEM;
-            }
-            hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys2, (int)nk, 0, 64, s);
-            k_heads<<<grid_for(nk, 256), 256, 0, s>>>(keys2, nk, heads, c->d_glob);
-            // records: certified ones already written + at most one per complex packet
-            uint64_t need = g.n_rec + nk;
-            fluere_record* old = c->d_recs;
-            uint64_t old_n = g.n_rec;
-            if (need > c->d_recs_cap) {
-                fluere_record* nr = nullptr;
-                if (hipMalloc(&nr, need * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
-                HIPCHECK(hipMemcpyAsync(nr, old, old_n * sizeof(fluere_record), hipMemcpyDeviceToDevice, s));
-                HIPCHECK(hipStreamSynchronize(s));
-                hipFree(old);
-                c->d_recs = nr;
-                c->d_recs_cap = need;
-            }
-            FsmArgs fs{c->d_batches, nb, T, c->d_glob, keys2, nk, heads, c->d_recs, c->d_recs_cap, c->use_mac};
-            k_fsm_flows<<<grid_for(g.n_complex, 64), 64, 0, s>>>(fs);
-            HIPCHECK(hipGetLastError());
+            // flows the certificate rejected: the exact state machine (exact.hip)
+            std::vector<Batch> hb(nb);
+            for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
+            ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 0, timeout_us, c->d_complex, c->d_glob,
+                       &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+            ExactResult er{};
+            if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
             HIPCHECK(hipEventRecord(c->ev2, s));
             HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
             HIPCHECK(hipStreamSynchronize(s));
-            hipFree(tmp); hipFree(keys); hipFree(keys2); hipFree(heads);
         }
         // records stay on the device; fluere_get_records copies and orders them
         n_rec = g.n_rec;
@@ -3644,8 +3216,28 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         c->host_recs = false;
         out.complex_flows = g.n_complex;
     } else {
-        // exact global state machine (the speculative Mode A results are discarded)
+        // exact global state machine (the speculative Mode A results are discarded):
+        // in parallel (exact.hip) when the timestamps are non-decreasing, else
+        // the sequential kernel below
         reset_record_counters(c);
+        std::vector<Batch> hb(nb);
+        for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
+        ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 1, timeout_us, c->d_complex, c->d_glob,
+                   &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+        ExactResult er{};
+        rc = getenv("FLUERE_SEQ_MODE_B") ? EXACT_FALLBACK : exact_run(J, s, &er);
+        if (rc < 0) return rc;
+        if (rc == FLUERE_OK) {
+            HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipEventRecord(c->ev2, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            n_rec = g.n_rec;
+            n_ended = g.n_ended;
+            updates = g.n_updates;
+            c->dev_n_rec = n_rec;
+            c->host_recs = false;
+            out.sequential_mode = 1;
+        } else {
         uint64_t N = c->n_total;
         SeqMeta* meta = nullptr;
         HeapEnt* heap = nullptr;
@@ -3684,7 +3276,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         for (auto& r : c->recs) updates += r.d_pkts;
         c->host_recs = true;
         c->dev_n_rec = n_rec;
-        out.sequential_mode = 1;
+        out.sequential_mode = 2;
+        }
     }
     c->n_ended = n_ended;
     c->have_results = true;
@@ -3747,7 +3340,7 @@ extern "C" void fluere_records_free(fluere_record* r) { free(r); }
 // ---------------------------------------------------------------------------
 extern "C" uint64_t fluere_synth_range_bytes(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n) {
     if (!cfg) return 0;
-    if (cfg->kind != FLUERE_SYNTH_IMIX) return n * 80;
+    if (cfg->kind != FLUERE_SYNTH_IMIX && cfg->kind != FLUERE_SYNTH_TCP) return n * 80;
     uint64_t s = 0;
     for (uint64_t i = first; i < first + n; i++) s += 16 + synth::frame_len(*cfg, i);
     return s;

@@ -67,7 +67,7 @@ FL_HD Flow flow(const fluere_synth_cfg& c, uint32_t f) {
 
 // Frame length of packet i (bytes on the wire, == caplen == orig_len).
 FL_HD uint32_t frame_len(const fluere_synth_cfg& c, uint64_t i) {
-    if (c.kind != FLUERE_SYNTH_IMIX) return 64;
+    if (c.kind != FLUERE_SYNTH_IMIX && c.kind != FLUERE_SYNTH_TCP) return 64;
     uint32_t r = (uint32_t)(rnd(c.seed, 14, i) % 12);
     return r < 7 ? 64 : (r < 11 ? 576 : 1500);
 }
@@ -112,6 +112,113 @@ FL_HD void put32le(uint8_t* p, uint32_t v) {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
 
+// ---------------------------------------------------------------------------
+// FLUERE_SYNTH_TCP: TCP as captures show it.  Packet i belongs to lane
+// l = i % L (L = n_flows concurrent lanes) at lane position j = i / L; a lane
+// runs a sequence of connections of a fixed length n (per lane), connection
+// m = j / n, position k = j % n.  Lane types (rnd(seed, 20, l) % 100):
+//   [0, 40)  TCP, 3-way handshake, data, 4-way close FIN -> ACK -> FIN -> ACK
+//            (the closer is the client or the server); half of these lanes
+//            reuse one 5-tuple for every connection (a closed key reopens)
+//   [40, 50) TCP, handshake, data, RST (either side)
+//   [50, 60) TCP, handshake, data, never closed
+//   [60, 65) TCP, mid-stream: the lane's first connection starts without a
+//            SYN (data, then the 4-way close); later connections are normal
+//   [65, 100) UDP, both directions
+// Lanes [0, E) (E = L / 64) carry 8 elephant flows: lane g of an elephant
+// (g = l % 8) opens it with a SYN at its first packet; every other packet of
+// those lanes is data, so each elephant holds ~1/512 of the capture.
+// In every reference rule this exercises: the SYN gate drops the peer's ACK /
+// FIN / ACK after the first FIN closed the flow (offline_fluereflows.rs:101-113,
+// 152-157), RST closes, reopened keys, flows that never see a SYN.
+// ---------------------------------------------------------------------------
+struct Pkt {
+    uint32_t a_ip, b_ip;        // client, server
+    uint16_t a_port, b_port;
+    uint8_t proto, rev, tflags;
+    uint8_t a_mac[6], b_mac[6];
+};
+
+FL_HD void lane_macs(const fluere_synth_cfg& c, uint64_t l, Pkt& p) {
+    uint64_t ma = rnd(c.seed, 7, l), mb = rnd(c.seed, 8, l);
+    for (int k = 0; k < 6; k++) {
+        p.a_mac[k] = (uint8_t)(ma >> (8 * k));
+        p.b_mac[k] = (uint8_t)(mb >> (8 * k));
+    }
+    p.a_mac[0] = (uint8_t)((p.a_mac[0] & 0xFC) | 0x02);
+    p.b_mac[0] = (uint8_t)((p.b_mac[0] & 0xFC) | 0x02);
+}
+
+FL_HD Pkt tcp_real(const fluere_synth_cfg& c, uint64_t i) {
+    Pkt p;
+    const uint64_t L = c.n_flows ? c.n_flows : 1;
+    const uint64_t l = i % L, j = i / L;
+    const uint64_t E = L / 64;
+    const bool data_rev = (rnd(c.seed, 2, i) % 100) < c.rev_pct;
+    const uint8_t data_flags = (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0));  // ACK (+PSH)
+    if (l < E) {  // elephant g: lane g opens it
+        const uint64_t g = l % 8;
+        lane_macs(c, g, p);
+        p.a_ip = 0x0A7F0000u | (uint32_t)g;
+        p.b_ip = 0x0AFF0000u | (uint32_t)g;
+        p.a_port = pick_port(rnd(c.seed, 4, g));
+        p.b_port = 443;
+        p.proto = 6;
+        const bool open = l == g && j == 0;
+        p.rev = open ? 0 : data_rev;
+        p.tflags = open ? 0x02 : data_flags;
+        return p;
+    }
+    lane_macs(c, l, p);
+    const uint32_t type = (uint32_t)(rnd(c.seed, 20, l) % 100);
+    const uint64_t lens[8] = {5, 7, 8, 12, 16, 24, 48, 200};
+    const uint64_t n = lens[rnd(c.seed, 22, l) & 7];
+    const uint64_t m = j / n, k = j % n;
+    const bool reuse = type < 40 && (rnd(c.seed, 23, l) & 1);
+    p.a_ip = 0x0A000000u | (uint32_t)(l & 0x7FFFFFu);
+    p.b_ip = 0x0A800000u | (uint32_t)(rnd(c.seed, 3, l) & 0x7FFFFFu);
+    p.a_port = pick_port(rnd(c.seed, 4, reuse ? l : l * 0x10001ull + m));
+    p.b_port = pick_port(rnd(c.seed, 5, l));
+    p.proto = type < 65 ? 6 : 17;
+    p.rev = data_rev;
+    p.tflags = data_flags;
+    if (p.proto == 17) return p;
+    const bool server_closes = rnd(c.seed, 24, l * 0x10001ull + m) & 1;
+    const bool midstream = type >= 60 && m == 0;
+    if (!midstream) {  // 3-way handshake
+        if (k == 0) { p.rev = 0; p.tflags = 0x02; return p; }            // SYN
+        if (k == 1) { p.rev = 1; p.tflags = 0x12; return p; }            // SYN+ACK
+        if (k == 2) { p.rev = 0; p.tflags = 0x10; return p; }            // ACK
+    }
+    if (type < 40 || type >= 60) {  // 4-way close in the last four packets
+        if (k + 4 >= n && n >= 7) {
+            const uint64_t q = k + 4 - n;  // 0 FIN, 1 ACK, 2 FIN, 3 ACK
+            const bool first_side = server_closes;  // rev of the first FIN
+            p.rev = (q == 0 || q == 3) ? first_side : !first_side;
+            p.tflags = (q == 0 || q == 2) ? 0x11 : 0x10;
+            return p;
+        }
+    } else if (type < 50) {  // RST after the data
+        if (k + 1 == n) { p.rev = server_closes; p.tflags = 0x04 | (rnd(c.seed, 25, i) & 1 ? 0x10 : 0); return p; }
+    }
+    return p;
+}
+
+// The header fields of packet i: the schedule of the kind.
+FL_HD Pkt pkt(const fluere_synth_cfg& c, uint64_t i) {
+    if (c.kind == FLUERE_SYNTH_TCP) return tcp_real(c, i);
+    Pkt p;
+    Slot s = slot(c, i);
+    Flow F = flow(c, s.f);
+    uint8_t tflags = s.tcp_flags;
+    if (tflags == 0xFF)
+        tflags = F.closer == 1 ? 0x11 : (F.closer == 2 ? 0x04 : (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0)));
+    p.a_ip = F.a_ip; p.b_ip = F.b_ip; p.a_port = F.a_port; p.b_port = F.b_port;
+    p.proto = F.proto; p.rev = s.rev; p.tflags = tflags;
+    for (int k = 0; k < 6; k++) { p.a_mac[k] = F.a_mac[k]; p.b_mac[k] = F.b_mac[k]; }
+    return p;
+}
+
 // Writes the 16-byte pcap record header and the frame of packet i at dst.
 // Returns bytes written (16 + frame_len).
 FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst) {
@@ -121,20 +228,17 @@ FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst)
     put32le(dst + 8, L);
     put32le(dst + 12, L);
     uint8_t* e = dst + 16;
-    Slot s = slot(c, i);
-    Flow F = flow(c, s.f);
-    uint8_t tflags = s.tcp_flags;
-    if (tflags == 0xFF)
-        tflags = F.closer == 1 ? 0x11 : (F.closer == 2 ? 0x04 : (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0)));
-    uint32_t sip = s.rev ? F.b_ip : F.a_ip, dip = s.rev ? F.a_ip : F.b_ip;
-    uint16_t sp = s.rev ? F.b_port : F.a_port, dp = s.rev ? F.a_port : F.b_port;
-    const uint8_t* smac = s.rev ? F.b_mac : F.a_mac;
-    const uint8_t* dmac = s.rev ? F.a_mac : F.b_mac;
+    const Pkt P = pkt(c, i);
+    const uint8_t tflags = P.tflags;
+    uint32_t sip = P.rev ? P.b_ip : P.a_ip, dip = P.rev ? P.a_ip : P.b_ip;
+    uint16_t sp = P.rev ? P.b_port : P.a_port, dp = P.rev ? P.a_port : P.b_port;
+    const uint8_t* smac = P.rev ? P.b_mac : P.a_mac;
+    const uint8_t* dmac = P.rev ? P.a_mac : P.b_mac;
     for (int k = 0; k < 6; k++) { e[k] = dmac[k]; e[6 + k] = smac[k]; }
     uint32_t o = 12;
     if (c.kind == FLUERE_SYNTH_VLAN64) {
         put16(e + 12, 0x8100);
-        put16(e + 14, (uint32_t)(rnd(c.seed, 17, s.f) & 0x0FFF));
+        put16(e + 14, (uint32_t)(rnd(c.seed, 17, P.a_ip & 0x7FFFFFu) & 0x0FFF));
         o = 16;
     }
     put16(e + o, 0x0800);
@@ -147,7 +251,7 @@ FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst)
     put16(ip + 4, (uint32_t)(rnd(c.seed, 11, i) & 0xFFFF));
     put16(ip + 6, 0x4000);  // DF
     ip[8] = (uint8_t)(32 + rnd(c.seed, 9, i) % 97);
-    ip[9] = F.proto;
+    ip[9] = P.proto;
     put16(ip + 10, 0);
     put32(ip + 12, sip);
     put32(ip + 16, dip);
@@ -159,7 +263,7 @@ FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst)
     uint32_t l4len = iplen - 20, hl;
     put16(l4, sp);
     put16(l4 + 2, dp);
-    if (F.proto == 6) {
+    if (P.proto == 6) {
         put32(l4 + 4, (uint32_t)rnd(c.seed, 18, i));
         put32(l4 + 8, (uint32_t)rnd(c.seed, 19, i));
         l4[12] = 0x50;

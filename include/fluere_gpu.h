@@ -108,7 +108,7 @@ typedef struct fluere_stats {
     uint64_t complex_flows;    /* flows resolved by the exact per-flow state machine */
     uint64_t records;          /* emitted records */
     uint64_t ended;            /* records in the ended prefix */
-    uint32_t sequential_mode;  /* 1 if expiries fired (global sequential state machine) */
+    uint32_t sequential_mode;  /* 0: no expiry can fire; 1: expiry sweep, parallel; 2: expiry sweep, sequential fallback */
     uint32_t pad;
     double parse_ms;           /* device time of the fused parse+key+aggregate kernel */
     double total_ms;           /* wall time of the whole run (fluere_run: host clock, submission to results) */
@@ -293,7 +293,9 @@ enum {
     FLUERE_SYNTH_UDP64 = 0,     /* 64-B Ethernet/IPv4/UDP */
     FLUERE_SYNTH_IMIX = 1,      /* 64/576/1500 (7:4:1), TCP+UDP, SYN first, FIN/RST last */
     FLUERE_SYNTH_VLAN64 = 2,    /* 802.1Q-tagged 64-B IPv4/UDP, MAC pairs */
-    FLUERE_SYNTH_MAC64 = 3      /* untagged 64-B IPv4/UDP, MAC pairs */
+    FLUERE_SYNTH_MAC64 = 3,     /* untagged 64-B IPv4/UDP, MAC pairs */
+    FLUERE_SYNTH_TCP = 4        /* IMIX sizes; TCP with handshakes, 4-way closes (the peer's packets after the
+                                   first FIN), RSTs, reopened keys, mid-stream starts, elephants; and UDP */
 };
 
 /* Size of the synthetic pcap file (24-B header + records). */

@@ -420,3 +420,38 @@ def test_offline_file_grows_flow_table(gpu, tmp_path):
     got = (tmp_path / "o" / "many_converted.csv").read_text()
     assert st["records"] == n
     assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "offline_file many flows")
+
+
+# ---- realistic TCP (FLUERE_SYNTH_TCP): the exact state machine at scale
+# (exact.hip).  Every close is a 4-way FIN handshake (the first FIN closes the
+# flow, the peer's ACK / FIN / ACK are SYN-gated away), RSTs, reopened keys,
+# flows without a SYN, elephants; with a timeout shorter than the capture the
+# hard-timeout sweep runs (Mode B, stale entries included).
+TCP_SYNTH = {
+    "tcp_200k": (200_000, 2_000, (600000, 50, 5, 1, 0)),
+    "tcp_2m": (2_000_000, 20_000, (600000, 20)),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TCP_SYNTH))
+def test_tcp_realistic_matches_oracle(gpu, name):
+    n, lanes, timeouts = TCP_SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, n, lanes, 0xF10E0007))
+    for t in timeouts:
+        want = pyoracle.offline(data, t)
+        csv, ne, st = _gpu_csv(data, t, max_flows=max(1 << 16, n // 2))
+        assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"{name} t={t}")
+        if t == 600000:
+            assert st["sequential_mode"] == 0 and st["complex_flows"] > 0
+        else:
+            assert st["sequential_mode"] == 1  # the parallel sweep, not the fallback
+
+
+def test_mode_b_fallback_on_backward_time(gpu):
+    """Timestamps that go backwards: the sweep order is not the FIFO the
+    parallel chase assumes, so the run takes the sequential kernel."""
+    data = golden_pcap("edge_keys")
+    want = pyoracle.offline(data, 1, True)
+    csv, ne, st = _gpu_csv(data, 1, use_mac=True)
+    assert st["sequential_mode"] == 2
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "edge_keys t=1 -M")
