@@ -30,12 +30,24 @@ CONFIGS = {
                workload="10M x 64B UDP, 1k 5-tuples per GPU (BASELINE configs[1])"),
     "c3": dict(kind=1, per_gpu=10_000_000, flows=100_000, seed=0xF10E0003, use_mac=False,
                workload="10M IMIX 64/576/1500 TCP+UDP, 100k flows per GPU (BASELINE configs[2])"),
-    "c4": dict(kind=1, per_gpu=12_500_000, flows=125_000, seed=0xF10E0004, use_mac=False,
-               workload="IMIX TCP+UDP, 12.5M packets / 125k flows per GPU (BASELINE configs[3] at 8 GPUs)"),
+    # BASELINE configs[3]: 100M IMIX packets, 1M flows over 8 GPUs; the flow
+    # count is global, so every 12.5M-packet shard sees nearly all 1M flows
+    "c4": dict(kind=1, per_gpu=12_500_000, flows=1_000_000, seed=0xF10E0004, use_mac=False,
+               workload="IMIX TCP+UDP, 12.5M packets per GPU, 1M flows in the whole capture (BASELINE configs[3])"),
     "c5": dict(kind=2, per_gpu=10_000_000, flows=50_000, seed=0xF10E0005, use_mac=True,
-               workload="10M x 64B VLAN-tagged, 50k MAC pairs, --useMAC (BASELINE configs[4]; header-only CSV)"),
+               workload="10M x 64B VLAN-tagged, 50k MAC pairs, --useMAC (BASELINE configs[4]; header-only CSV)",
+               note="drop-only path: the reference's vlan_keys misparse (keys.rs:417-435) skips every frame, "
+                    "so no packet is aggregated; see c5u for MAC-keyed aggregation"),
     "c5u": dict(kind=3, per_gpu=10_000_000, flows=50_000, seed=0xF10E0005, use_mac=True,
                 workload="10M x 64B untagged, 50k MAC pairs, --useMAC (BASELINE configs[4], untagged)"),
+    # realistic TCP (FLUERE_SYNTH_TCP): 4-way closes, RSTs, reopened keys,
+    # mid-stream starts, elephants -- the exact state machine (exact.hip) runs
+    # for every flow the certificate rejects; with -t 1000 (1 s, the capture
+    # spans 10 s) the hard-timeout sweep runs for every flow (Mode B)
+    "tcp": dict(kind=4, per_gpu=10_000_000, flows=100_000, seed=0xF10E0007, use_mac=False,
+                workload="10M IMIX, realistic TCP (+UDP), 100k concurrent lanes, -t 600000"),
+    "tcp_t1": dict(kind=4, per_gpu=10_000_000, flows=100_000, seed=0xF10E0007, use_mac=False, timeout_ms=1000,
+                   workload="10M IMIX, realistic TCP (+UDP), 100k concurrent lanes, -t 1000 (expiry sweep)"),
 }
 BYTES_PER_PKT = 80  # algorithmic: 16 B pcap record header + min(caplen, 64) B header window
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -79,7 +91,9 @@ def main():
     torch.cuda.synchronize()
     # N > 1: the context runs on torch's stream, so the collective of the
     # shard exchange is ordered after the export without a host wait
-    ctx = fluere_amd.FlowContext(use_mac=C["use_mac"], max_flows=max(1 << 16, 2 * C["flows"]), device=local,
+    max_flows = max(1 << 16, 2 * C["flows"]) if C["kind"] != 4 else n // 2
+    ctx = fluere_amd.FlowContext(timeout_ms=C.get("timeout_ms", 600000), use_mac=C["use_mac"], max_flows=max_flows,
+                                 device=local,
                                  stream=torch.cuda.current_stream().cuda_stream if world > 1 else None)
     exchange = fdist.ShardExchange(ctx) if world > 1 else None
     fdist.set_index_base(ctx, first)
@@ -152,7 +166,8 @@ def main():
             "config": {"workload": C["workload"], "packets_total": n_total, "flows": C["flows"],
                        "parallelism": (f"dp{world}: packet-range shards, RCCL all_gather flow-table merge"
                                        if world > 1 else "single GPU"),
-                       "use_mac": C["use_mac"]},
+                       "use_mac": C["use_mac"], "timeout_ms": C.get("timeout_ms", 600000),
+                       **({"note": C["note"]} if "note" in C else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_parse_agg", "kernel_ms": round(kernel_avg, 4),
@@ -163,6 +178,8 @@ def main():
             "aggregate_pass_ms": round(sum(pass_ms) / len(pass_ms), 4),
             "records": int(len(recs)),
             "records_ended": int(ne),
+            "complex_flows": int(st.get("complex_flows", 0)) if world == 1 else None,
+            "sequential_mode": int(st.get("sequential_mode", 0)) if world == 1 else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, C)
@@ -184,7 +201,8 @@ def cpu_baseline(cfg, C):
     old = os.sched_getaffinity(0)
     try:
         os.sched_setaffinity(0, {sorted(old)[0]})
-        best = min(pyoracle.offline(data, use_mac=C["use_mac"])["loop_seconds"] for _ in range(2))
+        best = min(pyoracle.offline(data, C.get("timeout_ms", 600000), use_mac=C["use_mac"])["loop_seconds"]
+                   for _ in range(2))
     finally:
         os.sched_setaffinity(0, old)
     return {"value": round(n / best / 1e6, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",

@@ -430,6 +430,7 @@ def test_offline_file_grows_flow_table(gpu, tmp_path):
 TCP_SYNTH = {
     "tcp_200k": (200_000, 2_000, (600000, 50, 5, 1, 0)),
     "tcp_2m": (2_000_000, 20_000, (600000, 20)),
+    "tcp_10m": (10_000_000, 100_000, (600000, 1000)),  # the bench's tcp / tcp_t1 workloads
 }
 
 
