@@ -27,7 +27,8 @@ OK = 0
 E_ARG, E_IO, E_PCAP, E_HIP, E_NOMEM, E_TABLE_FULL, E_UNSUPPORTED, E_STATE = range(-1, -9, -1)
 _ERR_NAMES = {
     E_ARG: "bad argument", E_IO: "I/O error", E_PCAP: "not a pcap capture", E_HIP: "HIP error / no GPU",
-    E_NOMEM: "out of memory", E_TABLE_FULL: "flow table full", E_UNSUPPORTED: "parser class not on the GPU",
+    E_NOMEM: "out of memory", E_TABLE_FULL: "flow table full",
+    E_UNSUPPORTED: "needs the hard-timeout sweep across shards (run the capture in one context)",
     E_STATE: "call order",
 }
 
@@ -95,12 +96,24 @@ SUMMARY_DTYPE = np.dtype([
     ("key", "<u4", 14), ("pkts", "<u4", 2), ("bytes", "<u8", 2), ("min_pkt", "<u4"), ("max_pkt", "<u4"),
     ("min_ttl", "<u4"), ("max_ttl", "<u4"), ("flag_cnt", "<u4", 8), ("first_all", "<u8"), ("first_create", "<u8"),
     ("finrst_min", "<u8"), ("last", "<u8"), ("first_time", "<u8"), ("last_time", "<u8"), ("first_sport", "<u2"),
-    ("first_dport", "<u2"), ("first_dir", "u1"), ("first_prot", "u1"), ("first_tos", "u1"), ("pad0", "u1"),
-    ("pad1", "<u4"), ("pad2", "<u4"),
+    ("first_dport", "<u2"), ("first_dir", "u1"), ("first_prot", "u1"), ("first_tos", "u1"), ("first_v6", "u1"),
+    ("first_src", "u1", 16), ("first_dst", "u1", 16), ("annex", "<u4"), ("shard", "<u4"), ("pad", "<u8", 4),
 ])
+PIECE_DTYPE = np.dtype([
+    ("pkts", "<u4", 2), ("bytes", "<u8", 2), ("min_pkt", "<u4"), ("max_pkt", "<u4"), ("min_ttl", "<u4"),
+    ("max_ttl", "<u4"), ("flag_cnt", "<u4", 8), ("last", "<u8"), ("last_time", "<u8"), ("first", "<u8"),
+    ("first_time", "<u8"), ("src", "u1", 16), ("dst", "u1", 16), ("v6", "u1"), ("prot", "u1"), ("tos", "u1"),
+    ("dir", "u1"), ("src_port", "<u2"), ("dst_port", "<u2"),
+])
+ANNEX_DTYPE = np.dtype([("key", "<u4", 14), ("flags", "<u4"), ("pad", "<u4"), ("f0", "<u8"), ("lead", PIECE_DTYPE),
+                        ("head", PIECE_DTYPE), ("tail", PIECE_DTYPE), ("pad2", "<u8")])
+SHARD_HEADER_DTYPE = np.dtype([("n_flows", "<u8"), ("n_annex", "<u8"), ("tmin", "<u8"), ("tmax", "<u8"),
+                               ("valid", "<u8"), ("dropped", "<u8"), ("err", "<u4"), ("shard", "<u4"),
+                               ("reserved", "<u8")])
 SHARD_HEADER_BYTES = 64  # fluere_shard_header
 SUMMARY_BYTES = SUMMARY_DTYPE.itemsize  # struct fluere_flow_summary
-assert SUMMARY_BYTES == 192
+assert SUMMARY_BYTES == 256 and PIECE_DTYPE.itemsize == 144 and ANNEX_DTYPE.itemsize == 512
+assert SHARD_HEADER_DTYPE.itemsize == SHARD_HEADER_BYTES
 
 _lib = None
 
@@ -146,11 +159,10 @@ def lib() -> ctypes.CDLL:
         "fluere_last_pass_ms": (ctypes.c_double, [P]),
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),
         "fluere_debug_raw": (I, [I, P, P, P, P, U64, P, P]),
-        "fluere_export_summaries": (I, [P, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
-        "fluere_merge_summaries": (I, [P, P, U64, U64, U64, ctypes.POINTER(Stats)]),
-        "fluere_shard_block_bytes": (U64, [U64]),
-        "fluere_export_device": (I, [P, P, U64]),
-        "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, ctypes.POINTER(Stats)]),
+        "fluere_shard_block_bytes": (U64, [U64, U64]),
+        "fluere_export_device": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.POINTER(U64),
+                                     ctypes.POINTER(U64)]),
+        "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, U64, ctypes.POINTER(Stats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -29,6 +29,14 @@ struct ExactJob {
     uint64_t* d_recs_cap;
     void** scratch;          // device scratch arena, reused across runs
     size_t* scratch_bytes;
+    // Shard mode (multi-GPU export): replay the complex[] flows from "no
+    // flow" over this shard's packets; instances that open and close inside
+    // the shard become records, the lead / head / tail pieces go to one annex
+    // per flow (fluere_flow_annex), annex_of[d] = its index.
+    int shard_mode;
+    fluere_flow_annex** annex;  // grown to the number of replayed flows
+    uint64_t* annex_cap;
+    uint32_t* annex_of;         // [fmax], NONE32 for flows without an annex (the caller fills it)
 };
 
 struct ExactResult {
@@ -36,6 +44,7 @@ struct ExactResult {
     uint64_t keys;        // flows replayed
     uint64_t instances;   // flow records (instances) produced
     int iterations;       // Mode B: passes until the processed-packet set was stable
+    uint64_t annexes;     // shard mode: annexes written (= keys)
 };
 
 // 0 on success; EXACT_FALLBACK when Mode B cannot be done in parallel here

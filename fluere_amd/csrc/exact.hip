@@ -45,7 +45,9 @@ namespace {
 constexpr uint64_t M40 = (1ull << 40) - 1;
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr int MAX_PASSES = 32;
-enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2 };
+enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2, K_LEAD = 3 };
+// shard mode: role of a run in the flow's annex
+enum : uint8_t { R_RECORD = 0, R_HEAD = 1, R_TAIL = 2, R_HEAD_TAIL = 3, R_LEAD = 4 };
 
 // One replayed packet (32 bytes).
 struct ExMeta {
@@ -195,6 +197,13 @@ struct ChaseArgs {
     unsigned long long* iie;  // sweep: the index of the creation that pushed the firing entry
     unsigned long long* ej;   // Mode B: sweep point of the entry pushed at this creation
     uint32_t* link;           // Mode B: next pending entry of the same orientation
+    // shard mode
+    int shard_mode;
+    uint8_t* irole;
+    uint32_t* ikey;           // key ordinal of the run (annex index)
+    fluere_flow_annex* annex;
+    uint32_t* annex_of;
+    const uint8_t* flow_key;  // TableSet::flow_key (56-byte canonical keys by dense id)
 };
 
 // first processed packet (capture-order index) k >= i_k with t_k >= exp -> its packet index
@@ -225,6 +234,30 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         }
     };
     uint32_t pos = p0;
+    // shard mode: from "no flow", the lead piece [p0, min(e0, f0 + 1)) and the
+    // roles of the instances (the first one, if created at or before f0, is
+    // the head; the one still open at the end, after f0, the tail)
+    const unsigned long long f0 = a.nf_rev[a.n - 1 - p0] & M40;
+    int n_inst = 0;
+    if (a.shard_mode) {
+        const unsigned long long e0 = a.ne_rev[a.n - 1 - p0] & M40;
+        const uint32_t lead_end = (uint32_t)min(e0 == M40 ? (unsigned long long)pend : e0,
+                                                f0 == M40 ? (unsigned long long)pend : f0 + 1);  // exclusive
+        const uint32_t d = a.sm[p0].d;
+        fluere_flow_annex& ax = a.annex[q];
+        const uint32_t* kw = reinterpret_cast<const uint32_t*>(a.flow_key + (size_t)d * 56);
+        for (int k = 0; k < 14; k++) ax.key[k] = kw[k];
+        ax.flags = (f0 != M40 ? 1u : 0u) | (lead_end > p0 ? 2u : 0u);
+        ax.f0 = f0 != M40 ? a.sm[f0].gidx : NONE64;
+        a.annex_of[d] = q;
+        if (lead_end > p0) {
+            a.sflag[p0] = 1;
+            a.iend[p0] = lead_end - 1;
+            a.ikind[p0] = K_LEAD;
+            a.irole[p0] = R_LEAD;
+            a.ikey[p0] = q;
+        }
+    }
     while (pos < pend) {
         const unsigned long long ce = a.ne_rev[a.n - 1 - pos] & M40;
         if (ce == M40) break;
@@ -272,6 +305,14 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         a.ikind[c] = kind;
         a.ij[c] = cj;
         a.iie[c] = cie;
+        if (a.shard_mode) {
+            const bool head = n_inst == 0 && (f0 == M40 || c <= f0);
+            const bool tail = kind == K_ACTIVE;
+            a.irole[c] = head ? (tail ? R_HEAD_TAIL : R_HEAD) : (tail ? R_TAIL : R_RECORD);
+            a.ikey[c] = q;
+            a.annex[q].flags |= (head ? 4u : 0u) | (tail && !head ? 8u : 0u);
+        }
+        n_inst++;
         if (a.mode_b && kind != K_ACTIVE) drop_upto(cj, true);
         pos = end + 1;
     }
@@ -324,7 +365,20 @@ struct RecArgs {
     unsigned long long* hi;  // Mode B order: (sweeping / closing index, phase)
     unsigned long long* lo;  //               (the firing entry's creation index)
     uint32_t* idx;
+    int shard_mode;
+    const uint8_t* irole;
+    const uint32_t* ikey;
+    fluere_flow_annex* annex;
 };
+
+__device__ __forceinline__ void piece_of(const Agg& g, fluere_flow_piece& pc) {
+    pc.pkts[0] = g.pk[0]; pc.pkts[1] = g.pk[1];
+    pc.bytes[0] = g.by[0]; pc.bytes[1] = g.by[1];
+    pc.min_pkt = g.mnp; pc.max_pkt = g.mxp; pc.min_ttl = g.mnt; pc.max_ttl = g.mxt;
+    for (int k = 0; k < 8; k++) pc.flag_cnt[k] = g.fl[k];
+    pc.last = g.lastg;
+    pc.last_time = g.lastt;
+}
 
 __global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -335,7 +389,32 @@ __global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
     uint32_t q = 0;
     uint8_t kind = K_ACTIVE;
     unsigned long long cj = NONE64, cie = 0;
-    if (lane_live) {
+    if (lane_live && a.shard_mode && a.irole[a.ist[a.ukeys[r]]] != R_RECORD) {
+        // a piece of the flow's annex (lead / head / tail), not a record
+        const uint32_t c = a.ist[a.ukeys[r]];
+        const ExMeta mc = a.sm[c];
+        const uint8_t role = a.irole[c];
+        fluere_flow_annex& ax = a.annex[a.ikey[c]];
+        fluere_flow_piece pc;
+        memset(&pc, 0, sizeof pc);
+        piece_of(a.aggs[r], pc);
+        pc.first = mc.gidx;
+        pc.first_time = mc.t;
+        if (role != R_LEAD) {
+            Parsed P;
+            parse_global(a.bs, a.nb, mc.gidx, a.macs != 0, P);
+            fluere_record sd;
+            fill_seed(sd, P);
+            for (int k = 0; k < 16; k++) { pc.src[k] = sd.source[k]; pc.dst[k] = sd.destination[k]; }
+            pc.v6 = sd.src_v6; pc.prot = sd.prot; pc.tos = sd.tos; pc.dir = mc.dir;
+            pc.src_port = sd.src_port; pc.dst_port = sd.dst_port;
+        }
+        if (role == R_LEAD) ax.lead = pc;
+        if (role == R_HEAD || role == R_HEAD_TAIL) ax.head = pc;
+        if (role == R_TAIL) ax.tail = pc;
+    }
+    const bool rec_live = lane_live && !(a.shard_mode && a.irole[a.ist[a.ukeys[r]]] != R_RECORD);
+    if (rec_live) {
         q = a.ukeys[r];
         const uint32_t c = a.ist[q];
         const ExMeta mc = a.sm[c];
@@ -363,10 +442,10 @@ __global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
         rec.order_key = kind == K_ACTIVE ? NONE64 : cj;
     }
     if (!a.mode_b) {
-        emit_record_wave(a.g, a.out, a.out_cap, rec, lane_live);
+        emit_record_wave(a.g, a.out, a.out_cap, rec, rec_live);
         return;
     }
-    if (lane_live) {
+    if (rec_live) {
         a.tmp[q] = rec;
         a.hi[q] = kind == K_ACTIVE ? NONE64 : (cj << 1) | (kind == K_SWEEP ? 1ull : 0ull);
         a.lo[q] = kind == K_SWEEP ? cie : 0ull;
@@ -435,6 +514,7 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
         add(n * sizeof(Agg)); add(16);                                // aggs, nruns/counters
         add(n * sizeof(fluere_record)); add(n * 8); add(n * 8);       // tmp, hi, lo
         add(n * 4); add(n * 4); add(n * 8); add(n * 4);               // idx, idx2, hi2, perm
+        add(n); add(n * 4);                                           // irole, ikey
         add(tmp);
         return b;
     };
@@ -516,6 +596,8 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     uint32_t* idx2 = A.take<uint32_t>(N);
     unsigned long long* hi2 = A.take<unsigned long long>(N);
     uint32_t* perm = A.take<uint32_t>(N);
+    uint8_t* irole = A.take<uint8_t>(N);
+    uint32_t* ikey = A.take<uint32_t>(N);
     tp = A.take<char>(tmp);
     const int iN = (int)N;
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, iN, s));
@@ -557,8 +639,21 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     const uint32_t n_keys = last[0] + last[1];
     R.keys = n_keys;
     if (J.mode_b && mono_bad) return EXACT_FALLBACK;
+    fluere_flow_annex* annex = nullptr;
+    if (J.shard_mode) {
+        if (n_keys > *J.annex_cap) {
+            hipFree(*J.annex);
+            *J.annex = nullptr;
+            *J.annex_cap = 0;
+            if (hipMalloc(J.annex, (size_t)n_keys * sizeof(fluere_flow_annex)) != hipSuccess) return FLUERE_E_NOMEM;
+            *J.annex_cap = n_keys;
+        }
+        annex = *J.annex;
+        R.annexes = n_keys;
+    }
     ChaseArgs ca{n, n_keys, heads, sm, sval, ne_rev, nf_rev, J.mode_b, J.timeout_us, cm, np_rev,
-                 sflag, iend, ikind, ij, iie, ej, link};
+                 sflag, iend, ikind, ij, iie, ej, link,
+                 J.shard_mode, irole, ikey, annex, J.annex_of, J.T.flow_key};
     // ---- 3..5. chase (Mode B: until the processed set is stable)
     for (int pass = 0;; pass++) {
         if (pass == MAX_PASSES) return EXACT_FALLBACK;
@@ -607,7 +702,7 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
         *J.d_recs_cap = want;
     }
     RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, ukeys, aggs, ctr, ist, sm, iend, ikind, ij, iie, J.g,
-               *J.d_recs, *J.d_recs_cap, tmpr, hi, lo, idx};
+               *J.d_recs, *J.d_recs_cap, tmpr, hi, lo, idx, J.shard_mode, irole, ikey, annex};
     // runs <= n (every run holds a packet)
     k_ex_records<<<gridn(n, 256), 256, 0, s>>>(ra);
     if (J.mode_b && n_inst) {

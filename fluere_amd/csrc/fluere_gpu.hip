@@ -52,7 +52,9 @@ using namespace fl;
 
 static_assert(sizeof(fluere_record) == 152, "fluere_record ABI");
 static_assert(sizeof(fluere_pkt_meta) == 128, "fluere_pkt_meta ABI");
-static_assert(sizeof(fluere_flow_summary) == 192, "fluere_flow_summary ABI");
+static_assert(sizeof(fluere_flow_summary) == 256, "fluere_flow_summary ABI");
+static_assert(sizeof(fluere_flow_piece) == 144, "fluere_flow_piece ABI");
+static_assert(sizeof(fluere_flow_annex) == 512, "fluere_flow_annex ABI");
 static_assert(sizeof(fluere_shard_header) == 64, "fluere_shard_header ABI");
 static_assert(sizeof(fluere_raw_hdr) == 64, "fluere_raw_hdr ABI");
 
@@ -1831,17 +1833,20 @@ __global__ void k_synth_write(fluere_synth_cfg c, uint64_t first, uint64_t n, ui
 }
 
 // ---------------------------------------------------------------------------
-// multi-GPU: per-flow summaries (export on every shard, merge on one)
+// multi-GPU exchange (include/fluere_gpu.h): every shard exports summaries and
+// annexes bucketed by owner; each owner merges its flows and composes, in
+// shard order, the flows whose record depends on packet order
 // ---------------------------------------------------------------------------
-struct FirstPay {
-    unsigned long long t_first, t_last;
-    uint16_t sp, dp;
-    uint8_t dir, prot, tos, pad;
-};
+// owner rank of a canonical key (the same on every rank)
+__device__ __forceinline__ uint32_t key_owner(const uint32_t* key, uint32_t n_owners) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+    for (int j = 0; j < 14; j++) h = synth::mix64(h ^ key[j]);
+    return (uint32_t)(((h >> 32) * (uint64_t)n_owners) >> 32);
+}
 
-__device__ __forceinline__ void export_one(const FinArgs& a, fluere_flow_summary* out, uint32_t d) {
+__device__ __forceinline__ void export_one(const FinArgs& a, fluere_flow_summary& s, uint32_t d) {
     const Acc& A = a.A;
-    fluere_flow_summary s;
     memset(&s, 0, sizeof s);
     const uint32_t* key = (const uint32_t*)(a.T.flow_key + (size_t)d * 56);
     for (int j = 0; j < 14; j++) s.key[j] = key[j];
@@ -1854,85 +1859,153 @@ __device__ __forceinline__ void export_one(const FinArgs& a, fluere_flow_summary
     if (s.first_create != NONE64) {
         Parsed P;
         parse_global(a.bs, a.nb, s.first_create, macs, P);
+        fluere_record sd;
+        fill_seed(sd, P);
         s.first_dir = canon_dir(P, macs);
-        s.first_sport = P.pi.rsp; s.first_dport = P.pi.rdp;
-        s.first_prot = P.pi.rprot; s.first_tos = P.pi.rtos;
+        s.first_sport = sd.src_port; s.first_dport = sd.dst_port;
+        s.first_prot = sd.prot; s.first_tos = sd.tos; s.first_v6 = sd.src_v6;
+        for (int k = 0; k < 16; k++) { s.first_src[k] = sd.source[k]; s.first_dst[k] = sd.destination[k]; }
         s.first_time = P.t;
     }
     Parsed Q;
     parse_global(a.bs, a.nb, s.last, macs, Q);
     s.last_time = Q.t;
-    out[d] = s;
+    s.annex = NONE32;
 }
 
-// grid-stride over the flows counted on the device (no host round trip)
-__global__ void __launch_bounds__(256) k_export(FinArgs a, fluere_flow_summary* out) {
+// A flow's local order dependence (shard side): trivial when its first FIN/RST
+// (if any) is its last packet and its first packet can create it (or none
+// can) -- then the summary alone determines its part of the state machine.
+__global__ void __launch_bounds__(256) k_local_cert(FinArgs a, uint32_t* annex_of) {
     const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) export_one(a, out, d);
-}
-
-// Shard block export (fluere_export_device): header + min(n_flows, cap) summaries.
-__global__ void __launch_bounds__(256) k_export_block(FinArgs a, uint8_t* blk, uint64_t cap) {
-    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    fluere_flow_summary* out = reinterpret_cast<fluere_flow_summary*>(blk + sizeof(fluere_shard_header));
-    const uint32_t ne = (uint32_t)min<uint64_t>(nf, cap);
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ne; d += gridDim.x * blockDim.x) export_one(a, out, d);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        fluere_shard_header h{};
-        h.n_flows = nf;
-        h.tmin = a.g->tmin;
-        h.tmax = a.g->tmax;
-        h.valid = a.g->valid;
-        h.dropped = a.g->dropped;
-        h.raw = a.g->raw;
-        h.err = *a.T.err;
-        *reinterpret_cast<fluere_shard_header*>(blk) = h;
+    for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
+        const uint32_t d = d0 + threadIdx.x;
+        bool cplx = false;
+        if (d < nf) {
+            const unsigned long long fa = a.A.fa[d], fc = a.A.fc[d], fr = a.A.fr[d], la = a.A.la[d];
+            cplx = !((fr == NONE64 || fr == la) && (fc == fa || fc == NONE64));
+            a.complex[d] = cplx ? 1 : 0;
+            annex_of[d] = NONE32;
+        }
+        const uint64_t cm = __ballot(cplx);
+        if (cm && (uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm))
+            atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
     }
 }
+
+struct ExportArgs {
+    FinArgs fa;
+    uint8_t* blocks;
+    uint32_t n_owners, shard;
+    uint64_t cap, cap_annex, block_bytes;
+    const uint32_t* annex_of;
+    const fluere_flow_annex* annex;
+};
+__device__ __forceinline__ fluere_shard_header* blk_hdr(uint8_t* blocks, uint64_t block_bytes, uint32_t o) {
+    return reinterpret_cast<fluere_shard_header*>(blocks + (size_t)o * block_bytes);
+}
+__device__ __forceinline__ fluere_flow_summary* blk_sum(uint8_t* blocks, uint64_t block_bytes, uint32_t o) {
+    return reinterpret_cast<fluere_flow_summary*>(blocks + (size_t)o * block_bytes + sizeof(fluere_shard_header));
+}
+__device__ __forceinline__ fluere_flow_annex* blk_annex(uint8_t* blocks, uint64_t block_bytes, uint64_t cap, uint32_t o) {
+    return reinterpret_cast<fluere_flow_annex*>(blocks + (size_t)o * block_bytes + sizeof(fluere_shard_header) +
+                                                cap * sizeof(fluere_flow_summary));
+}
+
+__global__ void k_export_hdr(ExportArgs a) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= a.n_owners) return;
+    fluere_shard_header h{};
+    const Glob* g = a.fa.g;
+    h.tmin = g->tmin; h.tmax = g->tmax; h.valid = g->valid; h.dropped = g->dropped;
+    h.err = *a.fa.T.err;
+    h.shard = a.shard;
+    *blk_hdr(a.blocks, a.block_bytes, o) = h;
+}
+
+__global__ void __launch_bounds__(256) k_export_owners(ExportArgs a) {
+    const uint32_t nf = min(*a.fa.T.n_flows, a.fa.T.fmax);
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) {
+        fluere_flow_summary s;
+        export_one(a.fa, s, d);
+        s.shard = a.shard;
+        const uint32_t o = key_owner(s.key, a.n_owners);
+        fluere_shard_header* h = blk_hdr(a.blocks, a.block_bytes, o);
+        const unsigned long long pos = atomicAdd(reinterpret_cast<unsigned long long*>(&h->n_flows), 1ull);
+        const uint32_t ax = a.annex_of[d];
+        if (ax != NONE32) {
+            const unsigned long long apos = atomicAdd(reinterpret_cast<unsigned long long*>(&h->n_annex), 1ull);
+            if (apos < a.cap_annex) {
+                blk_annex(a.blocks, a.block_bytes, a.cap, o)[apos] = a.annex[ax];
+                s.annex = (uint32_t)apos;
+            }
+        }
+        if (pos < a.cap) blk_sum(a.blocks, a.block_bytes, o)[pos] = s;
+    }
+}
+
+__global__ void k_export_need(ExportArgs a, unsigned long long* need) {
+    if (threadIdx.x || blockIdx.x) return;
+    unsigned long long m0 = 0, m1 = 0;
+    for (uint32_t o = 0; o < a.n_owners; o++) {
+        const fluere_shard_header* h = blk_hdr(a.blocks, a.block_bytes, o);
+        m0 = max(m0, (unsigned long long)h->n_flows);
+        m1 = max(m1, (unsigned long long)h->n_annex);
+    }
+    need[0] = m0;
+    need[1] = m1;
+}
+
+struct FirstPay {
+    unsigned long long t_first, t_last;
+    uint16_t sp, dp;
+    uint8_t dir, prot, tos, v6;
+    uint8_t src[16], dst[16];
+};
 
 struct MergeArgs {
     TableSet T;
     Acc A;
-    const fluere_flow_summary* in;
-    unsigned long long n;
+    unsigned long long n;  // n_shards * cap summary slots
     uint32_t* sd;
     FirstPay* pay;
     Glob* g;
     fluere_record* out;
     uint8_t* complex;
     uint64_t out_cap;
-    // gathered blocks (fluere_merge_gathered): summary i is entry i % cap of
-    // block i / cap; entries past the block's n_flows are skipped
+    // the gathered blocks: summary i is entry i % cap of block i / cap (the
+    // block of rank i / cap); entries past the block's n_flows are absent
     const uint8_t* blocks;
-    unsigned long long cap, block_bytes;
+    unsigned long long cap, cap_annex, block_bytes;
     Ctl* host_ctl;   // non-null: k_merge_finalize publishes the counters (publish_ctl)
     uint32_t seq;
 };
 
-// summary i of a merge (flat array, or gathered blocks); null when absent
+// summary i of a merge; null when absent
 __device__ __forceinline__ const fluere_flow_summary* merge_input(const MergeArgs& a, unsigned long long i) {
     if (i >= a.n) return nullptr;
-    if (!a.blocks) return a.in + i;
-    const uint8_t* blk = a.blocks + (i / a.cap) * a.block_bytes;
-    const fluere_shard_header* h = reinterpret_cast<const fluere_shard_header*>(blk);
+    uint8_t* blocks = const_cast<uint8_t*>(a.blocks);
+    const uint32_t b = (uint32_t)(i / a.cap);
     const unsigned long long j = i % a.cap;
-    if (j >= h->n_flows) return nullptr;
-    return reinterpret_cast<const fluere_flow_summary*>(blk + sizeof(fluere_shard_header)) + j;
+    if (j >= min((unsigned long long)blk_hdr(blocks, a.block_bytes, b)->n_flows, a.cap)) return nullptr;
+    return blk_sum(blocks, a.block_bytes, b) + j;
+}
+__device__ __forceinline__ const fluere_flow_annex* merge_annex(const MergeArgs& a, unsigned long long i, uint32_t k) {
+    return blk_annex(const_cast<uint8_t*>(a.blocks), a.block_bytes, a.cap, (uint32_t)(i / a.cap)) + k;
 }
 
 __global__ void __launch_bounds__(256) k_merge_insert(MergeArgs a) {
     unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (a.blocks && i < a.n && i % a.cap == 0) {  // the block's run counters
-        const fluere_shard_header* h = reinterpret_cast<const fluere_shard_header*>(a.blocks + (i / a.cap) * a.block_bytes);
+    if (i < a.n && i % a.cap == 0) {  // the block's run counters
+        const fluere_shard_header* h = blk_hdr(const_cast<uint8_t*>(a.blocks), a.block_bytes, (uint32_t)(i / a.cap));
         if (h->valid) {
             atomicAdd(&a.g->valid, (unsigned long long)h->valid);
             atomicMin(&a.g->tmin, (unsigned long long)h->tmin);
             atomicMax(&a.g->tmax, (unsigned long long)h->tmax);
         }
         if (h->dropped) atomicAdd(&a.g->dropped, (unsigned long long)h->dropped);
-        if (h->raw) atomicAdd(&a.g->raw, (unsigned long long)h->raw);
         if (h->err) atomicOr(a.T.err, h->err);
-        if (h->n_flows > a.cap) atomicOr(a.T.err, ERR_CAPACITY);  // the block was cut short
+        if (h->n_flows > a.cap || h->n_annex > a.cap_annex) atomicOr(a.T.err, ERR_CAPACITY);  // cut short
     }
     const fluere_flow_summary* sp = merge_input(a, i);
     if (!sp) {
@@ -1966,35 +2039,29 @@ __global__ void __launch_bounds__(256) k_merge_payload(MergeArgs a) {
     const fluere_flow_summary& s = *merge_input(a, i);
     // packet indices are global and unique: exactly one shard holds each
     if (s.first_create != NONE64 && s.first_create == a.A.fc[d]) {
-        a.pay[d].t_first = s.first_time;
-        a.pay[d].sp = s.first_sport; a.pay[d].dp = s.first_dport;
-        a.pay[d].dir = s.first_dir; a.pay[d].prot = s.first_prot; a.pay[d].tos = s.first_tos;
+        FirstPay& p = a.pay[d];
+        p.t_first = s.first_time;
+        p.sp = s.first_sport; p.dp = s.first_dport;
+        p.dir = s.first_dir; p.prot = s.first_prot; p.tos = s.first_tos; p.v6 = s.first_v6;
+        for (int k = 0; k < 16; k++) { p.src[k] = s.first_src[k]; p.dst[k] = s.first_dst[k]; }
     }
     if (s.last == a.A.la[d]) a.pay[d].t_last = s.last_time;
 }
 
-__device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t d) {
+__device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t d, fluere_record& r, bool& want,
+                                                   bool& cplx) {
     const Acc& A = a.A;
     unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
     if (fc == NONE64) return;
     if (!(fc == fa && (fr == NONE64 || fr == la))) {
         a.complex[d] = 1;
-        atomicAdd(&a.g->n_complex, 1ull);
+        cplx = true;
         return;
     }
     const FirstPay p = a.pay[d];
-    const uint32_t* key = (const uint32_t*)(a.T.flow_key + (size_t)d * 56);
-    fluere_record r;
     memset(&r, 0, sizeof r);
-    const bool v6 = (key[9] >> 8) & 1;
-    r.src_v6 = r.dst_v6 = v6;
-    const uint32_t* src = p.dir ? key + 4 : key;  // the creating packet's source endpoint
-    const uint32_t* dst = p.dir ? key : key + 4;
-    for (int k = 0; k < 4; k++)
-        for (int b = 0; b < 4; b++) {
-            r.source[4 * k + b] = (uint8_t)(src[k] >> (24 - 8 * b));
-            r.destination[4 * k + b] = (uint8_t)(dst[k] >> (24 - 8 * b));
-        }
+    r.src_v6 = r.dst_v6 = p.v6;
+    for (int k = 0; k < 16; k++) { r.source[k] = p.src[k]; r.destination[k] = p.dst[k]; }
     r.prot = p.prot; r.tos = p.tos; r.src_port = p.sp; r.dst_port = p.dp;
     uint32_t p0 = A.pk[0][d], p1 = A.pk[1][d];
     unsigned long long b0 = A.by[0][d], b1 = A.by[1][d];
@@ -2008,14 +2075,146 @@ __device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t 
     r.first = p.t_first;
     r.last = p.t_last;
     r.order_key = (fr == la) ? la : NONE64;
-    emit_record(a.g, a.out, a.out_cap, r);
+    want = true;
 }
 
 // grid-stride over the flows counted on the device (no host round trip)
 __global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
     const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nf; d += gridDim.x * blockDim.x) merge_finalize_one(a, d);
+    for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
+        const uint32_t d = d0 + threadIdx.x;
+        fluere_record r;
+        bool want = false, cplx = false;
+        if (d < nf) merge_finalize_one(a, d, r, want, cplx);
+        emit_record_wave(a.g, a.out, a.out_cap, r, want);
+        const uint64_t cm = __ballot(cplx);
+        if (cm && (uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm))
+            atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
+    }
     if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
+}
+
+// ---- composition of the order-dependent flows at their owner ----------------
+// the owner's summaries of complex flows, as (flow << 8 | shard, summary index)
+__global__ void __launch_bounds__(256) k_comp_collect(MergeArgs a, unsigned long long* keys, uint32_t* vals) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t d = a.sd[i];
+    if (d == FAIL || d >= a.T.fmax || !a.complex[d]) return;
+    const unsigned long long pos = atomicAdd(&a.g->n_keys, 1ull);
+    keys[pos] = ((unsigned long long)d << 8) | (i / a.cap);
+    vals[pos] = (uint32_t)i;
+}
+
+__device__ __forceinline__ void piece_clear(fluere_flow_piece& p) {
+    memset(&p, 0, sizeof p);
+    p.min_pkt = p.min_ttl = NONE32;
+}
+__device__ __forceinline__ void piece_add(fluere_flow_piece& f, const fluere_flow_piece& x) {
+    for (int q = 0; q < 2; q++) { f.pkts[q] += x.pkts[q]; f.bytes[q] += x.bytes[q]; }
+    f.min_pkt = min(f.min_pkt, x.min_pkt); f.max_pkt = max(f.max_pkt, x.max_pkt);
+    f.min_ttl = min(f.min_ttl, x.min_ttl); f.max_ttl = max(f.max_ttl, x.max_ttl);
+    for (int q = 0; q < 8; q++) f.flag_cnt[q] += x.flag_cnt[q];
+    if (x.pkts[0] + x.pkts[1] && (f.pkts[0] + f.pkts[1] == x.pkts[0] + x.pkts[1] || x.last > f.last)) {
+        f.last = x.last;
+        f.last_time = x.last_time;
+    }
+}
+// a trivial shard summary as one piece (its seed: the creating packet)
+__device__ __forceinline__ void piece_of_summary(const fluere_flow_summary& s, fluere_flow_piece& p) {
+    p.pkts[0] = s.pkts[0]; p.pkts[1] = s.pkts[1];
+    p.bytes[0] = s.bytes[0]; p.bytes[1] = s.bytes[1];
+    p.min_pkt = s.min_pkt; p.max_pkt = s.max_pkt; p.min_ttl = s.min_ttl; p.max_ttl = s.max_ttl;
+    for (int q = 0; q < 8; q++) p.flag_cnt[q] = s.flag_cnt[q];
+    p.last = s.last; p.last_time = s.last_time;
+    p.first = s.first_create; p.first_time = s.first_time;
+    for (int k = 0; k < 16; k++) { p.src[k] = s.first_src[k]; p.dst[k] = s.first_dst[k]; }
+    p.v6 = s.first_v6; p.prot = s.first_prot; p.tos = s.first_tos; p.dir = s.first_dir;
+    p.src_port = s.first_sport; p.dst_port = s.first_dport;
+}
+__device__ __forceinline__ void record_of_piece(const fluere_flow_piece& f, unsigned long long order, fluere_record& r) {
+    memset(&r, 0, sizeof r);
+    r.src_v6 = r.dst_v6 = f.v6;
+    for (int k = 0; k < 16; k++) { r.source[k] = f.src[k]; r.destination[k] = f.dst[k]; }
+    r.prot = f.prot; r.tos = f.tos; r.src_port = f.src_port; r.dst_port = f.dst_port;
+    const uint32_t o = f.dir;
+    r.d_pkts = f.pkts[0] + f.pkts[1];
+    r.d_octets = f.bytes[0] + f.bytes[1];
+    r.out_pkts = f.pkts[o]; r.in_pkts = f.pkts[1 - o];
+    r.out_bytes = f.bytes[o]; r.in_bytes = f.bytes[1 - o];
+    r.min_pkt = f.min_pkt; r.max_pkt = f.max_pkt;
+    r.min_ttl = (uint8_t)f.min_ttl; r.max_ttl = (uint8_t)f.max_ttl;
+    for (int q = 0; q < 8; q++) r.cnt[q] = f.flag_cnt[q];
+    r.first = f.first_time;
+    r.last = f.last_time;
+    r.order_key = order;
+}
+
+// One thread per complex flow: offline_fluereflows.rs:97-157 over the shards
+// in order, each shard as (A = its packets up to its first FIN/RST, f0, H =
+// the instance it creates from "no flow" up to f0, T = the instance open at
+// its end after f0).  Entering with a flow F open: F += A, closed at f0 (then
+// T, if any, is open).  Entering with none: H is emitted at f0 (or stays open
+// without f0), then T.
+__global__ void __launch_bounds__(64) k_compose(MergeArgs a, const unsigned long long* keys, const uint32_t* vals,
+                                                unsigned long long n) {
+    const unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n || (p > 0 && (keys[p - 1] >> 8) == (keys[p] >> 8))) return;
+    const unsigned long long d = keys[p] >> 8;
+    fluere_flow_piece F;
+    bool open = false;
+    for (unsigned long long q = p; q < n && (keys[q] >> 8) == d; q++) {
+        const unsigned long long i = vals[q];
+        const fluere_flow_summary& s = *merge_input(a, i);
+        fluere_flow_piece A, H, T;
+        bool has_f0, has_H, has_T;
+        unsigned long long f0;
+        if (s.annex == NONE32) {
+            piece_of_summary(s, A);
+            has_f0 = s.finrst_min != NONE64;
+            f0 = s.finrst_min;
+            has_H = s.first_create != NONE64;  // == first_all (the local certificate held)
+            H = A;
+            has_T = false;
+        } else {
+            const fluere_flow_annex& x = *merge_annex(a, i, s.annex);
+            has_f0 = x.flags & 1;
+            f0 = x.f0;
+            has_H = x.flags & 4;
+            has_T = x.flags & 8;
+            piece_clear(A);
+            if (x.flags & 2) piece_add(A, x.lead);
+            if (has_H) piece_add(A, x.head);
+            H = x.head;
+            T = x.tail;
+        }
+        fluere_record r;
+        if (open) {
+            piece_add(F, A);
+            if (has_f0) {
+                record_of_piece(F, f0, r);
+                emit_record(a.g, a.out, a.out_cap, r);
+                open = false;
+            }
+        } else if (has_f0) {
+            if (has_H) {
+                record_of_piece(H, f0, r);
+                emit_record(a.g, a.out, a.out_cap, r);
+            }
+        } else if (has_H) {
+            F = H;
+            open = true;
+        }
+        if (has_f0 && has_T) {
+            F = T;
+            open = true;
+        }
+    }
+    if (open) {
+        fluere_record r;
+        record_of_piece(F, NONE64, r);
+        emit_record(a.g, a.out, a.out_cap, r);
+    }
 }
 
 // test seam: insert canonical keys, return dense ids (flow dictionary checks)
@@ -2135,6 +2334,14 @@ struct fluere_ctx {
     void* d_stage = nullptr;    // hot-kernel partial aggregates (Stage)
     void* d_exact = nullptr;    // exact state machine scratch (exact.hip)
     size_t d_exact_bytes = 0;
+    // multi-GPU export: annexes of the shard's order-dependent flows, their
+    // index per flow, the largest per-owner counts; the final records the
+    // export produced (kept through the owner merge)
+    fluere_flow_annex* d_annex = nullptr;
+    uint64_t d_annex_cap = 0;
+    uint32_t* d_annex_of = nullptr;
+    void* d_need = nullptr;
+    uint64_t local_n_rec = 0, local_updates = 0, local_ended = 0;
     size_t d_stage_bytes = 0;
     bool generic_dirty = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
@@ -2305,6 +2512,9 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_slow);
     hipFree(c->d_stage);
     hipFree(c->d_exact);
+    hipFree(c->d_annex);
+    hipFree(c->d_annex_of);
+    hipFree(c->d_need);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -3394,43 +3604,88 @@ extern "C" int fluere_set_index_base(fluere_ctx* c, uint64_t base) {
     return FLUERE_OK;
 }
 
-extern "C" int fluere_export_summaries(fluere_ctx* c, fluere_flow_summary* d_out, uint64_t cap, uint64_t* n,
-                                       uint64_t* tmin, uint64_t* tmax) {
-    if (!c || !n) return FLUERE_E_ARG;
+extern "C" uint64_t fluere_shard_block_bytes(uint64_t cap, uint64_t cap_annex) {
+    return sizeof(fluere_shard_header) + cap * sizeof(fluere_flow_summary) + cap_annex * sizeof(fluere_flow_annex);
+}
+
+// Record buffer of at least `need` records, keeping the first `keep`.
+static int grow_recs_keep(fluere_ctx* c, uint64_t need, uint64_t keep) {
+    if (need <= c->d_recs_cap) return FLUERE_OK;
+    fluere_record* nr = nullptr;
+    const uint64_t cap = std::max<uint64_t>(need, 1024);
+    if (hipMalloc(&nr, cap * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
+    if (keep) HIPCHECK(hipMemcpyAsync(nr, c->d_recs, keep * sizeof(fluere_record), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    hipFree(c->d_recs);
+    c->d_recs = nr;
+    c->d_recs_cap = cap;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
+                                    uint64_t cap_annex, uint64_t* need, uint64_t* need_annex) {
+    if (!c || !d_blocks || !n_owners || !cap) return FLUERE_E_ARG;
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
     if ((rc = upload_batches(c))) return rc;
-    FinArgs fa{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
-    // a buffer for every possible flow: export first, then one readback
-    const bool one_pass = d_out && cap >= c->fmax;
-    if (one_pass) k_export<<<flow_grid(c), 256, 0, s>>>(fa, d_out);
-    HIPCHECK(hipGetLastError());
+    const TableSet T = tables_of(c);
+    const int nb = (int)c->batches.size();
+    if (!c->d_annex_of && hipMalloc(&c->d_annex_of, (size_t)c->fmax * 4) != hipSuccess) return FLUERE_E_NOMEM;
+    if (!c->d_need && hipMalloc(&c->d_need, 16) != hipSuccess) return FLUERE_E_NOMEM;
+    FinArgs fa{c->d_batches, nb, T, c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
+    // 1. flows whose part of the state machine depends on packet order here
+    reset_record_counters(c);
+    k_local_cert<<<flow_grid(c), 256, 0, s>>>(fa, c->d_annex_of);
     Glob g;
-    uint32_t nf_err[2];
-    if ((rc = fetch_ctl(c, g, nf_err))) return rc;
-    if (nf_err[1]) return FLUERE_E_TABLE_FULL;
-    uint32_t nf = std::min(nf_err[0], c->fmax);
-    *n = nf;
-    if (tmin) *tmin = g.tmin;
-    if (tmax) *tmax = g.tmax;
-    if (!d_out || one_pass) return FLUERE_OK;
-    if (cap < nf) return FLUERE_E_ARG;
-    k_export<<<flow_grid(c), 256, 0, s>>>(fa, d_out);
-    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
+    // 2. their annexes (and the records that open and close in this shard)
+    if (g.n_complex) {
+        std::vector<Batch> hb(nb);
+        for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
+        ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 0, c->timeout_ms * 1000ull, c->d_complex, c->d_glob,
+                   &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes,
+                   1, &c->d_annex, &c->d_annex_cap, c->d_annex_of};
+        ExactResult er{};
+        if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
+        HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    }
+    // 3. summaries + annexes into the owners' blocks
+    ExportArgs ea{fa, (uint8_t*)d_blocks, n_owners, shard, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
+                  c->d_annex_of, (const fluere_flow_annex*)c->d_annex};
+    k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
+    k_export_owners<<<flow_grid(c), 256, 0, s>>>(ea);
+    k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need);
+    HIPCHECK(hipGetLastError());
+    unsigned long long nd[2];
+    HIPCHECK(hipMemcpyAsync(nd, c->d_need, 16, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (need) *need = nd[0];
+    if (need_annex) *need_annex = nd[1];
+    // the final records this shard produced (kept through the merge)
+    c->local_n_rec = g.n_rec;
+    c->local_updates = g.n_updates;
+    c->local_ended = g.n_ended;
     return FLUERE_OK;
 }
 
-// Merge of shard summaries: a flat array (d_in, n) or gathered shard blocks
-// (blocks, n_shards * cap entries; tmin / tmax then come from the headers).
-static int merge_common(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, const uint8_t* blocks, uint64_t cap,
-                        uint64_t tmin, uint64_t tmax, fluere_stats* st) {
+extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap,
+                                     uint64_t cap_annex, fluere_stats* st) {
+    if (!c || (!d_blocks && n_shards) || (n_shards && !cap)) return FLUERE_E_ARG;
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
+    const uint64_t n = (uint64_t)n_shards * cap;
+    const uint64_t keep = c->local_n_rec;
     if ((rc = clear_flows(c))) return rc;
     c->precleaned = false;
+    {   // the records this rank's export produced stay first in d_recs
+        const unsigned long long cnt[3] = {keep, c->local_updates, c->local_ended};
+        char* gb = (char*)c->d_glob;
+        HIPCHECK(hipMemcpyAsync(gb + offsetof(Glob, n_rec), &cnt[0], 8, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipMemcpyAsync(gb + offsetof(Glob, n_updates), &cnt[1], 16, hipMemcpyHostToDevice, s));
+    }
     if (!c->d_pay && hipMalloc(&c->d_pay, (size_t)c->fmax * sizeof(FirstPay)) != hipSuccess) return FLUERE_E_NOMEM;
     if (std::max<uint64_t>(n, 1) > c->d_sd_cap) {
         hipFree(c->d_sd);
@@ -3439,12 +3694,12 @@ static int merge_common(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t
         if (hipMalloc(&c->d_sd, std::max<uint64_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
         c->d_sd_cap = std::max<uint64_t>(n, 1);
     }
-    if ((rc = ensure_recs(c, std::min<uint64_t>(std::max<uint64_t>(n, 1), std::max<uint64_t>(c->fmax, 1))))) return rc;
+    if ((rc = grow_recs_keep(c, keep + std::min<uint64_t>(std::max<uint64_t>(n, 1), c->fmax), keep))) return rc;
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
-    MergeArgs ma{tables_of(c), c->acc, d_in, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
-                 c->d_recs_cap, blocks, cap, fluere_shard_block_bytes(cap), c->h_ctl, seq};
-    // (no event markers: each adds a gap to the stream; timing is host wall)
+    MergeArgs ma{tables_of(c), c->acc, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
+                 c->d_recs_cap, (const uint8_t*)d_blocks, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
+                 c->h_ctl, seq};
     if (n) {
         k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
         k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
@@ -3456,59 +3711,62 @@ static int merge_common(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t
     if ((rc = wait_published(c, seq, g, nf_err))) return rc;
     if (nf_err[1] & ERR_CAPACITY) return FLUERE_E_ARG;  // a shard had more flows than its block holds
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
+    const uint64_t timeout_us = c->timeout_ms * 1000ull;
+    const bool expiry = g.valid && g.tmax >= g.tmin && g.tmax - g.tmin >= timeout_us;
+    if (g.n_complex && !expiry) {
+        // the order-dependent flows: compose the shards' pieces in shard order
+        unsigned long long *keys = nullptr, *keys2 = nullptr;
+        uint32_t *vals = nullptr, *vals2 = nullptr;
+        void* tmp = nullptr;
+        size_t tb = 0;
+        const uint64_t m = n;
+        if (hipMalloc(&keys, m * 8) != hipSuccess || hipMalloc(&keys2, m * 8) != hipSuccess ||
+            hipMalloc(&vals, m * 4) != hipSuccess || hipMalloc(&vals2, m * 4) != hipSuccess) {
+            hipFree(keys); hipFree(keys2); hipFree(vals); hipFree(vals2);
+            return FLUERE_E_NOMEM;
+        }
+        HIPCHECK(hipMemsetAsync(&c->d_glob->n_keys, 0, 8, s));
+        k_comp_collect<<<grid_for(n, 256), 256, 0, s>>>(ma, keys, vals);
+        unsigned long long nk = 0;
+        HIPCHECK(hipMemcpyAsync(&nk, &c->d_glob->n_keys, 8, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        // records: the certified ones + at most one per shard piece
+        if ((rc = grow_recs_keep(c, g.n_rec + 2 * nk, g.n_rec))) return rc;
+        ma.out = c->d_recs;
+        ma.out_cap = c->d_recs_cap;
+        int end_bit = 8;
+        while (end_bit < 64 && (1ull << (end_bit - 8)) <= c->fmax) end_bit++;
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys2, vals, vals2, (int)nk, 0, end_bit, s);
+        if (hipMalloc(&tmp, std::max<size_t>(tb, 16)) != hipSuccess) {
+            hipFree(keys); hipFree(keys2); hipFree(vals); hipFree(vals2);
+            return FLUERE_E_NOMEM;
+        }
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, (int)nk, 0, end_bit, s));
+        if (nk) k_compose<<<grid_for(nk, 64), 64, 0, s>>>(ma, keys2, vals2, nk);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        hipFree(tmp); hipFree(keys); hipFree(keys2); hipFree(vals); hipFree(vals2);
+    }
     const uint32_t nf = std::min(nf_err[0], c->fmax);
     c->dev_n_rec = g.n_rec;
     c->host_recs = false;
     c->have_results = true;
+    c->local_n_rec = c->local_updates = c->local_ended = 0;
     fluere_stats out{};
-    const double ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    const double ms_parse = 0;
-    if (blocks) {
-        tmin = g.tmin;
-        tmax = g.tmax;
-        out.valid = g.valid;
-        out.dropped_parse = g.dropped;
-        }
+    out.valid = g.valid;
+    out.dropped_parse = g.dropped;
     out.flows = nf;
     out.records = g.n_rec;
     out.ended = g.n_ended;
     out.complex_flows = g.n_complex;
-    out.parse_ms = ms_parse;
-    out.total_ms = ms_total;
+    out.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     out.updates = g.n_updates;
     if (st) *st = out;
-    // expiries or order-dependent flows across shards need the per-packet
-    // state machine, which the sharded path does not run yet
-    if (g.n_complex || (tmax >= tmin && tmax - tmin >= c->timeout_ms * 1000ull)) return FLUERE_E_UNSUPPORTED;
+    // the hard-timeout sweep (offline_fluereflows.rs:161-175) is not composed
+    // across shards: such a capture runs in one context
+    if (expiry) return FLUERE_E_UNSUPPORTED;
     return FLUERE_OK;
-}
-
-extern "C" int fluere_merge_summaries(fluere_ctx* c, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
-                                      uint64_t tmax, fluere_stats* st) {
-    if (!c || (!d_in && n)) return FLUERE_E_ARG;
-    return merge_common(c, d_in, n, nullptr, 0, tmin, tmax, st);
-}
-
-extern "C" uint64_t fluere_shard_block_bytes(uint64_t cap) {
-    return sizeof(fluere_shard_header) + cap * sizeof(fluere_flow_summary);
-}
-
-extern "C" int fluere_export_device(fluere_ctx* c, void* d_block, uint64_t cap) {
-    if (!c || !d_block) return FLUERE_E_ARG;
-    HIPCHECK(hipSetDevice(c->device));
-    int rc;
-    if ((rc = upload_batches(c))) return rc;
-    FinArgs fa{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(std::max<uint64_t>(cap, 1), 256), flow_grid(c)));
-    k_export_block<<<grid, 256, 0, c->stream>>>(fa, (uint8_t*)d_block, cap);
-    HIPCHECK(hipGetLastError());
-    return FLUERE_OK;
-}
-
-extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap,
-                                     fluere_stats* st) {
-    if (!c || (!d_blocks && n_shards) || (n_shards && !cap)) return FLUERE_E_ARG;
-    return merge_common(c, nullptr, (uint64_t)n_shards * cap, (const uint8_t*)d_blocks, cap, 0, 0, st);
 }
 
 extern "C" int fluere_debug_dense_ids(fluere_ctx* c, const uint32_t* d_keys, uint64_t n, uint32_t* d_out) {

@@ -1,18 +1,24 @@
 """Packet-range sharding over GPUs: one process per GPU (torch.distributed,
-backend "nccl" = RCCL on ROCm), flow-table merge as one all_gather of per-flow
-summaries over xGMI followed by a device merge on rank 0.
+backend "nccl" = RCCL on ROCm).  The one exchange is the flow-table merge:
+every rank exports its flows into one block per owner rank (owner = hash of
+the canonical key), one all-to-all over xGMI delivers them, and every owner
+merges and finalizes its own flows (fluere_export_device /
+fluere_merge_gathered in include/fluere_gpu.h).
 
-Reference: the offline loop is one sequential pass (offline_fluereflows.rs:68-176);
-shard r processes packets [r*N/G, (r+1)*N/G) with global packet indices, so the
-order-dependent record fields (first / last packet, FIN/RST position) merge as
-min / max of global indices.
+Reference: the offline loop is one sequential pass (offline_fluereflows.rs:68-176).
+Shard r processes packets [r*N/G, (r+1)*N/G) with global packet indices, so
+order-free record fields merge as sums / min / max, and the flows whose record
+depends on packet order are composed at their owner from per-shard pieces of
+the state machine (the annex of fluere_gpu.h).
 """
 from __future__ import annotations
 
 import ctypes
 
+import numpy as np
+
 from . import _lib
-from ._lib import SHARD_HEADER_BYTES, SUMMARY_BYTES, Stats, check
+from ._lib import RECORD_DTYPE, Stats, check
 
 
 def shard_range(n_packets: int, rank: int, world: int):
@@ -25,158 +31,160 @@ def set_index_base(ctx, base: int):
     check(_lib.lib().fluere_set_index_base(ctx._h, base), "fluere_set_index_base")
 
 
-ONE_PASS_BYTES = 256 << 20  # export buffers up to this size hold every possible flow
+def _pow2_at_least(n: int, lo: int) -> int:
+    c = max(1, lo)
+    while c < n:
+        c *= 2
+    return c
 
 
-def export_summaries(ctx, out=None):
-    """parse+key+aggregate this shard and export its flows -> (uint8 cuda tensor [n*192], tmin, tmax).
-
-    With a buffer for the context's whole flow capacity the export is one pass
-    with a single host round trip (fluere_capacity).  The buffer is cached on
-    the context unless `out` is given; the returned tensor is a view of it."""
-    import torch
-    L = _lib.lib()
-    ctx.parse_aggregate()
-    n, lo, hi = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-    cap = int(L.fluere_capacity(ctx._h))
-    if out is None:
-        out = getattr(ctx, "_export_buf", None)
-    if cap * SUMMARY_BYTES <= ONE_PASS_BYTES:
-        if out is None or out.numel() < cap * SUMMARY_BYTES:
-            out = torch.empty(max(cap, 1) * SUMMARY_BYTES, dtype=torch.uint8, device="cuda")
-        ctx._export_buf = out
-        check(L.fluere_export_summaries(ctx._h, out.data_ptr(), cap, ctypes.byref(n), ctypes.byref(lo),
-                                        ctypes.byref(hi)), "fluere_export_summaries")
-        return out[: n.value * SUMMARY_BYTES], lo.value, hi.value
-    check(L.fluere_export_summaries(ctx._h, None, 0, ctypes.byref(n), ctypes.byref(lo), ctypes.byref(hi)),
-          "fluere_export_summaries")
-    if out is None or out.numel() < n.value * SUMMARY_BYTES:
-        out = torch.empty(max(n.value, 1) * SUMMARY_BYTES, dtype=torch.uint8, device="cuda")
-    ctx._export_buf = out
-    check(L.fluere_export_summaries(ctx._h, out.data_ptr(), n.value, ctypes.byref(n), None, None),
-          "fluere_export_summaries")
-    return out[: n.value * SUMMARY_BYTES], lo.value, hi.value
-
-
-def merge_summaries(ctx, summaries, tmin: int, tmax: int) -> dict:
-    st = Stats()
-    n = summaries.numel() // SUMMARY_BYTES
-    check(_lib.lib().fluere_merge_summaries(ctx._h, summaries.data_ptr() if n else None, n, tmin, tmax,
-                                            ctypes.byref(st)), "fluere_merge_summaries")
-    return st.as_dict()
-
-
-NONE64 = (1 << 64) - 1  # tmin of a shard without valid packets
-
-
-def gather_summaries(summaries, tmin: int, tmax: int, group=None, dst: int = 0):
-    """All-gather every shard's flow summaries (RCCL over xGMI on GPUs, gloo on
-    CPU) -> (concatenated summaries in rank order, global tmin, global tmax) on
-    rank dst, None elsewhere.  Shards may be empty (tmin NONE64)."""
+def agree_need(need: int, need_annex: int, group=None, device=None):
+    """Largest per-owner counts over all ranks (every rank must size the
+    blocks alike): one small all-reduce."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    out_dev = summaries.device
-    # RCCL moves device tensors over xGMI; gloo (CPU tests, rehearsals) moves host copies
-    if dist.get_backend(group) == "gloo" and summaries.is_cuda:
-        summaries = summaries.cpu()
-    dev = summaries.device
-    # timestamps are microseconds (< 2^63); an empty shard travels as -1
-    meta = torch.tensor([summaries.numel() // SUMMARY_BYTES, tmin if tmin < (1 << 63) else -1, tmax],
-                        dtype=torch.int64, device=dev)
-    metas = torch.empty(world * 3, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(metas, meta, group=group)
-    m = metas.view(world, 3).cpu().tolist()  # one device->host copy
-    counts = [int(r[0]) for r in m]
-    lows = [int(r[1]) for r in m if int(r[1]) >= 0]
-    gmin = min(lows) if lows else NONE64
-    gmax = max(int(r[2]) for r in m)
-    cap = max(max(counts), 1) * SUMMARY_BYTES
-    send = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    send[: summaries.numel()] = summaries
-    recv = torch.empty(world * cap, dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(recv, send, group=group)
-    if rank != dst:
-        return None
-    parts = [recv[r * cap: r * cap + counts[r] * SUMMARY_BYTES] for r in range(world)]
-    return torch.cat(parts).to(out_dev), gmin, gmax
+    gloo = dist.get_backend(group) == "gloo"
+    t = torch.tensor([need, need_annex], dtype=torch.int64, device="cpu" if gloo else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    a, b = t.tolist()
+    return int(a), int(b)
 
 
-def gather_and_merge(ctx, summaries, tmin: int, tmax: int, group=None, dst: int = 0):
-    """All-gather every shard's summaries and merge them on rank dst (device
-    merge, fluere_merge_summaries).  Returns the merge stats on dst, None
-    elsewhere."""
+def exchange_blocks(send, recv, group=None):
+    """All-to-all of equal blocks: block o of rank r's `send` lands at block r
+    of rank o's `recv` (RCCL over xGMI; gloo moves host copies)."""
     import torch
-    got = gather_summaries(summaries, tmin, tmax, group, dst)
-    if got is None:
-        return None
-    allsum, gmin, gmax = got
-    torch.cuda.current_stream().synchronize()  # the collective ran on torch's stream, the merge runs on ctx's
-    return merge_summaries(ctx, allsum, gmin, gmax)
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo" and send.is_cuda:
+        s_h, r_h = send.cpu(), torch.empty(recv.numel(), dtype=recv.dtype)
+        dist.all_to_all_single(r_h, s_h, group=group)
+        recv.copy_(r_h)
+    else:
+        dist.all_to_all_single(recv, send, group=group)
 
 
 class ShardExchange:
-    """The multi-GPU step without host round trips in the middle: every rank
-    runs parse+key+aggregate over its shard and exports its flows into one
-    shard block (fluere_shard_header + `cap` summaries) on the device; one
-    all_gather moves the blocks (RCCL over xGMI); rank `dst` merges them on the
-    device (fluere_merge_gathered).  The only host reads are the gathered
-    headers (every rank checks that no shard had more than `cap` flows, and
-    grows `cap` and exchanges again if one had) and the merge's counters.
+    """The multi-GPU step: parse + key + aggregate over this rank's shard,
+    export into per-owner blocks (summaries of every flow, annexes of the flows
+    whose record depends on packet order in this shard, whose records that
+    open and close inside the shard stay here), agree on the block capacities,
+    one all-to-all, owner merge.  Every rank ends up holding the final records
+    of its own flows; gather_records() collects them on one rank.
 
     The context must run on torch's current stream (FlowContext(stream=
     torch.cuda.current_stream().cuda_stream)) so the collective is ordered
-    after the export; otherwise the context stream is synchronised first."""
+    after the export."""
 
-    def __init__(self, ctx, cap: int = 1024, group=None, dst: int = 0):
-        self.ctx, self.cap, self.group, self.dst = ctx, max(1, int(cap)), group, dst
+    def __init__(self, ctx, cap: int = 1024, cap_annex: int = 256, group=None):
+        self.ctx, self.group = ctx, group
+        self.cap, self.cap_annex = max(1, int(cap)), max(1, int(cap_annex))
         self._send = self._recv = None
 
     def _buffers(self, world, device):
         import torch
-        blk = int(_lib.lib().fluere_shard_block_bytes(self.cap))
-        if self._send is None or self._send.numel() != blk or self._send.device != device:
-            self._send = torch.empty(blk, dtype=torch.uint8, device=device)
+        blk = int(_lib.lib().fluere_shard_block_bytes(self.cap, self.cap_annex))
+        if self._send is None or self._send.numel() != world * blk or self._send.device != device:
+            self._send = torch.empty(world * blk, dtype=torch.uint8, device=device)
             self._recv = torch.empty(world * blk, dtype=torch.uint8, device=device)
         return blk
 
     def step(self, allow_unsupported: bool = False):
-        """One sharded pass; the merge stats on rank dst, None elsewhere.
-        Raises FluereError when the merge cannot give the exact result
-        (FLUERE_E_UNSUPPORTED) unless allow_unsupported."""
+        """One sharded pass; this rank's merge stats.  Raises FluereError when
+        the merge cannot give the exact result (FLUERE_E_UNSUPPORTED: the
+        capture needs the hard-timeout sweep) unless allow_unsupported."""
         import torch
         import torch.distributed as dist
         L = _lib.lib()
         ctx = self.ctx
         world = dist.get_world_size(self.group)
         rank = dist.get_rank(self.group)
-        gloo = dist.get_backend(self.group) == "gloo"
+        dev = torch.device("cuda", torch.cuda.current_device())
         ctx.parse_aggregate()
         while True:
-            blk = self._buffers(world, torch.device("cuda", torch.cuda.current_device()))
-            check(L.fluere_export_device(ctx._h, self._send.data_ptr(), self.cap), "fluere_export_device")
-            if ctx.stream is None or ctx.stream != torch.cuda.current_stream().cuda_stream:
-                torch.cuda.synchronize()  # the export ran on the context's own stream
-            if gloo:  # CPU rehearsal: host copies
-                recv_h = torch.empty(world * blk, dtype=torch.uint8)
-                dist.all_gather_into_tensor(recv_h, self._send.cpu(), group=self.group)
-                self._recv.copy_(recv_h)
-            else:
-                dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
-            # the headers' flow counts (one small device->host copy)
-            n = self._recv.view(world, blk)[:, :8].contiguous().view(torch.int64).cpu().tolist()
-            need = max(int(v[0]) for v in n)
-            if need <= self.cap:
+            self._buffers(world, dev)
+            need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
+            check(L.fluere_export_device(ctx._h, self._send.data_ptr(), world, rank, self.cap, self.cap_annex,
+                                         ctypes.byref(need), ctypes.byref(need_a)), "fluere_export_device")
+            n0, n1 = agree_need(need.value, need_a.value, self.group, dev)
+            if n0 <= self.cap and n1 <= self.cap_annex:
                 break
-            while self.cap < need:  # a shard had more flows: grow the blocks, exchange again
-                self.cap *= 2
-        if rank != self.dst:
-            return None
+            # a shard had more flows for some owner: grow the blocks, export again
+            self.cap = _pow2_at_least(n0, self.cap)
+            self.cap_annex = _pow2_at_least(n1, self.cap_annex)
+        exchange_blocks(self._send, self._recv, self.group)
         st = Stats()
-        rc = L.fluere_merge_gathered(ctx._h, self._recv.data_ptr(), world, self.cap, ctypes.byref(st))
+        rc = L.fluere_merge_gathered(ctx._h, self._recv.data_ptr(), world, self.cap, self.cap_annex,
+                                     ctypes.byref(st))
         if rc != _lib.E_UNSUPPORTED or not allow_unsupported:
             check(rc, "fluere_merge_gathered")
         d = st.as_dict()
         d["rc"] = rc
         return d
+
+    def gather_records(self, dst: int = 0):
+        """Every rank's records -> (records, n_ended) on rank dst in the
+        reference's order (ended prefix by emission order, then the active
+        flows); None elsewhere."""
+        import torch.distributed as dist
+        recs, _ = self.ctx.records()
+        parts = [None] * dist.get_world_size(self.group) if dist.get_rank(self.group) == dst else None
+        dist.gather_object(recs.tobytes(), parts, dst=dst, group=self.group)
+        if parts is None:
+            return None
+        return order_records([np.frombuffer(p, dtype=RECORD_DTYPE) for p in parts])
+
+
+NONE64 = (1 << 64) - 1
+
+
+def order_records(parts):
+    """Records of several ranks -> (records, n_ended): ended records by their
+    order key (the global index of the packet that ended them), then active."""
+    allr = np.concatenate(parts) if parts else np.zeros(0, dtype=RECORD_DTYPE)
+    order = np.lexsort((allr["first"], allr["order_key"]))
+    allr = allr[order]
+    return allr, int((allr["order_key"] != NONE64).sum())
+
+
+class LogicalShards:
+    """G shards on one device through the same export / merge code, with the
+    all-to-all done by device copies (SURVEY.md section 8e "testing without 8
+    GPUs"): contexts[r] holds packets [first_r, first_r + n_r)."""
+
+    def __init__(self, contexts, cap: int = 1024, cap_annex: int = 256):
+        self.ctxs = contexts
+        self.cap, self.cap_annex = cap, cap_annex
+
+    def run(self, allow_unsupported: bool = False):
+        import torch
+        L = _lib.lib()
+        G = len(self.ctxs)
+        for c in self.ctxs:
+            c.parse_aggregate()
+        while True:
+            blk = int(L.fluere_shard_block_bytes(self.cap, self.cap_annex))
+            sends, n0, n1 = [], 0, 0
+            for r, c in enumerate(self.ctxs):
+                send = torch.empty(G * blk, dtype=torch.uint8, device="cuda")
+                need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
+                check(L.fluere_export_device(c._h, send.data_ptr(), G, r, self.cap, self.cap_annex,
+                                             ctypes.byref(need), ctypes.byref(need_a)), "fluere_export_device")
+                sends.append(send)
+                n0, n1 = max(n0, need.value), max(n1, need_a.value)
+            if n0 <= self.cap and n1 <= self.cap_annex:
+                break
+            self.cap = _pow2_at_least(n0, self.cap)
+            self.cap_annex = _pow2_at_least(n1, self.cap_annex)
+        torch.cuda.synchronize()
+        stats = []
+        for o, c in enumerate(self.ctxs):
+            recv = torch.cat([s[o * blk:(o + 1) * blk] for s in sends])
+            st = Stats()
+            rc = L.fluere_merge_gathered(c._h, recv.data_ptr(), G, self.cap, self.cap_annex, ctypes.byref(st))
+            if rc != _lib.E_UNSUPPORTED or not allow_unsupported:
+                check(rc, "fluere_merge_gathered")
+            stats.append(st.as_dict())
+        return stats
+
+    def records(self):
+        return order_records([c.records()[0] for c in self.ctxs])

@@ -175,12 +175,26 @@ double fluere_last_pass_ms(fluere_ctx* ctx);
 int fluere_get_records(fluere_ctx* ctx, fluere_record** out, uint64_t* n, uint64_t* n_ended);
 void fluere_records_free(fluere_record* recs);
 
-/* ---- multi-GPU merge (one process per GPU; RCCL moves the bytes) -------- */
+/* ---- multi-GPU exchange (one process per GPU; RCCL moves the bytes) ----- */
 /* Packet-range sharding: rank r attaches packets [b_r, e_r) of the capture
  * with fluere_set_index_base(ctx, b_r) first, so every index is global.
- * After fluere_parse_aggregate each rank exports one summary per local flow;
- * the summaries of all ranks are gathered (RCCL all_gather over xGMI) and
- * merged on one rank, which then emits the records. */
+ * After fluere_parse_aggregate every rank exports its flows into one block
+ * per owner rank (owner = hash of the canonical key); one all-to-all over
+ * xGMI (RCCL) delivers to every owner the blocks of all ranks, in rank order;
+ * each owner merges its flows and builds their records.  No reference
+ * counterpart (the reference is single-threaded); the records equal the
+ * reference's on the whole capture.
+ *
+ * A summary carries a flow's order-free aggregate in one shard.  A flow whose
+ * record depends on packet order inside the shard (a FIN/RST before its last
+ * packet there, or a first packet that cannot create it) also carries an
+ * annex: the state machine of offline_fluereflows.rs:97-157 run over the
+ * shard's packets of the flow from "no flow": the lead piece (packets before
+ * the first create-eligible one, up to the first FIN/RST), the head instance
+ * (created in the shard, closed by that first FIN/RST or still open), the
+ * tail instance (open at the shard's end, after the first FIN/RST).  Records
+ * of instances that open and close between the two are final: the shard
+ * keeps them.  The owner composes summaries and annexes in shard order. */
 typedef struct fluere_flow_summary {
     uint32_t key[14];           /* canonical key words (DESIGN.md "Flow key") */
     uint32_t pkts[2];           /* per canonical direction */
@@ -189,45 +203,72 @@ typedef struct fluere_flow_summary {
     uint32_t flag_cnt[8];       /* fin syn rst psh ack urg ece cwr */
     uint64_t first_all, first_create, finrst_min, last; /* global packet indices */
     uint64_t first_time, last_time; /* times of packets first_create / last */
-    uint16_t first_sport, first_dport; /* FluereRecord ports of the creating packet */
-    uint8_t first_dir, first_prot, first_tos, pad0;
-    uint32_t pad1;
-} fluere_flow_summary;          /* 192 bytes */
+    uint16_t first_sport, first_dport; /* FluereRecord fields of the creating packet */
+    uint8_t first_dir, first_prot, first_tos, first_v6;
+    uint8_t first_src[16], first_dst[16];
+    uint32_t annex;             /* index of the flow's annex in the same block, or UINT32_MAX */
+    uint32_t shard;             /* exporting rank */
+    uint64_t pad[4];
+} fluere_flow_summary;          /* 256 bytes */
 
-/* Flow capacity of the context (max_flows clamped to the table size): a
- * summary buffer of this many entries lets fluere_export_summaries run in one
- * pass with a single host round trip. */
+/* A run of a flow's packets inside one shard: update_flow's order-free fields
+ * over the run, and (head / tail) the FluereRecord seed of its first packet. */
+typedef struct fluere_flow_piece {
+    uint32_t pkts[2];           /* per canonical direction */
+    uint64_t bytes[2];
+    uint32_t min_pkt, max_pkt, min_ttl, max_ttl;
+    uint32_t flag_cnt[8];
+    uint64_t last, last_time;   /* the run's last packet: global index, time */
+    uint64_t first, first_time; /* the run's first packet: global index, time */
+    uint8_t src[16], dst[16];   /* seed: FluereRecord source / destination, */
+    uint8_t v6, prot, tos, dir; /*       family, prot, tos, canonical direction */
+    uint16_t src_port, dst_port;
+} fluere_flow_piece;            /* 144 bytes */
+
+typedef struct fluere_flow_annex {
+    uint32_t key[14];
+    uint32_t flags;             /* 1 a FIN/RST in the shard (f0), 2 lead, 4 head, 8 tail */
+    uint32_t pad;
+    uint64_t f0;                /* global index of the shard's first FIN/RST of the flow */
+    fluere_flow_piece lead, head, tail;
+    uint64_t pad2;
+} fluere_flow_annex;            /* 512 bytes */
+
+/* Block header; the run counters are the exporting shard's (the same in each
+ * of its blocks). */
+typedef struct {
+    uint64_t n_flows;           /* summaries for this owner (> cap: the block was cut short) */
+    uint64_t n_annex;           /* annexes for this owner (> cap_annex: cut short) */
+    uint64_t tmin, tmax, valid, dropped;
+    uint32_t err, shard;
+    uint64_t reserved;
+} fluere_shard_header;          /* 64 bytes */
+
+/* Flow capacity of the context (max_flows clamped to the table size). */
 uint64_t fluere_capacity(fluere_ctx* ctx);
 /* Records attached to the context (every batch). */
 uint64_t fluere_total_packets(fluere_ctx* ctx);
 int fluere_set_index_base(fluere_ctx* ctx, uint64_t first_global_index);
-/* Export this context's flows after fluere_parse_aggregate.  tmin/tmax: time
- * range of the valid packets (for the expiry-mode decision). */
-int fluere_export_summaries(fluere_ctx* ctx, fluere_flow_summary* d_out, uint64_t cap, uint64_t* n,
-                            uint64_t* tmin, uint64_t* tmax);
-/* Merge n device-resident summaries (from every shard) into this context's
- * (cleared) flow table and build the records; then fluere_get_records. */
-int fluere_merge_summaries(fluere_ctx* ctx, const fluere_flow_summary* d_in, uint64_t n, uint64_t tmin,
-                           uint64_t tmax, fluere_stats* stats);
 
-/* Shard exchange without host round trips (the multi-GPU step): a shard
- * block is a 64-byte fluere_shard_header followed by cap summaries.
- * fluere_export_device enqueues (asynchronously, on the context stream) the
- * export of this context's flows after fluere_parse_aggregate into one block:
- * min(n_flows, cap) summaries; the header holds the true n_flows, so a reader
- * sees when cap was too small.  fluere_merge_gathered merges n_shards
- * consecutive blocks (as an all-gather leaves them) like
- * fluere_merge_summaries; FLUERE_E_ARG if a block holds more than cap flows.
- * No reference counterpart (the reference is single-threaded). */
-typedef struct {
-    uint64_t n_flows, tmin, tmax, valid, dropped, raw;
-    uint32_t err, pad;
-    uint64_t reserved;
-} fluere_shard_header;          /* 64 bytes */
-uint64_t fluere_shard_block_bytes(uint64_t cap);
-int fluere_export_device(fluere_ctx* ctx, void* d_block, uint64_t cap);
+/* Bytes of one block: header, cap summaries, cap_annex annexes. */
+uint64_t fluere_shard_block_bytes(uint64_t cap, uint64_t cap_annex);
+/* After fluere_parse_aggregate: export this shard (rank `shard`) into n_owners
+ * consecutive blocks at d_blocks (block o for owner rank o).  Runs the exact
+ * state machine over the shard's order-dependent flows first (their final
+ * records stay in this context).  *need / *need_annex (host, may be NULL): the
+ * largest per-owner counts, so a caller sees when cap / cap_annex were too
+ * small (the block header holds them too).  Synchronises the context stream. */
+int fluere_export_device(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
+                         uint64_t cap_annex, uint64_t* need, uint64_t* need_annex);
+/* Owner side: merge n_shards blocks (block r from rank r, consecutive, as an
+ * all-to-all leaves them) into this context's (cleared) flow table and build
+ * the owner's records; the context keeps the final records its own export
+ * produced, so fluere_get_records returns every record this rank holds.
+ * FLUERE_E_ARG if a block was cut short; FLUERE_E_UNSUPPORTED if the
+ * capture's span reaches the timeout (the sweep is not composed across shards:
+ * run the capture in one context). */
 int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
-                          fluere_stats* stats);
+                          uint64_t cap_annex, fluere_stats* stats);
 
 /* Test seam: insert n canonical keys (14 u32 words each, device memory) into
  * the flow dictionary and write each key's dense flow id. */

@@ -1,8 +1,10 @@
-"""Multi-rank host logic of the sharded path on CPU (gloo, world_size 2).
+"""Multi-rank host logic of the sharded path on CPU (gloo, world_size 2 and 3).
 
-The GPU path shards packets by contiguous range and exchanges one summary per
-flow (fluere_amd/dist.py); the device merge itself is covered on the GPU by
-test_gpu_parity.py::test_sharded_merge_equals_single.
+The GPU path shards packets by contiguous range; every rank exports one block
+per owner rank and one all-to-all delivers them (fluere_amd/dist.py).  The
+device export / merge / composition is covered on the GPU by
+test_gpu_parity.py (logical shards on one device, and a 2-rank gloo run of
+ShardExchange itself).
 """
 import os
 import socket
@@ -14,7 +16,6 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from fluere_amd import dist as fdist
-from fluere_amd._lib import SUMMARY_BYTES, SUMMARY_DTYPE
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 7, 1000, 10_000_001])
@@ -41,48 +42,54 @@ def _free_port():
     return p
 
 
-def _summaries(rank, n):
-    a = np.zeros(n, dtype=SUMMARY_DTYPE)
-    a["key"][:, 0] = rank * 1000 + np.arange(n)
-    a["pkts"][:, 0] = np.arange(n) + 1
-    a["last"] = (rank << 32) + np.arange(n)
-    return torch.from_numpy(a.view(np.uint8).copy())
-
-
-def _worker(rank, world, port, counts, tmins, tmaxs, q):
+def _worker(rank, world, port, blk, q):
+    """One rank of the exchange: block o of every rank's send buffer carries
+    (rank, o) in its bytes; after the all-to-all, rank o's receive buffer
+    must hold the blocks for o from ranks 0..world-1, in rank order.  Also the
+    capacity agreement (largest per-owner counts over all ranks)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        s = _summaries(rank, counts[rank])
-        got = fdist.gather_summaries(s, tmins[rank], tmaxs[rank], dst=0)
-        if rank == 0:
-            allsum, gmin, gmax = got
-            q.put((allsum.numpy().tobytes(), gmin, gmax))
-        else:
-            assert got is None
+        send = torch.zeros(world * blk, dtype=torch.uint8)
+        for o in range(world):
+            send[o * blk:(o + 1) * blk] = torch.arange(blk, dtype=torch.int64).to(torch.uint8) ^ (16 * rank + o)
+        recv = torch.empty_like(send)
+        fdist.exchange_blocks(send, recv)
+        need = fdist.agree_need(100 * rank + 7, 3 - rank)
+        q.put((rank, recv.numpy().tobytes(), need))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("counts,tmins,tmaxs", [
-    ([3, 5], [100, 50], [200, 400]),
-    ([4, 0], [10, fdist.NONE64], [20, 0]),      # an empty shard
-    ([0, 0], [fdist.NONE64, fdist.NONE64], [0, 0]),
-])
-def test_gather_summaries_gloo(counts, tmins, tmaxs):
-    world = 2
+@pytest.mark.parametrize("world,blk", [(2, 64), (2, 4096), (3, 256)])
+def test_exchange_blocks_gloo(world, blk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, counts, tmins, tmaxs, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, blk, q)) for r in range(world)]
     for p in procs:
         p.start()
-    raw, gmin, gmax = q.get(timeout=120)
+    got = dict((r, (raw, need)) for r, raw, need in (q.get(timeout=120) for _ in range(world)))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    want = b"".join(_summaries(r, counts[r]).numpy().tobytes() for r in range(world))
-    assert raw == want and len(raw) == sum(counts) * SUMMARY_BYTES
-    lows = [t for t in tmins if t != fdist.NONE64]
-    assert gmin == (min(lows) if lows else fdist.NONE64)
-    assert gmax == max(tmaxs)
+    base = np.arange(blk, dtype=np.int64).astype(np.uint8)
+    for o in range(world):
+        raw, need = got[o]
+        want = b"".join((base ^ (16 * r + o)).tobytes() for r in range(world))
+        assert raw == want, f"owner {o}: blocks out of place"
+        assert need == (100 * (world - 1) + 7, 3)
+
+
+def test_order_records_merges_ranks():
+    from fluere_amd._lib import RECORD_DTYPE
+    a = np.zeros(3, dtype=RECORD_DTYPE)
+    b = np.zeros(2, dtype=RECORD_DTYPE)
+    a["order_key"] = [40, fdist.NONE64, 7]
+    a["first"] = [1, 5, 2]
+    b["order_key"] = [fdist.NONE64, 12]
+    b["first"] = [3, 4]
+    recs, ne = fdist.order_records([a, b])
+    assert ne == 3
+    assert list(recs["order_key"][:3]) == [7, 12, 40]
+    assert list(recs["first"][3:]) == [3, 5]

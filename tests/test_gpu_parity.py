@@ -134,68 +134,85 @@ def test_rerun_is_idempotent(gpu):
     assert outs[0] == outs[1] == outs[2]
 
 
-def test_sharded_merge_equals_single(gpu):
-    """G logical shards on one device through the summary export/merge path."""
-    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
-    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
-    G = 4
-    per = cfg.n_packets // G
-    sums, tmin, tmax = [], None, None
+def _logical_shards(cfg, G, use_mac=False, max_flows=1 << 16, cap=1024, cap_annex=256, timeout_ms=600000):
+    """G shards of one synthetic capture on one device through the multi-GPU
+    export / owner merge (the all-to-all done by device copies)."""
+    ctxs = []
     for r in range(G):
-        with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
-            b, o, nbytes = fluere_amd.synth_device(cfg, r * per, per)
-            _lib.check(_lib.lib().fluere_set_index_base(ctx._h, r * per), "base")
-            ctx.add_device_batch(b, nbytes, o, per)
-            torch.cuda.synchronize()
-            s, lo, hi = fluere_amd.dist.export_summaries(ctx)
-            sums.append(s)
-            tmin = lo if tmin is None else min(tmin, lo)
-            tmax = hi if tmax is None else max(tmax, hi)
-    allsum = torch.cat(sums)
-    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
-        fluere_amd.dist.merge_summaries(ctx, allsum, tmin, tmax)
-        recs, ne = ctx.records()
-    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "sharded")
+        first, n = fluere_amd.dist.shard_range(cfg.n_packets, r, G)
+        ctx = fluere_amd.FlowContext(timeout_ms=timeout_ms, use_mac=use_mac, max_flows=max_flows)
+        fluere_amd.dist.set_index_base(ctx, first)
+        for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, first, n):
+            ctx.add_device_batch(b, nbytes, o, nb)
+        ctxs.append(ctx)
+    torch.cuda.synchronize()
+    ls = fluere_amd.dist.LogicalShards(ctxs, cap, cap_annex)
+    return ls, ctxs
 
 
-def test_gathered_blocks_merge_equals_single(gpu):
-    """The multi-GPU exchange format: every shard exports one device block
-    (fluere_export_device: header + cap summaries) into consecutive slots of
-    one buffer, as an all_gather leaves them; fluere_merge_gathered merges
-    them.  Also: a block cut short (more flows than cap) is an error."""
+@pytest.mark.parametrize("G", [1, 2, 4])
+def test_sharded_merge_equals_single(gpu, G):
+    """G logical shards on one device through the export / all-to-all / owner
+    merge path: every record equals the oracle's on the whole capture."""
     cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    ls, ctxs = _logical_shards(cfg, G, cap=64, cap_annex=8)  # small blocks: the capacity retry runs
+    ls.run()
+    recs, ne = ls.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"sharded G={G}")
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_sharded_realistic_tcp(gpu, G):
+    """Realistic TCP split into shards: FIN handshakes, SYN-gated peers,
+    reopened keys and elephants cross shard boundaries; the owners compose the
+    shards' pieces of the state machine (annexes) in shard order."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 400_000, 4_000, 0xF10E0017)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    ls, ctxs = _logical_shards(cfg, G, max_flows=1 << 18)
+    st = ls.run()
+    assert sum(x["complex_flows"] for x in st) > 0
+    recs, ne = ls.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"sharded tcp G={G}")
+    for c in ctxs:
+        c.close()
+
+
+def test_sharded_cut_short_block_is_an_error(gpu):
+    """A block with more flows than its capacity: the merge refuses it."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 40_000, 2000, 0xF10E0004)
     L = _lib.lib()
-    G = 4
-    per = cfg.n_packets // G
-    for cap, ok in ((4096, True), (1024, False)):
-        blk = int(L.fluere_shard_block_bytes(cap))
-        buf = torch.zeros(G * blk, dtype=torch.uint8, device="cuda")
-        ctxs = []
-        for r in range(G):
-            ctx = fluere_amd.FlowContext(max_flows=1 << 16)
-            b, o, nbytes = fluere_amd.synth_device(cfg, r * per, per)
-            _lib.check(L.fluere_set_index_base(ctx._h, r * per), "base")
-            ctx.add_device_batch(b, nbytes, o, per)
-            torch.cuda.synchronize()
-            ctx.parse_aggregate()
-            _lib.check(L.fluere_export_device(ctx._h, buf.data_ptr() + r * blk, cap), "export_device")
-            ctxs.append(ctx)
-        torch.cuda.synchronize()
-        hdr = buf.view(G, blk)[:, :8].contiguous().view(torch.int64).cpu().tolist()
-        assert sum(int(h[0]) for h in hdr) >= 4000
-        with fluere_amd.FlowContext(max_flows=1 << 16) as m:
-            st = _lib.Stats()
-            rc = L.fluere_merge_gathered(m._h, buf.data_ptr(), G, cap, ctypes.byref(st))
-            if ok:
-                _lib.check(rc, "merge_gathered")
-                recs, ne = m.records()
-                assert st.valid == cfg.n_packets
-                assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "gathered")
-            else:
-                assert rc == _lib.E_ARG
-        for ctx in ctxs:
-            ctx.close()
+    ls, ctxs = _logical_shards(cfg, 2)
+    for c in ctxs:
+        c.parse_aggregate()
+    cap, capa = 16, 16
+    blk = int(L.fluere_shard_block_bytes(cap, capa))
+    sends = []
+    for r, c in enumerate(ctxs):
+        send = torch.empty(2 * blk, dtype=torch.uint8, device="cuda")
+        need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(L.fluere_export_device(c._h, send.data_ptr(), 2, r, cap, capa, ctypes.byref(need),
+                                          ctypes.byref(need_a)), "export")
+        assert need.value > cap
+        sends.append(send)
+    recv = torch.cat([sends[0][:blk], sends[1][:blk]])
+    st = _lib.Stats()
+    assert L.fluere_merge_gathered(ctxs[0]._h, recv.data_ptr(), 2, cap, capa, ctypes.byref(st)) == _lib.E_ARG
+    for c in ctxs:
+        c.close()
+
+
+def test_sharded_expiry_is_unsupported(gpu):
+    """The hard-timeout sweep is not composed across shards: a capture whose
+    span reaches the timeout is refused by the merge, loudly."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 50_000, 500, 0xF10E0027)
+    ls, ctxs = _logical_shards(cfg, 2, timeout_ms=10)
+    with pytest.raises(FluereError):
+        ls.run()
+    for c in ctxs:
+        c.close()
 
 
 def test_c2_full_size_parity(gpu):
@@ -456,3 +473,69 @@ def test_mode_b_fallback_on_backward_time(gpu):
     csv, ne, st = _gpu_csv(data, 1, use_mac=True)
     assert st["sequential_mode"] == 2
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "edge_keys t=1 -M")
+
+
+def test_c4_recipe_8_shards_1m_flows(gpu):
+    """BASELINE configs[3]'s recipe (IMIX, 1M flows) at 20M packets through 8
+    logical shards: every shard sees nearly all 1M flows; the owners' merged
+    records equal the oracle's on the whole capture."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 20_000_000, 1_000_000, 0xF10E0004)
+    ls, ctxs = _logical_shards(cfg, 8, max_flows=1 << 21, cap=1 << 17, cap_annex=1 << 10)
+    st = ls.run()
+    recs, ne = ls.records()
+    for c in ctxs:
+        c.close()
+    assert len(recs) == 1_000_000
+    assert int(recs["d_pkts"].sum()) == cfg.n_packets
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "c4 recipe, 8 shards")
+
+
+def _shard_exchange_rank(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037)
+        first, n = fluere_amd.dist.shard_range(cfg.n_packets, rank, world)
+        ctx = fluere_amd.FlowContext(max_flows=1 << 18, stream=torch.cuda.current_stream().cuda_stream)
+        fluere_amd.dist.set_index_base(ctx, first)
+        for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, first, n):
+            ctx.add_device_batch(b, nbytes, o, nb)
+        torch.cuda.synchronize()
+        ex = fluere_amd.dist.ShardExchange(ctx, cap=128, cap_annex=16)
+        for _ in range(2):  # the first step grows the blocks, the second reuses them
+            ex.step()
+        got = ex.gather_records()
+        if rank == 0:
+            recs, ne = got
+            q.put((fluere_amd.format_csv(recs), ne))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_exchange_two_ranks_gloo(gpu):
+    """ShardExchange itself with two ranks (gloo moves the blocks; both ranks
+    on this GPU): export, capacity agreement, all-to-all, owner merge, record
+    gather -- against the oracle on the whole capture."""
+    import socket
+    import torch.multiprocessing as mp
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_exchange_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    csv, ne = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "ShardExchange gloo x2")
