@@ -5,8 +5,9 @@ pcap records already resident in HBM: parse (parse_keys + parse_fluereflow),
 exact flow key, update_flow aggregation and the record finalisation (the
 records are materialised in HBM: the reference's "Converted in" window also
 ends before the CSV export, offline_fluereflows.rs:178).  For N > 1 each rank
-aggregates its shard and the step adds the flow-table merge: one RCCL
-all_gather of per-flow summaries over xGMI + device merge/finalize on rank 0.
+aggregates its shard and the step adds the flow-table merge: every rank
+exports its flows into one block per owner rank, one RCCL all_to_all over
+xGMI, and each owner merges / finalizes its own flows (fluere_amd/dist.py).
 Weak scaling: every rank owns a fixed per-GPU shard of one global capture
 (packet-range sharding with global packet indices).
 
@@ -141,11 +142,17 @@ def main():
     else:
         kernel_avg = sum(kernel_ms) / len(kernel_ms)
 
+    # records of the whole job: every rank holds its own flows' records
+    recs, ne = ctx.records()
+    n_recs, n_ended = len(recs), ne
+    if world > 1:
+        t = torch.tensor([n_recs, n_ended], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        n_recs, n_ended = (int(x) for x in t.tolist())
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         mpps = n_total / (elapsed / args.steps) / 1e6
         achieved = BYTES_PER_PKT * n / (kernel_avg * 1e-3) / 1e9  # per-GPU launch (GB/s)
-        recs, ne = ctx.records()
         traffic = None
         prof = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(prof):
@@ -164,7 +171,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (counter-based generator, device-resident)",
             "config": {"workload": C["workload"], "packets_total": n_total, "flows": C["flows"],
-                       "parallelism": (f"dp{world}: packet-range shards, RCCL all_gather flow-table merge"
+                       "parallelism": (f"dp{world}: packet-range shards, owner-partitioned flow-table merge "
+                                       "(one RCCL all_to_all of per-owner blocks)"
                                        if world > 1 else "single GPU"),
                        "use_mac": C["use_mac"], "timeout_ms": C.get("timeout_ms", 600000),
                        **({"note": C["note"]} if "note" in C else {})},
@@ -176,8 +184,8 @@ def main():
                          "algorithmic_bytes_per_launch": BYTES_PER_PKT * n},
             "parse_key_mpps_per_gpu": round(n / (kernel_avg * 1e-3) / 1e6, 1),
             "aggregate_pass_ms": round(sum(pass_ms) / len(pass_ms), 4),
-            "records": int(len(recs)),
-            "records_ended": int(ne),
+            "records": int(n_recs),
+            "records_ended": int(n_ended),
             "complex_flows": int(st.get("complex_flows", 0)) if world == 1 else None,
             "sequential_mode": int(st.get("sequential_mode", 0)) if world == 1 else None,
         }
