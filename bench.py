@@ -108,8 +108,8 @@ def main():
             # parse + key + aggregate + finalize; the records stay in HBM
             st = ctx.run()
         else:
-            # per-shard aggregation, then the flow-table merge: one RCCL
-            # all_gather of the shard blocks + device merge/finalize on rank 0
+            # per-shard aggregation, then the flow-table merge: per-owner
+            # blocks, one RCCL all_to_all, each owner merges its own flows
             st = exchange.step()
         # HIP events around k_parse_agg on the context stream (fluere_stats.parse_ms)
         kernel_ms.append(st["parse_ms"] if world == 1 else ctx.last_kernel_ms())
