@@ -46,6 +46,7 @@
 #include "../../include/fluere_gpu.h"
 #include "device.h"
 #include "exact.h"
+#include "pcapng.h"
 #include "synth.h"
 
 using namespace fl;
@@ -2650,6 +2651,13 @@ static int64_t pcap_walk(const uint8_t* f, uint64_t nbytes, uint64_t* offs, uint
 }
 
 extern "C" int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint64_t* offsets, uint64_t cap) {
+    if (file && is_pcapng(file, nbytes)) {  // pcapng: the record count (offsets exist for classic files only)
+        if (offsets) return FLUERE_E_ARG;
+        std::vector<uint8_t> classic;
+        const int rc = pcapng_to_pcap(file, nbytes, classic);
+        if (rc) return rc;
+        return pcap_walk(classic.data(), classic.size(), nullptr, 0, nullptr, nullptr, nullptr);
+    }
     return pcap_walk(file, nbytes, offsets, cap, nullptr, nullptr, nullptr);
 }
 
@@ -2816,6 +2824,12 @@ struct Ingest {
 extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t nbytes) {
     if (!c || !file) return FLUERE_E_ARG;
     HIPCHECK(hipSetDevice(c->device));
+    if (is_pcapng(file, nbytes)) {  // libpcap reads pcapng too (pcapng.h)
+        std::vector<uint8_t> classic;
+        const int rc = pcapng_to_pcap(file, nbytes, classic);
+        if (rc) return rc;
+        return fluere_add_host_pcap(c, classic.data(), classic.size());
+    }
     Ingest in(c);
     int rc = in.begin(nbytes);
     if (rc) return rc;
@@ -2837,6 +2851,21 @@ extern "C" int fluere_add_pcap_file(fluere_ctx* c, const char* path) {
     struct stat stt;
     if (fstat(fd, &stt) != 0) { close(fd); return FLUERE_E_IO; }
     const uint64_t nbytes = (uint64_t)stt.st_size;
+    {
+        uint8_t head[4] = {0, 0, 0, 0};
+        if (nbytes >= 4 && pread(fd, head, 4, 0) == 4 && is_pcapng(head, 4)) {
+            // pcapng: read whole, rewrite as a classic image (pcapng.h)
+            std::vector<uint8_t> raw(nbytes);
+            uint64_t got = 0;
+            while (got < nbytes) {
+                const ssize_t r = pread(fd, raw.data() + got, nbytes - got, (off_t)got);
+                if (r <= 0) { close(fd); return FLUERE_E_IO; }
+                got += (uint64_t)r;
+            }
+            close(fd);
+            return fluere_add_host_pcap(c, raw.data(), nbytes);
+        }
+    }
     Ingest in(c);
     int rc = in.begin(nbytes);
     for (uint64_t k = 0, cs = 0; !rc && cs < nbytes; k++, cs += kIngestChunk) {

@@ -63,8 +63,7 @@ class FlowContext:
     def add_host_pcap(self, data: bytes):
         buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
         check(self._L.fluere_add_host_pcap(self._h, buf, len(data)), "fluere_add_host_pcap")
-        n = self._L.fluere_pcap_index(buf, len(data), None, 0)
-        self.n_packets += max(int(n), 0)
+        self.n_packets = int(self._L.fluere_total_packets(self._h))
 
     def add_pcap_file(self, path: str):
         """Stream a capture file to the device (pinned chunks, host-side index)."""

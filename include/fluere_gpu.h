@@ -125,7 +125,9 @@ int fluere_reset(fluere_ctx* ctx);
 /* ---- ingress ------------------------------------------------------------- */
 /* Index a classic pcap held in host memory: record offsets (relative to the
  * buffer) follow libpcap offline semantics (stop at the first bad record).
- * offsets may be NULL to count.  Returns number of records or <0. */
+ * offsets may be NULL to count.  Returns number of records or <0.  A pcapng
+ * capture is counted (offsets must be NULL: its records are not contiguous
+ * classic records). */
 int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint64_t* offsets, uint64_t cap);
 
 /* Attach a device-resident batch: `d_bytes` holds pcap records (the 24-byte
@@ -142,7 +144,9 @@ int fluere_add_device_batch(fluere_ctx* ctx, const uint8_t* d_bytes, uint64_t nb
 
 /* Copy a host pcap file image to the device (owned by ctx) and attach it.
  * The bytes stream through pinned staging chunks (copies overlap the next
- * chunk) while the record index is built on the host in one pass. */
+ * chunk) while the record index is built on the host in one pass.  A pcapng
+ * image (libpcap reads both) is first rewritten as classic records with
+ * microsecond timestamps. */
 int fluere_add_host_pcap(fluere_ctx* ctx, const uint8_t* file, uint64_t nbytes);
 /* The same, reading the capture file straight into the staging chunks
  * (Capture::from_file, offline_fluereflows.rs:44). */

@@ -527,8 +527,120 @@ static uint32_t rd32(const uint8_t* p, int swap) {
     return v;
 }
 
+/* pcapng (libpcap pcap-ng.c, read by pcap_open_offline at microsecond
+ * precision; third-party code, restated -- SURVEY Appendix C style):
+ * blocks in file order; a Section Header Block sets the byte order and
+ * forgets the interfaces; Interface Description Blocks give if_tsresol
+ * (option 9: 10^-b, or 2^-(b & 0x7f) when the high bit is set; default 10^-6),
+ * if_tsoffset (option 14, seconds) and the snaplen (0 or above 262144 ->
+ * 262144); Enhanced / obsolete Packet Blocks carry (interface, 64-bit time in
+ * the interface's units, caplen, len, data); Simple Packet Blocks carry no
+ * time (0) and caplen = min(len, block room, snaplen of interface 0); other
+ * blocks are skipped.  A truncated or malformed block, an unknown interface
+ * or caplen > 262144 ends the capture (pcap_next_ex error).  Time: sec =
+ * t / res + tsoffset, usec = (t % res) * 10^6 / res. */
+typedef struct { uint64_t res; int64_t off; uint32_t snap; } ng_if;
+
+static uint32_t rdx32(const uint8_t* p, int sw) { uint32_t v; memcpy(&v, p, 4); return sw ? __builtin_bswap32(v) : v; }
+static uint16_t rdx16(const uint8_t* p, int sw) { uint16_t v; memcpy(&v, p, 2); return sw ? __builtin_bswap16(v) : v; }
+
+static int64_t or_pcapng_index(const uint8_t* f, uint64_t n, or_pcap_rec** out) {
+    uint64_t cap = 1024, cnt = 0, pos = 0;
+    or_pcap_rec* r = (or_pcap_rec*)malloc(cap * sizeof *r);
+    ng_if ifs[256];
+    int nif = 0, sw = 0, have_shb = 0;
+    const uint32_t max_snap = 262144;
+    while (pos + 12 <= n) {
+        uint32_t type = rdx32(f + pos, sw);
+        if (type == 0x0A0D0D0Au) {
+            uint32_t bom;
+            memcpy(&bom, f + pos + 8, 4);
+            if (bom == 0x1A2B3C4Du) sw = 0;
+            else if (bom == 0x4D3C2B1Au) sw = 1;
+            else break;
+            if (pos + 16 > n || rdx16(f + pos + 12, sw) != 1) break; /* major version 1 */
+            have_shb = 1;
+            nif = 0;
+        } else if (!have_shb) {
+            break;
+        }
+        uint32_t total = rdx32(f + pos + 4, sw);
+        if (total < 12 || (total & 3) || pos + total > n) break;
+        const uint8_t* b = f + pos + 8;
+        uint32_t blen = total - 12;
+        int stop = 0;
+        if (type == 1) { /* IDB */
+            if (blen < 8 || nif == 256) { stop = 1; }
+            else {
+                ng_if x;
+                x.res = 1000000; x.off = 0;
+                x.snap = rdx32(b + 4, sw);
+                if (x.snap == 0 || x.snap > max_snap) x.snap = max_snap;
+                uint32_t o = 8;
+                while (o + 4 <= blen) {
+                    uint16_t code = rdx16(b + o, sw), len = rdx16(b + o + 2, sw);
+                    if (code == 0) break;
+                    if (o + 4 + len > blen) { stop = 1; break; }
+                    if (code == 9 && len >= 1) {
+                        uint8_t v = b[o + 4];
+                        unsigned __int128 res = 1;
+                        int e = v & 0x7f, bin = (v & 0x80) != 0;
+                        for (int k = 0; k < e && res <= (unsigned __int128)UINT64_MAX; k++) res *= bin ? 2 : 10;
+                        if (res > (unsigned __int128)UINT64_MAX) { stop = 1; break; }
+                        x.res = (uint64_t)res;
+                    } else if (code == 14 && len >= 8) {
+                        uint64_t v = (uint64_t)rdx32(b + o + 4, sw) | ((uint64_t)rdx32(b + o + 8, sw) << 32);
+                        if (sw) v = ((uint64_t)rdx32(b + o + 4, sw) << 32) | rdx32(b + o + 8, sw);
+                        x.off = (int64_t)v;
+                    }
+                    o += 4 + ((len + 3u) & ~3u);
+                }
+                if (!stop) ifs[nif++] = x;
+            }
+        } else if (type == 6 || type == 2 || type == 3) { /* EPB, OPB, SPB */
+            uint32_t ifid = 0, caplen, dataoff;
+            uint64_t t = 0;
+            if (type == 3) {
+                if (blen < 4 || nif == 0) { stop = 1; }
+                else {
+                    uint32_t len = rdx32(b, sw);
+                    caplen = len < blen - 4 ? len : blen - 4;
+                    if (caplen > ifs[0].snap) caplen = ifs[0].snap;
+                    dataoff = 4;
+                }
+            } else {
+                if (blen < 20) { stop = 1; }
+                else {
+                    ifid = type == 6 ? rdx32(b, sw) : rdx16(b, sw);
+                    t = ((uint64_t)rdx32(b + 4, sw) << 32) | rdx32(b + 8, sw);
+                    caplen = rdx32(b + 12, sw);
+                    dataoff = 20;
+                    if (ifid >= (uint32_t)nif || caplen > blen - 20) stop = 1;
+                }
+            }
+            if (!stop && caplen > max_snap) stop = 1;
+            if (!stop) {
+                const ng_if* x = &ifs[ifid];
+                if (cnt == cap) { cap *= 2; r = (or_pcap_rec*)realloc(r, cap * sizeof *r); }
+                r[cnt].data_off = pos + 8 + dataoff;
+                r[cnt].caplen = caplen;
+                uint64_t sec = type == 3 ? 0 : t / x->res;
+                uint64_t frac = type == 3 ? 0 : t % x->res;
+                r[cnt].ts_sec = (uint32_t)(sec + (uint64_t)x->off);
+                r[cnt].ts_usec = (uint32_t)(((unsigned __int128)frac * 1000000u) / x->res);
+                cnt++;
+            }
+        }
+        if (stop) break;
+        pos += total;
+    }
+    *out = r;
+    return (int64_t)cnt;
+}
+
 int64_t or_pcap_index(const uint8_t* f, uint64_t n, or_pcap_rec** out) {
     *out = NULL;
+    if (n >= 4 && rd32(f, 0) == 0x0A0D0D0Au) return or_pcapng_index(f, n, out);
     if (n < 24) return -1;
     uint32_t magic = rd32(f, 0);
     int swap = 0, nsec = 0;

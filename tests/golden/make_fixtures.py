@@ -13,6 +13,13 @@
   ethertype whose low byte is the test's protocol hint (keys.rs:279-296),
   parse_fluereflow's from_ethertype arm (fluereflows.rs:148-195) and
   parse_ports for an unknown IP protocol (ports.rs:47).
+* ``edge_pcapng[_swapped].pcap``: the same kind of traffic as pcapng (two
+  sections, interfaces at 10^-6 / 10^-9 / 2^-20 s with an if_tsoffset and
+  10^-3 s, Enhanced / Simple / obsolete Packet Blocks, blocks a reader skips,
+  a truncated last block), both byte orders.  libpcap reads pcapng for
+  pcap_open_offline (offline_fluereflows.rs:44); ``pcapng_expected()``
+  restates its conversion so tests/test_oracle.py can check the oracle's
+  reader against it.
 * ``edge_*.pcap``: hand-built captures for every edge the hot path has
   (SURVEY.md Appendix B.3).  Their golden CSVs are produced by the C oracle
   (oracle/fluere_oracle.c) and committed, so the GPU box needs neither the
@@ -228,6 +235,45 @@ def raw_vector_frames():
     return out
 
 
+def pcapng_items():
+    """(pcapng block items, the classic records libpcap yields for them:
+    (sec, usec, data, orig_len))."""
+    A, B, C = "10.0.0.1", "10.0.0.2", "10.0.0.3"
+    f1 = eth() + ipv4(A, B, 17, udp(1000, 2000, b"\x21" * 30))
+    f2 = eth() + ipv4(B, A, 17, udp(2000, 1000, b"\x22" * 12))
+    f3 = eth() + ipv4(A, C, 6, tcp(3000, 80, SYN))
+    f4 = eth() + ipv4(C, A, 6, tcp(80, 3000, SYN | ACK))
+    f5 = eth() + ipv4(A, C, 6, tcp(3000, 80, FIN | ACK))
+    f6 = eth() + ipv4(C, A, 6, tcp(80, 3000, ACK))
+    f7 = eth() + ipv4(A, B, 17, udp(1000, 2000, b"\x23" * 400))
+    T = 1_700_000_000
+    items = [("shb",),
+             ("idb", 0, None, None),                 # interface 0: microseconds, snaplen 0 -> 262144
+             ("idb", 65535, 9, None),                # interface 1: nanoseconds
+             ("idb", 0, 0x80 | 20, 3600),            # interface 2: 2^-20 s, +1 h offset
+             ("epb", 0, T * 10**6 + 5, f1),
+             ("nrb",),
+             ("epb", 1, T * 10**9 + 7_123_456, f2),
+             ("isb", 0),
+             ("epb", 2, (T - 3600) * 2**20 + 2**19 + 3, f3),
+             ("custom",),
+             ("spb", f4),                            # no time: 0.0
+             ("opb", 0, T * 10**6 + 999_999, f5),
+             ("epb", 1, T * 10**9 + 1_000_000_999, f7),
+             ("shb",),                               # a new section forgets the interfaces
+             ("idb", 0, 3, None),                    # milliseconds
+             ("epb", 0, T * 1000 + 1500, f6),
+             ("epb", 0, T * 1000 + 1501, f1)]
+    exp = [(T, 5, f1, len(f1)), (T, 7123, f2, len(f2)), (T, 500002, f3, len(f3)), (0, 0, f4, len(f4)),
+           (T, 999999, f5, len(f5)), (T + 1, 0, f7, len(f7)), (T + 1, 500000, f6, len(f6)),
+           (T + 1, 501000, f1, len(f1))]
+    return items, exp
+
+
+def pcapng_expected():
+    return pcap(pcapng_items()[1])
+
+
 # (timeout_ms, use_mac) combinations checked per fixture
 PARAMS = {
     "default": [(600000, False), (600000, True)],
@@ -258,6 +304,11 @@ def main():
     caps["edge_udp_bidir_swapped"] = pcap(fixtures()["edge_udp_bidir"], swapped=True)
     caps["edge_tcp_snap60"] = pcap(fixtures()["edge_tcp"], snaplen=60)
     caps["ref_ipv4_frame"] = ref
+    from pktbuild import pcapng
+    items = pcapng_items()[0]
+    ng = pcapng(items)
+    caps["edge_pcapng"] = ng + ng[12: 12 + 40][:20]  # a truncated block at the end
+    caps["edge_pcapng_swapped"] = pcapng(items, swapped=True)
     for name, data in sorted(caps.items()):
         open(os.path.join(HERE, name + ".pcap"), "wb").write(data)
         runs = []

@@ -67,3 +67,58 @@ def pcap(packets, nsec=False, swapped=False, snaplen=65535) -> bytes:
         orig = p[3] if len(p) > 3 else len(data)
         out.append(struct.pack(e + "IIII", sec, frac, len(data), orig) + data)
     return b"".join(out)
+
+
+def pcapng(items, swapped=False) -> bytes:
+    """A pcapng capture from block items, in order:
+      ("shb",)                                  Section Header Block
+      ("idb", snaplen, tsresol_byte, tsoffset)  Interface Description Block (None: option absent)
+      ("epb", ifid, t, frame[, orig_len])       Enhanced Packet Block (t in the interface's units)
+      ("opb", ifid, t, frame)                   obsolete Packet Block (type 2)
+      ("spb", frame[, orig_len])                Simple Packet Block
+      ("isb", ifid) / ("nrb",) / ("custom",)    blocks a reader skips
+    """
+    e = ">" if swapped else "<"
+
+    def block(btype, body: bytes) -> bytes:
+        body = body + b"\0" * (-len(body) % 4)
+        total = 12 + len(body)
+        return struct.pack(e + "II", btype, total) + body + struct.pack(e + "I", total)
+
+    def opt(code, value: bytes) -> bytes:
+        return struct.pack(e + "HH", code, len(value)) + value + b"\0" * (-len(value) % 4)
+
+    out = []
+    for it in items:
+        k = it[0]
+        if k == "shb":
+            out.append(block(0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1)))
+        elif k == "idb":
+            _, snap, tsres, tsoff = it
+            opts = b""
+            if tsres is not None:
+                opts += opt(9, bytes([tsres]))
+            if tsoff is not None:
+                opts += opt(14, struct.pack(e + "q", tsoff))
+            if opts:
+                opts += struct.pack(e + "HH", 0, 0)
+            out.append(block(1, struct.pack(e + "HHI", 1, 0, snap) + opts))
+        elif k == "epb":
+            ifid, t, frame = it[1], it[2], it[3]
+            orig = it[4] if len(it) > 4 else len(frame)
+            out.append(block(6, struct.pack(e + "IIIII", ifid, t >> 32, t & 0xFFFFFFFF, len(frame), orig) + frame))
+        elif k == "opb":
+            ifid, t, frame = it[1], it[2], it[3]
+            out.append(block(2, struct.pack(e + "HHIIII", ifid, 0, t >> 32, t & 0xFFFFFFFF, len(frame), len(frame))
+                             + frame))
+        elif k == "spb":
+            frame = it[1]
+            orig = it[2] if len(it) > 2 else len(frame)
+            out.append(block(3, struct.pack(e + "I", orig) + frame))
+        elif k == "isb":
+            out.append(block(5, struct.pack(e + "III", it[1], 0, 0)))
+        elif k == "nrb":
+            out.append(block(4, struct.pack(e + "HH", 0, 0)))
+        elif k == "custom":
+            out.append(block(0x00000BAD, struct.pack(e + "I", 32473) + b"custom"))
+    return b"".join(out)

@@ -539,3 +539,37 @@ def test_shard_exchange_two_ranks_gloo(gpu):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "ShardExchange gloo x2")
+
+
+def test_pcapng_file_ingest(gpu, tmp_path):
+    """A pcapng capture file (nanosecond interface, two sections) through
+    fluere_add_pcap_file / fluere_offline_file against the oracle on the same
+    bytes (libpcap reads pcapng for Capture::from_file, offline_fluereflows.rs:44)."""
+    import struct
+    import pktbuild as pb
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 60_000, 600, 0xF13E)
+    classic = fluere_amd.synth_pcap(cfg)
+    items, off, k = [("shb",), ("idb", 0, 9, None)], 24, 0
+    while off + 16 <= len(classic):
+        sec, usec, incl, orig = struct.unpack_from("<IIII", classic, off)
+        if k == 30_000:
+            items += [("shb",), ("idb", 0, None, None)]  # second section: microseconds
+        t = sec * 10**6 + usec if k >= 30_000 else (sec * 10**9 + usec * 1000 + 17)
+        items.append(("epb", 0, t, classic[off + 16: off + 16 + incl], orig))
+        off += 16 + incl
+        k += 1
+    data = pb.pcapng(items)
+    path = tmp_path / "cap.pcapng"
+    path.write_bytes(data)
+    want = pyoracle.offline(data)
+    assert want["packets"] == cfg.n_packets
+    assert pyoracle.offline(classic)["csv"] == want["csv"]
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_pcap_file(str(path))
+        assert ctx.n_packets == cfg.n_packets
+        ctx.run()
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "pcapng file")
+    st = fluere_amd.fluereflow_fileparse(fluere_amd.Args(fluere_amd.Files(file=str(path))), out_dir=str(tmp_path / "o"))
+    got = (tmp_path / "o" / "cap_converted.csv").read_text()
+    assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "pcapng fluere_offline_file")

@@ -63,3 +63,15 @@ def test_reference_analyze_packet_structure(data, size, has):
     assert pyoracle.analyze_structure(data) == (size, has)
     h = pyoracle.raw_call(RV.PARSE_ETHERTYPE, data, 0x3601)
     assert h["some"] and h["payload"] == (data[size:] if has and len(data) > size else None)
+
+
+@pytest.mark.parametrize("name", ["edge_pcapng", "edge_pcapng_swapped"])
+def test_pcapng_reads_like_libpcap(name):
+    """The oracle's pcapng reader against make_fixtures.pcapng_expected(): the
+    classic records libpcap's conversion (microseconds, per-interface
+    resolution and offset, SPB without time) yields for the same blocks."""
+    import make_fixtures as mf
+    a = pyoracle.offline(golden_pcap(name))
+    b = pyoracle.offline(mf.pcapng_expected())
+    assert a["packets"] == b["packets"] == 8
+    assert a["csv"] == b["csv"] and a["n_ended"] == b["n_ended"]
