@@ -106,7 +106,7 @@ PIECE_DTYPE = np.dtype([
     ("dir", "u1"), ("src_port", "<u2"), ("dst_port", "<u2"),
 ])
 ANNEX_DTYPE = np.dtype([("key", "<u4", 14), ("flags", "<u4"), ("pad", "<u4"), ("f0", "<u8"), ("lead", PIECE_DTYPE),
-                        ("head", PIECE_DTYPE), ("tail", PIECE_DTYPE), ("pad2", "<u8")])
+                        ("head", PIECE_DTYPE), ("tail", PIECE_DTYPE), ("mid_last", "<u8")])
 SHARD_HEADER_DTYPE = np.dtype([("n_flows", "<u8"), ("n_annex", "<u8"), ("tmin", "<u8"), ("tmax", "<u8"),
                                ("valid", "<u8"), ("dropped", "<u8"), ("err", "<u4"), ("shard", "<u4"),
                                ("reserved", "<u8")])
@@ -159,6 +159,11 @@ def lib() -> ctypes.CDLL:
         "fluere_last_pass_ms": (ctypes.c_double, [P]),
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),
         "fluere_debug_raw": (I, [I, P, P, P, P, U64, P, P]),
+        "fluere_live_open": (I, [ctypes.POINTER(Opts), ctypes.POINTER(P)]),
+        "fluere_live_close": (I, [P]),
+        "fluere_live_batch": (I, [P, P, U64, I, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                  ctypes.POINTER(I)]),
+        "fluere_live_finish": (I, [P, I, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "fluere_shard_block_bytes": (U64, [U64, U64]),
         "fluere_export_device": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.POINTER(U64),
                                      ctypes.POINTER(U64)]),

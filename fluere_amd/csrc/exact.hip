@@ -248,6 +248,7 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         const uint32_t* kw = reinterpret_cast<const uint32_t*>(a.flow_key + (size_t)d * 56);
         for (int k = 0; k < 14; k++) ax.key[k] = kw[k];
         ax.flags = (f0 != M40 ? 1u : 0u) | (lead_end > p0 ? 2u : 0u);
+        ax.mid_last = 0;
         ax.f0 = f0 != M40 ? a.sm[f0].gidx : NONE64;
         a.annex_of[d] = q;
         if (lead_end > p0) {
@@ -414,6 +415,9 @@ __global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
         if (role == R_TAIL) ax.tail = pc;
     }
     const bool rec_live = lane_live && !(a.shard_mode && a.irole[a.ist[a.ukeys[r]]] != R_RECORD);
+    if (rec_live && a.shard_mode)  // the flow's last processed packet among its in-shard records (live mode)
+        atomicMax(reinterpret_cast<unsigned long long*>(&a.annex[a.ikey[a.ist[a.ukeys[r]]]].mid_last),
+                  (unsigned long long)a.aggs[r].lastg + 1);
     if (rec_live) {
         q = a.ukeys[r];
         const uint32_t c = a.ist[q];

@@ -3819,3 +3819,320 @@ extern "C" int fluere_debug_raw(int fn, const uint8_t* d_bytes, const uint32_t* 
     HIPCHECK(hipStreamSynchronize(s));
     return FLUERE_OK;
 }
+
+// ===========================================================================
+// live mode (src/net/live_fluereflow.rs:196-376) on batched capture
+// ===========================================================================
+// A session keeps the flows that are open across batches: a flow dictionary
+// of its own (a second context's tables) and, per flow, the open instance as a
+// piece (seed + order-free aggregate).  Each batch runs the shard machinery of
+// the multi-GPU path with one owner (parse, order-free aggregate, the exact
+// state machine for order-dependent flows, summaries + annexes) and is
+// composed into the session state like the next shard of a capture.  The
+// checks the reference runs after a processed packet run once per batch,
+// after its last processed packet: the interval export with the idle-timeout
+// scan flow.last < time - timeout (:306-358); at the end, the duration scan
+// (:361-373) and the flush of every active flow (:379-392).
+namespace {
+
+struct LiveArgs {
+    const uint8_t* blk;
+    unsigned long long cap, cap_annex, block_bytes;
+    TableSet Tp;
+    uint32_t* pslots;
+    fluere_flow_piece* P;
+    uint8_t* P_open;
+    fluere_record* out;
+    unsigned long long* ctr;  // [0] records out, [1] 1 + index of the batch's last processed packet
+    unsigned long long out_cap;
+};
+
+__device__ __forceinline__ void live_emit(const LiveArgs& a, const fluere_flow_piece& f, unsigned long long order) {
+    fluere_record r;
+    record_of_piece(f, order, r);
+    const unsigned long long pos = atomicAdd(&a.ctr[0], 1ull);
+    if (pos < a.out_cap) a.out[pos] = r;
+}
+
+// one thread per flow of the batch: compose its piece of the state machine
+// with the session's open instance (the owner composition of k_compose with
+// the session state as the previous shards)
+__global__ void __launch_bounds__(256) k_live_compose(LiveArgs a) {
+    uint8_t* blocks = const_cast<uint8_t*>(a.blk);
+    const fluere_shard_header* h = blk_hdr(blocks, a.block_bytes, 0);
+    const unsigned long long nf = min((unsigned long long)h->n_flows, a.cap);
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nf) return;
+    const fluere_flow_summary& s = blk_sum(blocks, a.block_bytes, 0)[i];
+    CKey k;
+    for (int j = 0; j < 14; j++) k.w[j] = s.key[j];
+    const uint32_t p = dense_of_key(a.Tp, k, true, a.pslots, nullptr);
+    if (p == FAIL || p >= a.Tp.fmax) return;  // (the error word is set)
+    fluere_flow_piece F = a.P[p];
+    bool open = a.P_open[p] != 0;
+    const bool open_in = open;
+    fluere_flow_piece A, H, T;
+    bool has_f0, has_H, has_T;
+    unsigned long long f0, lastp = 0;
+    if (s.annex == NONE32) {
+        piece_of_summary(s, A);
+        has_f0 = s.finrst_min != NONE64;
+        f0 = s.finrst_min;
+        has_H = s.first_create != NONE64;
+        H = A;
+        has_T = false;
+        if (open_in || has_H) lastp = s.last + 1;  // every packet processed, or none (SYN-gated)
+    } else {
+        const fluere_flow_annex& x = blk_annex(blocks, a.block_bytes, a.cap, 0)[s.annex];
+        has_f0 = x.flags & 1;
+        f0 = x.f0;
+        has_H = x.flags & 4;
+        has_T = x.flags & 8;
+        piece_clear(A);
+        if (x.flags & 2) piece_add(A, x.lead);
+        if (has_H) piece_add(A, x.head);
+        H = x.head;
+        T = x.tail;
+        if (open_in) lastp = A.last + 1;
+        else if (has_H) lastp = H.last + 1;
+        lastp = max(lastp, (unsigned long long)x.mid_last);
+        if (has_T) lastp = max(lastp, T.last + 1);
+    }
+    if (open) {
+        piece_add(F, A);
+        if (has_f0) {
+            live_emit(a, F, f0);
+            open = false;
+        }
+    } else if (has_f0) {
+        if (has_H) live_emit(a, H, f0);
+    } else if (has_H) {
+        F = H;
+        open = true;
+    }
+    if (has_f0 && has_T) {
+        F = T;
+        open = true;
+    }
+    a.P[p] = F;
+    a.P_open[p] = open ? 1 : 0;
+    if (lastp) atomicMax(&a.ctr[1], lastp);
+}
+
+// idle-timeout / duration scan (lim: flow.last < lim expires) or the final flush (all)
+__global__ void __launch_bounds__(256) k_live_scan(LiveArgs a, unsigned long long lim, int all) {
+    const uint32_t np = min(*a.Tp.n_flows, a.Tp.fmax);
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
+        if (!a.P_open[p]) continue;
+        const fluere_flow_piece F = a.P[p];
+        if (!all && !(F.last_time < lim)) continue;
+        live_emit(a, F, NONE64);
+        a.P_open[p] = 0;
+    }
+}
+
+__global__ void k_live_time(const Batch* bs, int nb, unsigned long long gi, int macs, unsigned long long* t) {
+    if (threadIdx.x || blockIdx.x) return;
+    Parsed P;
+    parse_global(bs, nb, gi, macs != 0, P);
+    *t = P.t;
+}
+
+}  // namespace
+
+struct fluere_live {
+    fluere_ctx* batch = nullptr;    // the current batch: packets, flows, export
+    fluere_ctx* persist = nullptr;  // the session's flow dictionary (its tables only)
+    fluere_flow_piece* P = nullptr;
+    uint8_t* P_open = nullptr;
+    uint8_t* blk = nullptr;
+    uint64_t cap = 1024, cap_annex = 256, blk_bytes = 0;
+    fluere_record* out = nullptr;
+    uint64_t out_cap = 0;
+    unsigned long long* ctr = nullptr;
+    uint64_t base = 0;              // global index of the batch's first packet
+    uint64_t timeout_ms = 600000;
+    int use_mac = 0;
+    bool last_have = false;         // the last batch had a processed packet ...
+    uint64_t last_time = 0;         // ... at this time (the checks' `time`)
+    std::vector<fluere_record> pending;  // FIN/RST-closed records since the last export
+};
+
+extern "C" int fluere_live_open(const fluere_opts* o, fluere_live** out) {
+    if (!out) return FLUERE_E_ARG;
+    *out = nullptr;
+    fluere_opts def{};
+    def.timeout_ms = 600000;
+    if (!o) o = &def;
+    fluere_live* lv = new (std::nothrow) fluere_live();
+    if (!lv) return FLUERE_E_NOMEM;
+    int rc = fluere_open(o, &lv->batch);
+    if (!rc) rc = fluere_open(o, &lv->persist);
+    const uint64_t pmax = lv->persist ? lv->persist->fmax : 0;
+    if (!rc && (hipMalloc(&lv->P, pmax * sizeof(fluere_flow_piece)) != hipSuccess ||
+                hipMalloc(&lv->P_open, pmax) != hipSuccess || hipMalloc(&lv->ctr, 16) != hipSuccess))
+        rc = FLUERE_E_NOMEM;
+    if (!rc && hipMemset(lv->P_open, 0, pmax) != hipSuccess) rc = FLUERE_E_HIP;
+    if (rc) {
+        fluere_live_close(lv);
+        return rc;
+    }
+    lv->timeout_ms = o->timeout_ms;
+    lv->use_mac = o->use_mac ? 1 : 0;
+    *out = lv;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_live_close(fluere_live* lv) {
+    if (!lv) return FLUERE_OK;
+    fluere_close(lv->batch);
+    fluere_close(lv->persist);
+    hipFree(lv->P);
+    hipFree(lv->P_open);
+    hipFree(lv->blk);
+    hipFree(lv->out);
+    hipFree(lv->ctr);
+    delete lv;
+    return FLUERE_OK;
+}
+
+static LiveArgs live_args(fluere_live* lv) {
+    LiveArgs a{lv->blk, lv->cap, lv->cap_annex, lv->blk_bytes, tables_of(lv->persist), lv->persist->acc.slots,
+               lv->P, lv->P_open, lv->out, lv->ctr, lv->out_cap};
+    return a;
+}
+
+// records [0, ctr[0]) of lv->out -> host (appended to v)
+static int live_take(fluere_live* lv, std::vector<fluere_record>& v) {
+    hipStream_t s = lv->batch->stream;
+    unsigned long long n = 0;
+    HIPCHECK(hipMemcpyAsync(&n, lv->ctr, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (n > lv->out_cap) return FLUERE_E_NOMEM;
+    const size_t at = v.size();
+    v.resize(at + n);
+    if (n) HIPCHECK(hipMemcpyAsync(v.data() + at, lv->out, n * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemsetAsync(lv->ctr, 0, 8, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+static int live_ensure_out(fluere_live* lv, uint64_t need) {
+    if (need <= lv->out_cap) return FLUERE_OK;
+    hipFree(lv->out);
+    lv->out = nullptr;
+    lv->out_cap = 0;
+    if (hipMalloc(&lv->out, need * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
+    lv->out_cap = need;
+    return FLUERE_OK;
+}
+
+// an export's records: the FIN/RST-closed ones since the last export in their
+// order (the packet that closed them), then the scan's
+static int live_export(fluere_live* lv, std::vector<fluere_record>& scan, fluere_record** recs, uint64_t* n,
+                       uint64_t* n_ordered) {
+    std::stable_sort(lv->pending.begin(), lv->pending.end(),
+                     [](const fluere_record& x, const fluere_record& y) { return x.order_key < y.order_key; });
+    const uint64_t total = lv->pending.size() + scan.size();
+    *recs = (fluere_record*)malloc(std::max<uint64_t>(total, 1) * sizeof(fluere_record));
+    if (!*recs) return FLUERE_E_NOMEM;
+    if (!lv->pending.empty()) memcpy(*recs, lv->pending.data(), lv->pending.size() * sizeof(fluere_record));
+    if (!scan.empty()) memcpy(*recs + lv->pending.size(), scan.data(), scan.size() * sizeof(fluere_record));
+    *n = total;
+    if (n_ordered) *n_ordered = lv->pending.size();
+    lv->pending.clear();
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, int do_export,
+                                 fluere_record** recs, uint64_t* n, uint64_t* n_ordered, int* exported) {
+    if (!lv || !pcap || !recs || !n) return FLUERE_E_ARG;
+    *recs = nullptr;
+    *n = 0;
+    if (n_ordered) *n_ordered = 0;
+    if (exported) *exported = 0;
+    fluere_ctx* c = lv->batch;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = fluere_reset(c))) return rc;
+    if ((rc = fluere_set_index_base(c, lv->base))) return rc;
+    if ((rc = fluere_add_host_pcap(c, pcap, nbytes))) return rc;
+    lv->base += c->n_total;
+    lv->last_have = false;
+    if (c->n_total) {
+        if ((rc = fluere_parse_aggregate(c))) return rc;
+        for (;;) {  // one owner: the whole batch
+            const uint64_t bb = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
+            if (bb > lv->blk_bytes) {
+                hipFree(lv->blk);
+                lv->blk = nullptr;
+                lv->blk_bytes = 0;
+                if (hipMalloc(&lv->blk, bb) != hipSuccess) return FLUERE_E_NOMEM;
+                lv->blk_bytes = bb;
+            }
+            uint64_t need = 0, need_a = 0;
+            if ((rc = fluere_export_device(c, lv->blk, 1, 0, lv->cap, lv->cap_annex, &need, &need_a))) return rc;
+            if (need <= lv->cap && need_a <= lv->cap_annex) break;
+            while (lv->cap < need) lv->cap *= 2;
+            while (lv->cap_annex < need_a) lv->cap_annex *= 2;
+        }
+        // the records that opened and closed inside this batch
+        const size_t at = lv->pending.size();
+        lv->pending.resize(at + c->local_n_rec);
+        if (c->local_n_rec)
+            HIPCHECK(hipMemcpyAsync(lv->pending.data() + at, c->d_recs, c->local_n_rec * sizeof(fluere_record),
+                                    hipMemcpyDeviceToHost, s));
+        c->local_n_rec = c->local_updates = c->local_ended = 0;
+        if ((rc = live_ensure_out(lv, lv->cap + lv->persist->fmax))) return rc;
+        HIPCHECK(hipMemsetAsync(lv->ctr, 0, 16, s));
+        LiveArgs a = live_args(lv);
+        a.block_bytes = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
+        k_live_compose<<<grid_for(lv->cap, 256), 256, 0, s>>>(a);
+        HIPCHECK(hipGetLastError());
+        unsigned long long tend = 0;
+        HIPCHECK(hipMemcpyAsync(&tend, lv->ctr + 1, 8, hipMemcpyDeviceToHost, s));
+        uint32_t perr = 0;
+        HIPCHECK(hipMemcpyAsync(&perr, lv->persist->d_nflows + 1, 4, hipMemcpyDeviceToHost, s));
+        if ((rc = live_take(lv, lv->pending))) return rc;
+        if (perr) return FLUERE_E_TABLE_FULL;  // more distinct flows in the session than max_flows
+        if (tend) {
+            k_live_time<<<1, 64, 0, s>>>(c->d_batches, (int)c->batches.size(), tend - 1, c->use_mac, lv->ctr + 1);
+            HIPCHECK(hipMemcpyAsync(&lv->last_time, lv->ctr + 1, 8, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            lv->last_have = true;
+        }
+    }
+    if (!do_export || !lv->last_have) return FLUERE_OK;  // the interval check runs after a processed packet
+    std::vector<fluere_record> scan;
+    if (lv->timeout_ms > 0) {
+        LiveArgs a = live_args(lv);
+        a.block_bytes = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
+        k_live_scan<<<flow_grid(lv->persist), 256, 0, s>>>(a, lv->last_time - lv->timeout_ms * 1000ull, 0);
+        HIPCHECK(hipGetLastError());
+        if ((rc = live_take(lv, scan))) return rc;
+    }
+    if (exported) *exported = 1;
+    return live_export(lv, scan, recs, n, n_ordered);
+}
+
+extern "C" int fluere_live_finish(fluere_live* lv, int duration_end, fluere_record** recs, uint64_t* n,
+                                  uint64_t* n_ordered) {
+    if (!lv || !recs || !n) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(lv->batch->device));
+    hipStream_t s = lv->batch->stream;
+    int rc;
+    if ((rc = live_ensure_out(lv, lv->cap + lv->persist->fmax))) return rc;
+    std::vector<fluere_record> tail;
+    LiveArgs a = live_args(lv);
+    a.block_bytes = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
+    if (duration_end && lv->last_have) {  // the duration scan (no timeout > 0 guard, :364-366)
+        k_live_scan<<<flow_grid(lv->persist), 256, 0, s>>>(a, lv->last_time - lv->timeout_ms * 1000ull, 0);
+        HIPCHECK(hipGetLastError());
+        if ((rc = live_take(lv, tail))) return rc;
+    }
+    k_live_scan<<<flow_grid(lv->persist), 256, 0, s>>>(a, 0, 1);  // every active flow (:379-383)
+    HIPCHECK(hipGetLastError());
+    if ((rc = live_take(lv, tail))) return rc;
+    return live_export(lv, tail, recs, n, n_ordered);
+}

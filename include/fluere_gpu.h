@@ -235,7 +235,8 @@ typedef struct fluere_flow_annex {
     uint32_t pad;
     uint64_t f0;                /* global index of the shard's first FIN/RST of the flow */
     fluere_flow_piece lead, head, tail;
-    uint64_t pad2;
+    uint64_t mid_last;          /* 1 + index of the last packet of the instances that open and close
+                                   inside the shard (their records stay there); 0: none */
 } fluere_flow_annex;            /* 512 bytes */
 
 /* Block header; the run counters are the exporting shard's (the same in each
@@ -273,6 +274,32 @@ int fluere_export_device(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uin
  * run the capture in one context). */
 int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
                           uint64_t cap_annex, fluere_stats* stats);
+
+/* ---- live mode (src/net/live_fluereflow.rs:196-376) on batched capture --- */
+/* A live session: packets arrive in batches (a classic pcap image each: the
+ * records a capture ring delivered since the last call); flows stay open
+ * across batches.  Per packet the reference runs parse_keys /
+ * parse_fluereflow, the SYN gate (:226-269), update_flow (:288) and the
+ * FIN/RST close with the plugin hand-off (:290-303); there is no expiry wheel.
+ * The checks it runs after each processed packet run here once per batch,
+ * after the batch's last processed packet, with that packet's time:
+ *   fluere_live_batch(do_export = 1): the interval export (:306-358): flows
+ *     with flow.last < time - timeout expire (when timeout > 0), and the
+ *     FIN/RST-closed records since the last export plus the expired ones are
+ *     returned (*exported = 1) -- one CSV file / one plugin hand-off batch;
+ *   fluere_live_finish: the duration scan (duration_end, :361-373: the same
+ *     test without the timeout > 0 guard), then every flow still active, as
+ *     the last export (:379-392).
+ * Returned records: the first *n_ordered in the reference's order (the
+ * packet that closed them; order_key = its global index), the rest in the
+ * reference's HashMap order (unspecified; order_key = UINT64_MAX).  Free with
+ * fluere_records_free.  opts->max_flows bounds the session's distinct flows. */
+typedef struct fluere_live fluere_live;
+int fluere_live_open(const fluere_opts* opts, fluere_live** out);
+int fluere_live_close(fluere_live* lv);
+int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, int do_export, fluere_record** recs,
+                      uint64_t* n, uint64_t* n_ordered, int* exported);
+int fluere_live_finish(fluere_live* lv, int duration_end, fluere_record** recs, uint64_t* n, uint64_t* n_ordered);
 
 /* Test seam: insert n canonical keys (14 u32 words each, device memory) into
  * the flow dictionary and write each key's dense flow id. */

@@ -903,6 +903,135 @@ int or_offline_buffer(const uint8_t* file, uint64_t nbytes, uint64_t timeout_ms,
 
 void or_result_free(or_result* r) { free(r->recs); memset(r, 0, sizeof *r); }
 
+/* ---- live mode: src/net/live_fluereflow.rs:196-376 ---------------------- */
+static void live_push(or_live_result* o, const or_record* r, uint8_t kind) {
+    if (o->n == o->cap) {
+        o->cap = o->cap ? 2 * o->cap : 1024;
+        o->recs = (or_record*)realloc(o->recs, o->cap * sizeof *o->recs);
+        o->interval = (uint32_t*)realloc(o->interval, o->cap * sizeof *o->interval);
+        o->kind = (uint8_t*)realloc(o->kind, o->cap * sizeof *o->kind);
+    }
+    o->recs[o->n] = *r;
+    o->interval[o->n] = UINT32_MAX;  /* set at the export that writes it */
+    o->kind[o->n] = kind;
+    o->n++;
+}
+
+/* expire the active flows whose last update is older than time - timeout
+ * (u64 arithmetic wraps as in the release build); in creation order, the
+ * reference's HashMap order is unspecified */
+static int cmp_slot_seq(const void* a, const void* b) {
+    const slot* x = (const slot*)a;
+    const slot* y = (const slot*)b;
+    return x->seq < y->seq ? -1 : x->seq > y->seq;
+}
+static void live_scan(fmap* A, uint64_t time, uint64_t timeout_ms, uint8_t kind, or_live_result* o) {
+    const uint64_t lim = time - timeout_ms * 1000ull;
+    slot* ex = (slot*)malloc((A->n + 1) * sizeof(slot));  /* copies: erasing shifts slots */
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < A->cap; i++) if (A->s[i].used && A->s[i].rec.last < lim) ex[k++] = A->s[i];
+    qsort(ex, k, sizeof(slot), cmp_slot_seq);
+    for (uint64_t i = 0; i < k; i++) {
+        live_push(o, &ex[i].rec, kind);
+        fm_erase(A, fm_find(A, &ex[i].key));
+    }
+    free(ex);
+}
+
+int or_live_buffer(const uint8_t* file, uint64_t nbytes, const uint64_t* batch_end, const uint8_t* batch_export,
+                   uint64_t n_batches, uint64_t timeout_ms, int use_mac, int duration_end, or_live_result* out) {
+    memset(out, 0, sizeof *out);
+    or_pcap_rec* recs;
+    int64_t n = or_pcap_index(file, nbytes, &recs);
+    if (n < 0) return -1;
+    fmap A;
+    fm_init(&A, 1024);
+    uint64_t create_seq = 0, exported = 0;
+    int64_t i = 0;
+    for (uint64_t b = 0; b < n_batches; b++) {
+        int have = 0;      /* a processed packet in this batch (the checks run after one) */
+        uint64_t time = 0; /* its timestamp: the `time` of the checks (:306-373) */
+        for (; i < n && (uint64_t)i < batch_end[b]; i++) { /* :196-303 */
+            const uint8_t* d = file + recs[i].data_off;
+            uint32_t L = recs[i].caplen;
+            or_key key, rev;
+            int raw_k = 0, raw_f = 0;
+            if (or_parse_keys(d, L, &key, &rev, &raw_k)) continue;              /* :204-207 */
+            if (!use_mac) {                                                      /* :208-211 */
+                memset(key.smac, 0, 6); memset(key.dmac, 0, 6);
+                memset(rev.smac, 0, 6); memset(rev.dmac, 0, 6);
+            }
+            uint64_t doctets;
+            uint8_t fl[9];
+            or_record fd;
+            if (or_parse_fluereflow(d, L, recs[i].ts_sec, recs[i].ts_usec, &doctets, fl, &fd, &raw_f)) continue; /* :213-219 */
+            kbuf kb, rb;
+            key_buf(&key, &kb);
+            key_buf(&rev, &rb);
+            int is_rev;
+            slot* fl_s = fm_find(&A, &kb);                                       /* :224-269 */
+            if (fl_s) is_rev = 0;
+            else if ((fl_s = fm_find(&A, &rb))) is_rev = 1;
+            else {
+                if (fd.prot == 6 && fl[1] == 0) continue;                        /* SYN gate */
+                fl_s = fm_insert(&A, &kb);
+                fl_s->seq = create_seq++;
+                fl_s->rec = fd;
+                is_rev = 0;
+            }
+            const uint64_t t = (uint64_t)recs[i].ts_sec * 1000000ull + recs[i].ts_usec; /* :271-274 */
+            or_record* f = &fl_s->rec;                                           /* update_flow :288 */
+            uint32_t pkt = fd.min_pkt;
+            uint8_t ttl = fd.min_ttl;
+            f->d_pkts += 1;
+            f->d_octets += doctets;
+            if (pkt > f->max_pkt) f->max_pkt = pkt;
+            if (pkt < f->min_pkt) f->min_pkt = pkt;
+            if (ttl > f->max_ttl) f->max_ttl = ttl;
+            if (ttl < f->min_ttl) f->min_ttl = ttl;
+            for (int c = 0; c < 9; c++) f->cnt[c] += fl[c];
+            f->last = t;
+            if (is_rev) { f->in_pkts += 1; f->in_bytes += doctets; }
+            else { f->out_pkts += 1; f->out_bytes += doctets; }
+            if (fl[0] == 1 || fl[2] == 1) {                                      /* :296-302 plugin + records */
+                live_push(out, f, 0);
+                fm_erase(&A, fl_s);
+            }
+            have = 1;
+            time = t;
+        }
+        if (!have) continue;
+        if (batch_export[b]) {                                                   /* :306-358 interval export */
+            if (timeout_ms > 0) live_scan(&A, time, timeout_ms, 1, out);
+            for (uint64_t k = 0; k < out->n; k++) if (out->interval[k] == UINT32_MAX) out->interval[k] = (uint32_t)exported;
+            exported++;
+        }
+        if (b + 1 == n_batches && duration_end) live_scan(&A, time, timeout_ms, 2, out); /* :361-373 */
+    }
+    /* :379-392 every flow still active, then the last export */
+    slot** act = (slot**)malloc((A.n + 1) * sizeof(slot*));
+    uint64_t k = 0;
+    for (uint64_t j = 0; j < A.cap; j++) if (A.s[j].used) act[k++] = &A.s[j];
+    qsort(act, k, sizeof(slot*), cmp_seq);
+    for (uint64_t j = 0; j < k; j++) live_push(out, &act[j]->rec, 3);
+    free(act);
+    for (uint64_t j = 0; j < out->n; j++) if (out->interval[j] == UINT32_MAX) out->interval[j] = (uint32_t)exported;
+    out->n_exports = exported + 1;
+    out->packets = (uint64_t)n;
+    free(A.s);
+    free(recs);
+    return 0;
+}
+
+uint64_t or_record_size(void) { return sizeof(or_record); }
+
+void or_live_free(or_live_result* r) {
+    free(r->recs);
+    free(r->interval);
+    free(r->kind);
+    memset(r, 0, sizeof *r);
+}
+
 /* ---- CSV: src/utils/fluere_csv_exporter.rs:5-81 (csv 1.3, '\n' terminator) */
 static const char* CSV_HEADER =
     "source,destination,src_port,dst_port,prot,d_pkts,d_octets,in_pkts,out_pkts,in_bytes,out_bytes,"

@@ -158,6 +158,28 @@ int or_offline_buffer(const uint8_t* file, uint64_t nbytes, uint64_t timeout_ms,
                       or_result* out);
 void or_result_free(or_result* r);
 
+/* live mode (src/net/live_fluereflow.rs:196-376) over a capture cut into
+ * batches: packets [batch_end[b-1], batch_end[b]).  The checks the reference
+ * runs after a processed packet run once per batch, after its last processed
+ * packet (with that packet's time): the interval export when batch_export[b]
+ * (idle-timeout scan flow.last < time - timeout, :306-358), and after the last
+ * batch the duration scan when duration_end (:361-373).  Then every active
+ * flow (:379-383) and the last export.  Records in push order: FIN/RST closes
+ * in packet order; scans and the final flush in creation order (the reference
+ * iterates a HashMap: unspecified). */
+typedef struct {
+    or_record* recs;
+    uint32_t* interval; /* the export (CSV file) that writes the record */
+    uint8_t* kind;      /* 0 FIN/RST close, 1 idle-timeout scan, 2 duration scan, 3 active at the end */
+    uint64_t n, cap;
+    uint64_t n_exports;
+    uint64_t packets;
+} or_live_result;
+int or_live_buffer(const uint8_t* file, uint64_t nbytes, const uint64_t* batch_end, const uint8_t* batch_export,
+                   uint64_t n_batches, uint64_t timeout_ms, int use_mac, int duration_end, or_live_result* out);
+void or_live_free(or_live_result* r);
+uint64_t or_record_size(void);
+
 /* csv exporter (src/utils/fluere_csv_exporter.rs:5-81).  Returns bytes
  * written into buf (buf may be NULL to size). */
 uint64_t or_format_csv(const or_record* recs, uint64_t n, char* buf, uint64_t cap);

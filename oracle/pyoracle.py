@@ -42,6 +42,12 @@ class _OrRawHdr(ctypes.Structure):
                 ("payload_len", ctypes.c_uint32)]
 
 
+class _LiveResult(ctypes.Structure):
+    _fields_ = [("recs", ctypes.c_void_p), ("interval", ctypes.c_void_p), ("kind", ctypes.c_void_p),
+                ("n", ctypes.c_uint64), ("cap", ctypes.c_uint64), ("n_exports", ctypes.c_uint64),
+                ("packets", ctypes.c_uint64)]
+
+
 _RAW_FNS = ["or_raw_from_raw_packet", "or_raw_from_ethertype", "or_raw_parse_ethertype", "or_raw_parse_protocol",
             "or_raw_openvpn", "or_raw_icmp"]
 
@@ -74,6 +80,12 @@ def lib():
             fn.restype = ctypes.c_int
             fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32] + ([ctypes.c_uint32] if i < 4 else []) + \
                 [ctypes.POINTER(_OrRawHdr)]
+        L.or_live_buffer.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(_LiveResult)]
+        L.or_live_buffer.restype = ctypes.c_int
+        L.or_live_free.argtypes = [ctypes.POINTER(_LiveResult)]
+        L.or_record_size.restype = ctypes.c_uint64
         L.or_raw_analyze_structure.restype = None
         L.or_raw_analyze_structure.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                                ctypes.POINTER(ctypes.c_int)]
@@ -151,3 +163,35 @@ def analyze_structure(data: bytes):
     hs, hp = ctypes.c_uint32(), ctypes.c_int()
     L.or_raw_analyze_structure(buf, len(data), ctypes.byref(hs), ctypes.byref(hp))
     return hs.value, bool(hp.value)
+
+
+def live(pcap: bytes, batch_end, batch_export, timeout_ms: int = 600000, use_mac: bool = False,
+         duration_end: bool = False):
+    """live mode over batches (or_live_buffer) -> list of exports, each
+    dict(csv=str, n_ordered=int): the FIN/RST-closed rows first in order, the
+    rest in creation order (the reference's HashMap order is unspecified)."""
+    L = lib()
+    buf = (ctypes.c_uint8 * max(len(pcap), 1)).from_buffer_copy(pcap + b"\0")
+    be = np.ascontiguousarray(batch_end, dtype=np.uint64)
+    bx = np.ascontiguousarray(batch_export, dtype=np.uint8)
+    r = _LiveResult()
+    if L.or_live_buffer(buf, len(pcap), be.ctypes.data, bx.ctypes.data, len(be), timeout_ms, 1 if use_mac else 0,
+                        1 if duration_end else 0, ctypes.byref(r)) != 0:
+        raise ValueError("oracle: not a pcap")
+    try:
+        rs = int(L.or_record_size())
+        raw = ctypes.string_at(r.recs, r.n * rs) if r.n else b""
+        interval = np.frombuffer(ctypes.string_at(r.interval, 4 * r.n), dtype=np.uint32) if r.n else np.zeros(0, np.uint32)
+        kind = np.frombuffer(ctypes.string_at(r.kind, r.n), dtype=np.uint8) if r.n else np.zeros(0, np.uint8)
+        out = []
+        for k in range(r.n_exports):
+            idx = np.nonzero(interval == k)[0]
+            sel = b"".join(raw[int(j) * rs:(int(j) + 1) * rs] for j in idx)
+            sb = (ctypes.c_uint8 * max(len(sel), 1)).from_buffer_copy(sel + b"\0")
+            need = L.or_format_csv(sb, len(idx), None, 0)
+            cb = ctypes.create_string_buffer(need)
+            L.or_format_csv(sb, len(idx), cb, need)
+            out.append(dict(csv=cb.raw[:need].decode(), n_ordered=int((kind[idx] == 0).sum())))
+        return out
+    finally:
+        L.or_live_free(ctypes.byref(r))

@@ -573,3 +573,44 @@ def test_pcapng_file_ingest(gpu, tmp_path):
     st = fluere_amd.fluereflow_fileparse(fluere_amd.Args(fluere_amd.Files(file=str(path))), out_dir=str(tmp_path / "o"))
     got = (tmp_path / "o" / "cap_converted.csv").read_text()
     assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "pcapng fluere_offline_file")
+
+
+# ---- live mode on batched capture (fluere_amd/live.py, live_fluereflow.rs:196-376)
+LIVE_CASES = {
+    # kind, packets, lanes/flows, seed, interval ms (packet clock), batch packets, timeout ms, duration_end, -M
+    "tcp_t10": (_lib.SYNTH_TCP, 200_000, 2_000, 0xF10E0047, 20, 0, 10, True, False),
+    "tcp_t0_no_guard": (_lib.SYNTH_TCP, 120_000, 1_500, 0xF10E0057, 25, 7_000, 0, True, False),
+    "imix_small_batches": (_lib.SYNTH_IMIX, 150_000, 3_000, 0xF10E0067, 40, 5_000, 30, False, False),
+    "mac_keys": (_lib.SYNTH_MAC64, 100_000, 2_000, 0xF10E0077, 30, 0, 20, True, True),
+}
+
+
+@pytest.mark.parametrize("name", sorted(LIVE_CASES))
+def test_live_matches_oracle(gpu, name, tmp_path):
+    """Every export (CSV file / plugin hand-off batch) of the live mode equals
+    the oracle's: the FIN/RST-closed records in order, the idle-timeout,
+    duration and final-flush records as a multiset (HashMap order)."""
+    from fluere_amd import live
+    kind, n, f, seed, interval, bp, timeout, dur, mac = LIVE_CASES[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    batches = list(live.replay_batches(data, interval, bp))
+    ends, k = [], 0
+    for img, _ in batches:
+        k += sum(1 for _ in live.pcap_records(img))
+        ends.append(k)
+    want = pyoracle.live(data, ends, [e for _, e in batches], timeout, mac, dur)
+
+    class Plugin:  # fluere-plugin's process_data(table) (lib.rs:228-276)
+        def __init__(self):
+            self.seen = []
+
+        def process_data(self, vec):
+            self.seen.append(vec)
+
+    plug = Plugin()
+    args = fluere_amd.Args(fluere_amd.Files(csv="live"), fluere_amd.Parameters(use_mac=mac, timeout=timeout))
+    got = live.packet_capture(args, batches, out_dir=str(tmp_path), plugins=[plug], duration_end=dur)
+    assert len(got) == len(want) >= 2
+    for i, ((path, recs, n_ord), w) in enumerate(zip(got, want)):
+        assert_csv_equal(open(path).read(), n_ord, w["csv"], w["n_ordered"], f"{name} export {i}")
+    assert len(plug.seen) == sum(len(r) for _, r, _ in got)
