@@ -614,3 +614,30 @@ def test_live_matches_oracle(gpu, name, tmp_path):
     for i, ((path, recs, n_ord), w) in enumerate(zip(got, want)):
         assert_csv_equal(open(path).read(), n_ord, w["csv"], w["n_ordered"], f"{name} export {i}")
     assert len(plug.seen) == sum(len(r) for _, r, _ in got)
+
+
+def test_fluere_live_cli(gpu, tmp_path):
+    """`fluere live --replay` (the C++ CLI over the C ABI): its CSV files equal
+    the oracle's exports for the same interval batches."""
+    import subprocess
+    from fluere_amd import live
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 80_000, 800, 0xF10E0087))
+    path = tmp_path / "cap.pcap"
+    path.write_bytes(data)
+    out = tmp_path / "o"
+    subprocess.run([_lib.CLI_PATH, "live", "--replay", str(path), "-c", "lv", "-I", "15", "-t", "10", "-o", str(out)],
+                   check=True, capture_output=True)
+    batches = list(live.replay_batches(data, 15))
+    ends, k = [], 0
+    for img, _ in batches:
+        k += sum(1 for _ in live.pcap_records(img))
+        ends.append(k)
+    want = pyoracle.live(data, ends, [e for _, e in batches], 10, False, False)
+    files = sorted(out.glob("lv_*.csv"), key=lambda p: int(p.stem.split("_")[1]))
+    assert len(files) == len(want)
+    for f, w in zip(files, want):
+        got = f.read_text()
+        rows = got.splitlines()[1:]
+        # the CLI writes the export in order: FIN/RST-closed prefix first
+        assert_csv_equal(got, w["n_ordered"], w["csv"], w["n_ordered"], f.name)
+        assert len(rows) == w["csv"].count("\n") - 1
