@@ -124,6 +124,7 @@ struct AggArgs {
     unsigned long long* slow_n;
     int macs;
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
+    uint32_t nsub;             // k_merge_partials sub-passes per owner (a power of two; 0 = 1)
 };
 
 // Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
@@ -1140,18 +1141,21 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool macs = a.macs != 0;
-    for (int e = tid; e < MT; e += MB) {
-        m_key[e] = make_uint4(0, 0, 0, 0);
-        m_kx[e] = make_uint4(0, 0, 0, 0);
-        m_pk[0][e] = m_pk[1][e] = 0;
-        m_by[0][e] = m_by[1][e] = 0;
-        m_mn[0][e] = m_mn[1][e] = NONE32;
-        m_mx[0][e] = m_mx[1][e] = 0;
+    auto clear_table = [&]() {
+        for (int e = tid; e < MT; e += MB) {
+            m_key[e] = make_uint4(0, 0, 0, 0);
+            m_kx[e] = make_uint4(0, 0, 0, 0);
+            m_pk[0][e] = m_pk[1][e] = 0;
+            m_by[0][e] = m_by[1][e] = 0;
+            m_mn[0][e] = m_mn[1][e] = NONE32;
+            m_mx[0][e] = m_mx[1][e] = 0;
 #pragma unroll
-        for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
-        m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
-        m_la[e] = 0;
-    }
+            for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
+            m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
+            m_la[e] = 0;
+        }
+    };
+    clear_table();
     __syncthreads();
     if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 1] = wall_clock64();
     const Stage& S = a.S;
@@ -1187,6 +1191,17 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // Pass 0 takes the staged partials, pass 1 the spilled packets (each a
     // one-packet partial), through the same per-owner segment machinery.
     const int passes = n_spill_all ? 2 : 1;  // no spills: one pass
+    // Sub-passes: an owner with more flows than its LDS table holds merges
+    // them in nsub rounds, each taking the records whose key hash has the
+    // round's low bits (the others are skipped after their key is read); the
+    // table is flushed to the global accumulators after every round, so no
+    // record takes the per-record global path for want of an entry.
+    const uint32_t nsub = a.nsub ? a.nsub : 1;
+    for (uint32_t sub = 0; sub < nsub; sub++) {
+    if (sub) {
+        clear_table();
+        __syncthreads();
+    }
     for (int pass = 0; pass < passes; pass++)
     for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
         const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
@@ -1241,6 +1256,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 for (int q = 0; q < 5; q++) v[q] = src[q];
                 __builtin_memcpy(&p, v, sizeof p);
                 h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
+                if ((h & (nsub - 1)) != sub) continue;
                 if (macs) {
                     const uint4 xx = S.partx[o];
                     x0 = xx.x; x1 = xx.y; x2 = xx.z;
@@ -1260,6 +1276,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     h = lt_hash(k0, k1, k2, tag);
                     spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
                 }
+                if ((h & (nsub - 1)) != sub) continue;
             }
             // find or claim the merge entry (same protocol as the hot kernel)
             uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
@@ -1428,6 +1445,8 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         atomicAdd(&a.g->cyc_m_scan, c1 - c0);
         atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
     }
+    __syncthreads();
+    }  // sub-passes
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
     if (me == gridDim.x - 1 && tid < 64) reduce_stats();
@@ -1476,6 +1495,7 @@ struct FinArgs {
     uint64_t out_cap;
     Ctl* host_ctl;   // non-null: the last workgroup writes the run counters to this pinned host copy,
     uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
+    unsigned long long timeout_us;  // non-zero: skip the flows when expiries can fire (Mode B redoes every flow)
 };
 
 // Certified flow d -> its record; false when d has no record here (TCP flow
@@ -1553,7 +1573,9 @@ __device__ void publish_ctl(Glob* g, unsigned long long* done, Ctl* host_ctl, ui
 }
 
 __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
-    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    const Glob& gg = *a.g;
+    const bool mode_b = a.timeout_us && gg.valid && gg.tmax - gg.tmin >= a.timeout_us;
+    const uint32_t nf = mode_b ? 0u : min(*a.T.n_flows, a.T.fmax);
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
         const uint32_t d = d0 + threadIdx.x;
         fluere_record r;
@@ -3012,6 +3034,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         if (hipMalloc(&c->d_stage, need_max) != hipSuccess) return FLUERE_E_NOMEM;
         c->d_stage_bytes = need_max;
     }
+    // merge sub-passes: enough that an owner's share of the flows (the last
+    // run's count as the estimate) fits its 1024-entry LDS table at ~70 %
+    {
+        const uint64_t per_owner = c->last_nf / std::max<uint32_t>(1, merge_owners(c));
+        uint32_t ns = 1;
+        while (ns < 16 && per_owner > 700ull * ns) ns *= 2;
+        a.nsub = ns;
+    }
     P.nb = 0;
     for (auto& hb : c->batches) {
         if (!hb.b.n) continue;
@@ -3074,6 +3104,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
         if ((rc = ensure_recs(c, std::max<uint64_t>(c->d_recs_cap, std::min<uint64_t>(c->fmax, 1u << 16))))) return rc;
         P.fa = FinArgs{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob,
                        c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
+        P.fa.timeout_us = c->timeout_ms * 1000ull;
         P.fin_grid = flow_grid(c);
         P.spec_ca = P.ca;
         P.spec_ca.spec = 1;
@@ -3412,7 +3443,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     // the speculative cleanup behind the copy clears the flows exactly when
     // the run needs no more device work (the same test, on the same counters)
     const bool spec_cleared = P.spec && run_complete(g, nf_err[1], P.spec_ca.timeout_us, P.spec_ca.recs_cap);
-    if (spec_cleared) c->last_nf = nf_err[0];
+    if (!(nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = nf_err[0];
     debug_counters(c, &g);
     FinArgs fa = P.fa;
     fa.host_ctl = nullptr;  // re-launches below read the counters back with copies
@@ -3666,9 +3697,11 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     // 1. flows whose part of the state machine depends on packet order here
     reset_record_counters(c);
     k_local_cert<<<flow_grid(c), 256, 0, s>>>(fa, c->d_annex_of);
-    Glob g;
-    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    Ctl ctl;
+    HIPCHECK(hipMemcpyAsync(&ctl, c->d_glob, sizeof ctl, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
+    Glob g = ctl.g;
+    if (!(ctl.err & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = ctl.n_flows;  // (merge sub-pass estimate)
     // 2. their annexes (and the records that open and close in this shard)
     if (g.n_complex) {
         std::vector<Batch> hb(nb);
