@@ -124,7 +124,6 @@ struct AggArgs {
     unsigned long long* slow_n;
     int macs;
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
-    uint32_t nsub;             // k_merge_partials sub-passes per owner (a power of two; 0 = 1)
 };
 
 // Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
@@ -229,9 +228,9 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int LK_BITS = 11;
 constexpr int LK = 1 << LK_BITS;        // key entries (32 KiB)
 #ifndef FLUERE_NS
-#define FLUERE_NS 1280
+#define FLUERE_NS 1200
 #endif
-constexpr int NS = FLUERE_NS;                // aggregate slots (68 B each, 85 KiB)
+constexpr int NS = FLUERE_NS;                // aggregate slots (68 B each, 80 KiB)
 constexpr int LK_STEPS = 16;            // probe steps of two entries
 #ifndef FLUERE_HOT_PK
 #define FLUERE_HOT_PK 1
@@ -251,7 +250,21 @@ constexpr int LK_STEPS = 16;            // probe steps of two entries
 constexpr int PK = FLUERE_HOT_PK;       // packets per lane per hot-loop iteration
 static_assert(WIN_ITERS % PK == 0, "a window holds whole iterations");
 constexpr uint32_t LT_READY = 1u << 23, LT_CLAIM = 1u << 22, LT_SLOT = LT_CLAIM - 1;
-constexpr int MAX_OWNERS = 256;
+constexpr int MAX_OWNERS = 2048;
+// Per-owner counters of a window in LDS, two 16-bit counters per word: counts
+// and segment starts of one window stay below 65536 (<= 61440 packets, <= NS
+// slots), so a half never carries into its neighbour.
+__device__ __forceinline__ uint32_t own_get(const uint32_t* arr, uint32_t o) {
+    return (arr[o >> 1] >> ((o & 1) * 16)) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t own_add(uint32_t* arr, uint32_t o) {
+    return (atomicAdd(&arr[o >> 1], 1u << ((o & 1) * 16)) >> ((o & 1) * 16)) & 0xFFFFu;
+}
+__device__ __forceinline__ void own_set(uint32_t* arr, uint32_t o, uint32_t v) {  // (no concurrent writer of the word)
+    const uint32_t sh = (o & 1) * 16;
+    arr[o >> 1] = (arr[o >> 1] & ~(0xFFFFu << sh)) | (v << sh);
+}
+constexpr int OWN_WORDS = (MAX_OWNERS + 2) / 2;
 constexpr int SPILL_WG = WIN_ITERS * BLOCK;  // raw spilled packets per workgroup (one window)
 constexpr int NS_MAC = 768;
 #ifndef FLUERE_SPILL_NT
@@ -310,8 +323,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint32_t s_sk[NS];  // key entry of each slot
     __shared__ uint4 s_slab[BLOCK / 64][160];  // per wave: half a dense chunk's span (32 x 80 B)
     __shared__ uint32_t s_nslot, s_chunk, s_nspill;
-    __shared__ uint32_t s_own[MAX_OWNERS + 1];   // flush: per-owner counts -> segment starts
-    __shared__ uint32_t s_scnt[MAX_OWNERS + 1];  // spilled packets per owner (this window) -> segment starts
+    __shared__ uint32_t s_own[OWN_WORDS];   // flush: per-owner slot counts -> segment starts (packed, own_get)
+    __shared__ uint32_t s_scnt[OWN_WORDS];  // spilled packets per owner (this window) -> segment starts (packed)
     __shared__ unsigned long long s_sbase;
     __shared__ unsigned long long s_cnt[5], s_tmin, s_tmax;
     const int tid = threadIdx.x;
@@ -328,7 +341,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     }
     if (tid < 5) s_cnt[tid] = 0;
     if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; s_chunk = 0; s_nspill = 0; }
-    for (int o = tid; o <= MAX_OWNERS; o += BLOCK) s_scnt[o] = 0;
+    for (int o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
     __syncthreads();
 
     const Batch& B = a.B;
@@ -561,7 +574,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     if (MACS) dst[SPILL_WG] = make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]);
                     dst[(MACS ? 2 : 1) * SPILL_WG] = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24),
                                                                 loc, h.tf | (q[u].dir << 8));
-                    atomicAdd(&s_scnt[owner_of(hk[u], a.S.O)], 1u);
+                    own_add(s_scnt, owner_of(hk[u], a.S.O));
                     c_valid++;
                     tmin = min(tmin, (unsigned long long)h.t);
                     tmax = max(tmax, (unsigned long long)h.t);
@@ -661,7 +674,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         // counting sort of this window's flows by merge owner; a thread keeps
         // its slots' (at most two) owners and hashes in registers
         constexpr int SPT = (NS + BLOCK - 1) / BLOCK;  // slots per thread
-        for (uint32_t o = tid; o <= O; o += BLOCK) s_own[o] = 0;
+        for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_own[o] = 0;
         lds_barrier();
         uint32_t own[SPT], hh[SPT];
         uint4 kks[SPT];
@@ -681,22 +694,22 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 hh[k] = mac_hash(hh[k], xs.x, xs.y, xs.z);
             }
             own[k] = owner_of(hh[k], O);
-            atomicAdd(&s_own[own[k]], 1u);
+            own_add(s_own, own[k]);
         }
         lds_barrier();
         if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 4] = wall_clock64();
-        // exclusive scans over the owners (one wave each, 4 owners per lane):
-        // wave 0 the slot counts, wave 1 the spill counts
-        static_assert(MAX_OWNERS <= 256, "4 owners per lane");
+        // exclusive scans over the owners (one wave each, an even run of
+        // owners per lane, so no two lanes write one packed word): wave 0
+        // the slot counts, wave 1 the spill counts
+        static_assert(MAX_OWNERS % 2 == 0, "owner runs cover whole words");
         if (tid < 128) {
             uint32_t* arr = tid < 64 ? s_own : s_scnt;
             const uint32_t l = tid & 63;
-            uint32_t v[4], sum = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t o = l * 4 + q;
-                v[q] = o < O ? arr[o] : 0;
-                sum += v[q];
+            const uint32_t per = 2 * ((O + 127) / 128);
+            uint32_t sum = 0;
+            for (uint32_t q = 0; q < per; q++) {
+                const uint32_t o = l * per + q;
+                if (o < O) sum += own_get(arr, o);
             }
             uint32_t incl = sum;
 #pragma unroll
@@ -705,20 +718,22 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 if (l >= dlt) incl += y;
             }
             uint32_t run = incl - sum;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t o = l * 4 + q;
-                if (o < O) arr[o] = run;
-                run += v[q];
+            for (uint32_t q = 0; q < per; q++) {
+                const uint32_t o = l * per + q;
+                if (o < O) {
+                    const uint32_t v = own_get(arr, o);
+                    own_set(arr, o, run);
+                    run += v;
+                }
             }
-            if (l == 63) arr[O] = incl;
+            if (l == 63) own_set(arr, O, incl);
         }
         const uint32_t nsp = s_nspill;
         if (tid == 128) s_sbase = nsp ? atomicAdd(&a.g->n_spill, (unsigned long long)nsp) : 0ull;
         lds_barrier();
         for (uint32_t o = tid; o <= O; o += BLOCK) {
-            S.off[(size_t)o * S.n_sets + set] = s_own[o];
-            S.soff[(size_t)o * S.n_sets + set] = s_scnt[o];
+            S.off[(size_t)o * S.n_sets + set] = own_get(s_own, o);
+            S.soff[(size_t)o * S.n_sets + set] = own_get(s_scnt, o);
         }
         if (tid == 0) {
             S.base[set] = B.first + wbase;
@@ -759,7 +774,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     if (i >= nsp) continue;
                     const u32x4 v0 = av[u][0];
                     const uint32_t hsp = MACS ? av[u][1].w : lt_hash(v0.x, v0.y, v0.z, v0.w);
-                    const uint32_t pos = atomicAdd(&s_scnt[owner_of(hsp, O)], 1u);
+                    const uint32_t pos = own_add(s_scnt, owner_of(hsp, O));
                     uint4* dst = reinterpret_cast<uint4*>(S.spill) + sb + pos;
 #pragma unroll
                     for (int w = 0; w < SW; w++) {
@@ -779,7 +794,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             const uint4 kk = kks[k];
             const uint32_t tag = kk.w & 0xFF000000u;
             const uint32_t h = hh[k];
-            const size_t o = (size_t)set * NS + (FLUERE_FLUSH_LINEAR ? e : atomicAdd(&s_own[own[k]], 1u));
+            const size_t o = (size_t)set * NS + (FLUERE_FLUSH_LINEAR ? e : own_add(s_own, own[k]));
             uint4* dst = reinterpret_cast<uint4*>(S.part + o);
             if (FLUERE_FLUSH_LINEAR == 2 && kk.x != 0x12345678u) continue;  // diagnostics: no stores
             dst[0] = make_uint4(kk.x, kk.y, kk.z, tag);
@@ -800,7 +815,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         }
         lds_barrier();
         if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 6] = wall_clock64();
-        for (uint32_t o = tid; o <= MAX_OWNERS; o += BLOCK) s_scnt[o] = 0;
+        for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
         if (tid == 0) s_nspill = 0;
         lds_barrier();
         const unsigned long long f1 = clock64() - f0;
@@ -1141,21 +1156,18 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool macs = a.macs != 0;
-    auto clear_table = [&]() {
-        for (int e = tid; e < MT; e += MB) {
-            m_key[e] = make_uint4(0, 0, 0, 0);
-            m_kx[e] = make_uint4(0, 0, 0, 0);
-            m_pk[0][e] = m_pk[1][e] = 0;
-            m_by[0][e] = m_by[1][e] = 0;
-            m_mn[0][e] = m_mn[1][e] = NONE32;
-            m_mx[0][e] = m_mx[1][e] = 0;
+    for (int e = tid; e < MT; e += MB) {
+        m_key[e] = make_uint4(0, 0, 0, 0);
+        m_kx[e] = make_uint4(0, 0, 0, 0);
+        m_pk[0][e] = m_pk[1][e] = 0;
+        m_by[0][e] = m_by[1][e] = 0;
+        m_mn[0][e] = m_mn[1][e] = NONE32;
+        m_mx[0][e] = m_mx[1][e] = 0;
 #pragma unroll
-            for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
-            m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
-            m_la[e] = 0;
-        }
-    };
-    clear_table();
+        for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
+        m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
+        m_la[e] = 0;
+    }
     __syncthreads();
     if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 1] = wall_clock64();
     const Stage& S = a.S;
@@ -1191,17 +1203,6 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // Pass 0 takes the staged partials, pass 1 the spilled packets (each a
     // one-packet partial), through the same per-owner segment machinery.
     const int passes = n_spill_all ? 2 : 1;  // no spills: one pass
-    // Sub-passes: an owner with more flows than its LDS table holds merges
-    // them in nsub rounds, each taking the records whose key hash has the
-    // round's low bits (the others are skipped after their key is read); the
-    // table is flushed to the global accumulators after every round, so no
-    // record takes the per-record global path for want of an entry.
-    const uint32_t nsub = a.nsub ? a.nsub : 1;
-    for (uint32_t sub = 0; sub < nsub; sub++) {
-    if (sub) {
-        clear_table();
-        __syncthreads();
-    }
     for (int pass = 0; pass < passes; pass++)
     for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
         const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
@@ -1256,7 +1257,6 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 for (int q = 0; q < 5; q++) v[q] = src[q];
                 __builtin_memcpy(&p, v, sizeof p);
                 h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
-                if ((h & (nsub - 1)) != sub) continue;
                 if (macs) {
                     const uint4 xx = S.partx[o];
                     x0 = xx.x; x1 = xx.y; x2 = xx.z;
@@ -1276,7 +1276,6 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     h = lt_hash(k0, k1, k2, tag);
                     spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
                 }
-                if ((h & (nsub - 1)) != sub) continue;
             }
             // find or claim the merge entry (same protocol as the hot kernel)
             uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
@@ -1445,8 +1444,6 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         atomicAdd(&a.g->cyc_m_scan, c1 - c0);
         atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
     }
-    __syncthreads();
-    }  // sub-passes
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
     if (me == gridDim.x - 1 && tid < 64) reduce_stats();
@@ -2986,11 +2983,16 @@ static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, 
 // streams at the flush (C5u k_parse_agg 0.65 / 0.58 / 0.52 ms at 256 / 128 / 64
 // owners) but a slower merge (step 0.97 / 1.14 / 3.3 ms), so all are used.
 #ifndef FLUERE_MAC_OWNERS
-#define FLUERE_MAC_OWNERS 256
+#define FLUERE_MAC_OWNERS 2048
 #endif
 static uint32_t merge_owners(const fluere_ctx* c) {
+    // enough owners that each one's share of the flows (the last run's count
+    // as the estimate) fits its merge workgroup's 1024-entry LDS table at ~60 %
+    // load; at least one per CU
+    uint32_t o = 256;
+    while (o < (uint32_t)MAX_OWNERS && c->last_nf > 640ull * o) o *= 2;
     const int cap = c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS;
-    return (uint32_t)std::max(1, std::min(c->n_cu, cap));
+    return (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
 }
 
 static int plan_batches(fluere_ctx* c, PassPlan& P) {
@@ -3033,14 +3035,6 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         c->d_stage_bytes = 0;
         if (hipMalloc(&c->d_stage, need_max) != hipSuccess) return FLUERE_E_NOMEM;
         c->d_stage_bytes = need_max;
-    }
-    // merge sub-passes: enough that an owner's share of the flows (the last
-    // run's count as the estimate) fits its 1024-entry LDS table at ~70 %
-    {
-        const uint64_t per_owner = c->last_nf / std::max<uint32_t>(1, merge_owners(c));
-        uint32_t ns = 1;
-        while (ns < 16 && per_owner > 700ull * ns) ns *= 2;
-        a.nsub = ns;
     }
     P.nb = 0;
     for (auto& hb : c->batches) {
@@ -3701,7 +3695,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     HIPCHECK(hipMemcpyAsync(&ctl, c->d_glob, sizeof ctl, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
     Glob g = ctl.g;
-    if (!(ctl.err & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = ctl.n_flows;  // (merge sub-pass estimate)
+    if (!(ctl.err & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = ctl.n_flows;  // (merge owner estimate)
     // 2. their annexes (and the records that open and close in this shard)
     if (g.n_complex) {
         std::vector<Batch> hb(nb);
