@@ -11,7 +11,7 @@ xGMI, and each owner merges / finalizes its own flows (fluere_amd/dist.py).
 Weak scaling: every rank owns a fixed per-GPU shard of one global capture
 (packet-range sharding with global packet indices).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5u]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5u|tcp|tcp_t1|slow]
   torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
 """
 from __future__ import annotations
@@ -47,6 +47,11 @@ CONFIGS = {
     # spans 10 s) the hard-timeout sweep runs for every flow (Mode B)
     "tcp": dict(kind=4, per_gpu=10_000_000, flows=100_000, seed=0xF10E0007, use_mac=False,
                 workload="10M IMIX, realistic TCP (+UDP), 100k concurrent lanes, -t 600000"),
+    # the general parser's classes: every packet takes the slow
+    # list (parsed in k_merge_partials' tail, pre-aggregated per dense id in LDS)
+    "slow": dict(kind=5, per_gpu=10_000_000, flows=10_000, seed=0xF10E0008, use_mac=False,
+                 workload="10M general-parser packets at 128/576/1500 B (IPv6 1/2, VXLAN 1/4, IPv4 options 1/4), "
+                          "10k flows"),
     "tcp_t1": dict(kind=4, per_gpu=10_000_000, flows=100_000, seed=0xF10E0007, use_mac=False, timeout_ms=1000,
                    workload="10M IMIX, realistic TCP (+UDP), 100k concurrent lanes, -t 1000 (expiry sweep)"),
 }

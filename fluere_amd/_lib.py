@@ -32,7 +32,7 @@ _ERR_NAMES = {
     E_STATE: "call order",
 }
 
-SYNTH_UDP64, SYNTH_IMIX, SYNTH_VLAN64, SYNTH_MAC64, SYNTH_TCP = 0, 1, 2, 3, 4
+SYNTH_UDP64, SYNTH_IMIX, SYNTH_VLAN64, SYNTH_MAC64, SYNTH_TCP, SYNTH_SLOW = 0, 1, 2, 3, 4, 5
 
 
 class FluereError(RuntimeError):

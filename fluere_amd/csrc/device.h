@@ -136,15 +136,19 @@ __device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
     return m;
 }
 
-// mode: 0 production (fast path first), 1 general parser only
+// mode: 0 production (fast path first), 1 general parser only.  INL: the
+// general parser inlined (k_slow) instead of called out of line.
+template <bool INL = false>
 __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P);
+template <bool INL = false>
 __device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool macs, int mode, Parsed& P) {
     uint32_t off = B.offs[li];
     Win W;
     load_win(B, off, W);
-    parse_loaded(B, off, W, macs, mode, P);
+    parse_loaded<INL>(B, off, W, macs, mode, P);
 }
 // The record at batch offset off, its window W already loaded.
+template <bool INL>
 __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P) {
     bool sw = B.flags & 1;
     uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
@@ -156,9 +160,13 @@ __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const
     const uint8_t* fr = B.bytes + off + 16;
     bool fast = (mode == 0) && parse_fast(W, L, P.pi);
     if (!fast) {
-        PktInfo g;  // only this copy lives on the stack (parse_general is out of line)
-        parse_general(fr, L, g);
-        P.pi = g;
+        if constexpr (INL) {
+            parse_general_inl(fr, L, P.pi);
+        } else {
+            PktInfo g;  // only this copy lives on the stack (parse_general is out of line)
+            parse_general(fr, L, g);
+            P.pi = g;
+        }
     }
     const PktInfo& pi = P.pi;
     P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;

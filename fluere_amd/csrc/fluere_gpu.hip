@@ -99,8 +99,8 @@ struct Stage {
     // Spilled packets are stored as planes of 16-byte words (word w of every
     // record together), so a wave's loads and stores of one word are contiguous.
     Spill* spill_raw;             // [workgroup][word][WIN_ITERS * BLOCK] this window's spills, arrival order
-    Spill* spill;                 // [word][spill_cap] owner-grouped spills of every set (n_spill cursor)
-    unsigned long long spill_cap; // records per plane of spill (the batch's packet count)
+    Spill* spill;                 // [spill_cap] owner-grouped spills of every set, one 32-B record each (64 B with MACs)
+    unsigned long long spill_cap; // records of spill (the batch's packet count)
     uint32_t* soff;               // [(O + 1) * n_sets]: owner o's spills of set s = spill[sbase[s] + soff[o][s] ..)
     unsigned long long* sbase;    // [set] first spill of the set
     uint4* partx;                 // MAC runs: [set * NS + cell] the partial's MAC words and key hash
@@ -120,8 +120,13 @@ struct AggArgs {
     Acc A;
     Stage S;
     Glob* g;
-    uint32_t* slow;            // packets (batch-local indices) parse_fast did not take
-    unsigned long long* slow_n;
+    uint32_t* slow;            // packets (batch-local indices) the hot parser left to the general parser:
+                               // workgroup b's in slow[b * slow_region, + slow_cnt[b])
+    unsigned long long* slow_n;  // their total (the merge's "any slow packet" test)
+    uint32_t* slow_cnt;
+    uint32_t slow_region;      // packets a hot workgroup can see (its steps x BLOCK)
+    int slow_abl;              // diagnostics only (FLUERE_SLOW_ABL, wrong results): 1 no dictionary, 2 no parse
+    int slow_kernel;           // the slow list is k_slow's (launched behind the merge), not the merge tail's
     int macs;
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
 };
@@ -327,6 +332,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     __shared__ uint32_t s_scnt[OWN_WORDS];  // spilled packets per owner (this window) -> segment starts (packed)
     __shared__ unsigned long long s_sbase;
     __shared__ unsigned long long s_cnt[5], s_tmin, s_tmax;
+    __shared__ uint32_t s_slow;  // this workgroup's slow-list entries
     const int tid = threadIdx.x;
     // MAC kernels: LK / 2 key entries, each with its MAC sidecar at + LK / 2
     constexpr int LKL = MACS ? LK / 2 : LK, LKL_BITS = MACS ? LK_BITS - 1 : LK_BITS;
@@ -340,6 +346,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         s_fl[0][e] = s_fl[1][e] = s_fl[2][e] = s_fl[3][e] = 0;
     }
     if (tid < 5) s_cnt[tid] = 0;
+    if (tid == 0) s_slow = 0;
     if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_nslot = 0; s_chunk = 0; s_nspill = 0; }
     for (int o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
     __syncthreads();
@@ -581,17 +588,19 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 }
             }
             const bool slow = q[u].slow;
-            // slow list: wave-aggregated append (one global atomic per wave)
+            // slow list: wave-aggregated append into this workgroup's region
+            // (an LDS cursor; one global atomic per wave on a single counter
+            // serialised an all-slow capture: 1.9 ms for 10M packets)
             const uint64_t sm = __ballot(slow);
             if (sm) {
                 const uint32_t lead = __builtin_ctzll(sm);
-                unsigned long long b0 = 0;
-                if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(a.slow_n, (unsigned long long)__popcll(sm));
+                uint32_t b0 = 0;
+                if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(&s_slow, (uint32_t)__popcll(sm));
                 b0 = __shfl(b0, lead, 64);
                 if (slow) {
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                    a.slow[b0 + r] = (uint32_t)li[u];
+                    a.slow[(size_t)blockIdx.x * a.slow_region + b0 + r] = (uint32_t)li[u];
                 }
             }
         }
@@ -775,13 +784,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     const u32x4 v0 = av[u][0];
                     const uint32_t hsp = MACS ? av[u][1].w : lt_hash(v0.x, v0.y, v0.z, v0.w);
                     const uint32_t pos = own_add(s_scnt, owner_of(hsp, O));
-                    uint4* dst = reinterpret_cast<uint4*>(S.spill) + sb + pos;
+                    // one record per whole 32-byte sector (64 with MACs): a
+                    // scattered 16-byte plane word cost a sector write of its own
+                    uint4* dst = reinterpret_cast<uint4*>(S.spill) + (sb + pos) * (size_t)(2 * SPU);
 #pragma unroll
                     for (int w = 0; w < SW; w++) {
                         if (FLUERE_SPILL_NT & 1)
-                            __builtin_nontemporal_store(av[u][w], reinterpret_cast<u32x4*>(dst + (size_t)w * S.spill_cap));
+                            __builtin_nontemporal_store(av[u][w], reinterpret_cast<u32x4*>(dst + w));
                         else
-                            dst[(size_t)w * S.spill_cap] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
+                            dst[w] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
                     }
                 }
             }
@@ -995,6 +1006,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         st[5] = clock64() - cyc_start;
         st[6] = cyc_flush;
         st[7] = cyc_wait;
+        a.slow_cnt[blockIdx.x] = s_slow;
+        if (s_slow) atomicAdd(a.slow_n, (unsigned long long)s_slow);
         if (a.dbg) {
             const unsigned long long rt_end = wall_clock64();
             a.dbg[blockIdx.x * 8 + 0] = rt_start;
@@ -1125,7 +1138,111 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     __syncthreads();
     return scratch[wv] + incl - v;
 }
-__device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned long long stride);
+// ---------------------------------------------------------------------------
+// finalize (certified flows -> records; others -> complex)
+// ---------------------------------------------------------------------------
+struct FinArgs {
+    const Batch* bs;
+    int nb;
+    TableSet T;
+    Acc A;
+    Glob* g;
+    fluere_record* out;
+    uint8_t* complex;
+    int macs;
+    uint64_t out_cap;
+    Ctl* host_ctl;   // non-null: the last workgroup writes the run counters to this pinned host copy,
+    uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
+    unsigned long long timeout_us;  // non-zero: skip the flows when expiries can fire (Mode B redoes every flow)
+};
+
+// A flow's order-free aggregate (the accumulators of one dense id).
+struct AccVals {
+    unsigned long long fa, fc, fr, la;
+    uint32_t pk[2];
+    unsigned long long by[2];
+    uint32_t mn[2], mx[2], fl[8];
+};
+
+__device__ __forceinline__ void load_acc(const Acc& A, uint32_t d, AccVals& v) {
+    v.fa = A.fa[d]; v.fc = A.fc[d]; v.fr = A.fr[d]; v.la = A.la[d];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        v.pk[q] = A.pk[q][d];
+        v.by[q] = A.by[q][d];
+        v.mn[q] = A.mn[q][d];
+        v.mx[q] = A.mx[q][d];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) v.fl[q] = A.fl[q][d];
+}
+
+// Certified flow d -> its record; false when d has no record here (TCP flow
+// without a SYN: dropped; complex: marked for the per-flow state machine).
+__device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, const AccVals& v, fluere_record& r,
+                                              bool& cplx, unsigned long long& cplx_pkts) {
+    const unsigned long long fa = v.fa, fc = v.fc, fr = v.fr, la = v.la;
+    if (fc == NONE64) return false;  // TCP flow without any SYN: every packet is dropped (:101-113)
+    bool certified = fc == fa && (fr == NONE64 || fr == la);
+    if (!certified) {
+        a.complex[d] = 1;
+        cplx = true;
+        cplx_pkts = v.pk[0] + v.pk[1];
+        return false;
+    }
+    const bool macs = a.macs != 0;
+    // the first and the last packet: both offsets, then both windows, in flight together
+    const int bp = find_batch(a.bs, a.nb, fc), bq = find_batch(a.bs, a.nb, la);
+    const Batch& BP = a.bs[bp];
+    const Batch& BQ = a.bs[bq];
+    const uint32_t op = BP.offs[fc - BP.first], oq = BQ.offs[la - BQ.first];
+    Win WP, WQ;
+    load_win(BP, op, WP);
+    load_win(BQ, oq, WQ);
+    pin_win(WP);
+    pin_win(WQ);
+    Parsed P;
+    parse_loaded(BP, op, WP, macs, 0, P);
+    const uint8_t cd = canon_dir(P, macs);
+    fill_seed(r, P);
+    Parsed Q;
+    parse_loaded(BQ, oq, WQ, macs, 0, Q);
+    const uint32_t p0 = v.pk[0], p1 = v.pk[1];
+    const unsigned long long b0 = v.by[0], b1 = v.by[1];
+    r.d_pkts = p0 + p1;
+    r.d_octets = b0 + b1;
+    r.out_pkts = cd ? p1 : p0; r.in_pkts = cd ? p0 : p1;
+    r.out_bytes = cd ? b1 : b0; r.in_bytes = cd ? b0 : b1;
+    r.min_pkt = v.mn[0]; r.max_pkt = v.mx[0];
+    r.min_ttl = (uint8_t)v.mn[1]; r.max_ttl = (uint8_t)v.mx[1];
+    for (int q = 0; q < 8; q++) r.cnt[q] = v.fl[q];
+    r.cnt[8] = 0;
+    r.last = Q.t;
+    r.order_key = (fr == la) ? la : NONE64;
+    return true;
+}
+
+__device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluere_record& r, bool& cplx,
+                                             unsigned long long& cplx_pkts) {
+    AccVals v;
+    load_acc(a.A, d, v);
+    return finalize_vals(a, d, v, r, cplx, cplx_pkts);
+}
+
+// emit + complex-flow counters of one wave's flows (every lane of the wave)
+__device__ __forceinline__ void finalize_emit(const FinArgs& a, const fluere_record& r, bool want, bool cplx,
+                                              unsigned long long cplx_pkts) {
+    emit_record_wave(a.g, a.out, a.out_cap, r, want);
+    const uint64_t cm = __ballot(cplx);
+    if (cm) {
+        const unsigned long long pk = wave_sum(cplx_pkts);
+        if ((uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm)) {
+            atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
+            atomicAdd(&a.g->n_complex_pkts, pk);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint4 m_key[MT];
     __shared__ uint4 m_kx[MT];  // MAC runs: the MAC sidecar of each entry (w = 1 once written)
@@ -1264,11 +1381,11 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 part_of_stage(p, base, f);
             } else {
                 const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                const uint4* src = reinterpret_cast<const uint4*>(S.spill) + o;
-                const uint4 v0 = src[0], v1 = src[S.spill_cap];
+                const uint4* src = reinterpret_cast<const uint4*>(S.spill) + o * (size_t)(macs ? 4 : 2);
+                const uint4 v0 = src[0], v1 = src[1];
                 k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
                 if (macs) {  // {key}, {MAC words, hash}, {payload}
-                    const uint4 v2 = src[2 * S.spill_cap];
+                    const uint4 v2 = src[2];
                     x0 = v1.x; x1 = v1.y; x2 = v1.z;
                     h = v1.w;
                     spill_to_part(v2.x, v2.y, v2.z, v2.w, base, f);
@@ -1447,98 +1564,251 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
     if (me == gridDim.x - 1 && tid < 64) reduce_stats();
-    if (n_slow_all)
-        slow_packets(a, (unsigned long long)blockIdx.x * blockDim.x + tid, (unsigned long long)gridDim.x * blockDim.x);
+    if (n_slow_all && !a.slow_kernel) {
+        // The packets the hot kernel left to the general parser (IPv6, IPv4 options,
+        // ARP, VXLAN, VLAN, other IP protocols, short frames, keys without an LDS
+        // slot ...): general parser, dense id from the dictionary, then update_flow's
+        // order-free part pre-aggregated per dense id in this workgroup's LDS entries
+        // (one set of global atomics per flow and workgroup at the end, instead of
+        // ~14 per packet); a packet whose id finds no entry within 32 probes takes the
+        // global atomics directly.  Grid-stride over the device-side count (no host
+        // round trip); runs in the tail of k_merge_partials (one launch fewer per batch).
+        __syncthreads();  // the owner's entries are in the global accumulators: reuse them
+        for (int e = tid; e < MT; e += MB) {
+            m_key[e].x = NONE32;
+            m_pk[0][e] = m_pk[1][e] = 0;
+            m_by[0][e] = m_by[1][e] = 0;
+            m_mn[0][e] = m_mn[1][e] = NONE32;
+            m_mx[0][e] = m_mx[1][e] = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
+            m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
+            m_la[e] = 0;
+        }
+        // the hot workgroups' regions, flattened: exclusive scan of their counts
+        const uint32_t nwg = S.n_wg;  // <= MB
+        const uint32_t cnt = tid < (int)nwg ? a.slow_cnt[tid] : 0u;
+        const uint32_t st0 = block_exclusive_scan(cnt, m_scan);
+        if (tid < (int)nwg) m_start[tid] = st0;
+        __syncthreads();
+        const unsigned long long n = m_scan[MB / 64];
+        unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
+        const unsigned long long stride = (unsigned long long)gridDim.x * MB;
+        for (unsigned long long i = (unsigned long long)blockIdx.x * MB + tid; i < n; i += stride) {
+            uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
+            while (lo_w < hi_w) {
+                const uint32_t mid = (lo_w + hi_w + 1) >> 1;
+                if (m_start[mid] <= i) lo_w = mid;
+                else hi_w = mid - 1;
+            }
+            const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - m_start[lo_w])];
+            if (a.slow_abl == 2) { c_drop += li == NONE32; continue; }
+            Parsed P;
+            parse_record(a.B, li, macs, 1, P);
+            if (P.cls) { c_drop++; continue; }
+            c_valid++;
+            tmin = min(tmin, (unsigned long long)P.t);
+            tmax = max(tmax, (unsigned long long)P.t);
+            uint8_t dir = 0;
+            const uint32_t d = a.slow_abl == 1 ? (P.pi.sip[3] ^ P.pi.dip[3] ^ P.pi.ksp) % 8192u
+                                               : flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
+            if (d == FAIL || d >= a.T.fmax) continue;
+            const unsigned long long gi = a.B.first + li;
+            // single-word keys (the dense id): a CAS claims or finds an entry,
+            // nothing to publish, so the bounded probe needs no other lane
+            uint32_t e = (d * 0x9E3779B1u) >> 22;  // 10 bits: MT == 1024
+            bool in_lds = false;
+            for (int pr = 0; pr < 32; pr++) {
+                const uint32_t k = atomicCAS(&m_key[e].x, NONE32, d);
+                if (k == NONE32 || k == d) { in_lds = true; break; }
+                e = (e + 1) & (MT - 1);
+            }
+            if (!in_lds) { agg_global(a.A, d, dir, P.pi, gi); continue; }
+            const uint32_t tf = P.pi.tflags;
+            atomicAdd(&m_pk[dir][e], 1u);
+            atomicAdd(&m_by[dir][e], (unsigned long long)P.pi.doctets);
+            atomicMin(&m_mn[0][e], (uint32_t)P.pi.rpkt);
+            atomicMax(&m_mx[0][e], (uint32_t)P.pi.rpkt);
+            atomicMin(&m_mn[1][e], (uint32_t)P.pi.rttl);
+            atomicMax(&m_mx[1][e], (uint32_t)P.pi.rttl);
+            if (tf) {
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if ((tf >> q) & 1) atomicAdd(&m_fl[q][e], 1u);
+                if (tf & 5) atomicMin(&m_fr[e], gi);
+            }
+            atomicMin(&m_fa[e], gi);
+            if (P.pi.rprot != 6 || (tf & 2)) atomicMin(&m_fc[e], gi);
+            atomicMax(&m_la[e], gi + 1);
+        }
+        __syncthreads();
+        for (int e = tid; e < MT; e += MB) {
+            const uint32_t d = m_key[e].x;
+            if (d == NONE32) continue;
+            FlowPart f;
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                f.pk[q] = m_pk[q][e];
+                f.by[q] = m_by[q][e];
+                f.mn[q] = m_mn[q][e];
+                f.mx[q] = m_mx[q][e];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) f.fl[q] = m_fl[q][e];
+            f.fa = m_fa[e];
+            f.fc = m_fc[e];
+            f.fr = m_fr[e];
+            f.la = m_la[e];
+            part_to_global(a.A, d, f);
+        }
+        // run counters: one set of atomics per wave
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            c_valid += __shfl_xor(c_valid, o, 64);
+            c_drop += __shfl_xor(c_drop, o, 64);
+            tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, o, 64));
+            tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, o, 64));
+        }
+        if ((tid & 63) == 0) {
+            if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
+            if (c_drop) atomicAdd(&a.g->dropped, c_drop);
+        }
+    }
 }
 
-// The packets the hot kernel left to the general parser (IPv6, IPv4 options,
-// ARP, VXLAN, VLAN, other IP protocols, short frames, keys without an LDS
-// slot ...): general parser + direct global aggregation.  Grid-stride over
-// the device-side count, so no host round trip; runs in the tail of
-// k_merge_partials (one launch fewer per batch).
-__device__ void slow_packets(const AggArgs& a, unsigned long long i0, unsigned long long stride) {
-    const unsigned long long n = *a.slow_n;
+// ---------------------------------------------------------------------------
+// k_slow: the slow list when the last run had one (the host predicts it;
+// otherwise k_merge_partials' tail takes it).  The general parser inlined
+// (out of line, every packet saved and restored the callee's registers
+// through scratch: ~2.5 KB of scratch traffic per packet), the dictionary,
+// then update_flow's order-free part pre-aggregated per dense id in LDS
+// (ST entries per workgroup, 8 probes; else the global atomics).
+// ---------------------------------------------------------------------------
+constexpr int SB = 256;  // k_slow block
+constexpr int ST = 256;  // k_slow LDS entries
+__global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
+    __shared__ uint32_t s_key[ST], s_pk[2][ST], s_mn[2][ST], s_mx[2][ST], s_fl[8][ST];
+    __shared__ unsigned long long s_by[2][ST], s_fa[ST], s_fc[ST], s_fr[ST], s_la[ST];
+    __shared__ uint32_t s_start[MB + 1];
+    const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!n_slow_all) return;  // uniform
+    const int tid = threadIdx.x;
     const bool macs = a.macs != 0;
+    for (int e = tid; e < ST; e += SB) {
+        s_key[e] = NONE32;
+        s_pk[0][e] = s_pk[1][e] = 0;
+        s_by[0][e] = s_by[1][e] = 0;
+        s_mn[0][e] = s_mn[1][e] = NONE32;
+        s_mx[0][e] = s_mx[1][e] = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) s_fl[q][e] = 0;
+        s_fa[e] = s_fc[e] = s_fr[e] = NONE64;
+        s_la[e] = 0;
+    }
+    // the hot workgroups' regions, flattened (wave 0: an exclusive scan, an
+    // even run of regions per lane)
+    const uint32_t nwg = a.S.n_wg;  // <= MB
+    if (tid < 64) {
+        const uint32_t per = (nwg + 63) / 64;
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t w = tid * per + q;
+            if (w < nwg) sum += a.slow_cnt[w];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int dlt = 1; dlt < 64; dlt <<= 1) {
+            const uint32_t y = __shfl_up(incl, dlt, 64);
+            if (tid >= dlt) incl += y;
+        }
+        uint32_t run = incl - sum;
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t w = tid * per + q;
+            if (w < nwg) {
+                s_start[w] = run;
+                run += a.slow_cnt[w];
+            }
+        }
+        if (tid == 63) s_start[MB] = incl;
+    }
+    __syncthreads();
+    const unsigned long long n = s_start[MB];
     unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
-    for (unsigned long long i = i0; i < n; i += stride) {
-        const uint64_t li = a.slow[i];
+    const unsigned long long stride = (unsigned long long)gridDim.x * SB;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * SB + tid; i < n; i += stride) {
+        uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
+        while (lo_w < hi_w) {
+            const uint32_t mid = (lo_w + hi_w + 1) >> 1;
+            if (s_start[mid] <= i) lo_w = mid;
+            else hi_w = mid - 1;
+        }
+        const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - s_start[lo_w])];
         Parsed P;
-        parse_record(a.B, li, macs, 1, P);
+        parse_record<true>(a.B, li, macs, 1, P);
         if (P.cls) { c_drop++; continue; }
         c_valid++;
         tmin = min(tmin, (unsigned long long)P.t);
         tmax = max(tmax, (unsigned long long)P.t);
         uint8_t dir;
-        uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
+        const uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
         if (d == FAIL || d >= a.T.fmax) continue;
-        agg_global(a.A, d, dir, P.pi, a.B.first + li);
+        const unsigned long long gi = a.B.first + li;
+        uint32_t e = (d * 0x9E3779B1u) >> 24;  // 8 bits: ST == 256
+        bool in_lds = false;
+        for (int pr = 0; pr < 8; pr++) {
+            const uint32_t k = atomicCAS(&s_key[e], NONE32, d);
+            if (k == NONE32 || k == d) { in_lds = true; break; }
+            e = (e + 1) & (ST - 1);
+        }
+        if (!in_lds) { agg_global(a.A, d, dir, P.pi, gi); continue; }
+        const uint32_t tf = P.pi.tflags;
+        atomicAdd(&s_pk[dir][e], 1u);
+        atomicAdd(&s_by[dir][e], (unsigned long long)P.pi.doctets);
+        atomicMin(&s_mn[0][e], (uint32_t)P.pi.rpkt);
+        atomicMax(&s_mx[0][e], (uint32_t)P.pi.rpkt);
+        atomicMin(&s_mn[1][e], (uint32_t)P.pi.rttl);
+        atomicMax(&s_mx[1][e], (uint32_t)P.pi.rttl);
+        if (tf) {
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if ((tf >> q) & 1) atomicAdd(&s_fl[q][e], 1u);
+            if (tf & 5) atomicMin(&s_fr[e], gi);
+        }
+        atomicMin(&s_fa[e], gi);
+        if (P.pi.rprot != 6 || (tf & 2)) atomicMin(&s_fc[e], gi);
+        atomicMax(&s_la[e], gi + 1);
     }
-    if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
-    if (c_drop) atomicAdd(&a.g->dropped, c_drop);
-}
-
-// ---------------------------------------------------------------------------
-// finalize (certified flows -> records; others -> complex)
-// ---------------------------------------------------------------------------
-struct FinArgs {
-    const Batch* bs;
-    int nb;
-    TableSet T;
-    Acc A;
-    Glob* g;
-    fluere_record* out;
-    uint8_t* complex;
-    int macs;
-    uint64_t out_cap;
-    Ctl* host_ctl;   // non-null: the last workgroup writes the run counters to this pinned host copy,
-    uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
-    unsigned long long timeout_us;  // non-zero: skip the flows when expiries can fire (Mode B redoes every flow)
-};
-
-// Certified flow d -> its record; false when d has no record here (TCP flow
-// without a SYN: dropped; complex: marked for the per-flow state machine).
-__device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluere_record& r, bool& cplx,
-                                             unsigned long long& cplx_pkts) {
-    const Acc& A = a.A;
-    unsigned long long fa = A.fa[d], fc = A.fc[d], fr = A.fr[d], la = A.la[d];
-    if (fc == NONE64) return false;  // TCP flow without any SYN: every packet is dropped (:101-113)
-    bool certified = fc == fa && (fr == NONE64 || fr == la);
-    if (!certified) {
-        a.complex[d] = 1;
-        cplx = true;
-        cplx_pkts = A.pk[0][d] + A.pk[1][d];
-        return false;
+    __syncthreads();
+    for (int e = tid; e < ST; e += SB) {
+        const uint32_t d = s_key[e];
+        if (d == NONE32) continue;
+        FlowPart f;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            f.pk[q] = s_pk[q][e];
+            f.by[q] = s_by[q][e];
+            f.mn[q] = s_mn[q][e];
+            f.mx[q] = s_mx[q][e];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) f.fl[q] = s_fl[q][e];
+        f.fa = s_fa[e];
+        f.fc = s_fc[e];
+        f.fr = s_fr[e];
+        f.la = s_la[e];
+        part_to_global(a.A, d, f);
     }
-    const bool macs = a.macs != 0;
-    // the first and the last packet: both offsets, then both windows, in flight together
-    const int bp = find_batch(a.bs, a.nb, fc), bq = find_batch(a.bs, a.nb, la);
-    const Batch& BP = a.bs[bp];
-    const Batch& BQ = a.bs[bq];
-    const uint32_t op = BP.offs[fc - BP.first], oq = BQ.offs[la - BQ.first];
-    Win WP, WQ;
-    load_win(BP, op, WP);
-    load_win(BQ, oq, WQ);
-    pin_win(WP);
-    pin_win(WQ);
-    Parsed P;
-    parse_loaded(BP, op, WP, macs, 0, P);
-    const uint8_t cd = canon_dir(P, macs);
-    fill_seed(r, P);
-    Parsed Q;
-    parse_loaded(BQ, oq, WQ, macs, 0, Q);
-    uint32_t p0 = A.pk[0][d], p1 = A.pk[1][d];
-    unsigned long long b0 = A.by[0][d], b1 = A.by[1][d];
-    r.d_pkts = p0 + p1;
-    r.d_octets = b0 + b1;
-    r.out_pkts = cd ? p1 : p0; r.in_pkts = cd ? p0 : p1;
-    r.out_bytes = cd ? b1 : b0; r.in_bytes = cd ? b0 : b1;
-    r.min_pkt = A.mn[0][d]; r.max_pkt = A.mx[0][d];
-    r.min_ttl = (uint8_t)A.mn[1][d]; r.max_ttl = (uint8_t)A.mx[1][d];
-    for (int q = 0; q < 8; q++) r.cnt[q] = A.fl[q][d];
-    r.cnt[8] = 0;
-    r.last = Q.t;
-    r.order_key = (fr == la) ? la : NONE64;
-    return true;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        c_valid += __shfl_xor(c_valid, o, 64);
+        c_drop += __shfl_xor(c_drop, o, 64);
+        tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, o, 64));
+        tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, o, 64));
+    }
+    if ((tid & 63) == 0) {
+        if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
+        if (c_drop) atomicAdd(&a.g->dropped, c_drop);
+    }
 }
 
 // one thread per flow, grid-stride (uniform per workgroup) over the
@@ -1579,15 +1849,7 @@ __global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
         bool cplx = false;
         unsigned long long cplx_pkts = 0;
         const bool want = d < nf && finalize_one(a, d, r, cplx, cplx_pkts);
-        emit_record_wave(a.g, a.out, a.out_cap, r, want);
-        const uint64_t cm = __ballot(cplx);
-        if (cm) {
-            const unsigned long long pk = wave_sum(cplx_pkts);
-            if ((uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm)) {
-                atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
-                atomicAdd(&a.g->n_complex_pkts, pk);
-            }
-        }
+        finalize_emit(a, r, want, cplx, cplx_pkts);
     }
     if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
 }
@@ -1952,7 +2214,7 @@ __global__ void __launch_bounds__(256) k_export_owners(ExportArgs a) {
         const uint32_t o = key_owner(s.key, a.n_owners);
         fluere_shard_header* h = blk_hdr(a.blocks, a.block_bytes, o);
         const unsigned long long pos = atomicAdd(reinterpret_cast<unsigned long long*>(&h->n_flows), 1ull);
-        const uint32_t ax = a.annex_of[d];
+        const uint32_t ax = a.annex ? a.annex_of[d] : NONE32;  // (no annexes yet: a speculative export)
         if (ax != NONE32) {
             const unsigned long long apos = atomicAdd(reinterpret_cast<unsigned long long*>(&h->n_annex), 1ull);
             if (apos < a.cap_annex) {
@@ -2369,6 +2631,7 @@ struct fluere_ctx {
     hipEvent_t evk_first = nullptr;             // before the first k_parse_agg launch of the pass
     hipEvent_t ev_ctl = nullptr;                // after a run's counter copy (the speculative cleanup follows)
     uint64_t last_nf = 0;                       // flows of the last completed run (sizing only)
+    uint64_t last_n_slow = 0;                   // slow-list packets of the last run (k_slow prediction)
     bool pass_in_run = false;
     bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
     uint32_t run_seq = 0;                       // number of the last run that publishes its counters (Ctl::seq)
@@ -2447,7 +2710,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     auto fail = [&](int r) { rc = r; fluere_close(c); return r; };
     if (hipSetDevice(c->device) != hipSuccess) return fail(FLUERE_E_HIP);
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = std::min(prop.multiProcessorCount, MB);  // (slow-list regions: one per hot workgroup, <= MB)
     if (o->stream) c->stream = (hipStream_t)o->stream;
     else {
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLUERE_E_HIP);
@@ -3002,16 +3265,37 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     a.A = c->acc;
     a.g = c->d_glob;
     a.macs = c->use_mac;
+    // slow list: one region per hot workgroup (its steps x BLOCK packets),
+    // then the per-workgroup counts
+    auto hot_shape = [&](uint64_t n, unsigned& grid, uint64_t& steps) {
+        const uint64_t want = (n + BLOCK * 8 - 1) / (BLOCK * 8);
+        grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
+        const uint64_t per = (n + grid - 1) / grid;
+        steps = (per + BLOCK - 1) / BLOCK;
+    };
     uint64_t maxn = 1;
-    for (auto& hb : c->batches) maxn = std::max<uint64_t>(maxn, hb.b.n);
-    if (maxn > c->d_slow_cap) {
+    for (auto& hb : c->batches) {
+        if (!hb.b.n) continue;
+        unsigned grid;
+        uint64_t steps;
+        hot_shape(hb.b.n, grid, steps);
+        maxn = std::max<uint64_t>(maxn, (uint64_t)grid * steps * BLOCK);
+    }
+    const uint64_t slow_words = maxn + MB;
+    if (slow_words > c->d_slow_cap) {
         hipFree(c->d_slow);
         c->d_slow = nullptr;
-        if (hipMalloc(&c->d_slow, maxn * 4) != hipSuccess) return FLUERE_E_NOMEM;
-        c->d_slow_cap = maxn;
+        if (hipMalloc(&c->d_slow, slow_words * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_slow_cap = slow_words;
     }
     a.slow = c->d_slow;
+    a.slow_cnt = c->d_slow + maxn;
     a.slow_n = &c->d_glob->n_slow;
+    a.slow_abl = getenv("FLUERE_SLOW_ABL") ? atoi(getenv("FLUERE_SLOW_ABL")) : 0;
+    // k_slow when the last run had slow packets (a wrong guess costs only the
+    // merge tail's slower path, or an empty launch)
+    static const int slow_env = getenv("FLUERE_SLOW_KERNEL") ? atoi(getenv("FLUERE_SLOW_KERNEL")) : -1;
+    a.slow_kernel = slow_env >= 0 ? slow_env : (c->last_n_slow > 0 ? 1 : 0);
     if (getenv("FLUERE_DEBUG")) {
         if (!g_hot_dbg && hipMalloc(&g_hot_dbg, 4096 * 8 * 8) != hipSuccess) g_hot_dbg = nullptr;
         a.dbg = g_hot_dbg;
@@ -3048,13 +3332,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = merge_owners(c);
+        a.slow_region = (uint32_t)(steps * BLOCK);
         Stage& S = a.S;
         // layout (16-byte aligned pieces): parts | spill_raw | spill | sbase | base | off | soff
         S.part = (Part*)c->d_stage;
         S.spill_raw = (Spill*)(S.part + cells);
         S.spill = S.spill_raw + (size_t)grid * SPILL_WG * spill_units(c->use_mac);
         S.sbase = (unsigned long long*)(S.spill + hb.b.n * spill_units(c->use_mac));
-        S.spill_cap = hb.b.n;  // planes of 16-byte words: 2 (4 with MACs) per Spill unit
+        S.spill_cap = hb.b.n;  // records (32 B, or 64 B with MACs)
         S.base = S.sbase + sets;
         S.off = (uint32_t*)(S.base + sets);
         S.soff = S.off + (size_t)(O + 1) * sets;
@@ -3127,9 +3412,18 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         // the hot kernel): separate event markers would each add a gap to the
         // stream.  The first batch of a multi-batch pass starts evk_first.
         void* args[] = {const_cast<AggArgs*>(&a)};
+        static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, (i == 0 && P.nb > 1) ? c->evk_first : c->evk0,
                                     c->evk1, 0));
-        k_merge_partials<<<P.owners[i], MB, 0, s>>>(a);  // + the slow list
+        const auto t1 = std::chrono::steady_clock::now();
+        k_merge_partials<<<P.owners[i], MB, 0, s>>>(a);  // + the slow list (unless k_slow takes it)
+        if (a.slow_kernel) k_slow<<<(unsigned)c->n_cu * 8, SB, 0, s>>>(a);
+        if (hostprof) {
+            const auto t2 = std::chrono::steady_clock::now();
+            auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
+            fprintf(stderr, "[fluere] launch: hot %.1f merge %.1f us\n", us(t0, t1), us(t1, t2));
+        }
     }
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
@@ -3208,6 +3502,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
         kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
         event(c->evk1);
         kernel((const void*)k_merge_partials, P.owners[i], MB, a_agg[i]);
+        if (P.agg[i].slow_kernel) kernel((const void*)k_slow, (unsigned)c->n_cu * 8, SB, a_agg[i]);
     }
     void* a_fin[] = {&P.fa};
     if (P.finalize) {
@@ -3373,6 +3668,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     PassPlan P;
     if ((rc = plan_pass(c, P, true))) return rc;
     c->plan_nb = P.nb;
+    const auto t_plan = std::chrono::steady_clock::now();
     // hipGraph replay is opt-in (FLUERE_GRAPH=1): measured on MI355X / ROCm 7.2
     // it is slower than these few direct launches (C2 step 0.264 vs 0.257 ms)
     static const bool want_graph = getenv("FLUERE_GRAPH") != nullptr && getenv("FLUERE_DEBUG") == nullptr;
@@ -3438,6 +3734,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     // the run needs no more device work (the same test, on the same counters)
     const bool spec_cleared = P.spec && run_complete(g, nf_err[1], P.spec_ca.timeout_us, P.spec_ca.recs_cap);
     if (!(nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = nf_err[0];
+    c->last_n_slow = g.n_slow;
     debug_counters(c, &g);
     FinArgs fa = P.fa;
     fa.host_ctl = nullptr;  // re-launches below read the counters back with copies
@@ -3577,8 +3874,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         static auto t_prev_exit = std::chrono::steady_clock::now();
         const auto t_exit = std::chrono::steady_clock::now();
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        fprintf(stderr, "[fluere] host: since last exit %.1f | plan+enqueue %.1f | sync wait %.1f | after sync %.1f us\n",
-                us(t_prev_exit, t_run0), us(t_run0, t_enq), us(t_enq, t_sync), us(t_sync, t_exit));
+        fprintf(stderr, "[fluere] host: since last exit %.1f | plan %.1f enqueue %.1f | sync wait %.1f | after sync %.1f us\n",
+                us(t_prev_exit, t_run0), us(t_run0, t_plan), us(t_plan, t_enq), us(t_enq, t_sync), us(t_sync, t_exit));
         t_prev_exit = t_exit;
     }
     return FLUERE_OK;
@@ -3604,7 +3901,7 @@ extern "C" void fluere_records_free(fluere_record* r) { free(r); }
 // ---------------------------------------------------------------------------
 extern "C" uint64_t fluere_synth_range_bytes(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n) {
     if (!cfg) return 0;
-    if (cfg->kind != FLUERE_SYNTH_IMIX && cfg->kind != FLUERE_SYNTH_TCP) return n * 80;
+    if (cfg->kind != FLUERE_SYNTH_IMIX && cfg->kind != FLUERE_SYNTH_TCP && cfg->kind != FLUERE_SYNTH_SLOW) return n * 80;
     uint64_t s = 0;
     for (uint64_t i = first; i < first + n; i++) s += 16 + synth::frame_len(*cfg, i);
     return s;
@@ -3691,12 +3988,31 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     // 1. flows whose part of the state machine depends on packet order here
     reset_record_counters(c);
     k_local_cert<<<flow_grid(c), 256, 0, s>>>(fa, c->d_annex_of);
-    Ctl ctl;
-    HIPCHECK(hipMemcpyAsync(&ctl, c->d_glob, sizeof ctl, hipMemcpyDeviceToHost, s));
+    // 3. summaries (+ annexes) into the owners' blocks, enqueued behind it
+    //    speculatively: with no order-dependent flow (the common case) the
+    //    export needs ONE host round trip
+    ExportArgs ea{fa, (uint8_t*)d_blocks, n_owners, shard, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
+                  c->d_annex_of, (const fluere_flow_annex*)c->d_annex};
+    auto enqueue_export = [&](bool annexes) -> int {
+        ea.annex = annexes ? (const fluere_flow_annex*)c->d_annex : nullptr;
+        k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
+        k_export_owners<<<flow_grid(c), 256, 0, s>>>(ea);
+        k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need);
+        HIPCHECK(hipGetLastError());
+        return FLUERE_OK;
+    };
+    if ((rc = enqueue_export(false))) return rc;
+    struct {
+        Ctl ctl;
+        unsigned long long nd[2];
+    } back;
+    HIPCHECK(hipMemcpyAsync(&back.ctl, c->d_glob, sizeof back.ctl, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(back.nd, c->d_need, 16, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
-    Glob g = ctl.g;
-    if (!(ctl.err & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = ctl.n_flows;  // (merge owner estimate)
-    // 2. their annexes (and the records that open and close in this shard)
+    Glob g = back.ctl.g;
+    if (!(back.ctl.err & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = back.ctl.n_flows;  // (merge owner estimate)
+    // 2. order-dependent flows: their annexes (and the records that open and
+    //    close in this shard) from the exact state machine, then the export again
     if (g.n_complex) {
         std::vector<Batch> hb(nb);
         for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
@@ -3705,20 +4021,13 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
                    1, &c->d_annex, &c->d_annex_cap, c->d_annex_of};
         ExactResult er{};
         if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
+        if ((rc = enqueue_export(true))) return rc;
         HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipMemcpyAsync(back.nd, c->d_need, 16, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
     }
-    // 3. summaries + annexes into the owners' blocks
-    ExportArgs ea{fa, (uint8_t*)d_blocks, n_owners, shard, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
-                  c->d_annex_of, (const fluere_flow_annex*)c->d_annex};
-    k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
-    k_export_owners<<<flow_grid(c), 256, 0, s>>>(ea);
-    k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need);
-    HIPCHECK(hipGetLastError());
-    unsigned long long nd[2];
-    HIPCHECK(hipMemcpyAsync(nd, c->d_need, 16, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    if (need) *need = nd[0];
-    if (need_annex) *need_annex = nd[1];
+    if (need) *need = back.nd[0];
+    if (need_annex) *need_annex = back.nd[1];
     // the final records this shard produced (kept through the merge)
     c->local_n_rec = g.n_rec;
     c->local_updates = g.n_updates;

@@ -421,7 +421,10 @@ __device__ __forceinline__ uint8_t vlan_keys(const G& g, Span v, PktInfo& o) {
     return ST_UNKNOWN_ETHER;
 }
 
-__device__ __attribute__((noinline)) void parse_general(const uint8_t* d, uint32_t L, PktInfo& o) {
+// The general parser, inlined into its caller: k_slow, where every packet
+// takes it (an out-of-line call saves and restores the callee's registers
+// through scratch on every packet).
+__device__ __forceinline__ void parse_general_inl(const uint8_t* d, uint32_t L, PktInfo& o) {
     G g{d};
     o.kst = ST_OK; o.fst = ST_OK;
     o.v6 = 0; o.rv6 = 0; o.kproto = 0; o.ksp = o.kdp = 0;
@@ -558,6 +561,12 @@ __device__ __attribute__((noinline)) void parse_general(const uint8_t* d, uint32
         o.rsp = h.sport; o.rdp = h.dport;
         o.rpkt = h.length; o.rttl = 0; o.rprot = h.proto; o.rtos = 0; o.tflags = 0;
     }
+}
+
+// Out of line for every other caller (one copy, no register pressure in the
+// kernels whose packets rarely need it).
+__device__ __attribute__((noinline)) void parse_general(const uint8_t* d, uint32_t L, PktInfo& o) {
+    parse_general_inl(d, L, o);
 }
 
 }  // namespace fl

@@ -48,7 +48,7 @@ FL_HD Flow flow(const fluere_synth_cfg& c, uint32_t f) {
     F.b_port = pick_port(rnd(c.seed, 5, f));
     F.proto = 17;
     F.closer = 0;
-    if (c.kind == FLUERE_SYNTH_IMIX) {
+    if (c.kind == FLUERE_SYNTH_IMIX || c.kind == FLUERE_SYNTH_SLOW) {
         F.proto = (rnd(c.seed, 6, f) & 1) ? 6 : 17;
         if (F.proto == 6) {
             uint32_t r = (uint32_t)(rnd(c.seed, 15, f) % 100);
@@ -67,9 +67,9 @@ FL_HD Flow flow(const fluere_synth_cfg& c, uint32_t f) {
 
 // Frame length of packet i (bytes on the wire, == caplen == orig_len).
 FL_HD uint32_t frame_len(const fluere_synth_cfg& c, uint64_t i) {
-    if (c.kind != FLUERE_SYNTH_IMIX && c.kind != FLUERE_SYNTH_TCP) return 64;
+    if (c.kind != FLUERE_SYNTH_IMIX && c.kind != FLUERE_SYNTH_TCP && c.kind != FLUERE_SYNTH_SLOW) return 64;
     uint32_t r = (uint32_t)(rnd(c.seed, 14, i) % 12);
-    return r < 7 ? 64 : (r < 11 ? 576 : 1500);
+    return r < 7 ? (c.kind == FLUERE_SYNTH_SLOW ? 128 : 64) : (r < 11 ? 576 : 1500);
 }
 
 // Schedule: which flow packet i belongs to, its direction and TCP flags.
@@ -84,7 +84,7 @@ FL_HD Slot slot(const fluere_synth_cfg& c, uint64_t i) {
     uint64_t F = c.n_flows ? c.n_flows : 1;
     s.rev = (uint8_t)((rnd(c.seed, 2, i) % 100) < c.rev_pct);
     s.tcp_flags = (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0));  // ACK (+PSH)
-    if (c.kind == FLUERE_SYNTH_IMIX && c.n_packets >= 2 * F) {
+    if ((c.kind == FLUERE_SYNTH_IMIX || c.kind == FLUERE_SYNTH_SLOW) && c.n_packets >= 2 * F) {
         // [0, F): opening packet of flow i (forward; SYN for TCP)
         // [N-F, N): one packet per flow; TCP closers send FIN+ACK / RST here
         // otherwise: random flow, ACK (+PSH) for TCP
@@ -137,6 +137,7 @@ struct Pkt {
     uint16_t a_port, b_port;
     uint8_t proto, rev, tflags;
     uint8_t a_mac[6], b_mac[6];
+    uint8_t cls;                // FLUERE_SYNTH_SLOW: 0 IPv4, 1 IPv6, 2 VXLAN, 3 IPv4 with options
 };
 
 FL_HD void lane_macs(const fluere_synth_cfg& c, uint64_t l, Pkt& p) {
@@ -151,6 +152,7 @@ FL_HD void lane_macs(const fluere_synth_cfg& c, uint64_t l, Pkt& p) {
 
 FL_HD Pkt tcp_real(const fluere_synth_cfg& c, uint64_t i) {
     Pkt p;
+    p.cls = 0;
     const uint64_t L = c.n_flows ? c.n_flows : 1;
     const uint64_t l = i % L, j = i / L;
     const uint64_t E = L / 64;
@@ -215,6 +217,11 @@ FL_HD Pkt pkt(const fluere_synth_cfg& c, uint64_t i) {
         tflags = F.closer == 1 ? 0x11 : (F.closer == 2 ? 0x04 : (uint8_t)(0x10 | ((rnd(c.seed, 16, i) & 1) ? 0x08 : 0)));
     p.a_ip = F.a_ip; p.b_ip = F.b_ip; p.a_port = F.a_port; p.b_port = F.b_port;
     p.proto = F.proto; p.rev = s.rev; p.tflags = tflags;
+    p.cls = 0;
+    if (c.kind == FLUERE_SYNTH_SLOW) {
+        const uint32_t r = (uint32_t)(rnd(c.seed, 30, s.f) & 3);
+        p.cls = r < 2 ? 1 : (uint8_t)r;
+    }
     for (int k = 0; k < 6; k++) { p.a_mac[k] = F.a_mac[k]; p.b_mac[k] = F.b_mac[k]; }
     return p;
 }
@@ -222,7 +229,8 @@ FL_HD Pkt pkt(const fluere_synth_cfg& c, uint64_t i) {
 // Writes the 16-byte pcap record header and the frame of packet i at dst.
 // Returns bytes written (16 + frame_len).
 FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst) {
-    uint32_t L = frame_len(c, i);
+    const uint32_t L0 = frame_len(c, i);
+    uint32_t L = L0;
     put32le(dst + 0, kT0 + (uint32_t)(i / 1000000u));
     put32le(dst + 4, (uint32_t)(i % 1000000u));
     put32le(dst + 8, L);
@@ -241,26 +249,76 @@ FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst)
         put16(e + 14, (uint32_t)(rnd(c.seed, 17, P.a_ip & 0x7FFFFFu) & 0x0FFF));
         o = 16;
     }
-    put16(e + o, 0x0800);
-    uint8_t* ip = e + o + 2;
-    uint32_t iplen = L - (o + 2);
     uint32_t dsel = (uint32_t)(rnd(c.seed, 10, i) & 3);  // DSCP 0, 10, 46, 1 (1 is unmapped -> tos 0)
-    ip[0] = 0x45;
-    ip[1] = (uint8_t)((dsel == 0 ? 0 : dsel == 1 ? 10 : dsel == 2 ? 46 : 1) << 2);
-    put16(ip + 2, iplen);
-    put16(ip + 4, (uint32_t)(rnd(c.seed, 11, i) & 0xFFFF));
-    put16(ip + 6, 0x4000);  // DF
-    ip[8] = (uint8_t)(32 + rnd(c.seed, 9, i) % 97);
-    ip[9] = P.proto;
-    put16(ip + 10, 0);
-    put32(ip + 12, sip);
-    put32(ip + 16, dip);
-    uint32_t sum = 0;
-    for (int k = 0; k < 20; k += 2) sum += ((uint32_t)ip[k] << 8) | ip[k + 1];
-    while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
-    put16(ip + 10, ~sum & 0xFFFF);
-    uint8_t* l4 = ip + 20;
-    uint32_t l4len = iplen - 20, hl;
+    const uint32_t dscp = dsel == 0 ? 0 : dsel == 1 ? 10 : dsel == 2 ? 46 : 1;
+    const uint8_t ttl = (uint8_t)(32 + rnd(c.seed, 9, i) % 97);
+    if (P.cls == 2) {  // VXLAN: outer IPv4/UDP between two tunnel endpoints, then the inner frame
+        put16(e + o, 0x0800);
+        uint8_t* ip = e + o + 2;
+        const uint32_t iplen = L - (o + 2);
+        ip[0] = 0x45; ip[1] = 0;
+        put16(ip + 2, iplen);
+        put16(ip + 4, (uint32_t)(rnd(c.seed, 26, i) & 0xFFFF));
+        put16(ip + 6, 0x4000);
+        ip[8] = 64; ip[9] = 17;
+        put16(ip + 10, 0);
+        put32(ip + 12, 0xC0A80001u);  // 192.168.0.1 -> 192.168.0.2
+        put32(ip + 16, 0xC0A80002u);
+        uint32_t sum = 0;
+        for (int k = 0; k < 20; k += 2) sum += ((uint32_t)ip[k] << 8) | ip[k + 1];
+        while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+        put16(ip + 10, ~sum & 0xFFFF);
+        uint8_t* u = ip + 20;
+        put16(u, 49152 + (uint32_t)(rnd(c.seed, 27, i) & 0x3FFF));
+        put16(u + 2, 4789);
+        put16(u + 4, iplen - 20);
+        put16(u + 6, 0);
+        const uint8_t vx[8] = {0x08, 0, 0, 0, 0, 0, 0x64, 0};  // the VXLAN header keys.rs:23 matches (VNI 100)
+        for (int k = 0; k < 8; k++) u[8 + k] = vx[k];
+        e = u + 16;  // inner Ethernet frame
+        for (int k = 0; k < 6; k++) { e[k] = dmac[k]; e[6 + k] = smac[k]; }
+        L = L - (uint32_t)(e - (dst + 16));  // inner frame length
+    }
+    uint8_t* l4;
+    uint32_t l4len, hl;
+    if (P.cls == 1) {  // IPv6: fd00::<v4 address> endpoints
+        put16(e + o, 0x86DD);
+        uint8_t* ip = e + o + 2;
+        const uint32_t plen6 = L - (o + 2) - 40;
+        put32(ip, 0x60000000u | (dscp << 22) | (uint32_t)(rnd(c.seed, 11, i) & 0xFFFFF));
+        put16(ip + 4, plen6);
+        ip[6] = P.proto;
+        ip[7] = ttl;
+        for (int h = 0; h < 2; h++) {
+            uint8_t* a = ip + 8 + 16 * h;
+            for (int k = 0; k < 16; k++) a[k] = 0;
+            a[0] = 0xFD;
+            put32(a + 12, h ? dip : sip);
+        }
+        l4 = ip + 40;
+        l4len = plen6;
+    } else {  // IPv4 (cls 3: one 4-byte option word, ihl 6)
+        put16(e + o, 0x0800);
+        uint8_t* ip = e + o + 2;
+        const uint32_t iplen = L - (o + 2), ihl = P.cls == 3 ? 6 : 5;
+        ip[0] = (uint8_t)(0x40 | ihl);
+        ip[1] = (uint8_t)(dscp << 2);
+        put16(ip + 2, iplen);
+        put16(ip + 4, (uint32_t)(rnd(c.seed, 11, i) & 0xFFFF));
+        put16(ip + 6, 0x4000);  // DF
+        ip[8] = ttl;
+        ip[9] = P.proto;
+        put16(ip + 10, 0);
+        put32(ip + 12, sip);
+        put32(ip + 16, dip);
+        if (ihl == 6) put32(ip + 20, 0x01010100u);  // NOP NOP NOP EOL
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < 4 * ihl; k += 2) sum += ((uint32_t)ip[k] << 8) | ip[k + 1];
+        while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+        put16(ip + 10, ~sum & 0xFFFF);
+        l4 = ip + 4 * ihl;
+        l4len = iplen - 4 * ihl;
+    }
     put16(l4, sp);
     put16(l4 + 2, dp);
     if (P.proto == 6) {
@@ -285,7 +343,7 @@ FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst)
         for (uint32_t b = 0; b < 8 && k + b < plen; b++) pay[k + b] = (uint8_t)(w >> (8 * b));
     }
     if (plen && pay[0] == 0x08) pay[0] = 0x09;  // never a VXLAN prefix
-    return 16 + L;
+    return 16 + L0;
 }
 
 }  // namespace synth

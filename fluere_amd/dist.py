@@ -75,7 +75,7 @@ class ShardExchange:
     torch.cuda.current_stream().cuda_stream)) so the collective is ordered
     after the export."""
 
-    def __init__(self, ctx, cap: int = 1024, cap_annex: int = 256, group=None):
+    def __init__(self, ctx, cap: int = 64, cap_annex: int = 16, group=None):
         self.ctx, self.group = ctx, group
         self.cap, self.cap_annex = max(1, int(cap)), max(1, int(cap_annex))
         self._send = self._recv = None

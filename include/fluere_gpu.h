@@ -366,8 +366,10 @@ enum {
     FLUERE_SYNTH_IMIX = 1,      /* 64/576/1500 (7:4:1), TCP+UDP, SYN first, FIN/RST last */
     FLUERE_SYNTH_VLAN64 = 2,    /* 802.1Q-tagged 64-B IPv4/UDP, MAC pairs */
     FLUERE_SYNTH_MAC64 = 3,     /* untagged 64-B IPv4/UDP, MAC pairs */
-    FLUERE_SYNTH_TCP = 4        /* IMIX sizes; TCP with handshakes, 4-way closes (the peer's packets after the
+    FLUERE_SYNTH_TCP = 4,       /* IMIX sizes; TCP with handshakes, 4-way closes (the peer's packets after the
                                    first FIN), RSTs, reopened keys, mid-stream starts, elephants; and UDP */
+    FLUERE_SYNTH_SLOW = 5       /* the general parser's classes: IMIX schedule at 128/576/1500 B, per flow
+                                   IPv6 (1/2), VXLAN-encapsulated IPv4 (1/4) or IPv4 with options (1/4) */
 };
 
 /* Size of the synthetic pcap file (24-B header + records). */

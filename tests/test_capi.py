@@ -104,6 +104,32 @@ def test_synth_vlan_header_only_and_mac_keyed():
     assert pyoracle.offline(fluere_amd.synth_pcap(m), use_mac=True)["n"] == 50
 
 
+def test_synth_slow_classes():
+    """FLUERE_SYNTH_SLOW: every packet is valid for the reference parser and
+    lands in a general-parser class (IPv6, VXLAN inner IPv4, IPv4 options)."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_SLOW, 20_000, 400, 0x51077)
+    data = fluere_amd.synth_pcap(cfg)
+    r = pyoracle.offline(data)
+    assert r["valid"] == 20_000 and r["n"] == 400 and 0 < r["n_ended"] < 400
+    rows = [x.split(",") for x in r["csv"].splitlines()[1:]]
+    v6 = sum(x[0].startswith("fd00::") for x in rows)
+    assert 100 < v6 < 300  # half the flows
+    meta = pyoracle.parse_batch(data)
+    # VXLAN flows: the outer tunnel endpoints never appear as a key
+    assert not any(bytes(m["key_src"][:4]) == bytes([192, 168, 0, 1]) for m in meta[:2000])
+    # no packet of this kind fits the hot parser's shape (Ethernet/IPv4 ihl 5/TCP|UDP, not VXLAN)
+    import struct
+    off, n_hot = 24, 0
+    while off + 16 <= len(data):
+        incl = struct.unpack_from("<I", data, off + 8)[0]
+        f = data[off + 16: off + 16 + incl]
+        et, ihl, proto = f[12:14], f[14] & 15, f[23]
+        vx = proto == 17 and f[42:50] == bytes([8, 0, 0, 0, 0, 0, 0x64, 0])
+        n_hot += et == b"\x08\x00" and ihl == 5 and proto in (6, 17) and not vx
+        off += 16 + incl
+    assert n_hot == 0
+
+
 def test_device_batches_split_below_4gib(monkeypatch):
     """bench.py's C4 shard (12.5M IMIX packets, ~4.3 GiB) is attached as
     consecutive batches that each stay below 4 GiB (u32 record offsets) and

@@ -78,6 +78,13 @@ SYNTH = {
     # BASELINE configs[2] recipe at 1/5 size: 100k flows overflow every
     # workgroup's LDS table, so most packets take the spill path
     "c3_imix_2m": (_lib.SYNTH_IMIX, 2_000_000, 100_000, 0xF10E0003, False),
+    # the general parser's classes (IPv6, VXLAN, IPv4 options): the slow list,
+    # pre-aggregated per dense id in the merge kernel's LDS entries; with 60k
+    # flows most ids find no entry and take the global atomics
+    "slow_small": (_lib.SYNTH_SLOW, 200_000, 2_000, 0xF10E0008, False),
+    "slow_2m": (_lib.SYNTH_SLOW, 2_000_000, 10_000, 0xF10E0008, False),
+    "slow_many_flows": (_lib.SYNTH_SLOW, 300_000, 60_000, 0xF10E0018, False),
+    "slow_mac": (_lib.SYNTH_SLOW, 100_000, 3_000, 0xF10E0028, True),
 }
 
 
@@ -91,7 +98,38 @@ def test_synthetic_csv_matches_oracle(gpu, name):
     assert st["packets"] == n
 
 
-@pytest.mark.parametrize("kind", [_lib.SYNTH_UDP64, _lib.SYNTH_IMIX, _lib.SYNTH_VLAN64])
+@pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small"])
+def test_second_run_takes_slow_kernel(gpu, name):
+    """The first run of a context leaves the slow list to the merge kernel's
+    tail; a run after one that had slow packets gives it to k_slow (inlined
+    general parser, per-id LDS pre-aggregation).  Both equal the oracle."""
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=use_mac)
+    with fluere_amd.FlowContext(use_mac=use_mac, max_flows=max(1 << 16, 2 * f)) as ctx:
+        ctx.add_host_pcap(data)
+        for run in range(3):
+            ctx.run()
+            recs, ne = ctx.records()
+            assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"{name} run {run}")
+
+
+@pytest.mark.parametrize("name", sorted(manifest()))
+def test_fixture_second_run(gpu, name):
+    """Every fixture run twice on one context (the second run predicts the
+    slow list from the first: k_slow when the capture has general-parser packets)."""
+    m = manifest()[name]
+    data = golden_pcap(name)
+    run0 = m["runs"][0]
+    with fluere_amd.FlowContext(timeout_ms=run0["timeout_ms"], use_mac=run0["use_mac"], max_flows=1 << 16) as ctx:
+        ctx.add_host_pcap(data)
+        for k in range(2):
+            ctx.run()
+            recs, ne = ctx.records()
+            assert_csv_equal(fluere_amd.format_csv(recs), ne, golden_csv(run0["csv"]), run0["n_ended"], f"{name} run {k}")
+
+
+@pytest.mark.parametrize("kind", [_lib.SYNTH_UDP64, _lib.SYNTH_IMIX, _lib.SYNTH_VLAN64, _lib.SYNTH_TCP, _lib.SYNTH_SLOW])
 def test_device_generator_matches_host(gpu, kind):
     cfg = fluere_amd.synth_cfg(kind, 50_000, 300, 0xABCDEF)
     host = fluere_amd.synth_pcap(cfg)
