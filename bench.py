@@ -57,6 +57,7 @@ CONFIGS = {
 }
 BYTES_PER_PKT = 80  # algorithmic: 16 B pcap record header + min(caplen, 64) B header window
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0  # measured device copy rate (MI355X_MICROARCH.md)
 
 
 def main():
@@ -183,6 +184,8 @@ def main():
                        **({"note": C["note"]} if "note" in C else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         # also against the measured copy rate (MI355X_MICROARCH.md)
+                         "frac_vs_copy_6290": round(achieved / HBM_COPY_GBS, 4),
                          "kernel": "k_parse_agg", "kernel_ms": round(kernel_avg, 4),
                          # > 1: kernel_ms spans the first launch's start to the last one's end
                          "launches_per_step": len(batches),
@@ -218,8 +221,16 @@ def cpu_baseline(cfg, C):
                    for _ in range(2))
     finally:
         os.sched_setaffinity(0, old)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": round(n / best / 1e6, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} packets of the same synthetic capture, in memory, best of 2"}
+            "sample": f"first {n} packets of the same synthetic capture, in memory, best of 2",
+            "what": "C restatement of the reference CPU path (oracle/), 1 core; the Rust reference cannot be built here",
+            "cpu": model, "host_cpus": os.cpu_count()}
 
 
 if __name__ == "__main__":

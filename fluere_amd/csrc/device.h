@@ -65,7 +65,8 @@ struct Glob {
     unsigned long long n_keys, n_heads;
     unsigned long long generic_used;
     unsigned long long n_slow;
-    unsigned long long n_spill;  // k_parse_agg: spilled packets of the batch (sorted area cursor); next to n_slow
+    unsigned long long n_spill;  // k_parse_agg: the batch's overflow-list records (cursor); next to n_slow
+    unsigned long long n_dspill; // k_parse_agg: the batch's spills in owner segments; next to n_spill
     unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
     unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
@@ -73,7 +74,8 @@ struct Glob {
     unsigned long long clean_done;                        // k_cleanup: workgroups finished
     unsigned long long fin_done;                          // k_finalize: workgroups finished
 };
-static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8, "n_slow, n_spill are reset together");
+static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16,
+              "n_slow, n_spill, n_dspill are reset together");
 // One device allocation holds Glob and the dictionary counters right after it
 // (n_flows, err), so a run ends with ONE small device->host copy.
 struct Ctl {

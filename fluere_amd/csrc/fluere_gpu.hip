@@ -85,7 +85,7 @@ static_assert(sizeof(Part) == 80, "Part layout");
 // merged by its owner like a one-packet partial.
 struct alignas(16) Spill {
     uint32_t k0, k1, k2, tag;     // LDS key words (tag = proto << 24)
-    uint32_t doct, pt, loc, fl;   // pt = pkt | ttl << 16 | elig << 24; fl = tf | dir << 8
+    uint32_t doct, pt, loc, fl;   // pt = pkt | ttl << 16 | elig << 24; fl = tf | dir << 8 (| set << 9: overflow list)
 };
 static_assert(sizeof(Spill) == 32, "Spill layout");
 // MAC kernels: a spilled packet takes two records: {k0, k1, k2, tag},
@@ -98,11 +98,17 @@ struct Stage {
     unsigned long long* base;     // [set] global index of the window's first packet
     // Spilled packets are stored as planes of 16-byte words (word w of every
     // record together), so a wave's loads and stores of one word are contiguous.
-    Spill* spill_raw;             // [workgroup][word][WIN_ITERS * BLOCK] this window's spills, arrival order
-    Spill* spill;                 // [spill_cap] owner-grouped spills of every set, one 32-B record each (64 B with MACs)
+    // A spilled packet is stored where its merge owner reads it: segment o of
+    // its set holds up to cap_o records (32 B, 64 B with MACs: whole sectors),
+    // soff[o][set] of them.  The rare packets past cap_o (a key spilling a
+    // whole window) are appended raw per workgroup (planes of 16-byte words)
+    // and listed at the flush in spill (the overflow list, n_spill records).
+    Spill* dspill;                // [set][owner][cap_o] records
+    uint32_t cap_o;
+    Spill* spill_raw;             // [workgroup][word][WIN_ITERS * BLOCK] this window's overflow, arrival order
+    Spill* spill;                 // [spill_cap] the overflow list (one record each; fl bits 9.. = set)
     unsigned long long spill_cap; // records of spill (the batch's packet count)
-    uint32_t* soff;               // [(O + 1) * n_sets]: owner o's spills of set s = spill[sbase[s] + soff[o][s] ..)
-    unsigned long long* sbase;    // [set] first spill of the set
+    uint32_t* soff;               // [O * n_sets]: records in owner o's segment of set s
     uint4* partx;                 // MAC runs: [set * NS + cell] the partial's MAC words and key hash
     unsigned long long* wgs;      // [workgroup][WGS_N] run statistics of each hot-kernel workgroup (plain
                                   // stores; k_merge_partials sums them: no contended atomics at the end)
@@ -371,6 +377,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     uint32_t d_loops = 0, d_iters = 0;  // diagnostics (per wave, uniform)
     const uint64_t nsteps = end > beg ? (end - beg + stride - 1) / stride : 0;
     uint64_t wbase = beg;
+    uint32_t win = 0;  // this workgroup's window (set blockIdx.x * W + win)
 
     // PK packets per lane per iteration (steps st .. st+PK-1), processed
     // phase by phase so that the LDS round trips of the PK packets overlap
@@ -560,17 +567,45 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         for (int u = 0; u < PK; u++) {
             agg[u] = q[u].valid & (q[u].state == 1) & (q[u].slot < NSL);
             // a valid packet whose key has no LDS slot spills: a 32-byte record
-            // for its merge owner (wave-aggregated append to this workgroup's
-            // raw spill buffer; grouped by owner at the flush)
+            // (64 with MACs) straight into its merge owner's segment of this
+            // set; past the segment's capacity, to this workgroup's raw
+            // overflow buffer (wave-aggregated append; listed at the flush)
             const bool miss = q[u].valid & !agg[u];
             c_miss += miss ? 1 : 0;
-            const uint64_t mm_ = __ballot(miss);
+            bool ovf = false;
+            if (miss) {
+                const Hot& h = q[u].h;
+                const uint32_t loc = (uint32_t)(li[u] - wbase);
+                const bool elig = (h.proto != 6u) | ((h.tf & 2u) != 0);
+                const uint4 w_key = make_uint4(q[u].k0, q[u].k1, q[u].k2, q[u].tag);
+                const uint4 w_pay = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), loc,
+                                               h.tf | (q[u].dir << 8));
+                const uint32_t ow = owner_of(hk[u], a.S.O);
+                const uint32_t pos = own_add(s_scnt, ow);
+                if (pos < a.S.cap_o) {
+                    uint4* dst = reinterpret_cast<uint4*>(a.S.dspill) +
+                                 (((size_t)(blockIdx.x * a.S.W + win) * a.S.O + ow) * a.S.cap_o + pos) * (2 * SPU);
+                    dst[0] = w_key;
+                    if (MACS) {
+                        dst[1] = make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]);
+                        dst[2] = w_pay;
+                    } else {
+                        dst[1] = w_pay;
+                    }
+                } else {
+                    ovf = true;
+                }
+                c_valid++;
+                tmin = min(tmin, (unsigned long long)h.t);
+                tmax = max(tmax, (unsigned long long)h.t);
+            }
+            const uint64_t mm_ = __ballot(ovf);
             if (mm_) {
                 const uint32_t lead = __builtin_ctzll(mm_);
                 uint32_t b0 = 0;
                 if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(&s_nspill, (uint32_t)__popcll(mm_));
                 b0 = __shfl(b0, lead, 64);
-                if (miss) {
+                if (ovf) {
                     const Hot& h = q[u].h;
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm_ >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mm_, 0u));
@@ -581,10 +616,6 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     if (MACS) dst[SPILL_WG] = make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]);
                     dst[(MACS ? 2 : 1) * SPILL_WG] = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24),
                                                                 loc, h.tf | (q[u].dir << 8));
-                    own_add(s_scnt, owner_of(hk[u], a.S.O));
-                    c_valid++;
-                    tmin = min(tmin, (unsigned long long)h.t);
-                    tmax = max(tmax, (unsigned long long)h.t);
                 }
             }
             const bool slow = q[u].slow;
@@ -666,7 +697,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         }
     };
     unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_wait = 0, cyc_start = clock64(), rt_start = wall_clock64();
-    uint32_t win = 0;
+    uint32_t ovf_total = 0;  // (thread 0) overflow records of every window
     auto flush = [&]() {
         // the window's partial aggregates -> this workgroup's staging set
         // (plain coalesced stores, lane per slot); k_merge_partials merges them
@@ -707,12 +738,11 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         }
         lds_barrier();
         if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 4] = wall_clock64();
-        // exclusive scans over the owners (one wave each, an even run of
-        // owners per lane, so no two lanes write one packed word): wave 0
-        // the slot counts, wave 1 the spill counts
+        // exclusive scan of the slot counts over the owners (one wave, an
+        // even run of owners per lane, so no two lanes write one packed word)
         static_assert(MAX_OWNERS % 2 == 0, "owner runs cover whole words");
-        if (tid < 128) {
-            uint32_t* arr = tid < 64 ? s_own : s_scnt;
+        if (tid < 64) {
+            uint32_t* arr = s_own;
             const uint32_t l = tid & 63;
             const uint32_t per = 2 * ((O + 127) / 128);
             uint32_t sum = 0;
@@ -737,23 +767,21 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             }
             if (l == 63) own_set(arr, O, incl);
         }
-        const uint32_t nsp = s_nspill;
+        const uint32_t nsp = s_nspill;  // overflow records of this window
         if (tid == 128) s_sbase = nsp ? atomicAdd(&a.g->n_spill, (unsigned long long)nsp) : 0ull;
+        if (tid == 0) ovf_total += nsp;
         lds_barrier();
         for (uint32_t o = tid; o <= O; o += BLOCK) {
             S.off[(size_t)o * S.n_sets + set] = own_get(s_own, o);
-            S.soff[(size_t)o * S.n_sets + set] = own_get(s_scnt, o);
+            if (o < O) S.soff[(size_t)o * S.n_sets + set] = min(own_get(s_scnt, o), S.cap_o);
         }
-        if (tid == 0) {
-            S.base[set] = B.first + wbase;
-            S.sbase[set] = s_sbase;
-        }
+        if (tid == 0) S.base[set] = B.first + wbase;
         lds_barrier();
         if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 5] = wall_clock64();
-        // spilled packets -> owner-grouped segments of this set (the raw
-        // records were written by other waves of this workgroup: nontemporal
-        // loads, which bypass the CU's L1)
-        {
+        // overflow records -> the overflow list (the raw records were written
+        // by other waves of this workgroup: nontemporal loads, which bypass
+        // the CU's L1); the set goes into fl's high bits
+        if (nsp) {
             const uint4* raw = reinterpret_cast<const uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2 * SPU;
             const unsigned long long sb = s_sbase;
             // SU records per thread per round, all loads issued first (one
@@ -781,19 +809,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 for (int u = 0; u < SU; u++) {
                     const uint32_t i = i0 + u * BLOCK + tid;
                     if (i >= nsp) continue;
-                    const u32x4 v0 = av[u][0];
-                    const uint32_t hsp = MACS ? av[u][1].w : lt_hash(v0.x, v0.y, v0.z, v0.w);
-                    const uint32_t pos = own_add(s_scnt, owner_of(hsp, O));
-                    // one record per whole 32-byte sector (64 with MACs): a
-                    // scattered 16-byte plane word cost a sector write of its own
-                    uint4* dst = reinterpret_cast<uint4*>(S.spill) + (sb + pos) * (size_t)(2 * SPU);
+                    av[u][SW - 1].w |= set << 9;
+                    uint4* dst = reinterpret_cast<uint4*>(S.spill) + (sb + i) * (size_t)(2 * SPU);
 #pragma unroll
-                    for (int w = 0; w < SW; w++) {
-                        if (FLUERE_SPILL_NT & 1)
-                            __builtin_nontemporal_store(av[u][w], reinterpret_cast<u32x4*>(dst + w));
-                        else
-                            dst[w] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
-                    }
+                    for (int w = 0; w < SW; w++) dst[w] = make_uint4(av[u][w].x, av[u][w].y, av[u][w].z, av[u][w].w);
                 }
             }
         }
@@ -966,9 +985,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         const uint32_t set = blockIdx.x * a.S.W + w;
         for (uint32_t oo = tid; oo <= a.S.O; oo += BLOCK) {
             a.S.off[(size_t)oo * a.S.n_sets + set] = 0;
-            a.S.soff[(size_t)oo * a.S.n_sets + set] = 0;
+            if (oo < a.S.O) a.S.soff[(size_t)oo * a.S.n_sets + set] = 0;
         }
-        if (tid == 0) a.S.sbase[set] = 0;
     }
     // statistics: one record per workgroup (plain stores), summed by k_merge_partials
     if ((tid & 63) == 0 && d_loops && a.dbg) {
@@ -1008,6 +1026,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         st[7] = cyc_wait;
         a.slow_cnt[blockIdx.x] = s_slow;
         if (s_slow) atomicAdd(a.slow_n, (unsigned long long)s_slow);
+        // spills in owner segments: every LDS-table miss but the overflow
+        if (s_cnt[2] > ovf_total) atomicAdd(&a.g->n_dspill, s_cnt[2] - ovf_total);
         if (a.dbg) {
             const unsigned long long rt_end = wall_clock64();
             a.dbg[blockIdx.x * 8 + 0] = rt_start;
@@ -1083,6 +1103,24 @@ __device__ __forceinline__ void spill_to_part(uint32_t doct, uint32_t pt, uint32
     for (int q = 0; q < 8; q++) f.fl[q] = (tf >> q) & 1;
     f.fa = gi;
     f.fc = ((pt >> 24) & 1) ? gi : NONE64;
+    f.fr = (tf & 5) ? gi : NONE64;
+    f.la = gi + 1;
+}
+
+// One general-parser packet as a one-packet partial (update_flow's
+// order-free fields; positions are global packet indices, la = last + 1).
+__device__ __forceinline__ void pkt_to_part(const PktInfo& pi, uint8_t dir, unsigned long long gi, FlowPart& f) {
+    const uint32_t tf = pi.tflags;
+    f.pk[0] = dir ? 0 : 1;
+    f.pk[1] = dir ? 1 : 0;
+    f.by[0] = dir ? 0 : (unsigned long long)pi.doctets;
+    f.by[1] = dir ? (unsigned long long)pi.doctets : 0;
+    f.mn[0] = f.mx[0] = pi.rpkt;
+    f.mn[1] = f.mx[1] = pi.rttl;
+#pragma unroll
+    for (int q = 0; q < 8; q++) f.fl[q] = (tf >> q) & 1;
+    f.fa = gi;
+    f.fc = (pi.rprot != 6 || (tf & 2)) ? gi : NONE64;
     f.fr = (tf & 5) ? gi : NONE64;
     f.la = gi + 1;
 }
@@ -1271,6 +1309,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         pre_wb[q] = in ? a.S.base[set] : 0;
     }
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long n_dspill_all = __hip_atomic_load(&a.g->n_dspill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool macs = a.macs != 0;
     for (int e = tid; e < MT; e += MB) {
@@ -1317,9 +1356,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // exclusive scan of the segment lengths; threads then take partials from
     // the flattened index space (binary search for the set), so every thread
     // has about (partials / MB) of them with all their loads in flight.
-    // Pass 0 takes the staged partials, pass 1 the spilled packets (each a
-    // one-packet partial), through the same per-owner segment machinery.
-    const int passes = n_spill_all ? 2 : 1;  // no spills: one pass
+    // Pass 0 takes the staged partials, pass 1 the spilled packets in this
+    // owner's segments (each a one-packet partial), through the same
+    // machinery; the overflow list is the tail's.
+    const int passes = n_dspill_all ? 2 : 1;  // no spills: one pass
     for (int pass = 0; pass < passes; pass++)
     for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
         const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
@@ -1335,12 +1375,11 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 hi = pre_hi[q];
                 wb = pre_wb[q];
             } else if (set < c0s + nset) {
-                lo = offs[(size_t)me * S.n_sets + set];
-                hi = offs[(size_t)(me + 1) * S.n_sets + set];
+                lo = pass ? 0u : offs[(size_t)me * S.n_sets + set];
+                hi = offs[(size_t)(pass ? me : me + 1) * S.n_sets + set];  // pass 1: the segment's count
                 wb = S.base[set];
-                if (pass) rb = S.sbase[set];
             }
-            if (pass == 0) rb = (unsigned long long)set * NS;
+            rb = pass ? ((unsigned long long)set * S.O + me) * S.cap_o : (unsigned long long)set * NS;
             m_lo[tid * (MCH / MB) + q] = (uint32_t)(rb + lo);
             m_wb[tid * (MCH / MB) + q] = (uint32_t)(wb - a.B.first);
             len[q] = hi - lo;
@@ -1381,7 +1420,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 part_of_stage(p, base, f);
             } else {
                 const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                const uint4* src = reinterpret_cast<const uint4*>(S.spill) + o * (size_t)(macs ? 4 : 2);
+                const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)(macs ? 4 : 2);
                 const uint4 v0 = src[0], v1 = src[1];
                 k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
                 if (macs) {  // {key}, {MAC words, hash}, {payload}
@@ -1564,16 +1603,18 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
     if (me == gridDim.x - 1 && tid < 64) reduce_stats();
-    if (n_slow_all && !a.slow_kernel) {
-        // The packets the hot kernel left to the general parser (IPv6, IPv4 options,
-        // ARP, VXLAN, VLAN, other IP protocols, short frames, keys without an LDS
-        // slot ...): general parser, dense id from the dictionary, then update_flow's
-        // order-free part pre-aggregated per dense id in this workgroup's LDS entries
-        // (one set of global atomics per flow and workgroup at the end, instead of
-        // ~14 per packet); a packet whose id finds no entry within 32 probes takes the
-        // global atomics directly.  Grid-stride over the device-side count (no host
-        // round trip); runs in the tail of k_merge_partials (one launch fewer per batch).
-        __syncthreads();  // the owner's entries are in the global accumulators: reuse them
+    const bool tail_slow = n_slow_all && !a.slow_kernel;
+    if (tail_slow || n_spill_all) {
+        // The tail: the overflow list (spills past their owner segment's
+        // capacity: full keys, no parse) and, unless k_slow takes it, the
+        // slow list (packets the hot kernel left to the general parser: IPv6,
+        // IPv4 options, ARP, VXLAN, VLAN, other IP protocols, short frames).
+        // Each record: dense id from the dictionary, then update_flow's
+        // order-free part pre-aggregated per dense id in this workgroup's LDS
+        // entries (reused: the owner's flows are in the global accumulators);
+        // an id with no entry within 32 probes takes the global atomics.
+        // Grid-stride over device-side counts (no host round trip).
+        __syncthreads();
         for (int e = tid; e < MT; e += MB) {
             m_key[e].x = NONE32;
             m_pk[0][e] = m_pk[1][e] = 0;
@@ -1585,61 +1626,101 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
             m_la[e] = 0;
         }
-        // the hot workgroups' regions, flattened: exclusive scan of their counts
-        const uint32_t nwg = S.n_wg;  // <= MB
-        const uint32_t cnt = tid < (int)nwg ? a.slow_cnt[tid] : 0u;
-        const uint32_t st0 = block_exclusive_scan(cnt, m_scan);
-        if (tid < (int)nwg) m_start[tid] = st0;
-        __syncthreads();
-        const unsigned long long n = m_scan[MB / 64];
-        unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
-        const unsigned long long stride = (unsigned long long)gridDim.x * MB;
-        for (unsigned long long i = (unsigned long long)blockIdx.x * MB + tid; i < n; i += stride) {
-            uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
-            while (lo_w < hi_w) {
-                const uint32_t mid = (lo_w + hi_w + 1) >> 1;
-                if (m_start[mid] <= i) lo_w = mid;
-                else hi_w = mid - 1;
-            }
-            const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - m_start[lo_w])];
-            if (a.slow_abl == 2) { c_drop += li == NONE32; continue; }
-            Parsed P;
-            parse_record(a.B, li, macs, 1, P);
-            if (P.cls) { c_drop++; continue; }
-            c_valid++;
-            tmin = min(tmin, (unsigned long long)P.t);
-            tmax = max(tmax, (unsigned long long)P.t);
-            uint8_t dir = 0;
-            const uint32_t d = a.slow_abl == 1 ? (P.pi.sip[3] ^ P.pi.dip[3] ^ P.pi.ksp) % 8192u
-                                               : flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
-            if (d == FAIL || d >= a.T.fmax) continue;
-            const unsigned long long gi = a.B.first + li;
-            // single-word keys (the dense id): a CAS claims or finds an entry,
-            // nothing to publish, so the bounded probe needs no other lane
+        // single-word keys (the dense id): a CAS claims or finds an entry,
+        // nothing to publish, so the bounded probe needs no other lane
+        auto put = [&](uint32_t d, const FlowPart& f) {
             uint32_t e = (d * 0x9E3779B1u) >> 22;  // 10 bits: MT == 1024
-            bool in_lds = false;
             for (int pr = 0; pr < 32; pr++) {
                 const uint32_t k = atomicCAS(&m_key[e].x, NONE32, d);
-                if (k == NONE32 || k == d) { in_lds = true; break; }
+                if (k == NONE32 || k == d) {
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        if (f.pk[q]) {
+                            atomicAdd(&m_pk[q][e], f.pk[q]);
+                            atomicAdd(&m_by[q][e], f.by[q]);
+                        }
+                        atomicMin(&m_mn[q][e], f.mn[q]);
+                        atomicMax(&m_mx[q][e], f.mx[q]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
+                    if (f.fa != NONE64) atomicMin(&m_fa[e], f.fa);
+                    if (f.fc != NONE64) atomicMin(&m_fc[e], f.fc);
+                    if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
+                    if (f.la) atomicMax(&m_la[e], f.la);
+                    return;
+                }
                 e = (e + 1) & (MT - 1);
             }
-            if (!in_lds) { agg_global(a.A, d, dir, P.pi, gi); continue; }
-            const uint32_t tf = P.pi.tflags;
-            atomicAdd(&m_pk[dir][e], 1u);
-            atomicAdd(&m_by[dir][e], (unsigned long long)P.pi.doctets);
-            atomicMin(&m_mn[0][e], (uint32_t)P.pi.rpkt);
-            atomicMax(&m_mx[0][e], (uint32_t)P.pi.rpkt);
-            atomicMin(&m_mn[1][e], (uint32_t)P.pi.rttl);
-            atomicMax(&m_mx[1][e], (uint32_t)P.pi.rttl);
-            if (tf) {
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if ((tf >> q) & 1) atomicAdd(&m_fl[q][e], 1u);
-                if (tf & 5) atomicMin(&m_fr[e], gi);
+            part_to_global(a.A, d, f);
+        };
+        const unsigned long long gstride = (unsigned long long)gridDim.x * MB;
+        for (unsigned long long i = (unsigned long long)blockIdx.x * MB + tid; i < n_spill_all; i += gstride) {
+            const uint4* src = reinterpret_cast<const uint4*>(S.spill) + i * (macs ? 4 : 2);
+            const uint4 v0 = src[0], v1 = src[1];
+            uint32_t x0 = 0, x1 = 0, x2 = 0;
+            uint4 pay = v1;
+            if (macs) {
+                pay = src[2];
+                x0 = v1.x; x1 = v1.y; x2 = v1.z;
             }
-            atomicMin(&m_fa[e], gi);
-            if (P.pi.rprot != 6 || (tf & 2)) atomicMin(&m_fc[e], gi);
-            atomicMax(&m_la[e], gi + 1);
+            FlowPart f;
+            spill_to_part(pay.x, pay.y, pay.z, pay.w, S.base[pay.w >> 9], f);
+            uint32_t d;
+            if (macs && v0.w != 0xFF000000u) {
+                CKey ck;
+                mac_ckey(v0.x, v0.y, v0.z, v0.w, x0, x1, x2, ck);
+                d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+            } else {
+                d = staged_id(a.T, v0.x, v0.y, v0.z, v0.w, a.A.slots);
+            }
+            if (d != FAIL && d < a.T.fmax) put(d, f);
+        }
+        if (tail_slow) {
+            // the hot workgroups' regions, flattened: exclusive scan of their counts
+            const uint32_t nwg = S.n_wg;  // <= MB
+            const uint32_t cnt = tid < (int)nwg ? a.slow_cnt[tid] : 0u;
+            const uint32_t st0 = block_exclusive_scan(cnt, m_scan);
+            if (tid < (int)nwg) m_start[tid] = st0;
+            __syncthreads();
+            const unsigned long long n = m_scan[MB / 64];
+            unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
+            for (unsigned long long i = (unsigned long long)blockIdx.x * MB + tid; i < n; i += gstride) {
+                uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
+                while (lo_w < hi_w) {
+                    const uint32_t mid = (lo_w + hi_w + 1) >> 1;
+                    if (m_start[mid] <= i) lo_w = mid;
+                    else hi_w = mid - 1;
+                }
+                const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - m_start[lo_w])];
+                if (a.slow_abl == 2) { c_drop += li == NONE32; continue; }
+                Parsed P;
+                parse_record(a.B, li, macs, 1, P);
+                if (P.cls) { c_drop++; continue; }
+                c_valid++;
+                tmin = min(tmin, (unsigned long long)P.t);
+                tmax = max(tmax, (unsigned long long)P.t);
+                uint8_t dir = 0;
+                const uint32_t d = a.slow_abl == 1 ? (P.pi.sip[3] ^ P.pi.dip[3] ^ P.pi.ksp) % 8192u
+                                                   : flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
+                if (d == FAIL || d >= a.T.fmax) continue;
+                FlowPart f;
+                pkt_to_part(P.pi, dir, a.B.first + li, f);
+                put(d, f);
+            }
+            // run counters: one set of atomics per wave
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                c_valid += __shfl_xor(c_valid, o, 64);
+                c_drop += __shfl_xor(c_drop, o, 64);
+                tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, o, 64));
+                tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, o, 64));
+            }
+            if ((tid & 63) == 0) {
+                if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
+                if (c_drop) atomicAdd(&a.g->dropped, c_drop);
+            }
         }
         __syncthreads();
         for (int e = tid; e < MT; e += MB) {
@@ -1660,18 +1741,6 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             f.fr = m_fr[e];
             f.la = m_la[e];
             part_to_global(a.A, d, f);
-        }
-        // run counters: one set of atomics per wave
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            c_valid += __shfl_xor(c_valid, o, 64);
-            c_drop += __shfl_xor(c_drop, o, 64);
-            tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, o, 64));
-            tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, o, 64));
-        }
-        if ((tid & 63) == 0) {
-            if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
-            if (c_drop) atomicAdd(&a.g->dropped, c_drop);
         }
     }
 }
@@ -1749,8 +1818,9 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         c_valid++;
         tmin = min(tmin, (unsigned long long)P.t);
         tmax = max(tmax, (unsigned long long)P.t);
-        uint8_t dir;
-        const uint32_t d = flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
+        uint8_t dir = 0;
+        const uint32_t d = a.slow_abl == 1 ? (P.pi.sip[3] ^ P.pi.dip[3] ^ P.pi.ksp) % 8192u  // diagnostics only
+                                           : flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
         if (d == FAIL || d >= a.T.fmax) continue;
         const unsigned long long gi = a.B.first + li;
         uint32_t e = (d * 0x9E3779B1u) >> 24;  // 8 bits: ST == 256
@@ -3235,9 +3305,20 @@ struct PassPlan {
 };
 
 // Bytes of the hot kernel's staging area for one batch (Stage layout).
+// Capacity of an owner segment (records per set and owner): a window's
+// packets spread over the owners by hash, with 25 % headroom; bounded so
+// record indices of the segments fit u32 (k_merge_partials' set tables).
+static uint32_t owner_cap(size_t sets, uint32_t O) {
+    const char* force = getenv("FLUERE_OWNER_CAP");  // tests: a small capacity sends spills to the overflow list
+    uint64_t cap = force ? (uint64_t)std::max(1, atoi(force)) : (uint64_t)SPILL_WG / O * 5 / 4 + 32;
+    while (cap > 16 && (uint64_t)sets * O * cap >= (1ull << 32)) cap /= 2;
+    return (uint32_t)cap;
+}
+
 static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n, bool macs) {
-    return cells * (sizeof(Part) + (macs ? sizeof(uint4) : 0)) + ((size_t)grid * SPILL_WG + n) * spill_units(macs) * sizeof(Spill) +
-           2 * sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) +
+    return cells * (sizeof(Part) + (macs ? sizeof(uint4) : 0)) +
+           (sets * O * owner_cap(sets, O) + (size_t)grid * SPILL_WG + n) * spill_units(macs) * sizeof(Spill) +
+           sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) +
            (size_t)grid * WGS_N * sizeof(unsigned long long) + 64 + (macs ? 16 : 0);
 }
 
@@ -3334,13 +3415,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint32_t O = merge_owners(c);
         a.slow_region = (uint32_t)(steps * BLOCK);
         Stage& S = a.S;
-        // layout (16-byte aligned pieces): parts | spill_raw | spill | sbase | base | off | soff
+        // layout (16-byte aligned pieces): parts | owner segments | spill_raw | spill | base | off | soff
         S.part = (Part*)c->d_stage;
-        S.spill_raw = (Spill*)(S.part + cells);
+        S.cap_o = owner_cap(sets, O);
+        S.dspill = (Spill*)(S.part + cells);
+        S.spill_raw = S.dspill + sets * O * S.cap_o * spill_units(c->use_mac);
         S.spill = S.spill_raw + (size_t)grid * SPILL_WG * spill_units(c->use_mac);
-        S.sbase = (unsigned long long*)(S.spill + hb.b.n * spill_units(c->use_mac));
         S.spill_cap = hb.b.n;  // records (32 B, or 64 B with MACs)
-        S.base = S.sbase + sets;
+        S.base = (unsigned long long*)(S.spill + hb.b.n * spill_units(c->use_mac));
         S.off = (uint32_t*)(S.base + sets);
         S.soff = S.off + (size_t)(O + 1) * sets;
         S.wgs = (unsigned long long*)(((uintptr_t)(S.soff + (size_t)(O + 1) * sets) + 7) & ~(uintptr_t)7);
@@ -3401,7 +3483,7 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
     hipStream_t s = c->stream;
     for (int i = 0; i < P.nb; i++) {
         const AggArgs& a = P.agg[i];
-        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 16, s));  // n_slow, n_spill (k_cleanup zeroed them for batch 0)
+        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 24, s));  // n_slow, n_spill, n_dspill (k_cleanup zeroed them for batch 0)
         const unsigned grid = P.agg_grid[i];
         const void* fn = P.macs ? (const void*)k_parse_agg<0, true>
                          : P.abl == 1 ? (const void*)k_parse_agg<1, false>
@@ -3484,7 +3566,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
             hipMemsetParams mp{};
             mp.dst = &c->d_glob->n_slow;
             mp.elementSize = 4;
-            mp.width = 4;  // n_slow, n_spill
+            mp.width = 6;  // n_slow, n_spill, n_dspill
             mp.height = 1;
             mp.pitch = 16;
             mp.value = 0;

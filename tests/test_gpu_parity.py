@@ -98,6 +98,18 @@ def test_synthetic_csv_matches_oracle(gpu, name):
     assert st["packets"] == n
 
 
+@pytest.mark.parametrize("name", ["c3_imix_small", "c5u_mac_small", "many_flows", "slow_small"])
+def test_spill_overflow_list(gpu, name, monkeypatch):
+    """Owner segments of 3 records: nearly every spilled packet goes to the
+    overflow list (the merge kernel's tail) instead of its owner segment."""
+    monkeypatch.setenv("FLUERE_OWNER_CAP", "3")
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=use_mac)
+    csv, ne, st = _gpu_csv(data, use_mac=use_mac, max_flows=max(1 << 16, 2 * f))
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
+
+
 @pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small"])
 def test_second_run_takes_slow_kernel(gpu, name):
     """The first run of a context leaves the slow list to the merge kernel's
