@@ -167,6 +167,7 @@ def lib() -> ctypes.CDLL:
         "fluere_shard_block_bytes": (U64, [U64, U64]),
         "fluere_export_device": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.POINTER(U64),
                                      ctypes.POINTER(U64)]),
+        "fluere_export_async": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, P]),
         "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, U64, ctypes.POINTER(Stats)]),
     }
     for name, (res, args) in sig.items():

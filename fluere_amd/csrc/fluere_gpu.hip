@@ -2296,7 +2296,10 @@ __global__ void __launch_bounds__(256) k_export_owners(ExportArgs a) {
     }
 }
 
-__global__ void k_export_need(ExportArgs a, unsigned long long* need) {
+// need[0..1]: the largest per-owner summary / annex counts; info (may be
+// null): the same, then the shard's order-dependent flows and its flow count
+// (fluere_export_async: reduced over the ranks on the device, read once).
+__global__ void k_export_need(ExportArgs a, unsigned long long* need, unsigned long long* info) {
     if (threadIdx.x || blockIdx.x) return;
     unsigned long long m0 = 0, m1 = 0;
     for (uint32_t o = 0; o < a.n_owners; o++) {
@@ -2306,6 +2309,12 @@ __global__ void k_export_need(ExportArgs a, unsigned long long* need) {
     }
     need[0] = m0;
     need[1] = m1;
+    if (info) {
+        info[0] = m0;
+        info[1] = m1;
+        info[2] = a.fa.g->n_complex;
+        info[3] = min(*a.fa.T.n_flows, a.fa.T.fmax);
+    }
 }
 
 struct FirstPay {
@@ -2528,6 +2537,9 @@ __global__ void __launch_bounds__(64) k_compose(MergeArgs a, const unsigned long
             has_H = s.first_create != NONE64;  // == first_all (the local certificate held)
             H = A;
             has_T = false;
+        } else if (s.annex >= a.cap_annex) {  // a corrupt block: never read past its annexes
+            atomicOr(a.T.err, ERR_CAPACITY);
+            return;
         } else {
             const fluere_flow_annex& x = *merge_annex(a, i, s.annex);
             has_f0 = x.flags & 1;
@@ -2702,6 +2714,7 @@ struct fluere_ctx {
     hipEvent_t ev_ctl = nullptr;                // after a run's counter copy (the speculative cleanup follows)
     uint64_t last_nf = 0;                       // flows of the last completed run (sizing only)
     uint64_t last_n_slow = 0;                   // slow-list packets of the last run (k_slow prediction)
+    bool async_nf = false;                      // fluere_export_async left the shard's flow count in h_ctl->pad[0]
     bool pass_in_run = false;
     bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
     uint32_t run_seq = 0;                       // number of the last run that publishes its counters (Ctl::seq)
@@ -4079,7 +4092,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
         ea.annex = annexes ? (const fluere_flow_annex*)c->d_annex : nullptr;
         k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
         k_export_owners<<<flow_grid(c), 256, 0, s>>>(ea);
-        k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need);
+        k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need, nullptr);
         HIPCHECK(hipGetLastError());
         return FLUERE_OK;
     };
@@ -4114,6 +4127,40 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     c->local_n_rec = g.n_rec;
     c->local_updates = g.n_updates;
     c->local_ended = g.n_ended;
+    return FLUERE_OK;
+}
+
+// The common-case export without a host round trip: the certificate and the
+// summaries (no annexes) are enqueued, and d_info (device, 4 x u64) receives
+// {largest per-owner summary count, annex count, order-dependent flows, flow
+// count}.  The caller reduces d_info over the ranks (MAX) on the context's
+// stream and reads it once; if any rank has order-dependent flows, every rank
+// runs fluere_export_device instead (annexes), and blocks that were too small
+// are exported again with larger capacities.
+extern "C" int fluere_export_async(fluere_ctx* c, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
+                                   uint64_t cap_annex, unsigned long long* d_info) {
+    if (!c || !d_blocks || !n_owners || !cap || !d_info) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = upload_batches(c))) return rc;
+    const int nb = (int)c->batches.size();
+    if (!c->d_annex_of && hipMalloc(&c->d_annex_of, (size_t)c->fmax * 4) != hipSuccess) return FLUERE_E_NOMEM;
+    if (!c->d_need && hipMalloc(&c->d_need, 16) != hipSuccess) return FLUERE_E_NOMEM;
+    FinArgs fa{c->d_batches, nb, tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
+    reset_record_counters(c);
+    k_local_cert<<<flow_grid(c), 256, 0, s>>>(fa, c->d_annex_of);
+    ExportArgs ea{fa, (uint8_t*)d_blocks, n_owners, shard, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
+                  c->d_annex_of, nullptr};
+    k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
+    k_export_owners<<<flow_grid(c), 256, 0, s>>>(ea);
+    k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need, d_info);
+    HIPCHECK(hipGetLastError());
+    c->local_n_rec = c->local_updates = c->local_ended = 0;  // (no order-dependent flow: no local record)
+    // the shard's flow count, for the next pass's owner count: read after the
+    // merge's wait (a spare word of the pinned control copy)
+    HIPCHECK(hipMemcpyAsync(&c->h_ctl->pad[0], c->d_nflows, 4, hipMemcpyDeviceToHost, s));
+    c->async_nf = true;
     return FLUERE_OK;
 }
 
@@ -4156,6 +4203,10 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
     Glob g;
     uint32_t nf_err[2];
     if ((rc = wait_published(c, seq, g, nf_err))) return rc;
+    if (c->async_nf) {
+        c->last_nf = c->h_ctl->pad[0];
+        c->async_nf = false;
+    }
     if (nf_err[1] & ERR_CAPACITY) return FLUERE_E_ARG;  // a shard had more flows than its block holds
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
     const uint64_t timeout_us = c->timeout_ms * 1000ull;

@@ -79,6 +79,7 @@ class ShardExchange:
         self.ctx, self.group = ctx, group
         self.cap, self.cap_annex = max(1, int(cap)), max(1, int(cap_annex))
         self._send = self._recv = None
+        self._info = None
 
     def _buffers(self, world, device):
         import torch
@@ -91,7 +92,14 @@ class ShardExchange:
     def step(self, allow_unsupported: bool = False):
         """One sharded pass; this rank's merge stats.  Raises FluereError when
         the merge cannot give the exact result (FLUERE_E_UNSUPPORTED: the
-        capture needs the hard-timeout sweep) unless allow_unsupported."""
+        capture needs the hard-timeout sweep) unless allow_unsupported.
+
+        Common case: two host round trips per step -- the export (summaries,
+        no annexes) and a MAX all-reduce of its counts are enqueued behind the
+        pass and read once, then the all-to-all and the owner merge.  If any
+        rank has order-dependent flows, every rank exports again with annexes
+        (fluere_export_device); if a block was too small, every rank exports
+        again with larger blocks."""
         import torch
         import torch.distributed as dist
         L = _lib.lib()
@@ -99,13 +107,31 @@ class ShardExchange:
         world = dist.get_world_size(self.group)
         rank = dist.get_rank(self.group)
         dev = torch.device("cuda", torch.cuda.current_device())
+        gloo = dist.get_backend(self.group) == "gloo"
+        if self._info is None:
+            self._info = torch.zeros(4, dtype=torch.int64, device=dev)
         ctx.parse_aggregate()
+        annexes = False
         while True:
             self._buffers(world, dev)
-            need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
-            check(L.fluere_export_device(ctx._h, self._send.data_ptr(), world, rank, self.cap, self.cap_annex,
-                                         ctypes.byref(need), ctypes.byref(need_a)), "fluere_export_device")
-            n0, n1 = agree_need(need.value, need_a.value, self.group, dev)
+            if not annexes:
+                check(L.fluere_export_async(ctx._h, self._send.data_ptr(), world, rank, self.cap, self.cap_annex,
+                                            self._info.data_ptr()), "fluere_export_async")
+                if gloo:  # host copy (the context may run on a stream of its own here)
+                    torch.cuda.synchronize()
+                    t = self._info.cpu()
+                else:     # RCCL on torch's stream, which is the context's (see the class note)
+                    t = self._info
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                n0, n1, n_cplx, _ = (int(x) for x in t.tolist())
+                if n_cplx:
+                    annexes = True  # some rank has order-dependent flows: export with annexes
+                    continue
+            else:
+                need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
+                check(L.fluere_export_device(ctx._h, self._send.data_ptr(), world, rank, self.cap, self.cap_annex,
+                                             ctypes.byref(need), ctypes.byref(need_a)), "fluere_export_device")
+                n0, n1 = agree_need(need.value, need_a.value, self.group, dev)
             if n0 <= self.cap and n1 <= self.cap_annex:
                 break
             # a shard had more flows for some owner: grow the blocks, export again
@@ -179,6 +205,8 @@ class LogicalShards:
         stats = []
         for o, c in enumerate(self.ctxs):
             recv = torch.cat([s[o * blk:(o + 1) * blk] for s in sends])
+            # the contexts run on streams of their own: the copy must have landed
+            torch.cuda.current_stream().synchronize()
             st = Stats()
             rc = L.fluere_merge_gathered(c._h, recv.data_ptr(), G, self.cap, self.cap_annex, ctypes.byref(st))
             if rc != _lib.E_UNSUPPORTED or not allow_unsupported:

@@ -265,6 +265,15 @@ uint64_t fluere_shard_block_bytes(uint64_t cap, uint64_t cap_annex);
  * small (the block header holds them too).  Synchronises the context stream. */
 int fluere_export_device(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
                          uint64_t cap_annex, uint64_t* need, uint64_t* need_annex);
+/* The common case of fluere_export_device without a host round trip (no
+ * annexes): d_info (device memory, 4 x uint64) receives {largest per-owner
+ * summary count, annex count, order-dependent flows, flow count}.  The caller
+ * reduces d_info over the ranks (MAX, on the context's stream) and reads it
+ * once: if any rank has order-dependent flows every rank calls
+ * fluere_export_device instead; if a count exceeds cap / cap_annex every rank
+ * exports again with larger blocks. */
+int fluere_export_async(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
+                        uint64_t cap_annex, unsigned long long* d_info);
 /* Owner side: merge n_shards blocks (block r from rank r, consecutive, as an
  * all-to-all leaves them) into this context's (cleared) flow table and build
  * the owner's records; the context keeps the final records its own export

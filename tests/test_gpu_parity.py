@@ -248,6 +248,7 @@ def test_sharded_cut_short_block_is_an_error(gpu):
         assert need.value > cap
         sends.append(send)
     recv = torch.cat([sends[0][:blk], sends[1][:blk]])
+    torch.cuda.synchronize()  # (the context runs on a stream of its own)
     st = _lib.Stats()
     assert L.fluere_merge_gathered(ctxs[0]._h, recv.data_ptr(), 2, cap, capa, ctypes.byref(st)) == _lib.E_ARG
     for c in ctxs:
@@ -541,14 +542,22 @@ def test_c4_recipe_8_shards_1m_flows(gpu):
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "c4 recipe, 8 shards")
 
 
-def _shard_exchange_rank(rank, world, port, q):
+EXCHANGE_CASES = {
+    # order-dependent flows in every shard: the annex export (fluere_export_device)
+    "tcp": (_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037),
+    # UDP only: the one-round-trip export (fluere_export_async) every step
+    "udp": (_lib.SYNTH_UDP64, 400_000, 2_000, 0xF10E0038),
+}
+
+
+def _shard_exchange_rank(rank, world, port, q, case):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037)
+        cfg = fluere_amd.synth_cfg(*EXCHANGE_CASES[case])
         first, n = fluere_amd.dist.shard_range(cfg.n_packets, rank, world)
         ctx = fluere_amd.FlowContext(max_flows=1 << 18, stream=torch.cuda.current_stream().cuda_stream)
         fluere_amd.dist.set_index_base(ctx, first)
@@ -567,13 +576,14 @@ def _shard_exchange_rank(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_shard_exchange_two_ranks_gloo(gpu):
+@pytest.mark.parametrize("case", sorted(EXCHANGE_CASES))
+def test_shard_exchange_two_ranks_gloo(gpu, case):
     """ShardExchange itself with two ranks (gloo moves the blocks; both ranks
     on this GPU): export, capacity agreement, all-to-all, owner merge, record
     gather -- against the oracle on the whole capture."""
     import socket
     import torch.multiprocessing as mp
-    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037)
+    cfg = fluere_amd.synth_cfg(*EXCHANGE_CASES[case])
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
     sk = socket.socket()
     sk.bind(("127.0.0.1", 0))
@@ -581,14 +591,14 @@ def test_shard_exchange_two_ranks_gloo(gpu):
     sk.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_shard_exchange_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_shard_exchange_rank, args=(r, 2, port, q, case)) for r in range(2)]
     for p in procs:
         p.start()
     csv, ne = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "ShardExchange gloo x2")
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"ShardExchange gloo x2 {case}")
 
 
 def test_pcapng_file_ingest(gpu, tmp_path):
