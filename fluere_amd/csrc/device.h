@@ -141,7 +141,8 @@ __device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
 // mode: 0 production (fast path first), 1 general parser only.  INL: the
 // general parser inlined (k_slow) instead of called out of line.
 template <bool INL = false>
-__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P);
+__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P,
+                                             const uint8_t* staged = nullptr, uint32_t staged_n = 0);
 template <bool INL = false>
 __device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool macs, int mode, Parsed& P) {
     uint32_t off = B.offs[li];
@@ -151,7 +152,8 @@ __device__ __forceinline__ void parse_record(const Batch& B, uint64_t li, bool m
 }
 // The record at batch offset off, its window W already loaded.
 template <bool INL>
-__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P) {
+__device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const Win& W, bool macs, int mode, Parsed& P,
+                                             const uint8_t* staged, uint32_t staged_n) {
     bool sw = B.flags & 1;
     uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
     uint32_t L = min(incl, B.snap);
@@ -163,7 +165,7 @@ __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const
     bool fast = (mode == 0) && parse_fast(W, L, P.pi);
     if (!fast) {
         if constexpr (INL) {
-            parse_general_inl(fr, L, P.pi);
+            parse_general_inl(fr, L, P.pi, staged, min(staged_n, L));
         } else {
             PktInfo g;  // only this copy lives on the stack (parse_general is out of line)
             parse_general(fr, L, g);

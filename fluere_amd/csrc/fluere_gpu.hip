@@ -1754,11 +1754,13 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
 // (ST entries per workgroup, 8 probes; else the global atomics).
 // ---------------------------------------------------------------------------
 constexpr int SB = 256;  // k_slow block
-constexpr int ST = 256;  // k_slow LDS entries
-__global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
+constexpr int ST = 128;  // k_slow LDS entries
+constexpr int SSTAGE = 7;  // 16-byte pieces of a lane's staged frame (the first 112 bytes)
+__global__ void __launch_bounds__(SB, 3) k_slow(AggArgs a) {
     __shared__ uint32_t s_key[ST], s_pk[2][ST], s_mn[2][ST], s_mx[2][ST], s_fl[8][ST];
     __shared__ unsigned long long s_by[2][ST], s_fa[ST], s_fc[ST], s_fr[ST], s_la[ST];
     __shared__ uint32_t s_start[MB + 1];
+    __shared__ uint4 s_stage[SB][SSTAGE];  // per lane: the packet's first 112 frame bytes
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!n_slow_all) return;  // uniform
     const int tid = threadIdx.x;
@@ -1812,8 +1814,28 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             else hi_w = mid - 1;
         }
         const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - s_start[lo_w])];
+        // the record: its header + first 64 frame bytes as the register
+        // window, its first 112 frame bytes staged in this lane's LDS slot
+        // (the batch is readable 80 bytes past its end: never past that)
+        const uint32_t off = a.B.offs[li];
+        const uint8_t* rec = a.B.bytes + off;
+        const uint64_t room = a.B.nbytes + 64 > (uint64_t)off ? a.B.nbytes + 64 - off : 0;  // readable frame bytes
+        const uint32_t nst = (uint32_t)min<uint64_t>(SSTAGE, room / 16);
+        uint4 pc[SSTAGE + 1];
+#pragma unroll
+        for (int k = 0; k < SSTAGE + 1; k++) {
+            if (k < 5 || k <= (int)nst) __builtin_memcpy(&pc[k], rec + 16 * k, 16);  // (80 bytes always readable)
+            else pc[k] = make_uint4(0, 0, 0, 0);
+        }
+        Win W;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            W.w[4 * k + 0] = pc[k].x; W.w[4 * k + 1] = pc[k].y; W.w[4 * k + 2] = pc[k].z; W.w[4 * k + 3] = pc[k].w;
+        }
+#pragma unroll
+        for (int k = 0; k < SSTAGE; k++) s_stage[tid][k] = pc[k + 1];
         Parsed P;
-        parse_record<true>(a.B, li, macs, 1, P);
+        parse_loaded<true>(a.B, off, W, macs, 1, P, reinterpret_cast<const uint8_t*>(s_stage[tid]), 16 * nst);
         if (P.cls) { c_drop++; continue; }
         c_valid++;
         tmin = min(tmin, (unsigned long long)P.t);
@@ -1823,7 +1845,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
                                            : flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
         if (d == FAIL || d >= a.T.fmax) continue;
         const unsigned long long gi = a.B.first + li;
-        uint32_t e = (d * 0x9E3779B1u) >> 24;  // 8 bits: ST == 256
+        uint32_t e = (d * 0x9E3779B1u) >> 25;  // 7 bits: ST == 128
         bool in_lds = false;
         for (int pr = 0; pr < 8; pr++) {
             const uint32_t k = atomicCAS(&s_key[e], NONE32, d);

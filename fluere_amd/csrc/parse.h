@@ -127,10 +127,16 @@ __device__ __forceinline__ bool parse_fast(const Win& W, uint32_t L, PktInfo& o)
 // ---------------------------------------------------------------------------
 // General path: byte reads from global memory.  d = frame start, L = caplen.
 // ---------------------------------------------------------------------------
+// d: the frame in global memory.  s / sn: an optional staged copy of its
+// first sn bytes (k_slow keeps one per lane in LDS: the parser's byte reads
+// are a chain of dependent loads, an LDS round trip each instead of a global
+// one); sn = 0 reads everything from d.
 struct G {
     const uint8_t* d;
-    __device__ __forceinline__ uint32_t b(uint32_t k) const { return d[k]; }
-    __device__ __forceinline__ uint32_t be16(uint32_t k) const { return ((uint32_t)d[k] << 8) | d[k + 1]; }
+    const uint8_t* s = nullptr;
+    uint32_t sn = 0;
+    __device__ __forceinline__ uint32_t b(uint32_t k) const { return k < sn ? s[k] : d[k]; }
+    __device__ __forceinline__ uint32_t be16(uint32_t k) const { return (b(k) << 8) | b(k + 1); }
     __device__ __forceinline__ uint32_t be32(uint32_t k) const { return (be16(k) << 16) | be16(k + 2); }
 };
 
@@ -424,8 +430,9 @@ __device__ __forceinline__ uint8_t vlan_keys(const G& g, Span v, PktInfo& o) {
 // The general parser, inlined into its caller: k_slow, where every packet
 // takes it (an out-of-line call saves and restores the callee's registers
 // through scratch on every packet).
-__device__ __forceinline__ void parse_general_inl(const uint8_t* d, uint32_t L, PktInfo& o) {
-    G g{d};
+__device__ __forceinline__ void parse_general_inl(const uint8_t* d, uint32_t L, PktInfo& o, const uint8_t* staged = nullptr,
+                                                  uint32_t staged_n = 0) {
+    G g{d, staged, staged_n};
     o.kst = ST_OK; o.fst = ST_OK;
     o.v6 = 0; o.rv6 = 0; o.kproto = 0; o.ksp = o.kdp = 0;
     for (int k = 0; k < 4; k++) o.sip[k] = o.dip[k] = o.rsip[k] = o.rdip[k] = 0;
