@@ -3501,15 +3501,16 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
         P.fa = FinArgs{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob,
                        c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
         P.fa.timeout_us = c->timeout_ms * 1000ull;
-        P.fin_grid = flow_grid(c);
         P.spec_ca = P.ca;
         P.spec_ca.spec = 1;
         P.spec_ca.timeout_us = c->timeout_ms * 1000ull;
         P.spec_ca.recs_cap = c->d_recs_cap;
-        // grid-stride over the device flow count: any grid is correct; size it
-        // for the last known flow count
+        // grid-stride over the device flow count: any grid is correct; size
+        // them for the last known flow count (k_finalize's workgroups also
+        // count themselves done on one counter before the last one publishes)
         const uint64_t guess = c->last_nf ? c->last_nf : c->fmax;
-        P.spec_grid = (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(8, grid_for(guess, 256)));
+        P.fin_grid = (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(8, grid_for(guess, 256)));
+        P.spec_grid = P.fin_grid;
     }
     return FLUERE_OK;
 }
