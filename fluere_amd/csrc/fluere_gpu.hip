@@ -35,12 +35,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fluere_gpu.h"
@@ -3060,13 +3062,27 @@ constexpr uint64_t kIngestChunk = 32ull << 20;
 constexpr uint32_t kSnapMax = 262144;
 constexpr uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
 
+// Staging slots: reader threads fill slot k % kIngestSlots with chunk k
+// (pread from the file, or a copy of the host buffer) while the calling
+// thread indexes the chunks in order and enqueues their H2D copies.
+constexpr int kIngestSlots = 8;  // at most; FLUERE_INGEST_SLOTS / _READERS (diagnostics) pick fewer
+static int ingest_slots() {
+    static const int v = getenv("FLUERE_INGEST_SLOTS") ? std::max(2, std::min(kIngestSlots, atoi(getenv("FLUERE_INGEST_SLOTS")))) : 4;
+    return v;
+}
+static int ingest_readers() {
+    static const int v = getenv("FLUERE_INGEST_READERS") ? std::max(1, std::min(16, atoi(getenv("FLUERE_INGEST_READERS")))) : 3;
+    return v;
+}
+
 struct Ingest {
     fluere_ctx* c;
     uint64_t size = 0;
     uint8_t* d = nullptr;
-    uint8_t* pin[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    bool busy[2] = {false, false};
+    uint8_t* pin[kIngestSlots] = {};
+    hipEvent_t ev[kIngestSlots] = {};
+    bool busy[kIngestSlots] = {};
+    int nslots = 2;
     int sw = 0, ns = 0;
     uint32_t snap = kSnapMax;
     uint64_t pos = 24;
@@ -3078,9 +3094,9 @@ struct Ingest {
 
     explicit Ingest(fluere_ctx* cc) : c(cc) {}
     ~Ingest() {
-        for (int i = 0; i < 2; i++)
+        for (int i = 0; i < kIngestSlots; i++)
             if (busy[i]) hipEventSynchronize(ev[i]);  // no copy may read a freed staging chunk
-        for (int i = 0; i < 2; i++) {
+        for (int i = 0; i < kIngestSlots; i++) {
             if (ev[i]) hipEventDestroy(ev[i]);
             if (pin[i]) hipHostFree(pin[i]);
         }
@@ -3090,20 +3106,84 @@ struct Ingest {
         if (nbytes < 24) return FLUERE_E_PCAP;
         size = nbytes;
         if (hipMalloc(&d, nbytes + 256) != hipSuccess) return FLUERE_E_NOMEM;
-        for (int i = 0; i < 2; i++) {
+        nslots = ingest_slots();
+        const int ns_ = (int)std::min<uint64_t>(nslots, (nbytes + kIngestChunk - 1) / kIngestChunk);
+        const auto ta = std::chrono::steady_clock::now();
+        for (int i = 0; i < ns_; i++) {
             if (hipHostMalloc(&pin[i], kIngestChunk, hipHostMallocDefault) != hipSuccess) return FLUERE_E_NOMEM;
             if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return FLUERE_E_HIP;
         }
+        if (getenv("FLUERE_HOSTPROF"))
+            fprintf(stderr, "[fluere] ingest setup (device buffer, %d pinned slots): %.1f ms\n", ns_,
+                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - ta).count());
         return FLUERE_OK;
     }
     // staging slot for chunk k, free once its previous copy has completed
     uint8_t* slot(uint64_t k) {
-        const int i = (int)(k & 1);
+        const int i = (int)(k % nslots);
         if (busy[i]) {
             hipEventSynchronize(ev[i]);
             busy[i] = false;
         }
         return pin[i];
+    }
+    // Every chunk of [0, nbytes): fill(dst, offset, len) brings bytes into a
+    // staging slot (reader threads), feed() indexes and copies them in order.
+    template <class Fill>
+    int run(uint64_t nbytes, Fill fill) {
+        const uint64_t nch = (nbytes + kIngestChunk - 1) / kIngestChunk;
+        if (nch <= 1) {  // one chunk: no threads
+            for (uint64_t k = 0; k < nch; k++) {
+                const uint64_t cs = k * kIngestChunk, len = std::min(kIngestChunk, nbytes - cs);
+                if (!fill(slot(k), cs, len)) return FLUERE_E_IO;
+                const int rc = feed(k, cs, len);
+                if (rc) return rc;
+            }
+            return FLUERE_OK;
+        }
+        const int NS = nslots, NR = ingest_readers();
+        std::atomic<int64_t> filled[kIngestSlots];
+        for (auto& f : filled) f.store(-1);
+        std::atomic<int64_t> fed{-1};
+        std::atomic<bool> fail{false}, stop{false};
+        auto reader = [&](int t) {
+            for (uint64_t k = t; k < nch && !stop.load(); k += NR) {
+                const int i = (int)(k % NS);
+                // the slot's previous chunk (k - slots) indexed and its copy done
+                while ((int64_t)k - NS > fed.load() && !stop.load()) std::this_thread::yield();
+                if (stop.load()) return;
+                if (k >= (uint64_t)NS && hipEventSynchronize(ev[i]) != hipSuccess) { fail = true; stop = true; return; }
+                const uint64_t cs = k * kIngestChunk, len = std::min(kIngestChunk, nbytes - cs);
+                if (!fill(pin[i], cs, len)) { fail = true; stop = true; return; }
+                filled[i].store((int64_t)k);
+            }
+        };
+        static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        double wait_s = 0, feed_s = 0;
+        std::vector<std::thread> th;
+        for (int t = 0; t < NR; t++) th.emplace_back(reader, t);
+        int rc = FLUERE_OK;
+        for (uint64_t k = 0; k < nch && !rc; k++) {
+            const int i = (int)(k % NS);
+            const auto w0 = std::chrono::steady_clock::now();
+            while (filled[i].load() != (int64_t)k && !fail.load()) std::this_thread::yield();
+            const auto w1 = std::chrono::steady_clock::now();
+            if (fail.load()) { rc = FLUERE_E_IO; break; }
+            const uint64_t cs = k * kIngestChunk, len = std::min(kIngestChunk, nbytes - cs);
+            rc = feed(k, cs, len);
+            fed.store((int64_t)k);
+            wait_s += std::chrono::duration<double>(w1 - w0).count();
+            feed_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - w1).count();
+        }
+        stop = true;
+        for (auto& t : th) t.join();
+        if (hostprof)
+            fprintf(stderr, "[fluere] ingest %llu chunks, %d slots, %d readers: %.1f ms (main waits %.1f, indexes+enqueues %.1f)\n",
+                    (unsigned long long)nch, NS, NR,
+                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), 1e3 * wait_s,
+                    1e3 * feed_s);
+        return rc;
     }
     uint32_t rd32(const uint8_t* p) const {
         uint32_t v;
@@ -3112,7 +3192,7 @@ struct Ingest {
     }
     // chunk k = bytes [cs, cs + len) of the capture, already in slot(k)
     int feed(uint64_t k, uint64_t cs, uint64_t len) {
-        const uint8_t* b = pin[k & 1];
+        const uint8_t* b = pin[k % nslots];
         if (cs == 0) {  // pcap global header (libpcap offline)
             uint32_t magic;
             memcpy(&magic, b, 4);
@@ -3154,7 +3234,7 @@ struct Ingest {
             memmove(tail, tail + len, 16 - len);
             memcpy(tail + 16 - len, b, len);
         }
-        const int i = (int)(k & 1);
+        const int i = (int)(k % nslots);
         HIPCHECK(hipMemcpyAsync(d + cs, b, len, hipMemcpyHostToDevice, c->stream));
         HIPCHECK(hipEventRecord(ev[i], c->stream));
         busy[i] = true;
@@ -3173,7 +3253,7 @@ struct Ingest {
         }
         if (n) HIPCHECK(hipMemcpyAsync(d_offs, rel.data(), n * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHECK(hipStreamSynchronize(c->stream));  // rel is pageable; staging slots free
-        for (int i = 0; i < 2; i++) busy[i] = false;
+        for (int i = 0; i < kIngestSlots; i++) busy[i] = false;
         bool first = true;
         for (size_t q = 0; q < cut.size(); q++) {
             const size_t i0 = cut[q], i1 = q + 1 < cut.size() ? cut[q + 1] : n;
@@ -3220,12 +3300,11 @@ extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t
     Ingest in(c);
     int rc = in.begin(nbytes);
     if (rc) return rc;
-    for (uint64_t k = 0, cs = 0; cs < nbytes; k++, cs += kIngestChunk) {
-        const uint64_t len = std::min(kIngestChunk, nbytes - cs);
-        memcpy(in.slot(k), file + cs, len);
-        if ((rc = in.feed(k, cs, len))) return rc;
-    }
-    return in.finish();
+    rc = in.run(nbytes, [&](uint8_t* dst, uint64_t cs, uint64_t len) {
+        memcpy(dst, file + cs, len);
+        return true;
+    });
+    return rc ? rc : in.finish();
 }
 
 // File ingress for fluere_offline_file: read() straight into the pinned
@@ -3255,17 +3334,16 @@ extern "C" int fluere_add_pcap_file(fluere_ctx* c, const char* path) {
     }
     Ingest in(c);
     int rc = in.begin(nbytes);
-    for (uint64_t k = 0, cs = 0; !rc && cs < nbytes; k++, cs += kIngestChunk) {
-        const uint64_t len = std::min(kIngestChunk, nbytes - cs);
-        uint8_t* dst = in.slot(k);
-        uint64_t got = 0;
-        while (got < len) {
-            const ssize_t r = pread(fd, dst + got, len - got, (off_t)(cs + got));
-            if (r <= 0) { rc = FLUERE_E_IO; break; }
-            got += (uint64_t)r;
-        }
-        if (!rc) rc = in.feed(k, cs, len);
-    }
+    if (!rc)
+        rc = in.run(nbytes, [&](uint8_t* dst, uint64_t cs, uint64_t len) {
+            uint64_t got = 0;
+            while (got < len) {
+                const ssize_t r = pread(fd, dst + got, len - got, (off_t)(cs + got));
+                if (r <= 0) return false;
+                got += (uint64_t)r;
+            }
+            return true;
+        });
     close(fd);
     return rc ? rc : in.finish();
 }

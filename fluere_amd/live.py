@@ -67,7 +67,10 @@ class LiveSession:
 
     def batch(self, pcap: bytes, export: bool):
         """One batch; (records, n_ordered) when the interval export ran, else None."""
-        buf = (ctypes.c_uint8 * max(len(pcap), 1)).from_buffer_copy(pcap)
+        if isinstance(pcap, bytes):  # the bytes object's own buffer (no host copy)
+            buf = ctypes.cast(ctypes.c_char_p(pcap), ctypes.POINTER(ctypes.c_uint8))
+        else:
+            buf = (ctypes.c_uint8 * max(len(pcap), 1)).from_buffer_copy(pcap)
         p, n, no, ex = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
         check(self._L.fluere_live_batch(self._h, buf, len(pcap), 1 if export else 0, ctypes.byref(p), ctypes.byref(n),
                                         ctypes.byref(no), ctypes.byref(ex)), "fluere_live_batch")

@@ -1,0 +1,7 @@
+set -eo pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out
+timeout -k 10 300 python -u tools/live_bench.py --config c2 > $O/live_bench_c2.log 2>&1; tail -1 $O/live_bench_c2.log
+timeout -k 10 300 python -u tools/live_bench.py --config tcp --timeout-ms 1000 > $O/live_bench_tcp.log 2>&1; tail -1 $O/live_bench_tcp.log
+timeout -k 10 300 python -u tools/host_inclusive.py --config c2 > $O/host_inclusive_c2.log 2>&1; tail -1 $O/host_inclusive_c2.log
+timeout -k 10 300 python -u tools/host_inclusive.py --config c3 > $O/host_inclusive_c3.log 2>&1; tail -1 $O/host_inclusive_c3.log
