@@ -170,8 +170,13 @@ __device__ __forceinline__ uint32_t hot_parse(const Batch& B, uint32_t off, cons
     const uint32_t proto = w9 >> 24;
     // Ipv4Packet::payload() length: min(total_length - 20, caplen - 34)
     const uint32_t pe = min(tl > 20u ? tl - 20u : 0u, L > 34u ? L - 34u : 0u);
-    // (bitwise, not short-circuit: no branches)
-    const bool vx = (pe >= 16u) & ((W.w[14] >> 16) == 0x0008u) & (W.w[15] == 0u) & ((W.w[16] & 0xFFFFu) == 0x0064u);
+    // (bitwise, not short-circuit: no branches).  The VXLAN probe reads the
+    // 8 bytes after the UDP header view (record bytes 58..65, keys.rs:188);
+    // only bytes 58..63 are tested here, so the hot parser needs record bytes
+    // 0..63 alone (a 64-byte window): a packet whose bytes 58..63 read
+    // 08 00 00 00 00 00 goes to the general parser, which decides exactly
+    // (a TCP header never matches: its data offset is not 0).
+    const bool vx = (pe >= 16u) & ((W.w[14] >> 16) == 0x0008u) & (W.w[15] == 0u);
     const bool whole = (uint64_t)off + 16u + L <= B.nbytes;  // else a truncated last record
     const bool shape = whole & (L >= 34u) & ((w7 & 0x000FFFFFu) == 0x00050008u) & ((proto == 6u) | (proto == 17u)) & !vx;
     const bool tcp = proto == 6u;
@@ -966,8 +971,18 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 live[0] = true;  // dense chunks are whole
                 pin_win(W[0]);
             } else {
+                // the record's first 64 bytes (four 16-byte loads): all the
+                // hot parser reads; an 80-byte window straddles one more
+                // 64-byte memory segment for 3 in 16 alignments
                 o1[0] = osp;
-                load_win(B, osp, W[0]);
+                const uint8_t* p = B.bytes + osp;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    uint4 q;
+                    __builtin_memcpy(&q, p + 16 * k, 16);
+                    W[0].w[4 * k + 0] = q.x; W[0].w[4 * k + 1] = q.y; W[0].w[4 * k + 2] = q.z; W[0].w[4 * k + 3] = q.w;
+                }
+                W[0].w[16] = W[0].w[17] = W[0].w[18] = W[0].w[19] = 0u;
                 live[0] = lis[0] < end;
                 pin_win(W[0]);
             }
