@@ -307,6 +307,20 @@ __device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t g
     parse_record(bs[b], gi - bs[b].first, macs, 0, P);
 }
 
+// parse_microseconds (time.rs:5-7) of the record at batch offset off: the
+// record header alone (a record's `last` needs no parse of its frame).
+__device__ __forceinline__ uint64_t record_time(const Batch& B, uint32_t off) {
+    uint2 h;
+    __builtin_memcpy(&h, B.bytes + off, 8);  // (record offsets need not be aligned)
+    const bool sw = B.flags & 1;
+    const uint32_t sec = hdr_word(h.x, sw), frac = hdr_word(h.y, sw);
+    return (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);
+}
+__device__ __forceinline__ uint64_t time_global(const Batch* bs, int nb, uint64_t gi) {
+    const int b = find_batch(bs, nb, gi);
+    return record_time(bs[b], bs[b].offs[gi - bs[b].first]);
+}
+
 // Wave-aggregated emit_record: one atomic per counter per wave (a thread-per-
 // flow kernel that hits the three run counters per flow serialises on them).
 // All lanes of the wave must call it (want = this lane has a record).

@@ -1251,17 +1251,14 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
     const Batch& BP = a.bs[bp];
     const Batch& BQ = a.bs[bq];
     const uint32_t op = BP.offs[fc - BP.first], oq = BQ.offs[la - BQ.first];
-    Win WP, WQ;
+    Win WP;
     load_win(BP, op, WP);
-    load_win(BQ, oq, WQ);
+    const uint64_t t_last = record_time(BQ, oq);  // the last packet: its time only
     pin_win(WP);
-    pin_win(WQ);
     Parsed P;
     parse_loaded(BP, op, WP, macs, 0, P);
     const uint8_t cd = canon_dir(P, macs);
     fill_seed(r, P);
-    Parsed Q;
-    parse_loaded(BQ, oq, WQ, macs, 0, Q);
     const uint32_t p0 = v.pk[0], p1 = v.pk[1];
     const unsigned long long b0 = v.by[0], b1 = v.by[1];
     r.d_pkts = p0 + p1;
@@ -1272,7 +1269,7 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
     r.min_ttl = (uint8_t)v.mn[1]; r.max_ttl = (uint8_t)v.mx[1];
     for (int q = 0; q < 8; q++) r.cnt[q] = v.fl[q];
     r.cnt[8] = 0;
-    r.last = Q.t;
+    r.last = t_last;
     r.order_key = (fr == la) ? la : NONE64;
     return true;
 }
@@ -2115,10 +2112,19 @@ __device__ __host__ __forceinline__ bool run_complete(const Glob& g, uint32_t er
 }
 
 __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool tables) {
-    for (int t = 0; t < N_TABLES; t++) {
-        uint32_t s = a.A.slots[(size_t)d * N_TABLES + t];
-        if (tables && s != NONE32) { a.T.tab[t][2 * s] = EMPTY; a.T.tab[t][2 * s + 1] = EMPTY; }
-        a.A.slots[(size_t)d * N_TABLES + t] = NONE32;
+    // the flow's chain slots (an IPv4 flow uses 2 of the N_TABLES): read as
+    // 8-byte pairs, cleared only where set
+    uint2* row = reinterpret_cast<uint2*>(a.A.slots + (size_t)d * N_TABLES);
+    static_assert(N_TABLES % 2 == 0, "slot rows are whole 8-byte pairs");
+    uint2 sv[N_TABLES / 2];
+#pragma unroll
+    for (int t = 0; t < N_TABLES / 2; t++) sv[t] = row[t];
+#pragma unroll
+    for (int t = 0; t < N_TABLES / 2; t++) {
+        const uint32_t s0 = sv[t].x, s1 = sv[t].y;
+        if (tables && s0 != NONE32) { a.T.tab[2 * t][2 * s0] = EMPTY; a.T.tab[2 * t][2 * s0 + 1] = EMPTY; }
+        if (tables && s1 != NONE32) { a.T.tab[2 * t + 1][2 * s1] = EMPTY; a.T.tab[2 * t + 1][2 * s1 + 1] = EMPTY; }
+        if ((s0 & s1) != NONE32) row[t] = make_uint2(NONE32, NONE32);
     }
     a.A.pk[0][d] = a.A.pk[1][d] = 0;
     a.A.by[0][d] = a.A.by[1][d] = 0;
@@ -2258,9 +2264,7 @@ __device__ __forceinline__ void export_one(const FinArgs& a, fluere_flow_summary
         for (int k = 0; k < 16; k++) { s.first_src[k] = sd.source[k]; s.first_dst[k] = sd.destination[k]; }
         s.first_time = P.t;
     }
-    Parsed Q;
-    parse_global(a.bs, a.nb, s.last, macs, Q);
-    s.last_time = Q.t;
+    s.last_time = time_global(a.bs, a.nb, s.last);
     s.annex = NONE32;
 }
 
