@@ -349,6 +349,56 @@ __device__ __forceinline__ void emit_record_wave(Glob* g, fluere_record* out, ui
     }
 }
 
+// Block-level emit_record (256-thread blocks; every thread of the block calls
+// it, with uniform control flow): one set of counter atomics per block, the
+// block's records staged in LDS and written out as coalesced 8-byte words.
+// (A 152-byte record stored per lane, lane by lane, made the 1M-flow C4
+// finalize spend ~0.35 ms on its record writes.)
+constexpr int EMIT_BLOCK = 256;
+struct EmitLds {
+    unsigned long long w[EMIT_BLOCK / 64][3];  // per wave: records (-> exclusive prefix), updates, ended
+    unsigned long long base, n;
+    fluere_record rec[EMIT_BLOCK];
+};
+__device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_record* out, uint64_t cap,
+                                                  const fluere_record& r, bool want) {
+    static_assert(sizeof(fluere_record) % 8 == 0, "records are whole 8-byte words");
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(want), em = __ballot(want && r.order_key != NONE64);
+    const unsigned long long upd = wave_sum(want ? (unsigned long long)r.d_pkts : 0ull);
+    if (lane == 0) {
+        S.w[w][0] = __popcll(m);
+        S.w[w][1] = upd;
+        S.w[w][2] = __popcll(em);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t[3] = {0, 0, 0};
+        for (int k = 0; k < EMIT_BLOCK / 64; k++) {
+            const unsigned long long nk = S.w[k][0];
+            t[1] += S.w[k][1];
+            t[2] += S.w[k][2];
+            S.w[k][0] = t[0];  // exclusive prefix of the records
+            t[0] += nk;
+        }
+        S.base = t[0] ? atomicAdd(&g->n_rec, t[0]) : 0ull;
+        S.n = t[0];
+        if (t[1]) atomicAdd(&g->n_updates, t[1]);
+        if (t[2]) atomicAdd(&g->n_ended, t[2]);
+    }
+    __syncthreads();
+    if (want)
+        S.rec[S.w[w][0] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = r;
+    __syncthreads();
+    const unsigned long long base = S.base;
+    const unsigned long long n = base < cap ? min(S.n, cap - base) : 0ull;  // (records past the capacity: counted only)
+    constexpr uint32_t RW = sizeof(fluere_record) / 8;
+    const uint2* src = reinterpret_cast<const uint2*>(S.rec);
+    uint2* dst = reinterpret_cast<uint2*>(out + base);
+    for (uint32_t i = threadIdx.x; i < n * RW; i += EMIT_BLOCK) dst[i] = src[i];
+    __syncthreads();  // S is rewritten by the next call
+}
+
 __device__ __forceinline__ void update_flow(fluere_record& r, bool rev, const PktInfo& pi, uint64_t t) {
     // src/net/flows.rs:11-42 (u32 counters wrap like the release build)
     r.d_pkts += 1;

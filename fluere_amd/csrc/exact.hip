@@ -381,7 +381,8 @@ __device__ __forceinline__ void piece_of(const Agg& g, fluere_flow_piece& pc) {
     pc.last_time = g.lastt;
 }
 
-__global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
+__global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
+    __shared__ EmitLds S;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nr = *a.nruns;
     const bool lane_live = r < nr && !(a.ukeys[r] & 0x80000000u);
@@ -445,8 +446,8 @@ __global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
         cie = a.iie[c];
         rec.order_key = kind == K_ACTIVE ? NONE64 : cj;
     }
-    if (!a.mode_b) {
-        emit_record_wave(a.g, a.out, a.out_cap, rec, rec_live);
+    if (!a.mode_b) {  // (uniform: every thread of the block emits)
+        emit_record_block(S, a.g, a.out, a.out_cap, rec, rec_live);
         return;
     }
     if (rec_live) {
@@ -458,8 +459,9 @@ __global__ void __launch_bounds__(256) k_ex_records(RecArgs a) {
 }
 
 // Mode B: records in the reference's emission order; order_key = rank
-__global__ void __launch_bounds__(256) k_ex_emit_sorted(uint32_t n_inst, const uint32_t* perm, const fluere_record* tmp,
-                                                        Glob* g, fluere_record* out, uint64_t cap) {
+__global__ void __launch_bounds__(EMIT_BLOCK) k_ex_emit_sorted(uint32_t n_inst, const uint32_t* perm, const fluere_record* tmp,
+                                                               Glob* g, fluere_record* out, uint64_t cap) {
+    __shared__ EmitLds S;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     fluere_record rec;
     const bool live = r < n_inst;
@@ -469,7 +471,7 @@ __global__ void __launch_bounds__(256) k_ex_emit_sorted(uint32_t n_inst, const u
     } else {
         memset(&rec, 0, sizeof rec);
     }
-    emit_record_wave(g, out, cap, rec, live);
+    emit_record_block(S, g, out, cap, rec, live);
 }
 
 __global__ void __launch_bounds__(256) k_ex_gather_u64(uint32_t m, const uint32_t* id, const unsigned long long* h,

@@ -1282,9 +1282,9 @@ __device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluer
 }
 
 // emit + complex-flow counters of one wave's flows (every lane of the wave)
-__device__ __forceinline__ void finalize_emit(const FinArgs& a, const fluere_record& r, bool want, bool cplx,
+__device__ __forceinline__ void finalize_emit(EmitLds& S, const FinArgs& a, const fluere_record& r, bool want, bool cplx,
                                               unsigned long long cplx_pkts) {
-    emit_record_wave(a.g, a.out, a.out_cap, r, want);
+    emit_record_block(S, a.g, a.out, a.out_cap, r, want);
     const uint64_t cm = __ballot(cplx);
     if (cm) {
         const unsigned long long pk = wave_sum(cplx_pkts);
@@ -1945,17 +1945,20 @@ __device__ void publish_ctl(Glob* g, unsigned long long* done, Ctl* host_ctl, ui
     }
 }
 
-__global__ void __launch_bounds__(256) k_finalize(FinArgs a) {
+// k_finalize: one thread per flow (grid-stride); records appended per
+// workgroup (emit_record_block).
+__global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
     const Glob& gg = *a.g;
     const bool mode_b = a.timeout_us && gg.valid && gg.tmax - gg.tmin >= a.timeout_us;
     const uint32_t nf = mode_b ? 0u : min(*a.T.n_flows, a.T.fmax);
+    __shared__ EmitLds S;
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
         const uint32_t d = d0 + threadIdx.x;
         fluere_record r;
         bool cplx = false;
         unsigned long long cplx_pkts = 0;
         const bool want = d < nf && finalize_one(a, d, r, cplx, cplx_pkts);
-        finalize_emit(a, r, want, cplx, cplx_pkts);
+        finalize_emit(S, a, r, want, cplx, cplx_pkts);
     }
     if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
 }
@@ -2483,14 +2486,15 @@ __device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t 
 }
 
 // grid-stride over the flows counted on the device (no host round trip)
-__global__ void __launch_bounds__(256) k_merge_finalize(MergeArgs a) {
+__global__ void __launch_bounds__(EMIT_BLOCK) k_merge_finalize(MergeArgs a) {
     const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    __shared__ EmitLds S;
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
         const uint32_t d = d0 + threadIdx.x;
         fluere_record r;
         bool want = false, cplx = false;
         if (d < nf) merge_finalize_one(a, d, r, want, cplx);
-        emit_record_wave(a.g, a.out, a.out_cap, r, want);
+        emit_record_block(S, a.g, a.out, a.out_cap, r, want);
         const uint64_t cm = __ballot(cplx);
         if (cm && (uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm))
             atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
