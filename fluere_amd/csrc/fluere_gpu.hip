@@ -1311,35 +1311,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 0] = wall_clock64();
     // loads issued before the LDS initialisation (their latency overlaps it):
     // this owner's segment bounds of the first set chunk, and the run counters
-    const uint32_t me = blockIdx.x;
-    uint32_t pre_lo[MCH / MB], pre_hi[MCH / MB];
-    unsigned long long pre_wb[MCH / MB];
-#pragma unroll
-    for (int q = 0; q < MCH / MB; q++) {
-        const uint32_t set = tid * (MCH / MB) + q;
-        const bool in = set < a.S.n_sets;
-        pre_lo[q] = in ? a.S.off[(size_t)me * a.S.n_sets + set] : 0;
-        pre_hi[q] = in ? a.S.off[(size_t)(me + 1) * a.S.n_sets + set] : 0;
-        pre_wb[q] = in ? a.S.base[set] : 0;
-    }
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_dspill_all = __hip_atomic_load(&a.g->n_dspill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool macs = a.macs != 0;
-    for (int e = tid; e < MT; e += MB) {
-        m_key[e] = make_uint4(0, 0, 0, 0);
-        m_kx[e] = make_uint4(0, 0, 0, 0);
-        m_pk[0][e] = m_pk[1][e] = 0;
-        m_by[0][e] = m_by[1][e] = 0;
-        m_mn[0][e] = m_mn[1][e] = NONE32;
-        m_mx[0][e] = m_mx[1][e] = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
-        m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
-        m_la[e] = 0;
-    }
-    __syncthreads();
-    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 1] = wall_clock64();
     const Stage& S = a.S;
     auto reduce_stats = [&]() {
         // the hot kernel's per-workgroup statistics -> the run counters (one wave)
@@ -1366,257 +1341,287 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             atomicAdd(&g->cyc_flush0, v[7]);
         }
     };
-    // This owner's segment of every set, flattened: per chunk of MCH sets, an
-    // exclusive scan of the segment lengths; threads then take partials from
-    // the flattened index space (binary search for the set), so every thread
-    // has about (partials / MB) of them with all their loads in flight.
-    // Pass 0 takes the staged partials, pass 1 the spilled packets in this
-    // owner's segments (each a one-packet partial), through the same
-    // machinery; the overflow list is the tail's.
-    const int passes = n_dspill_all ? 2 : 1;  // no spills: one pass
-    for (int pass = 0; pass < passes; pass++)
-    for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
-        const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
-        const uint32_t* offs = pass ? S.soff : S.off;
-        uint32_t len[MCH / MB], tot = 0;
-#pragma unroll
+    // Owners o = blockIdx.x, + gridDim.x, ...: the grid is at most one workgroup
+    // per CU (one merge table fills a CU's LDS), so a workgroup merges several
+    // owners in turn rather than being dispatched again for each.
+    for (uint32_t me = blockIdx.x; me < S.O; me += gridDim.x) {
+        uint32_t pre_lo[MCH / MB], pre_hi[MCH / MB];
+        unsigned long long pre_wb[MCH / MB];
+    #pragma unroll
         for (int q = 0; q < MCH / MB; q++) {
-            const uint32_t set = c0s + tid * (MCH / MB) + q;
-            uint32_t lo = 0, hi = 0;
-            unsigned long long wb = 0, rb = 0;
-            if (pass == 0 && c0s == 0) {  // prefetched
-                lo = pre_lo[q];
-                hi = pre_hi[q];
-                wb = pre_wb[q];
-            } else if (set < c0s + nset) {
-                lo = pass ? 0u : offs[(size_t)me * S.n_sets + set];
-                hi = offs[(size_t)(pass ? me : me + 1) * S.n_sets + set];  // pass 1: the segment's count
-                wb = S.base[set];
-            }
-            rb = pass ? ((unsigned long long)set * S.O + me) * S.cap_o : (unsigned long long)set * NS;
-            m_lo[tid * (MCH / MB) + q] = (uint32_t)(rb + lo);
-            m_wb[tid * (MCH / MB) + q] = (uint32_t)(wb - a.B.first);
-            len[q] = hi - lo;
-            tot += len[q];
+            const uint32_t set = tid * (MCH / MB) + q;
+            const bool in = set < a.S.n_sets;
+            pre_lo[q] = in ? a.S.off[(size_t)me * a.S.n_sets + set] : 0;
+            pre_hi[q] = in ? a.S.off[(size_t)(me + 1) * a.S.n_sets + set] : 0;
+            pre_wb[q] = in ? a.S.base[set] : 0;
         }
-        uint32_t run = block_exclusive_scan(tot, m_scan) ;
-#pragma unroll
-        for (int q = 0; q < MCH / MB; q++) {
-            m_start[tid * (MCH / MB) + q] = run;
-            run += len[q];
+        for (int e = tid; e < MT; e += MB) {
+            m_key[e] = make_uint4(0, 0, 0, 0);
+            m_kx[e] = make_uint4(0, 0, 0, 0);
+            m_pk[0][e] = m_pk[1][e] = 0;
+            m_by[0][e] = m_by[1][e] = 0;
+            m_mn[0][e] = m_mn[1][e] = NONE32;
+            m_mx[0][e] = m_mx[1][e] = 0;
+    #pragma unroll
+            for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
+            m_fa[e] = m_fc[e] = m_fr[e] = NONE64;
+            m_la[e] = 0;
         }
         __syncthreads();
-        const uint32_t total = m_scan[MB / 64];
-        if (a.dbg && tid == 0 && c0s == 0 && pass == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 2] = wall_clock64();
-        for (uint32_t idx = tid; idx < total; idx += MB) {
-            uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
-            while (lo_i < hi_i) {
-                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-                if (m_start[mid] <= idx) lo_i = mid;
-                else hi_i = mid - 1;
-            }
-            const unsigned long long base = a.B.first + m_wb[lo_i];
-            uint32_t h, k0, k1, k2, tag, x0 = 0, x1 = 0, x2 = 0;
-            FlowPart f;
-            if (pass == 0) {
-                const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                Part p;
-                const uint4* src = reinterpret_cast<const uint4*>(S.part + o);
-                uint4 v[5];
-#pragma unroll
-                for (int q = 0; q < 5; q++) v[q] = src[q];
-                __builtin_memcpy(&p, v, sizeof p);
-                h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
-                if (macs) {
-                    const uint4 xx = S.partx[o];
-                    x0 = xx.x; x1 = xx.y; x2 = xx.z;
+        if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 1] = wall_clock64();
+        // This owner's segment of every set, flattened: per chunk of MCH sets, an
+        // exclusive scan of the segment lengths; threads then take partials from
+        // the flattened index space (binary search for the set), so every thread
+        // has about (partials / MB) of them with all their loads in flight.
+        // Pass 0 takes the staged partials, pass 1 the spilled packets in this
+        // owner's segments (each a one-packet partial), through the same
+        // machinery; the overflow list is the tail's.
+        const int passes = n_dspill_all ? 2 : 1;  // no spills: one pass
+        for (int pass = 0; pass < passes; pass++)
+        for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
+            const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
+            const uint32_t* offs = pass ? S.soff : S.off;
+            uint32_t len[MCH / MB], tot = 0;
+    #pragma unroll
+            for (int q = 0; q < MCH / MB; q++) {
+                const uint32_t set = c0s + tid * (MCH / MB) + q;
+                uint32_t lo = 0, hi = 0;
+                unsigned long long wb = 0, rb = 0;
+                if (pass == 0 && c0s == 0) {  // prefetched
+                    lo = pre_lo[q];
+                    hi = pre_hi[q];
+                    wb = pre_wb[q];
+                } else if (set < c0s + nset) {
+                    lo = pass ? 0u : offs[(size_t)me * S.n_sets + set];
+                    hi = offs[(size_t)(pass ? me : me + 1) * S.n_sets + set];  // pass 1: the segment's count
+                    wb = S.base[set];
                 }
-                part_of_stage(p, base, f);
-            } else {
-                const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)(macs ? 4 : 2);
-                const uint4 v0 = src[0], v1 = src[1];
-                k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
-                if (macs) {  // {key}, {MAC words, hash}, {payload}
-                    const uint4 v2 = src[2];
-                    x0 = v1.x; x1 = v1.y; x2 = v1.z;
-                    h = v1.w;
-                    spill_to_part(v2.x, v2.y, v2.z, v2.w, base, f);
+                rb = pass ? ((unsigned long long)set * S.O + me) * S.cap_o : (unsigned long long)set * NS;
+                m_lo[tid * (MCH / MB) + q] = (uint32_t)(rb + lo);
+                m_wb[tid * (MCH / MB) + q] = (uint32_t)(wb - a.B.first);
+                len[q] = hi - lo;
+                tot += len[q];
+            }
+            uint32_t run = block_exclusive_scan(tot, m_scan) ;
+    #pragma unroll
+            for (int q = 0; q < MCH / MB; q++) {
+                m_start[tid * (MCH / MB) + q] = run;
+                run += len[q];
+            }
+            __syncthreads();
+            const uint32_t total = m_scan[MB / 64];
+            if (a.dbg && tid == 0 && c0s == 0 && pass == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 2] = wall_clock64();
+            for (uint32_t idx = tid; idx < total; idx += MB) {
+                uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
+                while (lo_i < hi_i) {
+                    const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                    if (m_start[mid] <= idx) lo_i = mid;
+                    else hi_i = mid - 1;
+                }
+                const unsigned long long base = a.B.first + m_wb[lo_i];
+                uint32_t h, k0, k1, k2, tag, x0 = 0, x1 = 0, x2 = 0;
+                FlowPart f;
+                if (pass == 0) {
+                    const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
+                    Part p;
+                    const uint4* src = reinterpret_cast<const uint4*>(S.part + o);
+                    uint4 v[5];
+    #pragma unroll
+                    for (int q = 0; q < 5; q++) v[q] = src[q];
+                    __builtin_memcpy(&p, v, sizeof p);
+                    h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
+                    if (macs) {
+                        const uint4 xx = S.partx[o];
+                        x0 = xx.x; x1 = xx.y; x2 = xx.z;
+                    }
+                    part_of_stage(p, base, f);
                 } else {
-                    h = lt_hash(k0, k1, k2, tag);
-                    spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
-                }
-            }
-            // find or claim the merge entry (same protocol as the hot kernel)
-            uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
-            int state = 0, probes = 0;
-            for (int it = 0; it < 128; it++) {
-                if (state == 0) {
-                    const uint4 kk = m_key[e];
-                    bool xm = true;
-                    if (macs) {  // MAC words
-                        const uint4 xx = m_kx[e];
-                        xm = xx.w == 1u && xx.x == x0 && xx.y == x1 && xx.z == x2;
-                    }
-                    if (kk.w & LT_READY) {
-                        if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2 && xm) state = 1;
-                        else if (++probes == 64) state = 2;
-                        else e = (e + 1) & (MT - 1);
-                    } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
-                        m_key[e].x = k0;
-                        m_key[e].y = k1;
-                        m_key[e].z = k2;
-                        if (macs) m_kx[e] = make_uint4(x0, x1, x2, 1u);
-                        __threadfence_block();
-                        atomicExch(&m_key[e].w, tag | LT_READY);
-                        state = 1;
+                    const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
+                    const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)(macs ? 4 : 2);
+                    const uint4 v0 = src[0], v1 = src[1];
+                    k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
+                    if (macs) {  // {key}, {MAC words, hash}, {payload}
+                        const uint4 v2 = src[2];
+                        x0 = v1.x; x1 = v1.y; x2 = v1.z;
+                        h = v1.w;
+                        spill_to_part(v2.x, v2.y, v2.z, v2.w, base, f);
+                    } else {
+                        h = lt_hash(k0, k1, k2, tag);
+                        spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
                     }
                 }
-                if (__ballot(state == 0) == 0) break;
-            }
-            if (state == 1) {
-                // Many records land on one entry (a flow's partials from every
-                // set, its spilled packets), and LDS atomics on one address
-                // serialise: min / max and first / last positions are read
-                // first and written only where the record moves them (values
-                // move monotonically, so a stale read costs at most a
-                // redundant atomic).
-#if FLUERE_MERGE_GUARD
-                const uint32_t gmn0 = m_mn[0][e], gmn1 = m_mn[1][e], gmx0 = m_mx[0][e], gmx1 = m_mx[1][e];
-                const unsigned long long gfa = m_fa[e], gfc = m_fc[e], gla = m_la[e];
-#else
-                const uint32_t gmn0 = NONE32, gmn1 = NONE32, gmx0 = 0, gmx1 = 0;
-                const unsigned long long gfa = NONE64, gfc = NONE64, gla = 0;
-#endif
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    if (f.pk[q]) {
-                        atomicAdd(&m_pk[q][e], f.pk[q]);
-                        atomicAdd(&m_by[q][e], f.by[q]);
+                // find or claim the merge entry (same protocol as the hot kernel)
+                uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
+                int state = 0, probes = 0;
+                for (int it = 0; it < 128; it++) {
+                    if (state == 0) {
+                        const uint4 kk = m_key[e];
+                        bool xm = true;
+                        if (macs) {  // MAC words
+                            const uint4 xx = m_kx[e];
+                            xm = xx.w == 1u && xx.x == x0 && xx.y == x1 && xx.z == x2;
+                        }
+                        if (kk.w & LT_READY) {
+                            if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2 && xm) state = 1;
+                            else if (++probes == 64) state = 2;
+                            else e = (e + 1) & (MT - 1);
+                        } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
+                            m_key[e].x = k0;
+                            m_key[e].y = k1;
+                            m_key[e].z = k2;
+                            if (macs) m_kx[e] = make_uint4(x0, x1, x2, 1u);
+                            __threadfence_block();
+                            atomicExch(&m_key[e].w, tag | LT_READY);
+                            state = 1;
+                        }
                     }
-                    if (f.mn[q] < (q ? gmn1 : gmn0) || !FLUERE_MERGE_GUARD) atomicMin(&m_mn[q][e], f.mn[q]);
-                    if (f.mx[q] > (q ? gmx1 : gmx0) || !FLUERE_MERGE_GUARD) atomicMax(&m_mx[q][e], f.mx[q]);
+                    if (__ballot(state == 0) == 0) break;
                 }
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
-                if (f.fa != NONE64 && f.fa < gfa) atomicMin(&m_fa[e], f.fa);
-                if (f.fc != NONE64 && f.fc < gfc) atomicMin(&m_fc[e], f.fc);
-                if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
-                if (f.la && (f.la > gla || !FLUERE_MERGE_GUARD)) atomicMax(&m_la[e], f.la);
-            } else {
-                uint32_t d;
-                if (macs && tag != 0xFF000000u) {
-                    CKey ck;
-                    mac_ckey(k0, k1, k2, tag, x0, x1, x2, ck);
-                    d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+                if (state == 1) {
+                    // Many records land on one entry (a flow's partials from every
+                    // set, its spilled packets), and LDS atomics on one address
+                    // serialise: min / max and first / last positions are read
+                    // first and written only where the record moves them (values
+                    // move monotonically, so a stale read costs at most a
+                    // redundant atomic).
+    #if FLUERE_MERGE_GUARD
+                    const uint32_t gmn0 = m_mn[0][e], gmn1 = m_mn[1][e], gmx0 = m_mx[0][e], gmx1 = m_mx[1][e];
+                    const unsigned long long gfa = m_fa[e], gfc = m_fc[e], gla = m_la[e];
+    #else
+                    const uint32_t gmn0 = NONE32, gmn1 = NONE32, gmx0 = 0, gmx1 = 0;
+                    const unsigned long long gfa = NONE64, gfc = NONE64, gla = 0;
+    #endif
+    #pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        if (f.pk[q]) {
+                            atomicAdd(&m_pk[q][e], f.pk[q]);
+                            atomicAdd(&m_by[q][e], f.by[q]);
+                        }
+                        if (f.mn[q] < (q ? gmn1 : gmn0) || !FLUERE_MERGE_GUARD) atomicMin(&m_mn[q][e], f.mn[q]);
+                        if (f.mx[q] > (q ? gmx1 : gmx0) || !FLUERE_MERGE_GUARD) atomicMax(&m_mx[q][e], f.mx[q]);
+                    }
+    #pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
+                    if (f.fa != NONE64 && f.fa < gfa) atomicMin(&m_fa[e], f.fa);
+                    if (f.fc != NONE64 && f.fc < gfc) atomicMin(&m_fc[e], f.fc);
+                    if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
+                    if (f.la && (f.la > gla || !FLUERE_MERGE_GUARD)) atomicMax(&m_la[e], f.la);
                 } else {
-                    d = staged_id(a.T, k0, k1, k2, tag, a.A.slots);
+                    uint32_t d;
+                    if (macs && tag != 0xFF000000u) {
+                        CKey ck;
+                        mac_ckey(k0, k1, k2, tag, x0, x1, x2, ck);
+                        d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+                    } else {
+                        d = staged_id(a.T, k0, k1, k2, tag, a.A.slots);
+                    }
+                    if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
                 }
-                if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
+            }
+            __syncthreads();
+        }
+        // Dense ids: thread per entry (MT == MB).  The owner is the only inserter
+        // of its keys, so a claim (EMPTY -> PENDING) normally succeeds at once;
+        // the new ids of the whole workgroup come from ONE atomicAdd on the flow
+        // counter (a single hot address: per-flow increments would serialise).
+        if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 3] = wall_clock64();
+        static_assert(MT == MB, "one merge entry per thread");
+        if (tid == 0) m_nclaim = 0;
+        __syncthreads();
+        const unsigned long long c1 = clock64();
+        const int e = tid;
+        const uint4 kk = m_key[e];
+        const bool have = (kk.w & LT_READY) != 0;
+        const uint32_t tag = kk.w & 0xFF000000u;
+        uint32_t d = FAIL, s0 = FAIL, s1 = FAIL, rank = 0;
+        bool claimed = false, wait = false;
+        unsigned long long* val = nullptr;
+        if (have) {
+            if (tag == 0xFF000000u) {
+                d = kk.x;  // MAC kernels' partials carry dense ids
+            } else if (macs) {  // a spilled MAC-kernel key: one dictionary walk per flow and owner
+                const uint4 xx = m_kx[e];
+                CKey ck;
+                mac_ckey(kk.x, kk.y, kk.z, tag, xx.x, xx.y, xx.z, ck);
+                d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+            } else {       // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
+                unsigned long long v = EMPTY;
+                s0 = tab_slot(a.T, 0, ((uint64_t)kk.x << 32) | kk.y, true);
+                if (s0 != FAIL) s1 = tab_slot(a.T, 1, ((uint64_t)s0 << 40) | ((uint64_t)kk.z << 8) | (tag >> 24), true, &v);
+                if (s1 != FAIL) {
+                    val = &a.T.tab[1][2 * s1 + 1];
+                    if (v >= PENDING) v = atomicCAS(val, EMPTY, PENDING);
+                    if (v == EMPTY) {
+                        claimed = true;
+                        rank = atomicAdd(&m_nclaim, 1u);
+                    } else if (v == PENDING) {
+                        wait = true;
+                    } else {
+                        d = (uint32_t)v;
+                    }
+                }
             }
         }
         __syncthreads();
-    }
-    // Dense ids: thread per entry (MT == MB).  The owner is the only inserter
-    // of its keys, so a claim (EMPTY -> PENDING) normally succeeds at once;
-    // the new ids of the whole workgroup come from ONE atomicAdd on the flow
-    // counter (a single hot address: per-flow increments would serialise).
-    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 3] = wall_clock64();
-    static_assert(MT == MB, "one merge entry per thread");
-    if (tid == 0) m_nclaim = 0;
-    __syncthreads();
-    const unsigned long long c1 = clock64();
-    const int e = tid;
-    const uint4 kk = m_key[e];
-    const bool have = (kk.w & LT_READY) != 0;
-    const uint32_t tag = kk.w & 0xFF000000u;
-    uint32_t d = FAIL, s0 = FAIL, s1 = FAIL, rank = 0;
-    bool claimed = false, wait = false;
-    unsigned long long* val = nullptr;
-    if (have) {
-        if (tag == 0xFF000000u) {
-            d = kk.x;  // MAC kernels' partials carry dense ids
-        } else if (macs) {  // a spilled MAC-kernel key: one dictionary walk per flow and owner
-            const uint4 xx = m_kx[e];
-            CKey ck;
-            mac_ckey(kk.x, kk.y, kk.z, tag, xx.x, xx.y, xx.z, ck);
-            d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
-        } else {       // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
-            unsigned long long v = EMPTY;
-            s0 = tab_slot(a.T, 0, ((uint64_t)kk.x << 32) | kk.y, true);
-            if (s0 != FAIL) s1 = tab_slot(a.T, 1, ((uint64_t)s0 << 40) | ((uint64_t)kk.z << 8) | (tag >> 24), true, &v);
-            if (s1 != FAIL) {
-                val = &a.T.tab[1][2 * s1 + 1];
-                if (v >= PENDING) v = atomicCAS(val, EMPTY, PENDING);
-                if (v == EMPTY) {
-                    claimed = true;
-                    rank = atomicAdd(&m_nclaim, 1u);
-                } else if (v == PENDING) {
-                    wait = true;
-                } else {
+        if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 7] = wall_clock64();
+        if (tid == 0) m_base = m_nclaim ? atomicAdd(a.T.n_flows, m_nclaim) : 0;
+        __syncthreads();
+        if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 6] = wall_clock64();
+        if (claimed) {
+            d = m_base + rank;
+            if (d >= a.T.fmax) {
+                atomicOr(a.T.err, ERR_FLOWS_FULL);
+                d = FAIL;
+            } else {
+                uint32_t* dst = (uint32_t*)(a.T.flow_key + (size_t)d * 56);
+    #pragma unroll
+                for (int k = 0; k < 14; k++) dst[k] = k == 0 ? kk.x : k == 4 ? kk.y : k == 8 ? kk.z : k == 9 ? tag >> 24 : 0;
+    #pragma unroll
+                for (int j = 0; j < N_TABLES; j++) a.A.slots[(size_t)d * N_TABLES + j] = j == 0 ? s0 : j == 1 ? s1 : NONE32;
+            }
+            atomicExch(val, (unsigned long long)d);
+        }
+        for (int sp = 0; sp < (1 << 20); sp++) {  // a claim held elsewhere: poll (wave-uniform)
+            if (__ballot(wait) == 0) break;
+            if (wait) {
+                const unsigned long long v = __hip_atomic_load(val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v != PENDING && v != EMPTY) {
                     d = (uint32_t)v;
+                    wait = false;
                 }
             }
+            if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(16);
         }
-    }
-    __syncthreads();
-    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 7] = wall_clock64();
-    if (tid == 0) m_base = m_nclaim ? atomicAdd(a.T.n_flows, m_nclaim) : 0;
-    __syncthreads();
-    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 6] = wall_clock64();
-    if (claimed) {
-        d = m_base + rank;
-        if (d >= a.T.fmax) {
-            atomicOr(a.T.err, ERR_FLOWS_FULL);
-            d = FAIL;
-        } else {
-            uint32_t* dst = (uint32_t*)(a.T.flow_key + (size_t)d * 56);
-#pragma unroll
-            for (int k = 0; k < 14; k++) dst[k] = k == 0 ? kk.x : k == 4 ? kk.y : k == 8 ? kk.z : k == 9 ? tag >> 24 : 0;
-#pragma unroll
-            for (int j = 0; j < N_TABLES; j++) a.A.slots[(size_t)d * N_TABLES + j] = j == 0 ? s0 : j == 1 ? s1 : NONE32;
-        }
-        atomicExch(val, (unsigned long long)d);
-    }
-    for (int sp = 0; sp < (1 << 20); sp++) {  // a claim held elsewhere: poll (wave-uniform)
-        if (__ballot(wait) == 0) break;
-        if (wait) {
-            const unsigned long long v = __hip_atomic_load(val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v != PENDING && v != EMPTY) {
-                d = (uint32_t)v;
-                wait = false;
+        if (wait) atomicOr(a.T.err, ERR_SPIN);
+        if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 4] = wall_clock64();
+        if (have && d != FAIL && d < a.T.fmax) {
+            FlowPart f;
+    #pragma unroll
+            for (int q = 0; q < 2; q++) {
+                f.pk[q] = m_pk[q][e];
+                f.by[q] = m_by[q][e];
+                f.mn[q] = m_mn[q][e];
+                f.mx[q] = m_mx[q][e];
             }
+    #pragma unroll
+            for (int q = 0; q < 8; q++) f.fl[q] = m_fl[q][e];
+            f.fa = m_fa[e];
+            f.fc = m_fc[e];
+            f.fr = m_fr[e];
+            f.la = m_la[e];
+            part_to_global(a.A, d, f);
         }
-        if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(16);
-    }
-    if (wait) atomicOr(a.T.err, ERR_SPIN);
-    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 4] = wall_clock64();
-    if (have && d != FAIL && d < a.T.fmax) {
-        FlowPart f;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            f.pk[q] = m_pk[q][e];
-            f.by[q] = m_by[q][e];
-            f.mn[q] = m_mn[q][e];
-            f.mx[q] = m_mx[q][e];
+        if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 5] = wall_clock64();
+        if (tid == 0 && a.dbg) {  // diagnostics: contended atomics, debug runs only
+            atomicAdd(&a.g->cyc_m_scan, c1 - c0);
+            atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
         }
-#pragma unroll
-        for (int q = 0; q < 8; q++) f.fl[q] = m_fl[q][e];
-        f.fa = m_fa[e];
-        f.fc = m_fc[e];
-        f.fr = m_fr[e];
-        f.la = m_la[e];
-        part_to_global(a.A, d, f);
-    }
-    if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 5] = wall_clock64();
-    if (tid == 0 && a.dbg) {  // diagnostics: contended atomics, debug runs only
-        atomicAdd(&a.g->cyc_m_scan, c1 - c0);
-        atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
+        __syncthreads();  // (the next owner re-initialises the table)
     }
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
-    if (me == gridDim.x - 1 && tid < 64) reduce_stats();
+    if (blockIdx.x == gridDim.x - 1 && tid < 64) reduce_stats();
     const bool tail_slow = n_slow_all && !a.slow_kernel;
     if (tail_slow || n_spill_all) {
         // The tail: the overflow list (spills past their owner segment's
@@ -3636,7 +3641,8 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, (i == 0 && P.nb > 1) ? c->evk_first : c->evk0,
                                     c->evk1, 0));
         const auto t1 = std::chrono::steady_clock::now();
-        k_merge_partials<<<P.owners[i], MB, 0, s>>>(a);  // + the slow list (unless k_slow takes it)
+        // at most one merge workgroup per CU, each taking owners in turn
+        k_merge_partials<<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow takes it)
         if (a.slow_kernel) k_slow<<<(unsigned)c->n_cu * 8, SB, 0, s>>>(a);
         if (hostprof) {
             const auto t2 = std::chrono::steady_clock::now();
@@ -3720,7 +3726,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
                                              : (const void*)k_parse_agg<0, false>;
         kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
         event(c->evk1);
-        kernel((const void*)k_merge_partials, P.owners[i], MB, a_agg[i]);
+        kernel((const void*)k_merge_partials, std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, a_agg[i]);
         if (P.agg[i].slow_kernel) kernel((const void*)k_slow, (unsigned)c->n_cu * 8, SB, a_agg[i]);
     }
     void* a_fin[] = {&P.fa};
