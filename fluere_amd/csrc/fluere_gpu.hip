@@ -284,8 +284,7 @@ __device__ __forceinline__ void own_set(uint32_t* arr, uint32_t o, uint32_t v) {
 }
 constexpr int OWN_WORDS = (MAX_OWNERS + 2) / 2;
 constexpr int SPILL_WG = WIN_ITERS * BLOCK;  // raw spilled packets per workgroup (one window)
-constexpr int NS_MAC = 768;
-
+constexpr int NS_MAC = 768;  // MAC kernels: slots (the key table holds LK / 2 keys + sidecars)
 
 // merge owner of a flow: the top 24 hash bits scaled to [0, O) (multiply-shift)
 __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t O) {
