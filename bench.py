@@ -96,12 +96,17 @@ def main():
     # 4 GiB each (u32 record offsets; a C4 IMIX shard is ~4.4 GB)
     batches = fluere_amd.synth_device_batches(cfg, first, n)
     torch.cuda.synchronize()
-    # N > 1: the context runs on torch's stream, so the collective of the
-    # shard exchange is ordered after the export without a host wait
+    # N > 1: the context runs on torch's current stream (a stream of its own,
+    # not the null stream, made current), so RCCL orders the shard exchange's
+    # collectives after the export without a host wait
+    stream = None
+    if world > 1:
+        ts = torch.cuda.Stream()
+        torch.cuda.set_stream(ts)
+        stream = ts.cuda_stream
     max_flows = max(1 << 16, 2 * C["flows"]) if C["kind"] != 4 else n // 2
     ctx = fluere_amd.FlowContext(timeout_ms=C.get("timeout_ms", 600000), use_mac=C["use_mac"], max_flows=max_flows,
-                                 device=local,
-                                 stream=torch.cuda.current_stream().cuda_stream if world > 1 else None)
+                                 device=local, stream=stream)
     exchange = fdist.ShardExchange(ctx) if world > 1 else None
     fdist.set_index_base(ctx, first)
     for b, o, nbytes, nb in batches:
@@ -195,6 +200,8 @@ def main():
             "records": int(n_recs),
             "records_ended": int(n_ended),
             "complex_flows": int(st.get("complex_flows", 0)) if world == 1 else None,
+            # N > 1: bytes each rank sends to the others in the merge's all-to-all
+            "exchange_bytes_per_rank": int(exchange.bytes_sent) if world > 1 else None,
             "sequential_mode": int(st.get("sequential_mode", 0)) if world == 1 else None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -25,14 +25,15 @@ CLI_PATH = os.path.join(_HERE, "fluere")
 # enum fluere_status
 OK = 0
 E_ARG, E_IO, E_PCAP, E_HIP, E_NOMEM, E_TABLE_FULL, E_UNSUPPORTED, E_STATE = range(-1, -9, -1)
+NEED_SWEEP = 1  # fluere_merge_gathered: complete the merge with the sweep composition (fluere_sweep_*)
 _ERR_NAMES = {
     E_ARG: "bad argument", E_IO: "I/O error", E_PCAP: "not a pcap capture", E_HIP: "HIP error / no GPU",
     E_NOMEM: "out of memory", E_TABLE_FULL: "flow table full",
-    E_UNSUPPORTED: "needs the hard-timeout sweep across shards (run the capture in one context)",
+    E_UNSUPPORTED: "no exact result on this path",
     E_STATE: "call order",
 }
 
-SYNTH_UDP64, SYNTH_IMIX, SYNTH_VLAN64, SYNTH_MAC64, SYNTH_TCP, SYNTH_SLOW = 0, 1, 2, 3, 4, 5
+SYNTH_UDP64, SYNTH_IMIX, SYNTH_VLAN64, SYNTH_MAC64, SYNTH_TCP, SYNTH_SLOW, SYNTH_TCP_BACKTIME = 0, 1, 2, 3, 4, 5, 6
 
 
 class FluereError(RuntimeError):
@@ -130,7 +131,7 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C fluere_amd/csrc)")
     L = ctypes.CDLL(LIB_PATH)
-    P, U64, I64, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int
+    P, U64, I64, I, U32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32
     sig = {
         "fluere_abi_version": (I, []),
         "fluere_open": (I, [ctypes.POINTER(Opts), ctypes.POINTER(P)]),
@@ -169,6 +170,17 @@ def lib() -> ctypes.CDLL:
                                      ctypes.POINTER(U64)]),
         "fluere_export_async": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, P]),
         "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, U64, ctypes.POINTER(Stats)]),
+        "fluere_sweep_pack": (I, [P, U32, P, P]),
+        "fluere_sweep_load": (I, [P, P, U32, P]),
+        "fluere_sweep_index": (I, [P, P, ctypes.POINTER(U64)]),
+        "fluere_sweep_queries": (I, [P, U32, U32, P, P, P]),
+        "fluere_sweep_answer": (I, [P, P, U64, P]),
+        "fluere_sweep_points": (I, [P, P, P]),
+        "fluere_sweep_chase": (I, [P, P, P, ctypes.POINTER(I)]),
+        "fluere_sweep_seed_requests": (I, [P, U32, P, P, P]),
+        "fluere_sweep_seeds": (I, [P, P, U64, P]),
+        "fluere_sweep_finish": (I, [P, P, ctypes.POINTER(Stats)]),
+        "fluere_get_record_order": (I, [P, P, U64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -15,6 +15,47 @@
 
 namespace fl {
 
+// One replayed packet (32 bytes).
+struct ExMeta {
+    uint64_t t, gidx;
+    uint32_t d, pkt, doct;
+    uint8_t dir, tflags, ttl, bits;  // bits: 1 create-eligible, 2 FIN or RST
+};
+static_assert(sizeof(ExMeta) == 32, "ExMeta layout");
+
+// FluereRecord seed of a creating packet (fill_seed's fields that the
+// aggregate does not give): shipped from the shard that holds the packet to
+// the key's owner in sharded Mode B.  40 bytes.
+struct Seed {
+    uint8_t src[16], dst[16];
+    uint16_t sp, dp;
+    uint8_t v6, prot, tos, pad;
+};
+static_assert(sizeof(Seed) == 40, "Seed layout");
+
+// Max segment tree over the processed packets' times (exact.hip): P leaves
+// (a power of two >= n), tree[P + k] = t_k + 1 for a processed packet k, else
+// 0.  tree_first(tree, P, k0, x): the first leaf k >= k0 whose value is >= x,
+// or ~0 -- the sweep point of an entry (k0 = its creation, x = exp + 1) in any
+// timestamp order.
+uint64_t tree_leaves(uint64_t n);
+int tree_build(uint64_t n, const ExMeta* cm, const uint8_t* pr, unsigned long long* tree, uint64_t P, hipStream_t s);
+__device__ __forceinline__ uint64_t tree_first(const unsigned long long* tree, uint64_t P, uint64_t k0,
+                                               unsigned long long x) {
+    if (k0 >= P) return ~0ull;
+    uint64_t i = P + k0;
+    if (tree[i] >= x) return k0;
+    for (;;) {
+        while (i & 1) i >>= 1;  // climb while a right child (the root ends it: i == 1 -> 0)
+        if (i == 0) return ~0ull;
+        i += 1;                 // the right sibling's subtree holds the next leaves
+        if (tree[i] >= x) {
+            while (i < P) i = tree[2 * i] >= x ? 2 * i : 2 * i + 1;
+            return i - P;
+        }
+    }
+}
+
 struct ExactJob {
     const Batch* d_batches;  // device copy of the batches
     const Batch* h_batches;  // host copy (per-batch launches)
@@ -37,6 +78,11 @@ struct ExactJob {
     fluere_flow_annex** annex;  // grown to the number of replayed flows
     uint64_t* annex_cap;
     uint32_t* annex_of;         // [fmax], NONE32 for flows without an annex (the caller fills it)
+    // Sharded Mode B owner (fluere_sweep_*): the replayed packets are the
+    // shards' (ext_n of them, capture order, d = this context's dense ids)
+    // instead of a parse of the batches.
+    const ExMeta* ext_cm = nullptr;
+    uint64_t ext_n = 0;
 };
 
 struct ExactResult {
@@ -52,5 +98,31 @@ struct ExactResult {
 // within the pass limit): the caller runs the sequential kernel; else FLUERE_E_*.
 constexpr int EXACT_FALLBACK = 1;
 int exact_run(const ExactJob& job, hipStream_t s, ExactResult* res);
+
+// exact_run in phases, for the sharded Mode B owner, whose sweep points and
+// seeds come from the shards between the phases:
+//   exact_begin   replayed packets -> sorted per key, heads, next-eligible /
+//                 next-FIN scans (the job is copied; its pointers must live on)
+//   exact_pass    one chase + members pass; fext (device, capture order): the
+//                 sweep point of every packet, or null to compute them here;
+//                 pr_out (device, may be null): processed flag per packet;
+//                 *changed: the processed set changed (Mode B)
+//   exact_seed_requests  the creating packets' indices of the instances,
+//                 ascending (req) with their instance ordinals (q)
+//   exact_finish  records; seeds (device, by instance ordinal) or null to
+//                 parse the creating packets; aux_out (device, 2 per record)
+//                 or null: Mode B records keep order_key = the ending packet's
+//                 index and aux = {0 FIN/RST | exp + 1 sweep, firing creation}
+struct ExactSession;
+int exact_begin(const ExactJob& job, hipStream_t s, ExactSession** out);
+uint64_t exact_replayed(const ExactSession* S);
+int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out, bool* changed);
+int exact_seed_requests(ExactSession* S, unsigned long long* req, uint32_t* q, uint32_t* n_inst);
+int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out);
+const ExactResult& exact_result(const ExactSession* S);
+// Every valid packet of the job's batches (its flows in J.T) as ExMeta, in
+// capture order, into cm (room for every packet); *n = how many.
+int exact_collect(const ExactJob& job, hipStream_t s, ExMeta* cm, uint64_t* n);
+void exact_free(ExactSession* S);
 
 }  // namespace fl

@@ -19,19 +19,29 @@
 // j = the first *processed* packet (valid, not SYN-gated) at or after c with
 // t_j >= exp, where it evicts whatever flow is stored under its oriented key
 // then -- the instance it created, or a later one of the same orientation (a
-// stale entry).  Within one key the entries of an orientation fire in
-// creation order when timestamps are non-decreasing, so the chase keeps one
-// FIFO per orientation.  Records leave in the reference's order: by the
-// packet that ended them, FIN/RST before the sweep, sweeps by (exp, push
-// order) -- with non-decreasing timestamps the push order.
+// stale entry).  The BTreeMap pops entries by (exp, push order) (:161-175),
+// so per key and orientation the chase keeps its pending entries in a list
+// sorted by (sweep point, exp, creation): an instance ends at the head's
+// sweep point (or its FIN/RST first).  With non-decreasing timestamps every
+// insert lands at the tail (the list is a FIFO); when timestamps go backwards
+// the sweep point is found in a max segment tree over the processed packets'
+// times (first processed packet at or after c with t >= exp), not by a binary
+// search over the times.  Records leave in the reference's order: by the
+// packet that ended them, FIN/RST before the sweep, sweeps by (exp, push order).
 //
 // Which packets are processed depends on every key's instances (a TCP packet
 // without SYN of a key with no flow is skipped and sweeps nothing), and the
 // instances depend on the sweeps: the chase is iterated from "every valid
 // packet is processed" until the processed set is stable.  The system is
 // causal in packet order, so a stable assignment is the sequential one.
-// Captures whose timestamps go backwards (or with no fixed point within the
-// pass limit) return EXACT_FALLBACK to the caller's sequential kernel.
+// Without a fixed point within the pass limit the run returns EXACT_FALLBACK
+// to the caller's sequential kernel.
+//
+// Sharded (multi-GPU) Mode B: the owner of a key holds all of its packets'
+// metadata (shipped by the shards) and runs this same chase; the sweep points
+// come from the shards that hold the packets (ChaseArgs::fext), which compute
+// them over their own processed packets and ask later shards for the rest
+// (fluere_gpu.hip, fluere_sweep_*).
 #include "exact.h"
 
 #include <hipcub/hipcub.hpp>
@@ -48,14 +58,6 @@ constexpr int MAX_PASSES = 32;
 enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2, K_LEAD = 3 };
 // shard mode: role of a run in the flow's annex
 enum : uint8_t { R_RECORD = 0, R_HEAD = 1, R_TAIL = 2, R_HEAD_TAIL = 3, R_LEAD = 4 };
-
-// One replayed packet (32 bytes).
-struct ExMeta {
-    uint64_t t, gidx;
-    uint32_t d, pkt, doct;
-    uint8_t dir, tflags, ttl, bits;  // bits: 1 create-eligible, 2 FIN or RST
-};
-static_assert(sizeof(ExMeta) == 32, "ExMeta layout");
 
 // Per-instance aggregate of update_flow's order-free fields.
 struct Agg {
@@ -143,6 +145,14 @@ __global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta, const ui
     val[k] = k;
 }
 
+// sharded Mode B owner: sort keys of the shards' packets (capture order)
+__global__ void __launch_bounds__(256) k_ex_keys(uint64_t n, const ExMeta* cm, unsigned long long* key, uint32_t* val) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    key[k] = ((unsigned long long)cm[k].d << 40) | (cm[k].gidx & M40);
+    val[k] = (uint32_t)k;
+}
+
 // ---- 2. sorted view, key heads, next-eligible / next-FIN inputs -------------
 __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const unsigned long long* skey, const uint32_t* sval,
                                                    const ExMeta* cm, ExMeta* sm, uint32_t* hf,
@@ -176,6 +186,36 @@ __global__ void __launch_bounds__(256) k_ex_proc_in(uint64_t n, const uint8_t* p
     if (k < n) npr[n - 1 - k] = pr[k] ? k : M40;
 }
 
+}  // namespace
+
+// ---- max segment tree over the processed packets' times ---------------------
+// tree[P + k] = t_k + 1 if packet k (capture order) is processed, else 0;
+// tree[i] = max(tree[2i], tree[2i + 1]).  tree_first (exact.h) walks right
+// from leaf k0 to the first leaf >= x: O(log n), any timestamp order.
+__global__ void __launch_bounds__(256) k_tree_leaves(uint64_t n, uint64_t P, const ExMeta* cm, const uint8_t* pr,
+                                                     unsigned long long* tree) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < P) tree[P + k] = (k < n && pr[k]) ? cm[k].t + 1 : 0ull;
+}
+__global__ void __launch_bounds__(256) k_tree_level(uint64_t h, unsigned long long* tree) {
+    const uint64_t i = h + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 2 * h) tree[i] = max(tree[2 * i], tree[2 * i + 1]);
+}
+int tree_build(uint64_t n, const ExMeta* cm, const uint8_t* pr, unsigned long long* tree, uint64_t P, hipStream_t s) {
+    k_tree_leaves<<<(unsigned)((P + 255) / 256), 256, 0, s>>>(n, P, cm, pr, tree);
+    for (uint64_t h = P / 2; h >= 1; h /= 2)
+        k_tree_level<<<(unsigned)((h + 255) / 256), 256, 0, s>>>(h, tree);
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+uint64_t tree_leaves(uint64_t n) {
+    uint64_t P = 1;
+    while (P < n) P *= 2;
+    return P;
+}
+
+namespace {
+
 // ---- 4. the chase: one thread per key ----------------------------------------
 struct ChaseArgs {
     uint64_t n;
@@ -188,15 +228,20 @@ struct ChaseArgs {
     int mode_b;
     uint64_t timeout_us;
     const ExMeta* cm;   // capture order (Mode B sweep points)
-    const unsigned long long* np_rev;  // next processed (reversed min-scan)
+    const unsigned long long* np_rev;  // next processed (reversed min-scan; non-decreasing times)
+    const unsigned long long* tree;    // max segment tree (times that go backwards), or null
+    uint64_t tree_P;
+    const unsigned long long* fext;    // sharded Mode B: sweep point of every packet (capture order), or null
     // out, indexed by the instance's first position
     uint32_t* sflag;
     uint32_t* iend;
     uint8_t* ikind;
     unsigned long long* ij;   // FIN: its index; sweep: the sweeping packet's index
     unsigned long long* iie;  // sweep: the index of the creation that pushed the firing entry
+    unsigned long long* iex;  // sweep: that entry's exp
     unsigned long long* ej;   // Mode B: sweep point of the entry pushed at this creation
-    uint32_t* link;           // Mode B: next pending entry of the same orientation
+    uint32_t* link;           // Mode B: pending entries of an orientation, sorted: next
+    uint32_t* plink;          //                                               previous
     // shard mode
     int shard_mode;
     uint8_t* irole;
@@ -206,9 +251,21 @@ struct ChaseArgs {
     const uint8_t* flow_key;  // TableSet::flow_key (56-byte canonical keys by dense id)
 };
 
-// first processed packet (capture-order index) k >= i_k with t_k >= exp -> its packet index
-__device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, uint32_t k0, unsigned long long exp) {
-    // lower_bound over the non-decreasing times of the valid packets
+__device__ __forceinline__ unsigned long long exp_of(uint64_t t, uint64_t timeout_us) {
+    return t + timeout_us < t ? NONE64 : t + timeout_us;  // (saturating)
+}
+
+// sweep point of the entry pushed at sorted position c: the first processed
+// packet k >= c (capture order) with t_k >= exp -> its packet index
+__device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, uint32_t c, unsigned long long exp) {
+    const uint32_t k0 = a.sval[c];
+    if (a.fext) return a.fext[k0];
+    if (exp == NONE64) return NONE64;
+    if (a.tree) {
+        const uint64_t k = tree_first(a.tree, a.tree_P, k0, exp + 1);
+        return k >= a.n ? NONE64 : a.cm[k].gidx;
+    }
+    // non-decreasing times: lower_bound, then the next processed packet
     uint64_t lo = 0, hi = a.n;
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
@@ -226,12 +283,21 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
     if (q >= a.n_keys) return;
     const uint32_t p0 = a.heads[q];
     const uint32_t pend = q + 1 < a.n_keys ? a.heads[q + 1] : (uint32_t)a.n;
-    uint32_t qh[2] = {NOPOS, NOPOS}, qt[2] = {NOPOS, NOPOS};  // pending entries per orientation (FIFO)
+    // pending expiry entries per orientation, sorted by (sweep point, exp,
+    // creation): the BTreeMap's pop order among the entries that can evict
+    // this orientation's flow (offline_fluereflows.rs:161-175)
+    uint32_t qh[2] = {NOPOS, NOPOS}, qt[2] = {NOPOS, NOPOS};
     auto drop_upto = [&](unsigned long long lim, bool inclusive) {
         for (int x = 0; x < 2; x++) {
             while (qh[x] != NOPOS && (inclusive ? a.ej[qh[x]] <= lim : a.ej[qh[x]] < lim)) qh[x] = a.link[qh[x]];
             if (qh[x] == NOPOS) qt[x] = NOPOS;
+            else a.plink[qh[x]] = NOPOS;
         }
+    };
+    // x before y in the pop order (y is the newer creation on ties)
+    auto before = [&](uint32_t x, uint32_t y) {
+        if (a.ej[x] != a.ej[y]) return a.ej[x] < a.ej[y];
+        return exp_of(a.sm[x].t, a.timeout_us) < exp_of(a.sm[y].t, a.timeout_us);
     };
     uint32_t pos = p0;
     // shard mode: from "no flow", the lead piece [p0, min(e0, f0 + 1)) and the
@@ -269,19 +335,27 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         uint32_t front = NOPOS;
         if (a.mode_b) {
             drop_upto(mc.gidx, false);  // entries that fired while the key had no flow
-            const unsigned long long exp =
-                mc.t + a.timeout_us < mc.t ? NONE64 : mc.t + a.timeout_us;  // (saturating)
-            a.ej[c] = sweep_point(a, a.sval[c], exp);
-            a.link[c] = NOPOS;
-            if (qh[o] == NOPOS) qh[o] = qt[o] = c;
-            else { a.link[qt[o]] = c; qt[o] = c; }
+            a.ej[c] = sweep_point(a, c, exp_of(mc.t, a.timeout_us));
+            // sorted insert, from the tail (non-decreasing times: at the tail)
+            uint32_t p = qt[o];
+            while (p != NOPOS && before(c, p)) p = a.plink[p];
+            a.plink[c] = p;
+            if (p == NOPOS) {
+                a.link[c] = qh[o];
+                qh[o] = c;
+            } else {
+                a.link[c] = a.link[p];
+                a.link[p] = c;
+            }
+            if (a.link[c] == NOPOS) qt[o] = c;
+            else a.plink[a.link[c]] = c;
             front = qh[o];
             jf = a.ej[front];
         }
         const unsigned long long fe = a.nf_rev[a.n - 1 - c] & M40;
         uint32_t end;
         uint8_t kind;
-        unsigned long long cj = NONE64, cie = 0;
+        unsigned long long cj = NONE64, cie = 0, cex = 0;
         if (fe != M40 && (jf == NONE64 || a.sm[fe].gidx <= jf)) {  // FIN/RST first (the sweep runs after it)
             end = (uint32_t)fe;
             kind = K_FIN;
@@ -297,6 +371,7 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
             kind = K_SWEEP;
             cj = jf;
             cie = a.sm[front].gidx;
+            cex = exp_of(a.sm[front].t, a.timeout_us);
         } else {
             end = pend - 1;
             kind = K_ACTIVE;
@@ -306,6 +381,7 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         a.ikind[c] = kind;
         a.ij[c] = cj;
         a.iie[c] = cie;
+        a.iex[c] = cex;
         if (a.shard_mode) {
             const bool head = n_inst == 0 && (f0 == M40 || c <= f0);
             const bool tail = kind == K_ACTIVE;
@@ -359,17 +435,20 @@ struct RecArgs {
     const uint8_t* ikind;
     const unsigned long long* ij;
     const unsigned long long* iie;
+    const unsigned long long* iex;
     Glob* g;
     fluere_record* out;      // Mode A: the run's records (appended)
     uint64_t out_cap;
     fluere_record* tmp;      // Mode B: by instance, ordered afterwards
     unsigned long long* hi;  // Mode B order: (sweeping / closing index, phase)
     unsigned long long* lo;  //               (the firing entry's creation index)
+    unsigned long long* ex;  //               (the firing entry's exp; between hi and lo)
     uint32_t* idx;
     int shard_mode;
     const uint8_t* irole;
     const uint32_t* ikey;
     fluere_flow_annex* annex;
+    const Seed* seeds;       // sharded Mode B: FluereRecord seed of each instance's creating packet
 };
 
 __device__ __forceinline__ void piece_of(const Agg& g, fluere_flow_piece& pc) {
@@ -390,7 +469,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
     memset(&rec, 0, sizeof rec);
     uint32_t q = 0;
     uint8_t kind = K_ACTIVE;
-    unsigned long long cj = NONE64, cie = 0;
+    unsigned long long cj = NONE64, cie = 0, cex = 0;
     if (lane_live && a.shard_mode && a.irole[a.ist[a.ukeys[r]]] != R_RECORD) {
         // a piece of the flow's annex (lead / head / tail), not a record
         const uint32_t c = a.ist[a.ukeys[r]];
@@ -423,9 +502,17 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
         q = a.ukeys[r];
         const uint32_t c = a.ist[q];
         const ExMeta mc = a.sm[c];
-        Parsed P;
-        parse_global(a.bs, a.nb, mc.gidx, a.macs != 0, P);
-        fill_seed(rec, P);
+        if (a.seeds) {  // sharded Mode B: the creating packet is on another shard
+            const Seed sd = a.seeds[q];
+            for (int k = 0; k < 16; k++) { rec.source[k] = sd.src[k]; rec.destination[k] = sd.dst[k]; }
+            rec.src_v6 = rec.dst_v6 = sd.v6;
+            rec.prot = sd.prot; rec.tos = sd.tos; rec.src_port = sd.sp; rec.dst_port = sd.dp;
+            rec.first = mc.t;
+        } else {
+            Parsed P;
+            parse_global(a.bs, a.nb, mc.gidx, a.macs != 0, P);
+            fill_seed(rec, P);
+        }
         const Agg g = a.aggs[r];
         const uint32_t o = mc.dir;  // orientation of the creating packet
         rec.d_pkts = g.pk[0] + g.pk[1];
@@ -444,6 +531,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
         kind = a.ikind[c];
         cj = a.ij[c];
         cie = a.iie[c];
+        cex = a.iex[c];
         rec.order_key = kind == K_ACTIVE ? NONE64 : cj;
     }
     if (!a.mode_b) {  // (uniform: every thread of the block emits)
@@ -454,6 +542,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
         a.tmp[q] = rec;
         a.hi[q] = kind == K_ACTIVE ? NONE64 : (cj << 1) | (kind == K_SWEEP ? 1ull : 0ull);
         a.lo[q] = kind == K_SWEEP ? cie : 0ull;
+        a.ex[q] = kind == K_SWEEP ? cex : 0ull;
         a.idx[q] = q;
     }
 }
@@ -472,6 +561,44 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_emit_sorted(uint32_t n_inst, 
         memset(&rec, 0, sizeof rec);
     }
     emit_record_block(S, g, out, cap, rec, live);
+}
+
+// sharded Mode B: records in the reference's order at fixed positions; the
+// order stays global (order_key = the ending packet's index, aux = {0 for a
+// FIN/RST close, else exp + 1; the firing entry's creation}) so the records of
+// every owner merge by (order_key, aux) (fluere_get_record_order)
+__global__ void __launch_bounds__(256) k_ex_emit_owner(uint32_t n_inst, const uint32_t* perm, const fluere_record* tmp,
+                                                       const unsigned long long* hi, const unsigned long long* ex,
+                                                       const unsigned long long* lo, Glob* g, fluere_record* out,
+                                                       unsigned long long* aux) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = r < n_inst;
+    unsigned long long upd = 0, ended = 0;
+    if (live) {
+        const uint32_t q = perm[r];
+        const fluere_record rec = tmp[q];
+        out[r] = rec;
+        const unsigned long long h = hi[q];
+        aux[2 * r] = h == NONE64 ? 0ull : ((h & 1) ? ex[q] + 1 : 0ull);
+        aux[2 * r + 1] = h == NONE64 ? 0ull : lo[q];
+        upd = rec.d_pkts;
+        ended = rec.order_key != NONE64;
+    }
+    upd = wave_sum(upd);
+    ended = wave_sum(ended);
+    if ((threadIdx.x & 63) == 0) {
+        if (upd) atomicAdd(&g->n_updates, upd);
+        if (ended) atomicAdd(&g->n_ended, ended);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ex_seed_req(uint32_t n_inst, const uint32_t* ist, const ExMeta* sm,
+                                                     unsigned long long* req, uint32_t* q) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_inst) {
+        req[i] = sm[ist[i]].gidx;
+        q[i] = i;
+    }
 }
 
 __global__ void __launch_bounds__(256) k_ex_gather_u64(uint32_t m, const uint32_t* id, const unsigned long long* h,
@@ -497,14 +624,47 @@ struct Arena {
 
 }  // namespace
 
-int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
-    ExactResult R{};
+// One exact run, in phases (exact.h): the arena views and the host state
+// between them.
+struct ExactSession {
+    ExactJob J;
+    hipStream_t s;
+    ExactResult R;
+    uint64_t N = 0, n = 0;
+    uint32_t n_keys = 0, n_inst = 0;
+    bool mono = true;
+    size_t tmp = 0;
+    void* tp = nullptr;
+    ExMeta *cm, *sm;
+    unsigned long long *key, *skey, *re, *rf, *ne_rev, *nf_rev, *npr, *np_rev, *ej, *ij, *iie, *iex;
+    unsigned long long *hi, *lo, *ex, *hi2, *gk, *tree;
+    unsigned long long nrec_new = 0;
+    uint64_t tree_P = 0;
+    uint32_t *val, *sval, *hf, *hpos, *heads, *link, *plink, *sflag, *iend, *incl, *ist, *rk, *ukeys, *ctr;
+    uint32_t *idx, *idx2, *perm, *ikey;
+    uint8_t *pr, *ikind, *irole;
+    Agg* aggs;
+    fluere_record* tmpr;
+    fluere_flow_annex* annex = nullptr;
+    ChaseArgs ca;
+};
+
+void exact_free(ExactSession* S) { delete S; }
+
+int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
+    *out = nullptr;
     uint64_t N = 0;
-    for (int b = 0; b < J.nb; b++) N += J.h_batches[b].n;
-    if (!N) {
-        if (res) *res = R;
-        return FLUERE_OK;
-    }
+    if (J.ext_cm) N = J.ext_n;
+    else
+        for (int b = 0; b < J.nb; b++) N += J.h_batches[b].n;
+    ExactSession* S = new (std::nothrow) ExactSession();
+    if (!S) return FLUERE_E_NOMEM;
+    S->J = J;
+    S->s = s;
+    S->N = N;
+    *out = S;
+    if (!N) return FLUERE_OK;
+    const uint64_t P = J.mode_b ? tree_leaves(N) : 1;
     // ---- arena sizing: phase 1 (all packets) + phase 2 (replayed packets, at most N)
     auto bytes_for = [&](uint64_t n_all, uint64_t n, size_t tmp) {
         size_t b = 0;
@@ -515,12 +675,16 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
         add(n * 4); add(n * 4); add(n * 4);                           // hf, hpos, heads
         add(n * 8); add(n * 8); add(n * 8); add(n * 8);               // re, rf, ne_rev, nf_rev
         add(n); add(n * 8); add(n * 8); add(n * 8); add(n * 4);       // pr, npr, np_rev, ej, link
+        add(n * 4);                                                   // plink
         add(n * 4); add(n * 4); add(n); add(n * 8); add(n * 8);       // sflag, iend, ikind, ij, iie
+        add(n * 8);                                                   // iex
         add(n * 4); add(n * 4); add(n * 4); add(n * 4);               // incl, ist, rk, ukeys
         add(n * sizeof(Agg)); add(16);                                // aggs, nruns/counters
         add(n * sizeof(fluere_record)); add(n * 8); add(n * 8);       // tmp, hi, lo
+        add(n * 8); add(n * 8);                                       // ex, gk
         add(n * 4); add(n * 4); add(n * 8); add(n * 4);               // idx, idx2, hi2, perm
         add(n); add(n * 4);                                           // irole, ikey
+        if (J.mode_b) add(2 * P * 8);                                 // tree
         add(tmp);
         return b;
     };
@@ -542,6 +706,7 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
                                           (uint32_t*)nullptr, AggOp(), n, s);
         tmp = std::max(tmp, t);
     }
+    S->tmp = tmp;
     const size_t need = bytes_for(N, N, tmp);
     if (need > *J.scratch_bytes) {
         hipFree(*J.scratch);
@@ -557,68 +722,80 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     uint32_t* flag = A.take<uint32_t>(N);
     uint32_t* pos = A.take<uint32_t>(N);
     // ---- 1. metadata of every packet to replay, compacted in capture order
-    uint64_t off = 0;
-    for (int b = 0; b < J.nb; b++) {
-        const Batch& B = J.h_batches[b];
-        if (!B.n) continue;
-        k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, meta, flag, off);
-        off += B.n;
+    if (!J.ext_cm) {
+        uint64_t off = 0;
+        for (int b = 0; b < J.nb; b++) {
+            const Batch& B = J.h_batches[b];
+            if (!B.n) continue;
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, meta, flag, off);
+            off += B.n;
+        }
     }
-    void* tp = nullptr;
     size_t tb = tmp;
-    ExMeta* cm = A.take<ExMeta>(N);
-    unsigned long long* key = A.take<unsigned long long>(N);
-    uint32_t* val = A.take<uint32_t>(N);
-    unsigned long long* skey = A.take<unsigned long long>(N);
-    uint32_t* sval = A.take<uint32_t>(N);
-    ExMeta* sm = A.take<ExMeta>(N);
-    uint32_t* hf = A.take<uint32_t>(N);
-    uint32_t* hpos = A.take<uint32_t>(N);
-    uint32_t* heads = A.take<uint32_t>(N);
-    unsigned long long* re = A.take<unsigned long long>(N);
-    unsigned long long* rf = A.take<unsigned long long>(N);
-    unsigned long long* ne_rev = A.take<unsigned long long>(N);
-    unsigned long long* nf_rev = A.take<unsigned long long>(N);
-    uint8_t* pr = A.take<uint8_t>(N);
-    unsigned long long* npr = A.take<unsigned long long>(N);
-    unsigned long long* np_rev = A.take<unsigned long long>(N);
-    unsigned long long* ej = A.take<unsigned long long>(N);
-    uint32_t* link = A.take<uint32_t>(N);
-    uint32_t* sflag = A.take<uint32_t>(N);
-    uint32_t* iend = A.take<uint32_t>(N);
-    uint8_t* ikind = A.take<uint8_t>(N);
-    unsigned long long* ij = A.take<unsigned long long>(N);
-    unsigned long long* iie = A.take<unsigned long long>(N);
-    uint32_t* incl = A.take<uint32_t>(N);
-    uint32_t* ist = A.take<uint32_t>(N);
-    uint32_t* rk = A.take<uint32_t>(N);
-    uint32_t* ukeys = A.take<uint32_t>(N);
-    Agg* aggs = A.take<Agg>(N);
-    uint32_t* ctr = A.take<uint32_t>(4);  // [0] nruns, [1] non-monotonic, [2] changed
-    fluere_record* tmpr = A.take<fluere_record>(N);
-    unsigned long long* hi = A.take<unsigned long long>(N);
-    unsigned long long* lo = A.take<unsigned long long>(N);
-    uint32_t* idx = A.take<uint32_t>(N);
-    uint32_t* idx2 = A.take<uint32_t>(N);
-    unsigned long long* hi2 = A.take<unsigned long long>(N);
-    uint32_t* perm = A.take<uint32_t>(N);
-    uint8_t* irole = A.take<uint8_t>(N);
-    uint32_t* ikey = A.take<uint32_t>(N);
-    tp = A.take<char>(tmp);
-    const int iN = (int)N;
-    HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, iN, s));
-    uint32_t last[2] = {0, 0};
-    HIPCHECK(hipMemcpyAsync(&last[0], pos + N - 1, 4, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(&last[1], flag + N - 1, 4, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    const uint64_t n = (uint64_t)last[0] + last[1];
-    R.replayed = n;
-    if (!n) {
-        if (res) *res = R;
-        return FLUERE_OK;
+    ExMeta* cm = S->cm = A.take<ExMeta>(N);
+    unsigned long long* key = S->key = A.take<unsigned long long>(N);
+    uint32_t* val = S->val = A.take<uint32_t>(N);
+    unsigned long long* skey = S->skey = A.take<unsigned long long>(N);
+    uint32_t* sval = S->sval = A.take<uint32_t>(N);
+    ExMeta* sm = S->sm = A.take<ExMeta>(N);
+    uint32_t* hf = S->hf = A.take<uint32_t>(N);
+    uint32_t* hpos = S->hpos = A.take<uint32_t>(N);
+    uint32_t* heads = S->heads = A.take<uint32_t>(N);
+    unsigned long long* re = S->re = A.take<unsigned long long>(N);
+    unsigned long long* rf = S->rf = A.take<unsigned long long>(N);
+    unsigned long long* ne_rev = S->ne_rev = A.take<unsigned long long>(N);
+    unsigned long long* nf_rev = S->nf_rev = A.take<unsigned long long>(N);
+    uint8_t* pr = S->pr = A.take<uint8_t>(N);
+    S->npr = A.take<unsigned long long>(N);
+    S->np_rev = A.take<unsigned long long>(N);
+    S->ej = A.take<unsigned long long>(N);
+    S->link = A.take<uint32_t>(N);
+    S->plink = A.take<uint32_t>(N);
+    S->sflag = A.take<uint32_t>(N);
+    S->iend = A.take<uint32_t>(N);
+    S->ikind = A.take<uint8_t>(N);
+    S->ij = A.take<unsigned long long>(N);
+    S->iie = A.take<unsigned long long>(N);
+    S->iex = A.take<unsigned long long>(N);
+    S->incl = A.take<uint32_t>(N);
+    S->ist = A.take<uint32_t>(N);
+    S->rk = A.take<uint32_t>(N);
+    S->ukeys = A.take<uint32_t>(N);
+    S->aggs = A.take<Agg>(N);
+    uint32_t* ctr = S->ctr = A.take<uint32_t>(4);  // [0] nruns, [1] non-monotonic, [2] changed
+    S->tmpr = A.take<fluere_record>(N);
+    S->hi = A.take<unsigned long long>(N);
+    S->lo = A.take<unsigned long long>(N);
+    S->ex = A.take<unsigned long long>(N);
+    S->gk = A.take<unsigned long long>(N);
+    S->idx = A.take<uint32_t>(N);
+    S->idx2 = A.take<uint32_t>(N);
+    S->hi2 = A.take<unsigned long long>(N);
+    S->perm = A.take<uint32_t>(N);
+    S->irole = A.take<uint8_t>(N);
+    S->ikey = A.take<uint32_t>(N);
+    S->tree = J.mode_b ? A.take<unsigned long long>(2 * P) : nullptr;
+    S->tree_P = P;
+    void* tp = S->tp = A.take<char>(tmp);
+    uint64_t n;
+    if (J.ext_cm) {  // sharded Mode B owner: the shards' packets, already in capture order
+        n = N;
+        HIPCHECK(hipMemcpyAsync(cm, J.ext_cm, n * sizeof(ExMeta), hipMemcpyDeviceToDevice, s));
+        k_ex_keys<<<gridn(n, 256), 256, 0, s>>>(n, cm, key, val);
+    } else {
+        const int iN = (int)N;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, iN, s));
+        uint32_t last[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&last[0], pos + N - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipMemcpyAsync(&last[1], flag + N - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        n = (uint64_t)last[0] + last[1];
+        if (n) k_ex_compact<<<gridn(N, 256), 256, 0, s>>>(meta, flag, pos, N, cm, key, val);
     }
+    S->n = n;
+    S->R.replayed = n;
+    if (!n) return FLUERE_OK;
     const int in = (int)n;
-    k_ex_compact<<<gridn(N, 256), 256, 0, s>>>(meta, flag, pos, N, cm, key, val);
     // ---- 2. sort by (key, index); key heads; next eligible / FIN-RST
     int end_bit = 40;
     while (end_bit < 64 && (1ull << (end_bit - 40)) <= J.T.fmax) end_bit++;
@@ -632,6 +809,7 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     tb = tmp;
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, hf, hpos, in, s));
     k_ex_heads<<<gridn(n, 256), 256, 0, s>>>(n, hf, hpos, heads);
+    uint32_t last[2] = {0, 0};
     HIPCHECK(hipMemcpyAsync(&last[0], hpos + n - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipMemcpyAsync(&last[1], hf + n - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipMemsetAsync(ctr, 0, 16, s));
@@ -642,56 +820,103 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     uint32_t mono_bad = 0;
     HIPCHECK(hipMemcpyAsync(&mono_bad, ctr + 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
-    const uint32_t n_keys = last[0] + last[1];
-    R.keys = n_keys;
-    if (J.mode_b && mono_bad) return EXACT_FALLBACK;
-    fluere_flow_annex* annex = nullptr;
+    S->n_keys = last[0] + last[1];
+    S->R.keys = S->n_keys;
+    S->mono = !mono_bad;
     if (J.shard_mode) {
-        if (n_keys > *J.annex_cap) {
+        if (S->n_keys > *J.annex_cap) {
             hipFree(*J.annex);
             *J.annex = nullptr;
             *J.annex_cap = 0;
-            if (hipMalloc(J.annex, (size_t)n_keys * sizeof(fluere_flow_annex)) != hipSuccess) return FLUERE_E_NOMEM;
-            *J.annex_cap = n_keys;
+            if (hipMalloc(J.annex, (size_t)S->n_keys * sizeof(fluere_flow_annex)) != hipSuccess) return FLUERE_E_NOMEM;
+            *J.annex_cap = S->n_keys;
         }
-        annex = *J.annex;
-        R.annexes = n_keys;
+        S->annex = *J.annex;
+        S->R.annexes = S->n_keys;
     }
-    ChaseArgs ca{n, n_keys, heads, sm, sval, ne_rev, nf_rev, J.mode_b, J.timeout_us, cm, np_rev,
-                 sflag, iend, ikind, ij, iie, ej, link,
-                 J.shard_mode, irole, ikey, annex, J.annex_of, J.T.flow_key};
-    // ---- 3..5. chase (Mode B: until the processed set is stable)
-    for (int pass = 0;; pass++) {
-        if (pass == MAX_PASSES) return EXACT_FALLBACK;
-        R.iterations = pass + 1;
-        if (J.mode_b) {
-            k_ex_proc_in<<<gridn(n, 256), 256, 0, s>>>(n, pr, npr);
-            tb = tmp;
-            HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, npr, np_rev, hipcub::Min(), in, s));
+    S->ca = ChaseArgs{n, S->n_keys, heads, sm, sval, ne_rev, nf_rev, J.mode_b, J.timeout_us, cm, S->np_rev,
+                      (J.mode_b && !S->mono) ? S->tree : nullptr, P, nullptr,
+                      S->sflag, S->iend, S->ikind, S->ij, S->iie, S->iex, S->ej, S->link, S->plink,
+                      J.shard_mode, S->irole, S->ikey, S->annex, J.annex_of, J.T.flow_key};
+    return FLUERE_OK;
+}
+
+uint64_t exact_replayed(const ExactSession* S) { return S ? S->n : 0; }
+
+int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out, bool* changed) {
+    const ExactJob& J = S->J;
+    hipStream_t s = S->s;
+    const uint64_t n = S->n;
+    if (changed) *changed = false;
+    if (!n) return FLUERE_OK;
+    const int in = (int)n;
+    size_t tb;
+    S->R.iterations++;
+    S->ca.fext = fext;
+    if (J.mode_b && !fext) {  // the sweep-point index over this pass's processed packets
+        if (S->mono) {
+            k_ex_proc_in<<<gridn(n, 256), 256, 0, s>>>(n, S->pr, S->npr);
+            tb = S->tmp;
+            HIPCHECK(hipcub::DeviceScan::InclusiveScan(S->tp, tb, S->npr, S->np_rev, hipcub::Min(), in, s));
+        } else {
+            int rc = tree_build(n, S->cm, S->pr, S->tree, S->tree_P, s);
+            if (rc) return rc;
         }
-        HIPCHECK(hipMemsetAsync(sflag, 0, n * 4, s));
-        k_ex_chase<<<gridn(n_keys, 64), 64, 0, s>>>(ca);
-        tb = tmp;
-        HIPCHECK(hipcub::DeviceScan::InclusiveSum(tp, tb, sflag, incl, in, s));
-        k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, sflag, incl, ist);
-        HIPCHECK(hipMemsetAsync(ctr + 2, 0, 4, s));
-        k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, incl, ist, iend, rk, sval, J.mode_b ? pr : nullptr, ctr + 2);
-        HIPCHECK(hipGetLastError());
-        if (!J.mode_b) break;
-        uint32_t changed = 0;
-        HIPCHECK(hipMemcpyAsync(&changed, ctr + 2, 4, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
-        if (!changed) break;
     }
+    HIPCHECK(hipMemsetAsync(S->sflag, 0, n * 4, s));
+    k_ex_chase<<<gridn(S->n_keys, 64), 64, 0, s>>>(S->ca);
+    tb = S->tmp;
+    HIPCHECK(hipcub::DeviceScan::InclusiveSum(S->tp, tb, S->sflag, S->incl, in, s));
+    k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->incl, S->ist);
+    HIPCHECK(hipMemsetAsync(S->ctr + 2, 0, 4, s));
+    k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->rk, S->sval,
+                                                J.mode_b ? S->pr : nullptr, S->ctr + 2);
+    HIPCHECK(hipGetLastError());
+    if (pr_out) HIPCHECK(hipMemcpyAsync(pr_out, S->pr, n, hipMemcpyDeviceToDevice, s));
+    if (!J.mode_b) return FLUERE_OK;
+    uint32_t ch = 0;
+    HIPCHECK(hipMemcpyAsync(&ch, S->ctr + 2, 4, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (changed) *changed = ch != 0;
+    return FLUERE_OK;
+}
+
+int exact_seed_requests(ExactSession* S, unsigned long long* req, uint32_t* q, uint32_t* n_inst) {
+    hipStream_t s = S->s;
+    *n_inst = 0;
+    if (!S->n) return FLUERE_OK;
+    uint32_t ni = 0;
+    HIPCHECK(hipMemcpyAsync(&ni, S->incl + S->n - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    S->n_inst = ni;
+    if (ni) {
+        // (creation index, instance) sorted by index: grouped by holder shard
+        k_ex_seed_req<<<gridn(ni, 256), 256, 0, s>>>(ni, S->ist, S->sm, S->hi2, S->idx);
+        size_t tb = S->tmp;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->hi2, req, S->idx, q, (int)ni, 0, 64, s));
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    *n_inst = ni;
+    return FLUERE_OK;
+}
+
+int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out) {
+    const ExactJob& J = S->J;
+    hipStream_t s = S->s;
+    const uint64_t n = S->n;
+    if (!n) return FLUERE_OK;
+    const int in = (int)n;
+    size_t tb;
     uint32_t n_inst = 0;
-    HIPCHECK(hipMemcpyAsync(&n_inst, incl + n - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(&n_inst, S->incl + n - 1, 4, hipMemcpyDeviceToHost, s));
     // ---- 6. per-instance aggregates (segmented over the sorted packets)
     hipcub::CountingInputIterator<uint32_t> cnt(0);
-    hipcub::TransformInputIterator<Agg, ToAgg, hipcub::CountingInputIterator<uint32_t>> vit(cnt, ToAgg{sm});
-    tb = tmp;
-    HIPCHECK(hipcub::DeviceReduce::ReduceByKey(tp, tb, rk, ukeys, vit, aggs, ctr, AggOp(), in, s));
+    hipcub::TransformInputIterator<Agg, ToAgg, hipcub::CountingInputIterator<uint32_t>> vit(cnt, ToAgg{S->sm});
+    tb = S->tmp;
+    HIPCHECK(hipcub::DeviceReduce::ReduceByKey(S->tp, tb, S->rk, S->ukeys, vit, S->aggs, S->ctr, AggOp(), in, s));
     HIPCHECK(hipStreamSynchronize(s));
-    R.instances = n_inst;
+    S->R.instances = n_inst;
     // ---- 7. records
     Glob gh;
     HIPCHECK(hipMemcpyAsync(&gh, J.g, sizeof gh, hipMemcpyDeviceToHost, s));
@@ -707,25 +932,102 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
         *J.d_recs = nr;
         *J.d_recs_cap = want;
     }
-    RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, ukeys, aggs, ctr, ist, sm, iend, ikind, ij, iie, J.g,
-               *J.d_recs, *J.d_recs_cap, tmpr, hi, lo, idx, J.shard_mode, irole, ikey, annex};
+    RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, S->ukeys, S->aggs, S->ctr, S->ist, S->sm, S->iend, S->ikind,
+               S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, S->tmpr, S->hi, S->lo, S->ex, S->idx,
+               J.shard_mode, S->irole, S->ikey, S->annex, seeds};
     // runs <= n (every run holds a packet)
     k_ex_records<<<gridn(n, 256), 256, 0, s>>>(ra);
     if (J.mode_b && n_inst) {
-        // order by (closing / sweeping index, phase), then the firing entry's creation
+        // order by (closing / sweeping index, phase), then the firing entry's
+        // (exp, creation): stable radix sorts from the last key to the first
         const int ni = (int)n_inst;
-        tb = tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tp, tb, lo, hi2 /* lo sorted (unused) */, idx, idx2, ni, 0, 64, s));
-        // hi in lo-sorted order
-        k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, idx2, hi, lo);
-        tb = tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tp, tb, lo, hi2, idx2, perm, ni, 0, 64, s));
-        k_ex_emit_sorted<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, perm, tmpr, J.g, *J.d_recs, *J.d_recs_cap);
+        uint32_t* cur = S->idx;   // permutation so far (k_ex_records: the identity)
+        uint32_t* nxt = S->idx2;
+        tb = S->tmp;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->lo, S->hi2, cur, nxt, ni, 0, 64, s));
+        std::swap(cur, nxt);
+        if (!S->mono) {  // exp order differs from creation order only when times go backwards
+            k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, cur, S->ex, S->gk);
+            tb = S->tmp;
+            HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->gk, S->hi2, cur, nxt, ni, 0, 64, s));
+            std::swap(cur, nxt);
+        }
+        k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, cur, S->hi, S->gk);
+        tb = S->tmp;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->gk, S->hi2, cur, S->perm, ni, 0, 64, s));
+        if (aux_out) {
+            k_ex_emit_owner<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->perm, S->tmpr, S->hi, S->ex, S->lo,
+                                                               J.g, *J.d_recs + gh.n_rec, aux_out);
+            S->nrec_new = gh.n_rec + n_inst;
+            HIPCHECK(hipMemcpyAsync(reinterpret_cast<char*>(J.g) + offsetof(Glob, n_rec), &S->nrec_new, 8,
+                                    hipMemcpyHostToDevice, s));
+        } else {
+            k_ex_emit_sorted<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->perm, S->tmpr, J.g, *J.d_recs, *J.d_recs_cap);
+        }
     }
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(s));
-    if (res) *res = R;
     return FLUERE_OK;
+}
+
+const ExactResult& exact_result(const ExactSession* S) { return S->R; }
+
+int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out) {
+    *n_out = 0;
+    uint64_t N = 0;
+    for (int b = 0; b < J.nb; b++) N += J.h_batches[b].n;
+    if (!N) return FLUERE_OK;
+    ExMeta* meta = nullptr;
+    uint32_t *flag = nullptr, *pos = nullptr;
+    unsigned long long* key = nullptr;
+    uint32_t* val = nullptr;
+    void* tp = nullptr;
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)N, s);
+    int rc = FLUERE_OK;
+    if (hipMalloc(&meta, N * sizeof(ExMeta)) != hipSuccess || hipMalloc(&flag, N * 4) != hipSuccess ||
+        hipMalloc(&pos, N * 4) != hipSuccess || hipMalloc(&key, N * 8) != hipSuccess ||
+        hipMalloc(&val, N * 4) != hipSuccess || hipMalloc(&tp, std::max<size_t>(tb, 16)) != hipSuccess)
+        rc = FLUERE_E_NOMEM;
+    if (rc == FLUERE_OK) {
+        uint64_t off = 0;
+        for (int b = 0; b < J.nb; b++) {
+            const Batch& B = J.h_batches[b];
+            if (!B.n) continue;
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, meta, flag, off);
+            off += B.n;
+        }
+        uint32_t last[2] = {0, 0};
+        if (hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, (int)N, s) != hipSuccess ||
+            hipMemcpyAsync(&last[0], pos + N - 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(&last[1], flag + N - 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = FLUERE_E_HIP;
+        else {
+            k_ex_compact<<<gridn(N, 256), 256, 0, s>>>(meta, flag, pos, N, cm, key, val);
+            if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) rc = FLUERE_E_HIP;
+            *n_out = (uint64_t)last[0] + last[1];
+        }
+    }
+    hipFree(meta); hipFree(flag); hipFree(pos); hipFree(key); hipFree(val); hipFree(tp);
+    return rc;
+}
+
+int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
+    ExactSession* S = nullptr;
+    int rc = exact_begin(J, s, &S);
+    for (int pass = 0; rc == FLUERE_OK && S->n; pass++) {
+        if (pass == MAX_PASSES) {
+            rc = EXACT_FALLBACK;
+            break;
+        }
+        bool changed = false;
+        rc = exact_pass(S, nullptr, nullptr, &changed);
+        if (!J.mode_b || !changed) break;
+    }
+    if (rc == FLUERE_OK && S->n) rc = exact_finish(S, nullptr, nullptr);
+    if (res && S) *res = S->R;
+    exact_free(S);
+    return rc;
 }
 
 }  // namespace fl

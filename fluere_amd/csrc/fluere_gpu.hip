@@ -2300,6 +2300,7 @@ struct ExportArgs {
     uint64_t cap, cap_annex, block_bytes;
     const uint32_t* annex_of;
     const fluere_flow_annex* annex;
+    uint32_t* sumpos;  // [fmax]: each flow's summary position in its owner's block (the sweep's packet tags)
 };
 __device__ __forceinline__ fluere_shard_header* blk_hdr(uint8_t* blocks, uint64_t block_bytes, uint32_t o) {
     return reinterpret_cast<fluere_shard_header*>(blocks + (size_t)o * block_bytes);
@@ -2341,6 +2342,7 @@ __global__ void __launch_bounds__(256) k_export_owners(ExportArgs a) {
             }
         }
         if (pos < a.cap) blk_sum(a.blocks, a.block_bytes, o)[pos] = s;
+        a.sumpos[d] = (uint32_t)pos;
     }
 }
 
@@ -2358,10 +2360,14 @@ __global__ void k_export_need(ExportArgs a, unsigned long long* need, unsigned l
     need[0] = m0;
     need[1] = m1;
     if (info) {
+        const Glob* g = a.fa.g;
         info[0] = m0;
         info[1] = m1;
-        info[2] = a.fa.g->n_complex;
+        info[2] = g->n_complex;
         info[3] = min(*a.fa.T.n_flows, a.fa.T.fmax);
+        // the capture span, reducible with MAX: 2^62 - tmin and tmax (0: no valid packet)
+        info[4] = g->valid ? (1ull << 62) - g->tmin : 0ull;
+        info[5] = g->valid ? g->tmax : 0ull;
     }
 }
 
@@ -2388,6 +2394,7 @@ struct MergeArgs {
     unsigned long long cap, cap_annex, block_bytes;
     Ctl* host_ctl;   // non-null: k_merge_finalize publishes the counters (publish_ctl)
     uint32_t seq;
+    unsigned long long timeout_us;
 };
 
 // summary i of a merge; null when absent
@@ -2489,7 +2496,11 @@ __device__ __forceinline__ void merge_finalize_one(const MergeArgs& a, uint32_t 
 
 // grid-stride over the flows counted on the device (no host round trip)
 __global__ void __launch_bounds__(EMIT_BLOCK) k_merge_finalize(MergeArgs a) {
-    const uint32_t nf = min(*a.T.n_flows, a.T.fmax);
+    // a capture whose span reaches the timeout: no record here, the sweep
+    // composition (fluere_sweep_*) builds them all
+    const Glob* g = a.g;
+    const bool expiry = g->valid && g->tmax >= g->tmin && g->tmax - g->tmin >= a.timeout_us;
+    const uint32_t nf = expiry ? 0u : min(*a.T.n_flows, a.T.fmax);
     __shared__ EmitLds S;
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
         const uint32_t d = d0 + threadIdx.x;
@@ -2753,7 +2764,15 @@ struct fluere_ctx {
     fluere_flow_annex* d_annex = nullptr;
     uint64_t d_annex_cap = 0;
     uint32_t* d_annex_of = nullptr;
+    uint32_t* d_sumpos = nullptr;                // [fmax] summary position of each flow in its owner's block
     void* d_need = nullptr;
+    uint64_t merge_cap = 0;                      // the last merge's block capacity and shard count
+    uint32_t merge_shards = 0;
+    struct SweepState* sw = nullptr;             // sharded Mode B (fluere_sweep_*)
+    unsigned long long* d_recaux = nullptr;      // sharded Mode B: 2 order words per record
+    uint64_t d_recaux_cap = 0;
+    bool has_aux = false;                        // the results carry order words (d_recaux)
+    std::vector<unsigned long long> aux;         // host copy, in the order of recs
     uint64_t local_n_rec = 0, local_updates = 0, local_ended = 0;
     size_t d_stage_bytes = 0;
     bool generic_dirty = false;
@@ -2790,24 +2809,46 @@ static void reset_record_counters(fluere_ctx* c) {
 }
 
 // Host copy of device-resident records, ended prefix first in emission order
-// (order_key: global index of the closing packet), then active flows.
+// (order_key: global index of the closing packet; with order words, sharded
+// Mode B: then aux[0], aux[1]), then active flows.
 static int fetch_records(fluere_ctx* c) {
     if (c->host_recs) return FLUERE_OK;
     hipStream_t s = c->stream;
-    c->recs.resize(c->dev_n_rec);
-    if (c->dev_n_rec)
-        HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, c->dev_n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+    const uint64_t n = c->dev_n_rec;
+    c->recs.resize(n);
+    c->aux.assign(c->has_aux ? 2 * n : 0, 0ull);
+    if (n)
+        HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+    if (n && c->has_aux)
+        HIPCHECK(hipMemcpyAsync(c->aux.data(), c->d_recaux, 2 * n * 8, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
-    std::stable_sort(c->recs.begin(), c->recs.end(), [](const fluere_record& x, const fluere_record& y) {
-        if (x.order_key != y.order_key) return x.order_key < y.order_key;
-        return x.first < y.first;
+    std::vector<uint64_t> ix(n);
+    for (uint64_t i = 0; i < n; i++) ix[i] = i;
+    const auto& R = c->recs;
+    const auto& X = c->aux;
+    const bool ax = c->has_aux;
+    std::stable_sort(ix.begin(), ix.end(), [&](uint64_t a, uint64_t b) {
+        if (R[a].order_key != R[b].order_key) return R[a].order_key < R[b].order_key;
+        if (ax && X[2 * a] != X[2 * b]) return X[2 * a] < X[2 * b];
+        if (ax && X[2 * a + 1] != X[2 * b + 1]) return X[2 * a + 1] < X[2 * b + 1];
+        return R[a].first < R[b].first;
     });
+    std::vector<fluere_record> r2(n);
+    std::vector<unsigned long long> x2(X.size());
+    for (uint64_t i = 0; i < n; i++) {
+        r2[i] = R[ix[i]];
+        if (ax) { x2[2 * i] = X[2 * ix[i]]; x2[2 * i + 1] = X[2 * ix[i] + 1]; }
+    }
+    c->recs.swap(r2);
+    c->aux.swap(x2);
     uint64_t ne = 0;
     for (auto& r : c->recs) if (r.order_key != NONE64) ne++;
     c->n_ended = ne;
     c->host_recs = true;
     return FLUERE_OK;
 }
+
+static void sweep_free(fluere_ctx* c);
 
 static TableSet tables_of(fluere_ctx* c) {
     TableSet T;
@@ -2929,7 +2970,10 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_exact);
     hipFree(c->d_annex);
     hipFree(c->d_annex_of);
+    hipFree(c->d_sumpos);
     hipFree(c->d_need);
+    hipFree(c->d_recaux);
+    sweep_free(c);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -3879,6 +3923,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     // device timing: evk0 / evk1 around the hot kernel only (each event marker
     // costs a gap on the stream); the run's total is host wall time
     c->pass_in_run = true;
+    c->has_aux = false;
+    c->aux.clear();
     const auto t_run0 = std::chrono::steady_clock::now();
     const TableSet T = tables_of(c);
     const int nb = (int)c->batches.size();
@@ -4118,12 +4164,25 @@ extern "C" int fluere_get_records(fluere_ctx* c, fluere_record** out, uint64_t* 
 
 extern "C" void fluere_records_free(fluere_record* r) { free(r); }
 
+extern "C" int fluere_get_record_order(fluere_ctx* c, uint64_t* aux, uint64_t n) {
+    if (!c || (!aux && n)) return FLUERE_E_ARG;
+    if (!c->have_results) return FLUERE_E_STATE;
+    int rc = fetch_records(c);
+    if (rc) return rc;
+    if (n != c->recs.size()) return FLUERE_E_ARG;
+    for (uint64_t i = 0; i < n; i++) {
+        aux[2 * i] = c->has_aux ? c->aux[2 * i] : 0;
+        aux[2 * i + 1] = c->has_aux ? c->aux[2 * i + 1] : 0;
+    }
+    return FLUERE_OK;
+}
+
 // ---------------------------------------------------------------------------
 // synthetic captures
 // ---------------------------------------------------------------------------
 extern "C" uint64_t fluere_synth_range_bytes(const fluere_synth_cfg* cfg, uint64_t first, uint64_t n) {
     if (!cfg) return 0;
-    if (cfg->kind != FLUERE_SYNTH_IMIX && cfg->kind != FLUERE_SYNTH_TCP && cfg->kind != FLUERE_SYNTH_SLOW) return n * 80;
+    if (cfg->kind != FLUERE_SYNTH_IMIX && !synth::tcp_kind(cfg->kind) && cfg->kind != FLUERE_SYNTH_SLOW) return n * 80;
     uint64_t s = 0;
     for (uint64_t i = first; i < first + n; i++) s += 16 + synth::frame_len(*cfg, i);
     return s;
@@ -4205,6 +4264,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     const TableSet T = tables_of(c);
     const int nb = (int)c->batches.size();
     if (!c->d_annex_of && hipMalloc(&c->d_annex_of, (size_t)c->fmax * 4) != hipSuccess) return FLUERE_E_NOMEM;
+    if (!c->d_sumpos && hipMalloc(&c->d_sumpos, (size_t)c->fmax * 4) != hipSuccess) return FLUERE_E_NOMEM;
     if (!c->d_need && hipMalloc(&c->d_need, 16) != hipSuccess) return FLUERE_E_NOMEM;
     FinArgs fa{c->d_batches, nb, T, c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
     // 1. flows whose part of the state machine depends on packet order here
@@ -4214,7 +4274,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     //    speculatively: with no order-dependent flow (the common case) the
     //    export needs ONE host round trip
     ExportArgs ea{fa, (uint8_t*)d_blocks, n_owners, shard, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
-                  c->d_annex_of, (const fluere_flow_annex*)c->d_annex};
+                  c->d_annex_of, (const fluere_flow_annex*)c->d_annex, c->d_sumpos};
     auto enqueue_export = [&](bool annexes) -> int {
         ea.annex = annexes ? (const fluere_flow_annex*)c->d_annex : nullptr;
         k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
@@ -4273,12 +4333,13 @@ extern "C" int fluere_export_async(fluere_ctx* c, void* d_blocks, uint32_t n_own
     if ((rc = upload_batches(c))) return rc;
     const int nb = (int)c->batches.size();
     if (!c->d_annex_of && hipMalloc(&c->d_annex_of, (size_t)c->fmax * 4) != hipSuccess) return FLUERE_E_NOMEM;
+    if (!c->d_sumpos && hipMalloc(&c->d_sumpos, (size_t)c->fmax * 4) != hipSuccess) return FLUERE_E_NOMEM;
     if (!c->d_need && hipMalloc(&c->d_need, 16) != hipSuccess) return FLUERE_E_NOMEM;
     FinArgs fa{c->d_batches, nb, tables_of(c), c->acc, c->d_glob, nullptr, c->d_complex, c->use_mac};
     reset_record_counters(c);
     k_local_cert<<<flow_grid(c), 256, 0, s>>>(fa, c->d_annex_of);
     ExportArgs ea{fa, (uint8_t*)d_blocks, n_owners, shard, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
-                  c->d_annex_of, nullptr};
+                  c->d_annex_of, nullptr, c->d_sumpos};
     k_export_hdr<<<grid_for(n_owners, 64), 64, 0, s>>>(ea);
     k_export_owners<<<flow_grid(c), 256, 0, s>>>(ea);
     k_export_need<<<1, 64, 0, s>>>(ea, (unsigned long long*)c->d_need, d_info);
@@ -4320,7 +4381,7 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
     const uint32_t seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
     MergeArgs ma{tables_of(c), c->acc, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
                  c->d_recs_cap, (const uint8_t*)d_blocks, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
-                 c->h_ctl, seq};
+                 c->h_ctl, seq, c->timeout_ms * 1000ull};
     if (n) {
         k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
         k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
@@ -4388,9 +4449,521 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
     out.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     out.updates = g.n_updates;
     if (st) *st = out;
-    // the hard-timeout sweep (offline_fluereflows.rs:161-175) is not composed
-    // across shards: such a capture runs in one context
-    if (expiry) return FLUERE_E_UNSUPPORTED;
+    // the hard-timeout sweep (offline_fluereflows.rs:161-175): the records
+    // come from the sweep composition (fluere_sweep_*), which reads the
+    // summary -> flow mapping of this merge
+    c->merge_cap = cap;
+    c->merge_shards = n_shards;
+    c->has_aux = false;
+    if (expiry) return FLUERE_NEED_SWEEP;
+    return FLUERE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// sharded Mode B: the hard-timeout sweep composed across shards
+// ---------------------------------------------------------------------------
+// When the capture's span reaches the timeout, an expiry entry pushed at a
+// creation fires at the first *processed* packet of the whole capture with
+// t >= exp (offline_fluereflows.rs:103-119,161-175): shards are coupled.  The
+// composition (driven by fluere_amd/dist.py):
+//   1. every shard (holder) ships the metadata of its valid packets to the
+//      keys' owners (32 B each, capture order within an owner): each owner
+//      then holds every packet of its keys, in capture order;
+//   2. per pass, every holder computes the sweep point of each of its
+//      create-eligible packets over the packets processed so far -- first in
+//      its own shard (max segment tree over the processed times), else by a
+//      query to the first later shard whose latest processed time reaches
+//      exp -- and ships the points to the owners, who run the exact chase
+//      (exact.hip) and send back which packets were processed; repeated until
+//      no owner's processed set changes (the single-GPU fixed point);
+//   3. the owners ask the holders for the FluereRecord seeds of the creating
+//      packets and build the records; their order stays global (order_key =
+//      the ending packet's index plus two order words, fluere_get_record_order).
+struct SweepState {
+    // holder (this shard's packets)
+    ExMeta* hcm = nullptr;              // valid packets, capture order (d = local flow)
+    uint64_t hn = 0;
+    uint32_t* hperm = nullptr;          // pack position -> local index
+    uint8_t* hpr = nullptr;             // processed (local index)
+    unsigned long long* hF = nullptr;   // sweep point (local index)
+    unsigned long long* tree = nullptr;
+    uint64_t P = 0;
+    uint32_t* qk = nullptr;             // the local index of each query (grouped by target shard)
+    uint64_t nq = 0;
+    uint32_t n_owners = 0;
+    std::vector<uint64_t> counts;       // packets per owner
+    // owner (its keys' packets from every shard)
+    ExMeta* ocm = nullptr;
+    uint64_t on = 0;
+    ExactSession* es = nullptr;
+    unsigned long long* req = nullptr;  // creating packets of the instances (ascending)
+    uint32_t* reqq = nullptr;           // their instance ordinals
+    uint32_t n_inst = 0;
+    Seed* seeds = nullptr;              // by instance ordinal
+    int passes = 0;
+    // scratch
+    uint32_t *k1 = nullptr, *k2 = nullptr, *v1 = nullptr;
+    unsigned long long* misc = nullptr; // small device scratch (counts)
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    uint32_t* err = nullptr;
+};
+
+static void sweep_free(fluere_ctx* c) {
+    SweepState* w = c->sw;
+    if (!w) return;
+    hipFree(w->hcm); hipFree(w->hperm); hipFree(w->hpr); hipFree(w->hF); hipFree(w->tree); hipFree(w->qk);
+    hipFree(w->ocm); hipFree(w->req); hipFree(w->reqq); hipFree(w->seeds);
+    hipFree(w->k1); hipFree(w->k2); hipFree(w->v1); hipFree(w->misc); hipFree(w->tmp); hipFree(w->err);
+    if (w->es) exact_free(w->es);
+    delete w;
+    c->sw = nullptr;
+}
+
+static int sw_tmp(SweepState* w, size_t need) {
+    if (need <= w->tmp_bytes) return FLUERE_OK;
+    hipFree(w->tmp);
+    w->tmp = nullptr;
+    w->tmp_bytes = 0;
+    if (hipMalloc(&w->tmp, need) != hipSuccess) return FLUERE_E_NOMEM;
+    w->tmp_bytes = need;
+    return FLUERE_OK;
+}
+
+static int bits_for(uint64_t v) {  // radix sort width for keys in [0, v]
+    int b = 1;
+    while (b < 64 && (v >> b)) b++;
+    return b;
+}
+
+__global__ void __launch_bounds__(256) k_sw_owner(const ExMeta* cm, uint64_t n, const uint8_t* flow_key,
+                                                  uint32_t n_owners, uint32_t* okey, uint32_t* val) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    okey[k] = key_owner(reinterpret_cast<const uint32_t*>(flow_key + (size_t)cm[k].d * 56), n_owners);
+    val[k] = (uint32_t)k;
+}
+
+// counts[r] = entries equal to r among n sorted keys, r < m
+__global__ void k_sw_kcount(const uint32_t* keys, uint64_t n, uint32_t m, unsigned long long* counts) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    auto lb = [&](uint32_t v) {
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < v) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    counts[r] = lb(r + 1) - lb(r);
+}
+
+// the packet records for the owners: d = the flow's summary position in its block
+__global__ void __launch_bounds__(256) k_sw_pack(const ExMeta* cm, const uint32_t* perm, uint64_t n,
+                                                 const uint32_t* sumpos, ExMeta* out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    ExMeta m = cm[perm[p]];
+    m.d = sumpos[m.d];
+    out[p] = m;
+}
+
+// owner: (shard s, summary position j) -> this context's flow id (the merge's sd)
+__global__ void __launch_bounds__(256) k_sw_load(const ExMeta* in, uint64_t n, const unsigned long long* seg,
+                                                 uint32_t n_shards, const uint32_t* sd, uint64_t cap, uint32_t fmax,
+                                                 ExMeta* out, uint32_t* err) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t sh = 0;
+    while (sh + 1 < n_shards && seg[sh + 1] <= i) sh++;
+    ExMeta m = in[i];
+    const uint32_t d = m.d < cap ? sd[sh * cap + m.d] : FAIL;
+    if (d == FAIL || d >= fmax) {
+        atomicOr(err, 1u);
+        m.d = 0;
+    } else {
+        m.d = d;
+    }
+    out[i] = m;
+}
+
+__global__ void __launch_bounds__(256) k_sw_feedback(const uint8_t* back, const uint32_t* perm, uint64_t n, uint8_t* pr) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) pr[perm[p]] = back[p];
+}
+
+// sweep point of every create-eligible packet, in this shard or a query
+__global__ void __launch_bounds__(256) k_sw_points(const ExMeta* cm, uint64_t n, const unsigned long long* tree,
+                                                   uint64_t P, unsigned long long timeout_us, uint32_t rank,
+                                                   uint32_t n_ranks, const unsigned long long* maxt,
+                                                   unsigned long long* F, uint32_t* tkey, uint32_t* val) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const ExMeta m = cm[k];
+    unsigned long long f = NONE64;
+    uint32_t target = n_ranks;  // none
+    const unsigned long long exp = m.t + timeout_us < m.t ? NONE64 : m.t + timeout_us;
+    if ((m.bits & 1) && exp != NONE64) {
+        const uint64_t j = tree_first(tree, P, k, exp + 1);
+        if (j < n) f = cm[j].gidx;
+        else
+            for (uint32_t r = rank + 1; r < n_ranks; r++)
+                if (maxt[r] >= exp + 1) { target = r; break; }
+    }
+    F[k] = f;
+    tkey[k] = target;
+    val[k] = (uint32_t)k;
+}
+
+__global__ void __launch_bounds__(256) k_sw_qpack(const ExMeta* cm, const uint32_t* qk, uint64_t nq,
+                                                  unsigned long long timeout_us, unsigned long long* q) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nq) q[i] = cm[qk[i]].t + timeout_us;  // (queried only when it does not saturate)
+}
+
+__global__ void __launch_bounds__(256) k_sw_answer(const unsigned long long* q, uint64_t nq, const unsigned long long* tree,
+                                                   uint64_t P, const ExMeta* cm, uint64_t n, unsigned long long* ans) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const uint64_t j = tree_first(tree, P, 0, q[i] + 1);
+    ans[i] = j < n ? cm[j].gidx : NONE64;
+}
+
+__global__ void __launch_bounds__(256) k_sw_fill(const unsigned long long* ans, const uint32_t* qk, uint64_t nq,
+                                                 unsigned long long* F) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nq) F[qk[i]] = ans[i];
+}
+
+__global__ void __launch_bounds__(256) k_sw_fpack(const unsigned long long* F, const uint32_t* perm, uint64_t n,
+                                                  unsigned long long* out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) out[p] = F[perm[p]];
+}
+
+// requests (ascending packet indices) per holder shard: first[r] .. first[r + 1]
+__global__ void k_sw_rcount(const unsigned long long* req, uint64_t n, const unsigned long long* first, uint32_t n_ranks,
+                            unsigned long long* counts) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_ranks) return;
+    auto lb = [&](unsigned long long v) {
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (req[mid] < v) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    counts[r] = lb(first[r + 1]) - lb(first[r]);
+}
+
+__global__ void __launch_bounds__(256) k_sw_seed(const Batch* bs, int nb, const unsigned long long* req, uint64_t n,
+                                                 int macs, Seed* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Parsed P;
+    parse_global(bs, nb, req[i], macs != 0, P);
+    fluere_record r;
+    fill_seed(r, P);
+    Seed sd;
+    for (int k = 0; k < 16; k++) { sd.src[k] = r.source[k]; sd.dst[k] = r.destination[k]; }
+    sd.sp = r.src_port; sd.dp = r.dst_port;
+    sd.v6 = r.src_v6; sd.prot = r.prot; sd.tos = r.tos; sd.pad = 0;
+    out[i] = sd;
+}
+
+__global__ void __launch_bounds__(256) k_sw_seed_scatter(const Seed* in, const uint32_t* q, uint64_t n, Seed* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[q[i]] = in[i];
+}
+
+static int sw_state(fluere_ctx* c) {
+    if (!c->sw) {
+        c->sw = new (std::nothrow) SweepState();
+        if (!c->sw) return FLUERE_E_NOMEM;
+        if (hipMalloc(&c->sw->misc, 4096 * 8) != hipSuccess || hipMalloc(&c->sw->err, 4) != hipSuccess)
+            return FLUERE_E_NOMEM;
+    }
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_pack(fluere_ctx* c, uint32_t n_owners, uint64_t* counts, void* d_send) {
+    if (!c || !n_owners || n_owners > 4096 || !counts) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = sw_state(c))) return rc;
+    SweepState* w = c->sw;
+    if (!d_send || w->n_owners != n_owners || !w->hcm) {
+        // (re)index: this shard's valid packets and their owners
+        sweep_free(c);
+        if ((rc = sw_state(c))) return rc;
+        w = c->sw;
+        if ((rc = upload_batches(c))) return rc;
+        const uint64_t N = c->n_total;
+        const uint64_t M = std::max<uint64_t>(N, 1);
+        w->P = tree_leaves(M);
+        if (hipMalloc(&w->hcm, M * sizeof(ExMeta)) != hipSuccess || hipMalloc(&w->hperm, M * 4) != hipSuccess ||
+            hipMalloc(&w->hpr, M) != hipSuccess || hipMalloc(&w->hF, M * 8) != hipSuccess ||
+            hipMalloc(&w->tree, 2 * w->P * 8) != hipSuccess || hipMalloc(&w->qk, M * 4) != hipSuccess ||
+            hipMalloc(&w->k1, M * 4) != hipSuccess || hipMalloc(&w->k2, M * 4) != hipSuccess ||
+            hipMalloc(&w->v1, M * 4) != hipSuccess)
+            return FLUERE_E_NOMEM;
+        std::vector<Batch> hb(c->batches.size());
+        for (size_t i = 0; i < hb.size(); i++) hb[i] = c->batches[i].b;
+        ExactJob J{c->d_batches, hb.data(), (int)hb.size(), tables_of(c), c->use_mac, 1, c->timeout_ms * 1000ull,
+                   nullptr, c->d_glob, nullptr, nullptr, nullptr, nullptr};
+        if ((rc = exact_collect(J, s, w->hcm, &w->hn))) return rc;
+        const uint64_t n = w->hn;
+        HIPCHECK(hipMemsetAsync(w->misc, 0, n_owners * 8, s));
+        if (n) {
+            k_sw_owner<<<grid_for(n, 256), 256, 0, s>>>(w->hcm, n, c->d_flow_key, n_owners, w->k1, w->v1);
+            size_t tb = 0;
+            (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, w->k1, w->k2, w->v1, w->hperm, (int)n, 0,
+                                                     bits_for(n_owners), s);
+            if ((rc = sw_tmp(w, tb))) return rc;
+            HIPCHECK(hipcub::DeviceRadixSort::SortPairs(w->tmp, tb, w->k1, w->k2, w->v1, w->hperm, (int)n, 0,
+                                                        bits_for(n_owners), s));
+            k_sw_kcount<<<grid_for(n_owners, 256), 256, 0, s>>>(w->k2, n, n_owners, w->misc);
+            HIPCHECK(hipMemsetAsync(w->hpr, 1, n, s));  // first guess: every valid packet is processed
+        }
+        w->counts.assign(n_owners, 0);
+        HIPCHECK(hipMemcpyAsync(w->counts.data(), w->misc, n_owners * 8, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipStreamSynchronize(s));
+        w->n_owners = n_owners;
+    }
+    for (uint32_t o = 0; o < n_owners; o++) counts[o] = w->counts[o];
+    if (d_send && w->hn) {
+        k_sw_pack<<<grid_for(w->hn, 256), 256, 0, s>>>(w->hcm, w->hperm, w->hn, c->d_sumpos, (ExMeta*)d_send);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipStreamSynchronize(s));
+    }
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_load(fluere_ctx* c, const void* d_recv, uint32_t n_shards, const uint64_t* counts) {
+    if (!c || !c->sw || !n_shards || n_shards > 4095 || !counts) return FLUERE_E_ARG;
+    if (n_shards != c->merge_shards || !c->d_sd) return FLUERE_E_STATE;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    std::vector<unsigned long long> seg(n_shards + 1, 0);
+    for (uint32_t r = 0; r < n_shards; r++) seg[r + 1] = seg[r] + counts[r];
+    const uint64_t n = seg[n_shards];
+    if (n && !d_recv) return FLUERE_E_ARG;
+    hipFree(w->ocm);
+    w->ocm = nullptr;
+    if (hipMalloc(&w->ocm, std::max<uint64_t>(n, 1) * sizeof(ExMeta)) != hipSuccess) return FLUERE_E_NOMEM;
+    w->on = n;
+    HIPCHECK(hipMemcpyAsync(w->misc, seg.data(), (n_shards + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemsetAsync(w->err, 0, 4, s));
+    if (n)
+        k_sw_load<<<grid_for(n, 256), 256, 0, s>>>((const ExMeta*)d_recv, n, w->misc, n_shards, c->d_sd,
+                                                   c->merge_cap, c->fmax, w->ocm, w->err);
+    uint32_t err = 0;
+    HIPCHECK(hipMemcpyAsync(&err, w->err, 4, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (err) return FLUERE_E_ARG;  // a packet of a flow the merge does not hold
+    if (w->es) exact_free(w->es);
+    w->es = nullptr;
+    w->passes = 0;
+    std::vector<Batch> hb(c->batches.size());
+    for (size_t i = 0; i < hb.size(); i++) hb[i] = c->batches[i].b;
+    ExactJob J{c->d_batches, hb.data(), (int)hb.size(), tables_of(c), c->use_mac, 1, c->timeout_ms * 1000ull,
+               nullptr, c->d_glob, &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+    J.ext_cm = w->ocm;
+    J.ext_n = n;
+    ExactSession* es = nullptr;
+    int rc = exact_begin(J, s, &es);
+    w->es = es;
+    return rc;
+}
+
+extern "C" int fluere_sweep_index(fluere_ctx* c, const uint8_t* d_pr, uint64_t* max_time) {
+    if (!c || !c->sw || !max_time) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    const uint64_t n = w->hn;
+    if (d_pr && n) k_sw_feedback<<<grid_for(n, 256), 256, 0, s>>>(d_pr, w->hperm, n, w->hpr);
+    int rc = tree_build(n, w->hcm, w->hpr, w->tree, w->P, s);
+    if (rc) return rc;
+    unsigned long long root = 0;
+    HIPCHECK(hipMemcpyAsync(&root, w->tree + 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    *max_time = n ? root : 0;  // 1 + the latest processed packet's time (0: none)
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_queries(fluere_ctx* c, uint32_t n_ranks, uint32_t rank, const uint64_t* max_times,
+                                    uint64_t* qcounts, void* d_q) {
+    if (!c || !c->sw || !n_ranks || n_ranks > 4095 || rank >= n_ranks || !max_times || !qcounts) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    const uint64_t n = w->hn;
+    const unsigned long long T = c->timeout_ms * 1000ull;
+    if (!d_q) {
+        HIPCHECK(hipMemcpyAsync(w->misc, max_times, n_ranks * 8, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipMemsetAsync(w->misc + 2048, 0, (n_ranks + 1) * 8, s));
+        std::vector<uint64_t> cnt(n_ranks + 1, 0);
+        w->nq = 0;
+        if (n) {
+            k_sw_points<<<grid_for(n, 256), 256, 0, s>>>(w->hcm, n, w->tree, w->P, T, rank, n_ranks, w->misc, w->hF,
+                                                         w->k1, w->v1);
+            // queries grouped by target shard (n_ranks: none), capture order within one
+            size_t tb = 0;
+            (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, w->k1, w->k2, w->v1, w->qk, (int)n, 0,
+                                                     bits_for(n_ranks), s);
+            int rc = sw_tmp(w, tb);
+            if (rc) return rc;
+            HIPCHECK(hipcub::DeviceRadixSort::SortPairs(w->tmp, tb, w->k1, w->k2, w->v1, w->qk, (int)n, 0,
+                                                        bits_for(n_ranks), s));
+            k_sw_kcount<<<grid_for(n_ranks + 1, 256), 256, 0, s>>>(w->k2, n, n_ranks + 1, w->misc + 2048);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipMemcpyAsync(cnt.data(), w->misc + 2048, (n_ranks + 1) * 8, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+        }
+        for (uint32_t r = 0; r < n_ranks; r++) { qcounts[r] = cnt[r]; w->nq += cnt[r]; }
+        return FLUERE_OK;
+    }
+    for (uint32_t r = 0; r < n_ranks; r++) qcounts[r] = 0;
+    uint64_t nq = w->nq;
+    if (nq) k_sw_qpack<<<grid_for(nq, 256), 256, 0, s>>>(w->hcm, w->qk, nq, T, (unsigned long long*)d_q);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_answer(fluere_ctx* c, const void* d_q, uint64_t n, void* d_ans) {
+    if (!c || !c->sw || (n && (!d_q || !d_ans))) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    if (n)
+        k_sw_answer<<<grid_for(n, 256), 256, 0, s>>>((const unsigned long long*)d_q, n, w->tree, w->P, w->hcm, w->hn,
+                                                     (unsigned long long*)d_ans);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_points(fluere_ctx* c, const void* d_ans, void* d_f) {
+    if (!c || !c->sw || (c->sw->nq && !d_ans) || (c->sw->hn && !d_f)) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    if (w->nq) k_sw_fill<<<grid_for(w->nq, 256), 256, 0, s>>>((const unsigned long long*)d_ans, w->qk, w->nq, w->hF);
+    if (w->hn) k_sw_fpack<<<grid_for(w->hn, 256), 256, 0, s>>>(w->hF, w->hperm, w->hn, (unsigned long long*)d_f);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_chase(fluere_ctx* c, const void* d_f, void* d_pr, int* changed) {
+    if (!c || !c->sw || !c->sw->es || !changed) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    SweepState* w = c->sw;
+    if (w->on && (!d_f || !d_pr)) return FLUERE_E_ARG;
+    if (++w->passes > 64) return FLUERE_E_UNSUPPORTED;  // no fixed point (cannot happen: the system is causal)
+    bool ch = false;
+    int rc = exact_pass(w->es, (const unsigned long long*)d_f, (uint8_t*)d_pr, &ch);
+    *changed = ch ? 1 : 0;
+    return rc;
+}
+
+extern "C" int fluere_sweep_seed_requests(fluere_ctx* c, uint32_t n_ranks, const uint64_t* rank_first,
+                                          uint64_t* counts, void* d_req) {
+    if (!c || !c->sw || !c->sw->es || !n_ranks || n_ranks > 4095 || !rank_first || !counts) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    if (!d_req) {
+        hipFree(w->req); hipFree(w->reqq);
+        w->req = nullptr; w->reqq = nullptr;
+        const uint64_t M = std::max<uint64_t>(w->on, 1);
+        if (hipMalloc(&w->req, M * 8) != hipSuccess || hipMalloc(&w->reqq, M * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        int rc = exact_seed_requests(w->es, w->req, w->reqq, &w->n_inst);
+        if (rc) return rc;
+        HIPCHECK(hipMemcpyAsync(w->misc, rank_first, (n_ranks + 1) * 8, hipMemcpyHostToDevice, s));
+        k_sw_rcount<<<grid_for(n_ranks, 256), 256, 0, s>>>(w->req, w->n_inst, w->misc, n_ranks, w->misc + 2048);
+        HIPCHECK(hipGetLastError());
+        std::vector<unsigned long long> cnt(n_ranks);
+        HIPCHECK(hipMemcpyAsync(cnt.data(), w->misc + 2048, n_ranks * 8, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        uint64_t tot = 0;
+        for (uint32_t r = 0; r < n_ranks; r++) { counts[r] = cnt[r]; tot += cnt[r]; }
+        if (tot != w->n_inst) return FLUERE_E_ARG;  // a creating packet outside every shard's range
+        return FLUERE_OK;
+    }
+    if (w->n_inst) HIPCHECK(hipMemcpyAsync(d_req, w->req, (size_t)w->n_inst * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_seeds(fluere_ctx* c, const void* d_req, uint64_t n, void* d_seeds) {
+    if (!c || (n && (!d_req || !d_seeds))) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = upload_batches(c))) return rc;
+    if (n)
+        k_sw_seed<<<grid_for(n, 256), 256, 0, s>>>(c->d_batches, (int)c->batches.size(), (const unsigned long long*)d_req,
+                                                   n, c->use_mac, (Seed*)d_seeds);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_sweep_finish(fluere_ctx* c, const void* d_seeds, fluere_stats* st) {
+    if (!c || !c->sw || !c->sw->es) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SweepState* w = c->sw;
+    const uint32_t ni = w->n_inst;
+    if (ni && !d_seeds) return FLUERE_E_ARG;
+    hipFree(w->seeds);
+    w->seeds = nullptr;
+    if (hipMalloc(&w->seeds, std::max<uint32_t>(ni, 1) * sizeof(Seed)) != hipSuccess) return FLUERE_E_NOMEM;
+    if (ni) k_sw_seed_scatter<<<grid_for(ni, 256), 256, 0, s>>>((const Seed*)d_seeds, w->reqq, ni, w->seeds);
+    // the records of this rank: only the sweep's (the merge emitted none)
+    Glob g;
+    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    const uint64_t want = g.n_rec + ni;
+    if (want > c->d_recaux_cap) {
+        hipFree(c->d_recaux);
+        c->d_recaux = nullptr;
+        c->d_recaux_cap = 0;
+        if (hipMalloc(&c->d_recaux, std::max<uint64_t>(want, 1) * 16) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_recaux_cap = std::max<uint64_t>(want, 1);
+    }
+    if (g.n_rec) HIPCHECK(hipMemsetAsync(c->d_recaux, 0, g.n_rec * 16, s));
+    int rc = exact_finish(w->es, w->seeds, c->d_recaux + 2 * g.n_rec);
+    if (rc) return rc;
+    HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    c->dev_n_rec = g.n_rec;
+    c->host_recs = false;
+    c->has_aux = true;
+    c->have_results = true;
+    if (st) {
+        fluere_stats out{};
+        out.valid = g.valid;
+        out.dropped_parse = g.dropped;
+        out.records = g.n_rec;
+        out.ended = g.n_ended;
+        out.updates = g.n_updates;
+        out.complex_flows = exact_result(w->es).keys;
+        out.sequential_mode = 1;
+        *st = out;
+    }
+    exact_free(w->es);
+    w->es = nullptr;
     return FLUERE_OK;
 }
 

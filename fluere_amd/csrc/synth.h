@@ -65,9 +65,22 @@ FL_HD Flow flow(const fluere_synth_cfg& c, uint32_t f) {
     return F;
 }
 
+FL_HD bool tcp_kind(uint32_t k) { return k == FLUERE_SYNTH_TCP || k == FLUERE_SYNTH_TCP_BACKTIME; }
+
+// Capture time of packet i, microseconds after kT0: +1 us per packet; with
+// FLUERE_SYNTH_TCP_BACKTIME 1 % of the packets carry a time up to 5 ms earlier
+// (merged or multi-queue captures are slightly out of order).
+FL_HD uint64_t time_us(const fluere_synth_cfg& c, uint64_t i) {
+    if (c.kind == FLUERE_SYNTH_TCP_BACKTIME && rnd(c.seed, 32, i) % 100 == 0) {
+        const uint64_t back = 1 + rnd(c.seed, 33, i) % 5000;
+        return i >= back ? i - back : 0;
+    }
+    return i;
+}
+
 // Frame length of packet i (bytes on the wire, == caplen == orig_len).
 FL_HD uint32_t frame_len(const fluere_synth_cfg& c, uint64_t i) {
-    if (c.kind != FLUERE_SYNTH_IMIX && c.kind != FLUERE_SYNTH_TCP && c.kind != FLUERE_SYNTH_SLOW) return 64;
+    if (c.kind != FLUERE_SYNTH_IMIX && !tcp_kind(c.kind) && c.kind != FLUERE_SYNTH_SLOW) return 64;
     uint32_t r = (uint32_t)(rnd(c.seed, 14, i) % 12);
     return r < 7 ? (c.kind == FLUERE_SYNTH_SLOW ? 128 : 64) : (r < 11 ? 576 : 1500);
 }
@@ -208,7 +221,7 @@ FL_HD Pkt tcp_real(const fluere_synth_cfg& c, uint64_t i) {
 
 // The header fields of packet i: the schedule of the kind.
 FL_HD Pkt pkt(const fluere_synth_cfg& c, uint64_t i) {
-    if (c.kind == FLUERE_SYNTH_TCP) return tcp_real(c, i);
+    if (tcp_kind(c.kind)) return tcp_real(c, i);
     Pkt p;
     Slot s = slot(c, i);
     Flow F = flow(c, s.f);
@@ -231,8 +244,9 @@ FL_HD Pkt pkt(const fluere_synth_cfg& c, uint64_t i) {
 FL_HD uint32_t write_record(const fluere_synth_cfg& c, uint64_t i, uint8_t* dst) {
     const uint32_t L0 = frame_len(c, i);
     uint32_t L = L0;
-    put32le(dst + 0, kT0 + (uint32_t)(i / 1000000u));
-    put32le(dst + 4, (uint32_t)(i % 1000000u));
+    const uint64_t ts = time_us(c, i);
+    put32le(dst + 0, kT0 + (uint32_t)(ts / 1000000u));
+    put32le(dst + 4, (uint32_t)(ts % 1000000u));
     put32le(dst + 8, L);
     put32le(dst + 12, L);
     uint8_t* e = dst + 16;

@@ -10,6 +10,20 @@ Shard r processes packets [r*N/G, (r+1)*N/G) with global packet indices, so
 order-free record fields merge as sums / min / max, and the flows whose record
 depends on packet order are composed at their owner from per-shard pieces of
 the state machine (the annex of fluere_gpu.h).
+
+When the capture's span reaches the timeout, the hard-timeout sweep
+(offline_fluereflows.rs:103-119,161-175) couples the shards: an expiry entry
+fires at the first processed packet of the whole capture with t >= exp.  The
+merge is then completed by the sweep composition (_sweep_compose): the shards
+ship their packets' metadata to the keys' owners, compute the sweep points over
+their own packets (asking later shards for the rest), and the owners run the
+exact chase until the processed-packet set is stable (fluere_sweep_* in
+include/fluere_gpu.h).
+
+The protocol is written once (_shard_step) over a small communicator: _DistComm
+(torch.distributed, one context per process) for ShardExchange, _LocalComm
+(device copies, G contexts in one process) for LogicalShards -- the latter is
+SURVEY.md section 8e's "testing without 8 GPUs" and runs the same calls.
 """
 from __future__ import annotations
 
@@ -20,6 +34,9 @@ import numpy as np
 from . import _lib
 from ._lib import RECORD_DTYPE, Stats, check
 
+NONE64 = (1 << 64) - 1
+SPAN_BIAS = 1 << 62  # fluere_export_async d_info[4] = SPAN_BIAS - earliest valid time
+
 
 def shard_range(n_packets: int, rank: int, world: int):
     per = (n_packets + world - 1) // world
@@ -29,6 +46,7 @@ def shard_range(n_packets: int, rank: int, world: int):
 
 def set_index_base(ctx, base: int):
     check(_lib.lib().fluere_set_index_base(ctx._h, base), "fluere_set_index_base")
+    ctx.index_base = int(base)
 
 
 def _pow2_at_least(n: int, lo: int) -> int:
@@ -63,89 +81,383 @@ def exchange_blocks(send, recv, group=None):
         dist.all_to_all_single(recv, send, group=group)
 
 
+def exchange_var(send, send_counts, elem: int, group=None):
+    """All-to-all with per-destination sizes: send holds send_counts[o]
+    elements of `elem` bytes for rank o, in rank order.  Returns (recv,
+    recv_counts): recv_counts[s] elements from rank s, in rank order."""
+    import torch
+    import torch.distributed as dist
+    gloo = dist.get_backend(group) == "gloo"
+    world = dist.get_world_size(group)
+    dev = "cpu" if gloo else send.device
+    sc = torch.tensor(np.asarray(send_counts, dtype=np.int64), dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = np.asarray(rc.tolist(), dtype=np.uint64)
+    n_out = int(recv_counts.sum()) * elem
+    ins = [int(x) * elem for x in send_counts]
+    outs = [int(x) * elem for x in recv_counts]
+    if gloo:
+        s_h = send[: sum(ins)].cpu() if send.is_cuda else send[: sum(ins)]
+        r_h = torch.empty(n_out, dtype=torch.uint8)
+        dist.all_to_all_single(r_h, s_h, outs, ins, group=group)
+        recv = torch.empty(max(1, n_out), dtype=torch.uint8, device=send.device)
+        recv[:n_out].copy_(r_h)
+    else:
+        recv = torch.empty(max(1, n_out), dtype=torch.uint8, device=send.device)
+        dist.all_to_all_single(recv[:n_out], send[: sum(ins)], outs, ins, group=group)
+    return recv, recv_counts
+
+
+class _DistComm:
+    """This process's one context over torch.distributed.  With RCCL the
+    collectives run on torch's current stream; a context on a stream of its
+    own is synchronised around them (the library's calls that feed a
+    collective end with their stream drained, and a collective's output is
+    waited for before the library reads it)."""
+
+    def __init__(self, group, ctx):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.ranks = [dist.get_rank(group)]
+        self.gloo = dist.get_backend(group) == "gloo"
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        cur = torch.cuda.current_stream().cuda_stream
+        self.same_stream = ctx.stream is not None and int(ctx.stream) != 0 and int(ctx.stream) == int(cur)
+
+    def _before(self):
+        import torch
+        if not self.same_stream:
+            torch.cuda.synchronize()  # the context's kernels (any stream) before the collective
+
+    def _after(self):
+        import torch
+        if not self.same_stream and not self.gloo:
+            torch.cuda.current_stream().synchronize()  # the collective before the context reads its output
+
+    def allreduce_max_dev(self, tensors):
+        import torch.distributed as dist
+        (t,) = tensors
+        self._before()
+        x = t.cpu() if self.gloo else t
+        dist.all_reduce(x, op=dist.ReduceOp.MAX, group=self.group)
+        self._after()
+        return np.asarray(x.tolist(), dtype=np.int64)
+
+    def allreduce_max(self, arrays):
+        import torch
+        import torch.distributed as dist
+        (a,) = arrays
+        t = torch.tensor(np.asarray(a, dtype=np.int64), device="cpu" if self.gloo else self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return np.asarray(t.tolist(), dtype=np.int64)
+
+    def allgather(self, arrays):
+        import torch
+        import torch.distributed as dist
+        (a,) = arrays
+        a = np.asarray(a, dtype=np.int64)
+        t = torch.tensor(a, device="cpu" if self.gloo else self.device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return np.stack([np.asarray(o.tolist(), dtype=np.int64) for o in out])
+
+    def all_to_all_equal(self, sends, recvs):
+        (s,), (r,) = sends, recvs
+        self._before()
+        exchange_blocks(s, r, self.group)
+        self._after()
+
+    def all_to_all_v(self, sends, counts, elem):
+        (s,), (c,) = sends, counts
+        self._before()
+        r, rc = exchange_var(s, c, elem, self.group)
+        self._after()
+        return [r], [rc]
+
+
+class _LocalComm:
+    """G contexts of one process (logical shards on one device): every
+    collective is a set of device copies."""
+
+    def __init__(self, n):
+        self.world = n
+        self.ranks = list(range(n))
+
+    @staticmethod
+    def _sync():
+        import torch
+        torch.cuda.synchronize()  # (the contexts run on streams of their own)
+
+    def allreduce_max_dev(self, tensors):
+        self._sync()
+        return np.max(np.stack([np.asarray(t.tolist(), dtype=np.int64) for t in tensors]), axis=0)
+
+    def allreduce_max(self, arrays):
+        return np.max(np.stack([np.asarray(a, dtype=np.int64) for a in arrays]), axis=0)
+
+    def allgather(self, arrays):
+        return np.stack([np.asarray(a, dtype=np.int64) for a in arrays])
+
+    def all_to_all_equal(self, sends, recvs):
+        self._sync()
+        G = self.world
+        blk = sends[0].numel() // G
+        for o in range(G):
+            for r in range(G):
+                recvs[o][r * blk:(r + 1) * blk].copy_(sends[r][o * blk:(o + 1) * blk])
+        self._sync()
+
+    def all_to_all_v(self, sends, counts, elem):
+        import torch
+        self._sync()
+        G = self.world
+        offs = [np.concatenate([[0], np.cumsum(np.asarray(c, dtype=np.uint64))]).astype(np.int64) for c in counts]
+        recvs, rcounts = [], []
+        for o in range(G):
+            parts = [sends[r][int(offs[r][o]) * elem:int(offs[r][o + 1]) * elem] for r in range(G)]
+            n = sum(p.numel() for p in parts)
+            out = torch.empty(max(1, n), dtype=torch.uint8, device="cuda")
+            if n:
+                torch.cat(parts, out=out[:n])
+            recvs.append(out)
+            rcounts.append(np.asarray([counts[r][o] for r in range(G)], dtype=np.uint64))
+        self._sync()
+        return recvs, rcounts
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _buf(nbytes: int):
+    import torch
+    return torch.empty(max(1, int(nbytes)), dtype=torch.uint8, device="cuda")
+
+
+def _arr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _sweep_compose(comm, ctxs, rank_first):
+    """The hard-timeout sweep across shards (include/fluere_gpu.h,
+    fluere_sweep_*): every local context is a holder (its packet range) and an
+    owner (its flows).  rank_first: first global packet index of every rank,
+    plus the total (world + 1 entries)."""
+    L = _lib.lib()
+    W = comm.world
+    u64 = np.uint64
+    # 1-2. packets to their keys' owners
+    counts, sends = [], []
+    for c in ctxs:
+        cnt = np.zeros(W, u64)
+        check(L.fluere_sweep_pack(c._h, W, _arr(cnt), None), "fluere_sweep_pack")
+        b = _buf(int(cnt.sum()) * 32)
+        check(L.fluere_sweep_pack(c._h, W, _arr(cnt), b.data_ptr()), "fluere_sweep_pack")
+        counts.append(cnt)
+        sends.append(b)
+    recvs, rcounts = comm.all_to_all_v(sends, counts, 32)
+    for c, r, rc in zip(ctxs, recvs, rcounts):
+        rc = np.ascontiguousarray(rc, dtype=u64)
+        check(L.fluere_sweep_load(c._h, r.data_ptr(), W, _arr(rc)), "fluere_sweep_load")
+    del sends, recvs
+    # 3. the processed-packet fixed point
+    back = [None] * len(ctxs)
+    passes = 0
+    while True:
+        passes += 1
+        mts = []
+        for c, b in zip(ctxs, back):
+            m = ctypes.c_uint64()
+            check(L.fluere_sweep_index(c._h, _ptr(b), ctypes.byref(m)), "fluere_sweep_index")
+            mts.append(np.array([m.value & ((1 << 63) - 1)], dtype=np.int64))
+        allmax = np.ascontiguousarray(comm.allgather(mts).reshape(W).astype(u64))
+        qsends, qcounts = [], []
+        for c, rk in zip(ctxs, comm.ranks):
+            qc = np.zeros(W, u64)
+            check(L.fluere_sweep_queries(c._h, W, rk, _arr(allmax), _arr(qc), None), "fluere_sweep_queries")
+            b = _buf(int(qc.sum()) * 8)
+            tmp = np.zeros(W, u64)
+            check(L.fluere_sweep_queries(c._h, W, rk, _arr(allmax), _arr(tmp), b.data_ptr()), "fluere_sweep_queries")
+            qsends.append(b)
+            qcounts.append(qc)
+        qrecv, qrc = comm.all_to_all_v(qsends, qcounts, 8)
+        asends = []
+        for c, q, n in zip(ctxs, qrecv, qrc):
+            n = int(np.asarray(n, dtype=u64).sum())
+            a = _buf(n * 8)
+            check(L.fluere_sweep_answer(c._h, q.data_ptr(), n, a.data_ptr()), "fluere_sweep_answer")
+            asends.append(a)
+        arecv, _ = comm.all_to_all_v(asends, qrc, 8)
+        fsends = []
+        for c, a, cnt in zip(ctxs, arecv, counts):
+            f = _buf(int(cnt.sum()) * 8)
+            check(L.fluere_sweep_points(c._h, a.data_ptr(), f.data_ptr()), "fluere_sweep_points")
+            fsends.append(f)
+        frecv, _ = comm.all_to_all_v(fsends, counts, 8)
+        prs, chg = [], []
+        for c, f, rc in zip(ctxs, frecv, rcounts):
+            p = _buf(int(np.asarray(rc, dtype=u64).sum()))
+            ch = ctypes.c_int()
+            check(L.fluere_sweep_chase(c._h, f.data_ptr(), p.data_ptr(), ctypes.byref(ch)), "fluere_sweep_chase")
+            prs.append(p)
+            chg.append(np.array([ch.value], dtype=np.int64))
+        if not int(comm.allreduce_max(chg)[0]):
+            break
+        back, _ = comm.all_to_all_v(prs, rcounts, 1)
+    # 4. seeds of the creating packets from their holders
+    rf = np.ascontiguousarray(np.asarray(rank_first, dtype=u64))
+    reqs, scounts = [], []
+    for c in ctxs:
+        sc = np.zeros(W, u64)
+        check(L.fluere_sweep_seed_requests(c._h, W, _arr(rf), _arr(sc), None), "fluere_sweep_seed_requests")
+        b = _buf(int(sc.sum()) * 8)
+        check(L.fluere_sweep_seed_requests(c._h, W, _arr(rf), _arr(sc), b.data_ptr()), "fluere_sweep_seed_requests")
+        reqs.append(b)
+        scounts.append(sc)
+    rrecv, rrc = comm.all_to_all_v(reqs, scounts, 8)
+    ssends = []
+    for c, q, n in zip(ctxs, rrecv, rrc):
+        n = int(np.asarray(n, dtype=u64).sum())
+        b = _buf(n * 40)
+        check(L.fluere_sweep_seeds(c._h, q.data_ptr(), n, b.data_ptr()), "fluere_sweep_seeds")
+        ssends.append(b)
+    srecv, _ = comm.all_to_all_v(ssends, rrc, 40)
+    # 5. records
+    stats = []
+    for c, sd in zip(ctxs, srecv):
+        st = Stats()
+        check(L.fluere_sweep_finish(c._h, sd.data_ptr(), ctypes.byref(st)), "fluere_sweep_finish")
+        d = st.as_dict()
+        d["sweep_passes"] = passes
+        stats.append(d)
+    return stats
+
+
+class _StepState:
+    def __init__(self, cap, cap_annex):
+        self.cap, self.cap_annex = max(1, int(cap)), max(1, int(cap_annex))
+        self.sends = self.recvs = None
+        self.blk = 0
+        self.infos = None
+        self.bytes_sent = 0  # per local context, last step: the blocks' bytes for other ranks
+
+
+def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
+    """One sharded pass over every local context (parse + key + aggregate,
+    export, capacity agreement, all-to-all, owner merge; the sweep
+    composition when the span reaches the timeout).  Returns the merge stats
+    of every local context."""
+    import torch
+    L = _lib.lib()
+    W = comm.world
+    for c in ctxs:
+        c.parse_aggregate()
+    if S.infos is None or len(S.infos) != len(ctxs):
+        S.infos = [torch.zeros(6, dtype=torch.int64, device="cuda") for _ in ctxs]
+    annexes = expiry = False
+    timeout_us = int(ctxs[0].timeout_ms) * 1000
+    while True:
+        blk = int(L.fluere_shard_block_bytes(S.cap, S.cap_annex))
+        if S.sends is None or S.blk != blk or len(S.sends) != len(ctxs):
+            S.sends = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in ctxs]
+            S.recvs = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in ctxs]
+            S.blk = blk
+        if not annexes:
+            for c, rk, s, info in zip(ctxs, comm.ranks, S.sends, S.infos):
+                check(L.fluere_export_async(c._h, s.data_ptr(), W, rk, S.cap, S.cap_annex, info.data_ptr()),
+                      "fluere_export_async")
+            n0, n1, n_cplx, _, span0, span1 = (int(x) for x in comm.allreduce_max_dev(S.infos))
+            expiry = span0 > 0 and span1 - (SPAN_BIAS - span0) >= timeout_us
+            if n_cplx and not expiry:
+                annexes = True  # some rank has order-dependent flows: export with annexes
+                continue
+        else:
+            n0 = n1 = 0
+            needs = []
+            for c, rk, s in zip(ctxs, comm.ranks, S.sends):
+                need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
+                check(L.fluere_export_device(c._h, s.data_ptr(), W, rk, S.cap, S.cap_annex, ctypes.byref(need),
+                                             ctypes.byref(need_a)), "fluere_export_device")
+                needs.append(np.array([need.value, need_a.value], dtype=np.int64))
+            n0, n1 = (int(x) for x in comm.allreduce_max(needs))
+        if n0 <= S.cap and n1 <= S.cap_annex:
+            break
+        # a shard had more flows for some owner: grow the blocks, export again
+        S.cap = _pow2_at_least(n0, S.cap)
+        S.cap_annex = _pow2_at_least(n1, S.cap_annex)
+    S.bytes_sent = (W - 1) * blk
+    comm.all_to_all_equal(S.sends, S.recvs)
+    stats, rcs = [], []
+    for c, r in zip(ctxs, S.recvs):
+        st = Stats()
+        rc = L.fluere_merge_gathered(c._h, r.data_ptr(), W, S.cap, S.cap_annex, ctypes.byref(st))
+        if rc not in (_lib.OK, _lib.NEED_SWEEP):
+            check(rc, "fluere_merge_gathered")
+        rcs.append(rc)
+        d = st.as_dict()
+        d["rc"] = rc
+        stats.append(d)
+    if any(rc == _lib.NEED_SWEEP for rc in rcs):
+        if not expiry or not all(rc == _lib.NEED_SWEEP for rc in rcs):
+            raise _lib.FluereError(_lib.E_STATE, "sharded merge: ranks disagree on the capture span")
+        stats = _sweep_compose(comm, ctxs, rank_first_fn())
+        for d in stats:
+            d["rc"] = _lib.NEED_SWEEP
+    return stats
+
+
 class ShardExchange:
     """The multi-GPU step: parse + key + aggregate over this rank's shard,
     export into per-owner blocks (summaries of every flow, annexes of the flows
     whose record depends on packet order in this shard, whose records that
     open and close inside the shard stay here), agree on the block capacities,
-    one all-to-all, owner merge.  Every rank ends up holding the final records
-    of its own flows; gather_records() collects them on one rank.
+    one all-to-all, owner merge -- and, when the capture's span reaches the
+    timeout, the sweep composition.  Every rank ends up holding the final
+    records of its own flows; gather_records() collects them on one rank.
 
-    The context must run on torch's current stream (FlowContext(stream=
-    torch.cuda.current_stream().cuda_stream)) so the collective is ordered
-    after the export."""
+    Run the context on torch's current stream (a non-default torch.cuda.Stream
+    made current, FlowContext(stream=that_stream.cuda_stream)) so RCCL orders
+    the collectives after the export without host waits; a context on a
+    stream of its own is synchronised around every collective instead."""
 
     def __init__(self, ctx, cap: int = 64, cap_annex: int = 16, group=None):
         self.ctx, self.group = ctx, group
-        self.cap, self.cap_annex = max(1, int(cap)), max(1, int(cap_annex))
-        self._send = self._recv = None
-        self._info = None
+        self._S = _StepState(cap, cap_annex)
+        self._comm = None
+        self._rank_first = None
 
-    def _buffers(self, world, device):
-        import torch
-        blk = int(_lib.lib().fluere_shard_block_bytes(self.cap, self.cap_annex))
-        if self._send is None or self._send.numel() != world * blk or self._send.device != device:
-            self._send = torch.empty(world * blk, dtype=torch.uint8, device=device)
-            self._recv = torch.empty(world * blk, dtype=torch.uint8, device=device)
-        return blk
+    @property
+    def cap(self):
+        return self._S.cap
 
-    def step(self, allow_unsupported: bool = False):
-        """One sharded pass; this rank's merge stats.  Raises FluereError when
-        the merge cannot give the exact result (FLUERE_E_UNSUPPORTED: the
-        capture needs the hard-timeout sweep) unless allow_unsupported.
+    @property
+    def cap_annex(self):
+        return self._S.cap_annex
 
-        Common case: two host round trips per step -- the export (summaries,
-        no annexes) and a MAX all-reduce of its counts are enqueued behind the
-        pass and read once, then the all-to-all and the owner merge.  If any
-        rank has order-dependent flows, every rank exports again with annexes
-        (fluere_export_device); if a block was too small, every rank exports
-        again with larger blocks."""
-        import torch
-        import torch.distributed as dist
-        L = _lib.lib()
-        ctx = self.ctx
-        world = dist.get_world_size(self.group)
-        rank = dist.get_rank(self.group)
-        dev = torch.device("cuda", torch.cuda.current_device())
-        gloo = dist.get_backend(self.group) == "gloo"
-        if self._info is None:
-            self._info = torch.zeros(4, dtype=torch.int64, device=dev)
-        ctx.parse_aggregate()
-        annexes = False
-        while True:
-            self._buffers(world, dev)
-            if not annexes:
-                check(L.fluere_export_async(ctx._h, self._send.data_ptr(), world, rank, self.cap, self.cap_annex,
-                                            self._info.data_ptr()), "fluere_export_async")
-                if gloo:  # host copy (the context may run on a stream of its own here)
-                    torch.cuda.synchronize()
-                    t = self._info.cpu()
-                else:     # RCCL on torch's stream, which is the context's (see the class note)
-                    t = self._info
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-                n0, n1, n_cplx, _ = (int(x) for x in t.tolist())
-                if n_cplx:
-                    annexes = True  # some rank has order-dependent flows: export with annexes
-                    continue
-            else:
-                need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
-                check(L.fluere_export_device(ctx._h, self._send.data_ptr(), world, rank, self.cap, self.cap_annex,
-                                             ctypes.byref(need), ctypes.byref(need_a)), "fluere_export_device")
-                n0, n1 = agree_need(need.value, need_a.value, self.group, dev)
-            if n0 <= self.cap and n1 <= self.cap_annex:
-                break
-            # a shard had more flows for some owner: grow the blocks, export again
-            self.cap = _pow2_at_least(n0, self.cap)
-            self.cap_annex = _pow2_at_least(n1, self.cap_annex)
-        exchange_blocks(self._send, self._recv, self.group)
-        st = Stats()
-        rc = L.fluere_merge_gathered(ctx._h, self._recv.data_ptr(), world, self.cap, self.cap_annex,
-                                     ctypes.byref(st))
-        if rc != _lib.E_UNSUPPORTED or not allow_unsupported:
-            check(rc, "fluere_merge_gathered")
-        d = st.as_dict()
-        d["rc"] = rc
-        return d
+    @property
+    def bytes_sent(self):
+        """Bytes this rank's last step sent to other ranks in the merge's all-to-all."""
+        return self._S.bytes_sent
+
+    def _rank_first_fn(self):
+        if self._rank_first is None:
+            comm = self._comm
+            mine = np.array([getattr(self.ctx, "index_base", 0), self.ctx.n_packets], dtype=np.int64)
+            g = comm.allgather([mine])
+            first = [int(x) for x in g[:, 0]]
+            total = max(int(a + b) for a, b in g)
+            self._rank_first = first + [total]
+        return self._rank_first
+
+    def step(self):
+        """One sharded pass; this rank's merge stats."""
+        if self._comm is None:
+            self._comm = _DistComm(self.group, self.ctx)
+        (st,) = _shard_step(self._comm, [self.ctx], self._S, self._rank_first_fn)
+        return st
 
     def gather_records(self, dst: int = 0):
         """Every rank's records -> (records, n_ended) on rank dst in the
@@ -153,66 +465,59 @@ class ShardExchange:
         flows); None elsewhere."""
         import torch.distributed as dist
         recs, _ = self.ctx.records()
+        aux = self.ctx.record_order(len(recs))
         parts = [None] * dist.get_world_size(self.group) if dist.get_rank(self.group) == dst else None
-        dist.gather_object(recs.tobytes(), parts, dst=dst, group=self.group)
+        dist.gather_object((recs.tobytes(), aux.tobytes()), parts, dst=dst, group=self.group)
         if parts is None:
             return None
-        return order_records([np.frombuffer(p, dtype=RECORD_DTYPE) for p in parts])
+        return order_records([np.frombuffer(p[0], dtype=RECORD_DTYPE) for p in parts],
+                             [np.frombuffer(p[1], dtype=np.uint64).reshape(-1, 2) for p in parts])
 
 
-NONE64 = (1 << 64) - 1
-
-
-def order_records(parts):
+def order_records(parts, auxes=None):
     """Records of several ranks -> (records, n_ended): ended records by their
-    order key (the global index of the packet that ended them), then active."""
+    order key (the global index of the packet that ended them, then the sweep
+    composition's order words), then active."""
     allr = np.concatenate(parts) if parts else np.zeros(0, dtype=RECORD_DTYPE)
-    order = np.lexsort((allr["first"], allr["order_key"]))
+    if auxes is not None and len(auxes):
+        aux = np.concatenate([a.reshape(-1, 2) for a in auxes]) if len(allr) else np.zeros((0, 2), np.uint64)
+    else:
+        aux = np.zeros((len(allr), 2), dtype=np.uint64)
+    order = np.lexsort((allr["first"], aux[:, 1], aux[:, 0], allr["order_key"]))
     allr = allr[order]
     return allr, int((allr["order_key"] != NONE64).sum())
 
 
 class LogicalShards:
-    """G shards on one device through the same export / merge code, with the
-    all-to-all done by device copies (SURVEY.md section 8e "testing without 8
-    GPUs"): contexts[r] holds packets [first_r, first_r + n_r)."""
+    """G shards on one device through the same export / merge / sweep calls,
+    with every collective done by device copies (SURVEY.md section 8e "testing
+    without 8 GPUs"): contexts[r] holds packets [first_r, first_r + n_r)."""
 
     def __init__(self, contexts, cap: int = 1024, cap_annex: int = 256):
         self.ctxs = contexts
-        self.cap, self.cap_annex = cap, cap_annex
+        self._S = _StepState(cap, cap_annex)
+        self._comm = _LocalComm(len(contexts))
 
-    def run(self, allow_unsupported: bool = False):
-        import torch
-        L = _lib.lib()
-        G = len(self.ctxs)
-        for c in self.ctxs:
-            c.parse_aggregate()
-        while True:
-            blk = int(L.fluere_shard_block_bytes(self.cap, self.cap_annex))
-            sends, n0, n1 = [], 0, 0
-            for r, c in enumerate(self.ctxs):
-                send = torch.empty(G * blk, dtype=torch.uint8, device="cuda")
-                need, need_a = ctypes.c_uint64(), ctypes.c_uint64()
-                check(L.fluere_export_device(c._h, send.data_ptr(), G, r, self.cap, self.cap_annex,
-                                             ctypes.byref(need), ctypes.byref(need_a)), "fluere_export_device")
-                sends.append(send)
-                n0, n1 = max(n0, need.value), max(n1, need_a.value)
-            if n0 <= self.cap and n1 <= self.cap_annex:
-                break
-            self.cap = _pow2_at_least(n0, self.cap)
-            self.cap_annex = _pow2_at_least(n1, self.cap_annex)
-        torch.cuda.synchronize()
-        stats = []
-        for o, c in enumerate(self.ctxs):
-            recv = torch.cat([s[o * blk:(o + 1) * blk] for s in sends])
-            # the contexts run on streams of their own: the copy must have landed
-            torch.cuda.current_stream().synchronize()
-            st = Stats()
-            rc = L.fluere_merge_gathered(c._h, recv.data_ptr(), G, self.cap, self.cap_annex, ctypes.byref(st))
-            if rc != _lib.E_UNSUPPORTED or not allow_unsupported:
-                check(rc, "fluere_merge_gathered")
-            stats.append(st.as_dict())
-        return stats
+    @property
+    def cap(self):
+        return self._S.cap
+
+    @property
+    def cap_annex(self):
+        return self._S.cap_annex
+
+    def _rank_first(self):
+        first = [int(getattr(c, "index_base", 0)) for c in self.ctxs]
+        total = max(f + int(c.n_packets) for f, c in zip(first, self.ctxs))
+        return first + [total]
+
+    def run(self):
+        return _shard_step(self._comm, self.ctxs, self._S, self._rank_first)
 
     def records(self):
-        return order_records([c.records()[0] for c in self.ctxs])
+        parts, auxes = [], []
+        for c in self.ctxs:
+            r, _ = c.records()
+            parts.append(r)
+            auxes.append(c.record_order(len(r)))
+        return order_records(parts, auxes)

@@ -34,6 +34,9 @@ class FlowContext:
         check(L.fluere_open(ctypes.byref(o), ctypes.byref(h)), "fluere_open")
         self._h = h
         self.stream = stream  # HIP stream handle the context runs on (None: its own)
+        self.timeout_ms = int(timeout_ms)
+        self.use_mac = bool(use_mac)
+        self.index_base = 0  # global index of the first packet (dist.set_index_base)
         self._keep = []  # device buffers the batches point into
         self.n_packets = 0
 
@@ -80,12 +83,9 @@ class FlowContext:
         self._keep.extend([d_bytes, d_offsets, *keep])
         self.n_packets += n
 
-    def run(self, allow_unsupported: bool = False) -> dict:
+    def run(self) -> dict:
         st = Stats()
-        rc = self._L.fluere_run(self._h, ctypes.byref(st))
-        if rc == _lib.E_UNSUPPORTED and allow_unsupported:
-            rc = 0
-        check(rc, "fluere_run")
+        check(self._L.fluere_run(self._h, ctypes.byref(st)), "fluere_run")
         return st.as_dict()
 
     def parse_aggregate(self):
@@ -111,6 +111,14 @@ class FlowContext:
         finally:
             self._L.fluere_records_free(p)
         return np.frombuffer(raw, dtype=RECORD_DTYPE).copy(), ne.value
+
+    def record_order(self, n: int) -> np.ndarray:
+        """The two order words of each record of records() (n of them; zero
+        except after the sharded sweep composition, dist.py)."""
+        out = np.zeros((n, 2), dtype=np.uint64)
+        check(self._L.fluere_get_record_order(self._h, out.ctypes.data_as(ctypes.c_void_p) if n else None, n),
+              "fluere_get_record_order")
+        return out
 
     def parse_batch(self, general_only: bool = False) -> np.ndarray:
         """Per-packet parse_keys / parse_fluereflow view (PKT_META_DTYPE)."""

@@ -40,13 +40,17 @@ enum fluere_status {
     FLUERE_OK = 0,
     FLUERE_E_ARG = -1,         /* bad argument */
     FLUERE_E_IO = -2,          /* file open/read/write failed (FluereError::IoError) */
-    FLUERE_E_PCAP = -3,        /* not a classic pcap file (FluereError::PcapError) */
+    FLUERE_E_PCAP = -3,        /* not a pcap or pcapng capture (FluereError::PcapError) */
     FLUERE_E_HIP = -4,         /* HIP runtime error / no device */
     FLUERE_E_NOMEM = -5,       /* device or host allocation failed */
     FLUERE_E_TABLE_FULL = -6,  /* flow dictionary capacity exceeded: reopen with larger max_flows */
-    FLUERE_E_UNSUPPORTED = -7, /* the sharded merge cannot give the exact result (expiries inside the capture) */
+    FLUERE_E_UNSUPPORTED = -7, /* no exact result on this path (sharded sweep without a fixed point; never seen) */
     FLUERE_E_STATE = -8        /* call order violated */
 };
+/* Positive status (not an error): fluere_merge_gathered merged the summaries
+ * of a capture whose span reaches the timeout; its records come from the
+ * sweep composition (fluere_sweep_*). */
+#define FLUERE_NEED_SWEEP 1
 
 /* NetError per packet (src/net/mod.rs:28-36). */
 enum fluere_pkt_status {
@@ -266,10 +270,13 @@ uint64_t fluere_shard_block_bytes(uint64_t cap, uint64_t cap_annex);
 int fluere_export_device(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
                          uint64_t cap_annex, uint64_t* need, uint64_t* need_annex);
 /* The common case of fluere_export_device without a host round trip (no
- * annexes): d_info (device memory, 4 x uint64) receives {largest per-owner
- * summary count, annex count, order-dependent flows, flow count}.  The caller
- * reduces d_info over the ranks (MAX, on the context's stream) and reads it
- * once: if any rank has order-dependent flows every rank calls
+ * annexes): d_info (device memory, 6 x uint64) receives {largest per-owner
+ * summary count, annex count, order-dependent flows, flow count, 2^62 - the
+ * earliest valid time, the latest valid time} (the last two 0 without a valid
+ * packet).  The caller reduces d_info over the ranks (MAX, on the context's
+ * stream) and reads it once: if the capture's span (latest - earliest) reaches
+ * the timeout, the merge is completed by the sweep composition below (no
+ * annexes); else if any rank has order-dependent flows every rank calls
  * fluere_export_device instead; if a count exceeds cap / cap_annex every rank
  * exports again with larger blocks. */
 int fluere_export_async(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint32_t shard, uint64_t cap,
@@ -278,11 +285,63 @@ int fluere_export_async(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint
  * all-to-all leaves them) into this context's (cleared) flow table and build
  * the owner's records; the context keeps the final records its own export
  * produced, so fluere_get_records returns every record this rank holds.
- * FLUERE_E_ARG if a block was cut short; FLUERE_E_UNSUPPORTED if the
- * capture's span reaches the timeout (the sweep is not composed across shards:
- * run the capture in one context). */
+ * FLUERE_E_ARG if a block was cut short.  FLUERE_NEED_SWEEP (> 0) if the
+ * capture's span reaches the timeout: the flows are merged but have no record
+ * yet; every rank completes the merge with the fluere_sweep_* sequence. */
 int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
                           uint64_t cap_annex, fluere_stats* stats);
+
+/* ---- the hard-timeout sweep across shards (offline_fluereflows.rs:103-119,
+ * 161-175): an expiry entry pushed at a flow's creation fires at the first
+ * processed packet of the WHOLE capture with t >= exp, so shards are coupled.
+ * Every rank is both a holder (of its packet range) and an owner (of its
+ * flows, as in the merge); after fluere_merge_gathered returned
+ * FLUERE_NEED_SWEEP (the export made without annexes), every rank runs:
+ *   1. fluere_sweep_pack (holder): counts[o] = this shard's valid packets of
+ *      owner o's flows; with d_send, their 32-byte records, owner-major,
+ *      capture order within an owner.  All-to-all (split sizes from counts).
+ *   2. fluere_sweep_load (owner): the records received, shard-major (counts[s]
+ *      from shard s).
+ *   3. a fixed point over the processed packets, per pass:
+ *      a. fluere_sweep_index (holder): apply the owners' processed flags
+ *         (d_pr: 1 byte per packed packet in the pack order, as the reverse
+ *         all-to-all of step e leaves them; NULL on the first pass); *max_time
+ *         = 1 + the latest processed packet's time (0: none).  All-gather.
+ *      b. fluere_sweep_queries (holder): sweep points of its create-eligible
+ *         packets; those past its own processed packets become queries to the
+ *         first later shard whose max_time reaches exp: qcounts[r]; with d_q,
+ *         the queries (8 bytes each, grouped by shard).  All-to-all.
+ *      c. fluere_sweep_answer (answering shard): n queries -> packet indices
+ *         (8 bytes each, same order).  All-to-all back.
+ *      d. fluere_sweep_points (holder): the answers -> d_f, 8 bytes per packed
+ *         packet (the pack order).  All-to-all (as step 1, 8-byte elements).
+ *      e. fluere_sweep_chase (owner): the exact chase with those sweep points;
+ *         d_pr: 1 byte per loaded packet (processed); *changed.  MAX over the
+ *         ranks; reverse all-to-all of d_pr; stop when no rank changed.
+ *   4. fluere_sweep_seed_requests (owner): the creating packets of its flow
+ *      instances (8-byte global indices, ascending), counts[r] per holder
+ *      (rank_first[r] = first global index of rank r, n_ranks + 1 entries).
+ *      All-to-all; fluere_sweep_seeds (holder): 40-byte FluereRecord seeds,
+ *      same order; all-to-all back.
+ *   5. fluere_sweep_finish (owner): the records (fluere_get_records).  Their
+ *      order is global: order_key = the index of the packet that ended them,
+ *      then fluere_get_record_order's two words {0 for a FIN/RST close, else
+ *      exp + 1; the creation index of the firing entry}. */
+int fluere_sweep_pack(fluere_ctx* ctx, uint32_t n_owners, uint64_t* counts, void* d_send);
+int fluere_sweep_load(fluere_ctx* ctx, const void* d_recv, uint32_t n_shards, const uint64_t* counts);
+int fluere_sweep_index(fluere_ctx* ctx, const uint8_t* d_pr, uint64_t* max_time);
+int fluere_sweep_queries(fluere_ctx* ctx, uint32_t n_ranks, uint32_t rank, const uint64_t* max_times,
+                         uint64_t* qcounts, void* d_q);
+int fluere_sweep_answer(fluere_ctx* ctx, const void* d_q, uint64_t n, void* d_ans);
+int fluere_sweep_points(fluere_ctx* ctx, const void* d_ans, void* d_f);
+int fluere_sweep_chase(fluere_ctx* ctx, const void* d_f, void* d_pr, int* changed);
+int fluere_sweep_seed_requests(fluere_ctx* ctx, uint32_t n_ranks, const uint64_t* rank_first, uint64_t* counts,
+                               void* d_req);
+int fluere_sweep_seeds(fluere_ctx* ctx, const void* d_req, uint64_t n, void* d_seeds);
+int fluere_sweep_finish(fluere_ctx* ctx, const void* d_seeds, fluere_stats* stats);
+/* Two order words per record, in fluere_get_records' order (n = its count):
+ * non-zero only after fluere_sweep_finish. */
+int fluere_get_record_order(fluere_ctx* ctx, uint64_t* aux, uint64_t n);
 
 /* ---- live mode (src/net/live_fluereflow.rs:196-376) on batched capture --- */
 /* A live session: packets arrive in batches (a classic pcap image each: the
@@ -378,7 +437,8 @@ enum {
     FLUERE_SYNTH_TCP = 4,       /* IMIX sizes; TCP with handshakes, 4-way closes (the peer's packets after the
                                    first FIN), RSTs, reopened keys, mid-stream starts, elephants; and UDP */
     FLUERE_SYNTH_SLOW = 5       /* the general parser's classes: IMIX schedule at 128/576/1500 B, per flow
-                                   IPv6 (1/2), VXLAN-encapsulated IPv4 (1/4) or IPv4 with options (1/4) */
+                                   IPv6 (1/2), VXLAN-encapsulated IPv4 (1/4) or IPv4 with options (1/4) */,
+    FLUERE_SYNTH_TCP_BACKTIME = 6 /* FLUERE_SYNTH_TCP with 1 % of the timestamps up to 5 ms early (out of order) */
 };
 
 /* Size of the synthetic pcap file (24-B header + records). */

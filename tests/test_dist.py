@@ -93,3 +93,66 @@ def test_order_records_merges_ranks():
     assert ne == 3
     assert list(recs["order_key"][:3]) == [7, 12, 40]
     assert list(recs["first"][3:]) == [3, 5]
+
+
+def _var_worker(rank, world, port, q):
+    """exchange_var: rank r sends (r + 1) * (o + 1) records of 3 bytes to rank
+    o, each byte = 16 * r + o; every rank receives its segments in rank order
+    with the right counts.  Also the communicator's all-gather and MAX."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        counts = np.array([(rank + 1) * (o + 1) for o in range(world)], dtype=np.uint64)
+        send = torch.cat([torch.full((int(c) * 3,), 16 * rank + o, dtype=torch.uint8) for o, c in enumerate(counts)])
+        recv, rc = fdist.exchange_var(send, counts, 3)
+        n = int(rc.sum()) * 3
+        comm = fdist._DistComm.__new__(fdist._DistComm)
+        comm.group, comm.world, comm.ranks, comm.gloo = None, world, [rank], True
+        comm.device = torch.device("cpu")
+        comm.same_stream = True
+        g = comm.allgather([np.array([rank, 10 * rank], dtype=np.int64)])
+        m = comm.allreduce_max([np.array([rank, -rank], dtype=np.int64)])
+        q.put((rank, recv[:n].numpy().tobytes(), [int(x) for x in rc], g.tolist(), m.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_var_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_var_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for o in range(world):
+        raw, rc, g, m = got[o]
+        assert rc == [(r + 1) * (o + 1) for r in range(world)]
+        want = b"".join(bytes([16 * r + o]) * (3 * (r + 1) * (o + 1)) for r in range(world))
+        assert raw == want
+        assert g == [[r, 10 * r] for r in range(world)]
+        assert m == [world - 1, 0]
+
+
+
+def test_order_records_sweep_words():
+    """Sharded sweep records: ties of the ending packet's index are broken by
+    the order words (FIN/RST close first, then by exp, then by the firing
+    entry's creation), not by `first`."""
+    from fluere_amd._lib import RECORD_DTYPE
+    a = np.zeros(3, dtype=RECORD_DTYPE)
+    b = np.zeros(2, dtype=RECORD_DTYPE)
+    a["order_key"] = [50, 50, fdist.NONE64]
+    a["first"] = [1, 2, 3]
+    b["order_key"] = [50, 20]
+    b["first"] = [0, 9]
+    aa = np.array([[101, 7], [101, 3], [0, 0]], dtype=np.uint64)
+    ab = np.array([[0, 0], [0, 0]], dtype=np.uint64)
+    recs, ne = fdist.order_records([a, b], [aa, ab])
+    assert ne == 4
+    assert list(recs["order_key"]) == [20, 50, 50, 50, fdist.NONE64]
+    assert list(recs["first"]) == [9, 0, 2, 1, 3]

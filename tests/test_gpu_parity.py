@@ -255,13 +255,34 @@ def test_sharded_cut_short_block_is_an_error(gpu):
         c.close()
 
 
-def test_sharded_expiry_is_unsupported(gpu):
-    """The hard-timeout sweep is not composed across shards: a capture whose
-    span reaches the timeout is refused by the merge, loudly."""
-    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 50_000, 500, 0xF10E0027)
-    ls, ctxs = _logical_shards(cfg, 2, timeout_ms=10)
-    with pytest.raises(FluereError):
-        ls.run()
+SWEEP_SHARDS = {
+    # realistic TCP whose span reaches the timeout: the hard-timeout sweep
+    # composed across shards (dist._sweep_compose); 2M packets span 2 s
+    "tcp_2m_t1000": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0017, 1000),
+    "tcp_400k_t10": (_lib.SYNTH_TCP, 400_000, 4_000, 0xF10E0017, 10),
+    # 1 % of the timestamps up to 5 ms early: entries fire out of creation order
+    "backtime_400k_t10": (_lib.SYNTH_TCP_BACKTIME, 400_000, 4_000, 0xF10E0047, 10),
+    "backtime_2m_t1000": (_lib.SYNTH_TCP_BACKTIME, 2_000_000, 20_000, 0xF10E0047, 1000),
+}
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+@pytest.mark.parametrize("name", sorted(SWEEP_SHARDS))
+def test_sharded_expiry_sweep(gpu, name, G):
+    """A capture whose span reaches the timeout over G logical shards: the
+    shards ship their packets to the keys' owners, compute sweep points over
+    their own processed packets (later shards answer the rest), and the owners
+    chase until the processed set is stable (offline_fluereflows.rs:103-119,
+    161-175) -- the records and their order equal the oracle's."""
+    kind, n, lanes, seed, t = SWEEP_SHARDS[name]
+    cfg = fluere_amd.synth_cfg(kind, n, lanes, seed)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg), t)
+    ls, ctxs = _logical_shards(cfg, G, max_flows=1 << 20, timeout_ms=t)
+    st = ls.run()
+    assert all(x["rc"] == _lib.NEED_SWEEP for x in st)
+    recs, ne = ls.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"{name} G={G}")
+    assert ne == want["n_ended"] and ne > 0
     for c in ctxs:
         c.close()
 
@@ -282,6 +303,37 @@ def test_c2_full_size_parity(gpu):
     assert np.all(recs["in_pkts"] + recs["out_pkts"] == recs["d_pkts"])
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "c2-10M")
+
+
+FULL_SIZE = {
+    # BASELINE configs[2]: 10M IMIX (3.7 GB), 100k flows
+    "c3": (_lib.SYNTH_IMIX, 10_000_000, 100_000, 0xF10E0003, False),
+    # BASELINE configs[4]: 10M x 64 B 802.1Q, 50k MAC pairs, -M (header-only
+    # CSV, keys.rs:417-435) and the same frames untagged (50k MAC-keyed rows)
+    "c5": (_lib.SYNTH_VLAN64, 10_000_000, 50_000, 0xF10E0005, True),
+    "c5u": (_lib.SYNTH_MAC64, 10_000_000, 50_000, 0xF10E0005, True),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FULL_SIZE))
+def test_full_size_parity(gpu, name):
+    """BASELINE configs at full size, generated in HBM as the bench does,
+    against the oracle on the identical host image."""
+    kind, n, flows, seed, use_mac = FULL_SIZE[name]
+    cfg = fluere_amd.synth_cfg(kind, n, flows, seed)
+    with fluere_amd.FlowContext(use_mac=use_mac, max_flows=max(1 << 16, 2 * flows)) as ctx:
+        for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, 0, n):
+            ctx.add_device_batch(b, nbytes, o, nb)
+        torch.cuda.synchronize()
+        st = ctx.run()
+        recs, ne = ctx.records()
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg), use_mac=use_mac)
+    assert st["packets"] == n
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"{name} full size")
+    if name == "c5":
+        assert len(recs) == 0  # the vlan_keys misparse drops every frame
+    else:
+        assert len(recs) >= flows if name == "c3" else len(recs) == flows
 
 
 @pytest.mark.parametrize("n_keys,dup", [(64, 1), (5000, 1), (5000, 4), (100_000, 3)])
@@ -516,14 +568,46 @@ def test_tcp_realistic_matches_oracle(gpu, name):
             assert st["sequential_mode"] == 1  # the parallel sweep, not the fallback
 
 
-def test_mode_b_fallback_on_backward_time(gpu):
-    """Timestamps that go backwards: the sweep order is not the FIFO the
-    parallel chase assumes, so the run takes the sequential kernel."""
+def test_mode_b_backward_time_fixture(gpu):
+    """Timestamps that go backwards (edge_keys): the sweep points come from
+    the max segment tree and the pending entries are kept in pop order, so the
+    parallel sweep runs (sequential_mode 1); the sequential kernel, forced,
+    agrees."""
+    data = golden_pcap("edge_keys")
+    want = pyoracle.offline(data, 1, True)
+    csv, ne, st = _gpu_csv(data, 1, use_mac=True)
+    assert st["sequential_mode"] == 1
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "edge_keys t=1 -M")
+
+
+def test_mode_b_sequential_kernel_forced(gpu, monkeypatch):
+    monkeypatch.setenv("FLUERE_SEQ_MODE_B", "1")
     data = golden_pcap("edge_keys")
     want = pyoracle.offline(data, 1, True)
     csv, ne, st = _gpu_csv(data, 1, use_mac=True)
     assert st["sequential_mode"] == 2
-    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "edge_keys t=1 -M")
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "edge_keys t=1 -M (sequential)")
+
+
+BACKTIME = {
+    "backtime_200k": (200_000, 2_000, (10, 100)),
+    "backtime_2m": (2_000_000, 20_000, (10, 1000)),
+    "backtime_10m": (10_000_000, 100_000, (1000,)),  # the bench's tcp_t1 workload, out of order
+}
+
+
+@pytest.mark.parametrize("name", sorted(BACKTIME))
+def test_backward_timestamps_parallel_sweep(gpu, name):
+    """1 % of the timestamps up to 5 ms early (FLUERE_SYNTH_TCP_BACKTIME):
+    expiry entries fire out of creation order; the parallel sweep (not the
+    one-thread kernel) equals the oracle."""
+    n, lanes, timeouts = BACKTIME[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP_BACKTIME, n, lanes, 0xF10E0047))
+    for t in timeouts:
+        want = pyoracle.offline(data, t)
+        csv, ne, st = _gpu_csv(data, t, max_flows=max(1 << 16, n // 2))
+        assert st["sequential_mode"] == 1
+        assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"{name} t={t}")
 
 
 def test_c4_recipe_8_shards_1m_flows(gpu):
@@ -544,9 +628,12 @@ def test_c4_recipe_8_shards_1m_flows(gpu):
 
 EXCHANGE_CASES = {
     # order-dependent flows in every shard: the annex export (fluere_export_device)
-    "tcp": (_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037),
+    "tcp": (_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037, 600000),
     # UDP only: the one-round-trip export (fluere_export_async) every step
-    "udp": (_lib.SYNTH_UDP64, 400_000, 2_000, 0xF10E0038),
+    "udp": (_lib.SYNTH_UDP64, 400_000, 2_000, 0xF10E0038, 600000),
+    # span >= timeout: the sweep composition over the process group
+    "tcp_sweep": (_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037, 10),
+    "backtime_sweep": (_lib.SYNTH_TCP_BACKTIME, 300_000, 3_000, 0xF10E0047, 10),
 }
 
 
@@ -557,9 +644,13 @@ def _shard_exchange_rank(rank, world, port, q, case):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = fluere_amd.synth_cfg(*EXCHANGE_CASES[case])
+        kind, n_pk, lanes, seed, t = EXCHANGE_CASES[case]
+        cfg = fluere_amd.synth_cfg(kind, n_pk, lanes, seed)
         first, n = fluere_amd.dist.shard_range(cfg.n_packets, rank, world)
-        ctx = fluere_amd.FlowContext(max_flows=1 << 18, stream=torch.cuda.current_stream().cuda_stream)
+        # the context on a torch stream of its own (not the null stream), made current
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
+        ctx = fluere_amd.FlowContext(timeout_ms=t, max_flows=1 << 18, stream=stream.cuda_stream)
         fluere_amd.dist.set_index_base(ctx, first)
         for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, first, n):
             ctx.add_device_batch(b, nbytes, o, nb)
@@ -583,8 +674,8 @@ def test_shard_exchange_two_ranks_gloo(gpu, case):
     gather -- against the oracle on the whole capture."""
     import socket
     import torch.multiprocessing as mp
-    cfg = fluere_amd.synth_cfg(*EXCHANGE_CASES[case])
-    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    kind, n_pk, lanes, seed, t = EXCHANGE_CASES[case]
+    want = pyoracle.offline(fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n_pk, lanes, seed)), t)
     sk = socket.socket()
     sk.bind(("127.0.0.1", 0))
     port = sk.getsockname()[1]
