@@ -53,6 +53,7 @@ namespace fl {
 namespace {
 
 constexpr uint64_t M40 = (1ull << 40) - 1;
+constexpr uint64_t HI_ACTIVE = (1ull << 41) - 1;  // Mode B order key of an active record (after every ended one)
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr int MAX_PASSES = 32;
 enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2, K_LEAD = 3 };
@@ -130,39 +131,39 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
         }
     }
     flag[off + li] = take;
-    meta[off + li] = m;
+    if (take) meta[off + li] = m;  // (k_ex_compact reads the taken ones only)
 }
 
 // compaction in capture order: cm[k] = the k-th replayed packet; sort keys (key, index)
 __global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta, const uint32_t* flag, const uint32_t* pos,
-                                                    uint64_t n, ExMeta* cm, unsigned long long* key, uint32_t* val) {
+                                                    uint64_t n, ExMeta* cm, uint32_t* key, uint32_t* val) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !flag[i]) return;
     const uint32_t k = pos[i];
     const ExMeta m = meta[i];
     cm[k] = m;
-    key[k] = ((unsigned long long)m.d << 40) | (m.gidx & M40);
+    key[k] = m.d;  // (a stable sort by flow keeps capture order within a flow)
     val[k] = k;
 }
 
 // sharded Mode B owner: sort keys of the shards' packets (capture order)
-__global__ void __launch_bounds__(256) k_ex_keys(uint64_t n, const ExMeta* cm, unsigned long long* key, uint32_t* val) {
+__global__ void __launch_bounds__(256) k_ex_keys(uint64_t n, const ExMeta* cm, uint32_t* key, uint32_t* val) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
-    key[k] = ((unsigned long long)cm[k].d << 40) | (cm[k].gidx & M40);
+    key[k] = cm[k].d;
     val[k] = (uint32_t)k;
 }
 
 // ---- 2. sorted view, key heads, next-eligible / next-FIN inputs -------------
-__global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const unsigned long long* skey, const uint32_t* sval,
+__global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* skey, const uint32_t* sval,
                                                    const ExMeta* cm, ExMeta* sm, uint32_t* hf,
                                                    unsigned long long* re, unsigned long long* rf) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const ExMeta m = cm[sval[p]];
     sm[p] = m;
-    const unsigned long long d = skey[p] >> 40;
-    hf[p] = (p == 0 || (skey[p - 1] >> 40) != d) ? 1u : 0u;
+    const unsigned long long d = skey[p];
+    hf[p] = (p == 0 || skey[p - 1] != skey[p]) ? 1u : 0u;
     // reversed, so an inclusive min-scan gives the first eligible / FIN-RST
     // position at or after p within the key (low 40 bits M40: none)
     re[n - 1 - p] = (d << 40) | ((m.bits & 1) ? p : M40);
@@ -540,7 +541,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
     }
     if (rec_live) {
         a.tmp[q] = rec;
-        a.hi[q] = kind == K_ACTIVE ? NONE64 : (cj << 1) | (kind == K_SWEEP ? 1ull : 0ull);
+        a.hi[q] = kind == K_ACTIVE ? HI_ACTIVE : (cj << 1) | (kind == K_SWEEP ? 1ull : 0ull);
         a.lo[q] = kind == K_SWEEP ? cie : 0ull;
         a.ex[q] = kind == K_SWEEP ? cex : 0ull;
         a.idx[q] = q;
@@ -579,8 +580,8 @@ __global__ void __launch_bounds__(256) k_ex_emit_owner(uint32_t n_inst, const ui
         const fluere_record rec = tmp[q];
         out[r] = rec;
         const unsigned long long h = hi[q];
-        aux[2 * r] = h == NONE64 ? 0ull : ((h & 1) ? ex[q] + 1 : 0ull);
-        aux[2 * r + 1] = h == NONE64 ? 0ull : lo[q];
+        aux[2 * r] = h == HI_ACTIVE ? 0ull : ((h & 1) ? ex[q] + 1 : 0ull);
+        aux[2 * r + 1] = h == HI_ACTIVE ? 0ull : lo[q];
         upd = rec.d_pkts;
         ended = rec.order_key != NONE64;
     }
@@ -636,7 +637,8 @@ struct ExactSession {
     size_t tmp = 0;
     void* tp = nullptr;
     ExMeta *cm, *sm;
-    unsigned long long *key, *skey, *re, *rf, *ne_rev, *nf_rev, *npr, *np_rev, *ej, *ij, *iie, *iex;
+    uint32_t *key, *skey;
+    unsigned long long *re, *rf, *ne_rev, *nf_rev, *npr, *np_rev, *ej, *ij, *iie, *iex;
     unsigned long long *hi, *lo, *ex, *hi2, *gk, *tree;
     unsigned long long nrec_new = 0;
     uint64_t tree_P = 0;
@@ -670,8 +672,8 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         size_t b = 0;
         auto add = [&](size_t x) { b += ((x + 255) & ~(size_t)255) + 256; };
         add(n_all * sizeof(ExMeta)); add(n_all * 4); add(n_all * 4);  // meta, flag, pos
-        add(n * sizeof(ExMeta)); add(n * 8); add(n * 4);              // cm, key, val
-        add(n * 8); add(n * 4); add(n * sizeof(ExMeta));              // skey, sval, sm
+        add(n * sizeof(ExMeta)); add(n * 4); add(n * 4);              // cm, key, val
+        add(n * 4); add(n * 4); add(n * sizeof(ExMeta));              // skey, sval, sm
         add(n * 4); add(n * 4); add(n * 4);                           // hf, hpos, heads
         add(n * 8); add(n * 8); add(n * 8); add(n * 8);               // re, rf, ne_rev, nf_rev
         add(n); add(n * 8); add(n * 8); add(n * 8); add(n * 4);       // pr, npr, np_rev, ej, link
@@ -696,6 +698,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         (void)hipcub::DeviceScan::InclusiveSum(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, n, s); tmp = std::max(tmp, t);
         (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 64, s);
+        tmp = std::max(tmp, t);
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 32, s);
         tmp = std::max(tmp, t);
         (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                           hipcub::Min(), n, s);
@@ -733,9 +738,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     }
     size_t tb = tmp;
     ExMeta* cm = S->cm = A.take<ExMeta>(N);
-    unsigned long long* key = S->key = A.take<unsigned long long>(N);
+    uint32_t* key = S->key = A.take<uint32_t>(N);
     uint32_t* val = S->val = A.take<uint32_t>(N);
-    unsigned long long* skey = S->skey = A.take<unsigned long long>(N);
+    uint32_t* skey = S->skey = A.take<uint32_t>(N);
     uint32_t* sval = S->sval = A.take<uint32_t>(N);
     ExMeta* sm = S->sm = A.take<ExMeta>(N);
     uint32_t* hf = S->hf = A.take<uint32_t>(N);
@@ -796,9 +801,11 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     S->R.replayed = n;
     if (!n) return FLUERE_OK;
     const int in = (int)n;
-    // ---- 2. sort by (key, index); key heads; next eligible / FIN-RST
-    int end_bit = 40;
-    while (end_bit < 64 && (1ull << (end_bit - 40)) <= J.T.fmax) end_bit++;
+    // ---- 2. sort by (key, index): a stable sort by key of the capture-order
+    // packets (LSD radix: ceil(log2 fmax) bits, not key + index); key heads;
+    // next eligible / FIN-RST
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) < J.T.fmax) end_bit++;
     tb = tmp;
     HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tp, tb, key, skey, val, sval, in, 0, end_bit, s));
     k_ex_gather<<<gridn(n, 256), 256, 0, s>>>(n, skey, sval, cm, sm, hf, re, rf);
@@ -944,7 +951,7 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
         uint32_t* cur = S->idx;   // permutation so far (k_ex_records: the identity)
         uint32_t* nxt = S->idx2;
         tb = S->tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->lo, S->hi2, cur, nxt, ni, 0, 64, s));
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->lo, S->hi2, cur, nxt, ni, 0, 40, s));
         std::swap(cur, nxt);
         if (!S->mono) {  // exp order differs from creation order only when times go backwards
             k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, cur, S->ex, S->gk);
@@ -954,7 +961,7 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
         }
         k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, cur, S->hi, S->gk);
         tb = S->tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->gk, S->hi2, cur, S->perm, ni, 0, 64, s));
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->gk, S->hi2, cur, S->perm, ni, 0, 41, s));
         if (aux_out) {
             k_ex_emit_owner<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->perm, S->tmpr, S->hi, S->ex, S->lo,
                                                                J.g, *J.d_recs + gh.n_rec, aux_out);
@@ -979,14 +986,14 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
     if (!N) return FLUERE_OK;
     ExMeta* meta = nullptr;
     uint32_t *flag = nullptr, *pos = nullptr;
-    unsigned long long* key = nullptr;
+    uint32_t* key = nullptr;
     uint32_t* val = nullptr;
     void* tp = nullptr;
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)N, s);
     int rc = FLUERE_OK;
     if (hipMalloc(&meta, N * sizeof(ExMeta)) != hipSuccess || hipMalloc(&flag, N * 4) != hipSuccess ||
-        hipMalloc(&pos, N * 4) != hipSuccess || hipMalloc(&key, N * 8) != hipSuccess ||
+        hipMalloc(&pos, N * 4) != hipSuccess || hipMalloc(&key, N * 4) != hipSuccess ||
         hipMalloc(&val, N * 4) != hipSuccess || hipMalloc(&tp, std::max<size_t>(tb, 16)) != hipSuccess)
         rc = FLUERE_E_NOMEM;
     if (rc == FLUERE_OK) {

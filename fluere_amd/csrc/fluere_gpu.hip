@@ -5100,6 +5100,35 @@ __global__ void __launch_bounds__(256) k_live_scan(LiveArgs a, unsigned long lon
     }
 }
 
+// session dictionary compaction: the open flows' keys and pieces out ...
+__global__ void __launch_bounds__(256) k_live_collect(LiveArgs a, const uint8_t* flow_key, uint8_t* ckey,
+                                                      fluere_flow_piece* cpiece, unsigned long long* cnt) {
+    const uint32_t np = min(*a.Tp.n_flows, a.Tp.fmax);
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
+        if (!a.P_open[p]) continue;
+        const unsigned long long i = atomicAdd(cnt, 1ull);
+        const uint4* src = reinterpret_cast<const uint4*>(flow_key + (size_t)p * 56);
+        uint2* dst = reinterpret_cast<uint2*>(ckey + i * 56);
+        const uint2* s2 = reinterpret_cast<const uint2*>(src);
+        for (int k = 0; k < 7; k++) dst[k] = s2[k];
+        cpiece[i] = a.P[p];
+        a.P_open[p] = 0;
+    }
+}
+// ... and back into the cleared dictionary (new dense ids)
+__global__ void __launch_bounds__(256) k_live_reinsert(LiveArgs a, const uint8_t* ckey, const fluere_flow_piece* cpiece,
+                                                       unsigned long long n) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    CKey k;
+    const uint32_t* kw = reinterpret_cast<const uint32_t*>(ckey + i * 56);
+    for (int j = 0; j < 14; j++) k.w[j] = kw[j];
+    const uint32_t p = dense_of_key(a.Tp, k, true, a.pslots, nullptr);
+    if (p == FAIL || p >= a.Tp.fmax) return;  // (the error word is set)
+    a.P[p] = cpiece[i];
+    a.P_open[p] = 1;
+}
+
 __global__ void k_live_time(const Batch* bs, int nb, unsigned long long gi, int macs, unsigned long long* t) {
     if (threadIdx.x || blockIdx.x) return;
     Parsed P;
@@ -5124,7 +5153,12 @@ struct fluere_live {
     int use_mac = 0;
     bool last_have = false;         // the last batch had a processed packet ...
     uint64_t last_time = 0;         // ... at this time (the checks' `time`)
+    bool export_due = false;        // an interval elapsed: export after the next processed packet
     std::vector<fluere_record> pending;  // FIN/RST-closed records since the last export
+    uint64_t persist_nf = 0;        // flows in the session dictionary (open or not)
+    uint8_t* ckey = nullptr;        // compaction scratch: open flows' keys and pieces
+    fluere_flow_piece* cpiece = nullptr;
+    uint64_t ccap = 0;
 };
 
 extern "C" int fluere_live_open(const fluere_opts* o, fluere_live** out) {
@@ -5161,6 +5195,8 @@ extern "C" int fluere_live_close(fluere_live* lv) {
     hipFree(lv->blk);
     hipFree(lv->out);
     hipFree(lv->ctr);
+    hipFree(lv->ckey);
+    hipFree(lv->cpiece);
     delete lv;
     return FLUERE_OK;
 }
@@ -5213,6 +5249,42 @@ static int live_export(fluere_live* lv, std::vector<fluere_record>& scan, fluere
     return FLUERE_OK;
 }
 
+// The session dictionary keeps a key until it is compacted: flows closed by
+// FIN/RST or expired by a scan leave the reference's active_flow
+// (live_fluereflow.rs:299,336,371), so the session's state is bounded by its
+// open flows.  When the dictionary cannot take a batch's new flows, the open
+// flows are re-inserted into a cleared dictionary.
+static int live_compact(fluere_live* lv) {
+    fluere_ctx* pc = lv->persist;
+    hipStream_t s = lv->batch->stream;
+    const uint64_t fmax = pc->fmax;
+    if (lv->ccap < fmax) {
+        hipFree(lv->ckey);
+        hipFree(lv->cpiece);
+        lv->ckey = nullptr;
+        lv->cpiece = nullptr;
+        lv->ccap = 0;
+        if (hipMalloc(&lv->ckey, fmax * 56) != hipSuccess ||
+            hipMalloc(&lv->cpiece, fmax * sizeof(fluere_flow_piece)) != hipSuccess)
+            return FLUERE_E_NOMEM;
+        lv->ccap = fmax;
+    }
+    LiveArgs a = live_args(lv);
+    HIPCHECK(hipMemsetAsync(lv->ctr + 1, 0, 8, s));
+    k_live_collect<<<flow_grid(pc), 256, 0, s>>>(a, pc->d_flow_key, lv->ckey, lv->cpiece, lv->ctr + 1);
+    unsigned long long n = 0;
+    HIPCHECK(hipMemcpyAsync(&n, lv->ctr + 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    int rc = clear_flows(pc);  // (on the dictionary context's stream)
+    if (rc) return rc;
+    HIPCHECK(hipStreamSynchronize(pc->stream));
+    if (n) k_live_reinsert<<<grid_for(n, 256), 256, 0, s>>>(a, lv->ckey, lv->cpiece, n);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
+    lv->persist_nf = n;
+    return FLUERE_OK;
+}
+
 extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, int do_export,
                                  fluere_record** recs, uint64_t* n, uint64_t* n_ordered, int* exported) {
     if (!lv || !pcap || !recs || !n) return FLUERE_E_ARG;
@@ -5231,6 +5303,7 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
     lv->last_have = false;
     if (c->n_total) {
         if ((rc = fluere_parse_aggregate(c))) return rc;
+        uint64_t need_nf = 0;
         for (;;) {  // one owner: the whole batch
             const uint64_t bb = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
             if (bb > lv->blk_bytes) {
@@ -5242,6 +5315,7 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
             }
             uint64_t need = 0, need_a = 0;
             if ((rc = fluere_export_device(c, lv->blk, 1, 0, lv->cap, lv->cap_annex, &need, &need_a))) return rc;
+            need_nf = need;
             if (need <= lv->cap && need_a <= lv->cap_annex) break;
             while (lv->cap < need) lv->cap *= 2;
             while (lv->cap_annex < need_a) lv->cap_annex *= 2;
@@ -5253,6 +5327,12 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
             HIPCHECK(hipMemcpyAsync(lv->pending.data() + at, c->d_recs, c->local_n_rec * sizeof(fluere_record),
                                     hipMemcpyDeviceToHost, s));
         c->local_n_rec = c->local_updates = c->local_ended = 0;
+        // room for the batch's flows in the session dictionary (need: the
+        // batch's flow count, one owner): compact it first when short
+        if (lv->persist_nf + need_nf > lv->persist->fmax) {
+            if ((rc = live_compact(lv))) return rc;
+            if (lv->persist_nf + need_nf > lv->persist->fmax) return FLUERE_E_TABLE_FULL;  // too many open flows
+        }
         if ((rc = live_ensure_out(lv, lv->cap + lv->persist->fmax))) return rc;
         HIPCHECK(hipMemsetAsync(lv->ctr, 0, 16, s));
         LiveArgs a = live_args(lv);
@@ -5261,10 +5341,11 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
         HIPCHECK(hipGetLastError());
         unsigned long long tend = 0;
         HIPCHECK(hipMemcpyAsync(&tend, lv->ctr + 1, 8, hipMemcpyDeviceToHost, s));
-        uint32_t perr = 0;
-        HIPCHECK(hipMemcpyAsync(&perr, lv->persist->d_nflows + 1, 4, hipMemcpyDeviceToHost, s));
+        uint32_t pnf[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(pnf, lv->persist->d_nflows, 8, hipMemcpyDeviceToHost, s));
         if ((rc = live_take(lv, lv->pending))) return rc;
-        if (perr) return FLUERE_E_TABLE_FULL;  // more distinct flows in the session than max_flows
+        if (pnf[1]) return FLUERE_E_TABLE_FULL;  // (cannot happen: room was made above)
+        lv->persist_nf = pnf[0];
         if (tend) {
             k_live_time<<<1, 64, 0, s>>>(c->d_batches, (int)c->batches.size(), tend - 1, c->use_mac, lv->ctr + 1);
             HIPCHECK(hipMemcpyAsync(&lv->last_time, lv->ctr + 1, 8, hipMemcpyDeviceToHost, s));
@@ -5272,7 +5353,11 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
             lv->last_have = true;
         }
     }
-    if (!do_export || !lv->last_have) return FLUERE_OK;  // the interval check runs after a processed packet
+    // the interval check runs after a processed packet: an interval that
+    // elapsed in a batch without one exports at the next batch with one
+    if (do_export) lv->export_due = true;
+    if (!lv->export_due || !lv->last_have) return FLUERE_OK;
+    lv->export_due = false;
     std::vector<fluere_record> scan;
     if (lv->timeout_ms > 0) {
         LiveArgs a = live_args(lv);

@@ -241,23 +241,32 @@ def _arr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def _sweep_compose(comm, ctxs, rank_first):
-    """The hard-timeout sweep across shards (include/fluere_gpu.h,
-    fluere_sweep_*): every local context is a holder (its packet range) and an
-    owner (its flows).  rank_first: first global packet index of every rank,
-    plus the total (world + 1 entries)."""
+def _sweep_pack(comm, ctxs):
+    """Step 1 of the sweep composition, run after the export and before the
+    owner merge (which replaces the context's flow table with its owner's):
+    every shard's valid packets as 32-byte records per owner rank."""
     L = _lib.lib()
     W = comm.world
-    u64 = np.uint64
-    # 1-2. packets to their keys' owners
     counts, sends = [], []
     for c in ctxs:
-        cnt = np.zeros(W, u64)
+        cnt = np.zeros(W, np.uint64)
         check(L.fluere_sweep_pack(c._h, W, _arr(cnt), None), "fluere_sweep_pack")
         b = _buf(int(cnt.sum()) * 32)
         check(L.fluere_sweep_pack(c._h, W, _arr(cnt), b.data_ptr()), "fluere_sweep_pack")
         counts.append(cnt)
         sends.append(b)
+    return counts, sends
+
+
+def _sweep_compose(comm, ctxs, rank_first, counts, sends):
+    """The hard-timeout sweep across shards (include/fluere_gpu.h,
+    fluere_sweep_*): every local context is a holder (its packet range) and an
+    owner (its flows).  rank_first: first global packet index of every rank,
+    plus the total (world + 1 entries); counts / sends: _sweep_pack's."""
+    L = _lib.lib()
+    W = comm.world
+    u64 = np.uint64
+    # 1-2. packets to their keys' owners
     recvs, rcounts = comm.all_to_all_v(sends, counts, 32)
     for c, r, rc in zip(ctxs, recvs, rcounts):
         rc = np.ascontiguousarray(rc, dtype=u64)
@@ -389,6 +398,7 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
         S.cap = _pow2_at_least(n0, S.cap)
         S.cap_annex = _pow2_at_least(n1, S.cap_annex)
     S.bytes_sent = (W - 1) * blk
+    packed = _sweep_pack(comm, ctxs) if expiry else None
     comm.all_to_all_equal(S.sends, S.recvs)
     stats, rcs = [], []
     for c, r in zip(ctxs, S.recvs):
@@ -403,7 +413,7 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
     if any(rc == _lib.NEED_SWEEP for rc in rcs):
         if not expiry or not all(rc == _lib.NEED_SWEEP for rc in rcs):
             raise _lib.FluereError(_lib.E_STATE, "sharded merge: ranks disagree on the capture span")
-        stats = _sweep_compose(comm, ctxs, rank_first_fn())
+        stats = _sweep_compose(comm, ctxs, rank_first_fn(), *packed)
         for d in stats:
             d["rc"] = _lib.NEED_SWEEP
     return stats

@@ -948,6 +948,7 @@ int or_live_buffer(const uint8_t* file, uint64_t nbytes, const uint64_t* batch_e
     fm_init(&A, 1024);
     uint64_t create_seq = 0, exported = 0;
     int64_t i = 0;
+    int export_due = 0;  /* the interval elapsed: the export runs after the next processed packet */
     for (uint64_t b = 0; b < n_batches; b++) {
         int have = 0;      /* a processed packet in this batch (the checks run after one) */
         uint64_t time = 0; /* its timestamp: the `time` of the checks (:306-373) */
@@ -1000,8 +1001,10 @@ int or_live_buffer(const uint8_t* file, uint64_t nbytes, const uint64_t* batch_e
             have = 1;
             time = t;
         }
+        if (batch_export[b]) export_due = 1;
         if (!have) continue;
-        if (batch_export[b]) {                                                   /* :306-358 interval export */
+        if (export_due) {                                                        /* :306-358 interval export */
+            export_due = 0;
             if (timeout_ms > 0) live_scan(&A, time, timeout_ms, 1, out);
             for (uint64_t k = 0; k < out->n; k++) if (out->interval[k] == UINT32_MAX) out->interval[k] = (uint32_t)exported;
             exported++;

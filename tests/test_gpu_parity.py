@@ -767,6 +767,55 @@ def test_live_matches_oracle(gpu, name, tmp_path):
     assert len(plug.seen) == sum(len(r) for _, r, _ in got)
 
 
+def test_live_session_reclaims_closed_flows(gpu, tmp_path):
+    """A session whose capture holds many more distinct flow keys than
+    max_flows (reopened TCP connections, idle-expired UDP): closed and expired
+    flows leave the session (live_fluereflow.rs:299,336,371), so the
+    dictionary is compacted instead of filling up; every export equals the
+    oracle's."""
+    from fluere_amd import live
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 600_000, 1_000, 0xF10E0097))
+    batches = list(live.replay_batches(data, 20, 20_000))
+    ends, k = [], 0
+    for img, _ in batches:
+        k += sum(1 for _ in live.pcap_records(img))
+        ends.append(k)
+    want = pyoracle.live(data, ends, [e for _, e in batches], 10, False, True)
+    n_keys = sum(w["csv"].count("\n") - 1 for w in want)
+    assert n_keys > 3 * 4096  # records (one per flow instance) far beyond the dictionary
+    args = fluere_amd.Args(fluere_amd.Files(csv="live"), fluere_amd.Parameters(use_mac=False, timeout=10))
+    got = live.packet_capture(args, batches, out_dir=str(tmp_path), duration_end=True, max_flows=4096)
+    assert len(got) == len(want)
+    for i, ((path, recs, n_ord), w) in enumerate(zip(got, want)):
+        assert_csv_equal(open(path).read(), n_ord, w["csv"], w["n_ordered"], f"reclaim export {i}")
+
+
+def test_live_export_waits_for_a_processed_packet(gpu, tmp_path):
+    """An interval that elapses in a batch without a processed packet (here:
+    TCP packets without SYN of unknown flows) exports after the next processed
+    packet, not with the interval after it (live_fluereflow.rs:306)."""
+    import pktbuild as pb
+    from fluere_amd import live
+    recs = []
+    for i in range(6):  # batch 1: UDP flows (processed)
+        recs.append((1_700_000_000, i, pb.eth() + pb.ipv4("10.0.0.1", f"10.0.1.{i}", 17, pb.udp(1000 + i, 2000))))
+    for i in range(6):  # batch 2: TCP ACKs of unknown flows (all SYN-gated: nothing processed)
+        recs.append((1_700_000_000, 100 + i,
+                     pb.eth() + pb.ipv4("10.0.2.1", f"10.0.3.{i}", 6, pb.tcp(3000 + i, 80, pb.ACK, b"x" * 8))))
+    for i in range(6):  # batch 3: more UDP
+        recs.append((1_700_000_000, 5000 + i, pb.eth() + pb.ipv4("10.0.4.1", f"10.0.5.{i}", 17, pb.udp(4000 + i, 2000))))
+    data = pb.pcap(recs)
+    imgs = [pb.pcap(recs[0:6]), pb.pcap(recs[6:12]), pb.pcap(recs[12:18])]
+    batches = [(imgs[0], False), (imgs[1], True), (imgs[2], False)]
+    want = pyoracle.live(data, [6, 12, 18], [False, True, False], 1, False, False)
+    args = fluere_amd.Args(fluere_amd.Files(csv="live"), fluere_amd.Parameters(use_mac=False, timeout=1))
+    got = live.packet_capture(args, batches, out_dir=str(tmp_path))
+    assert len(got) == len(want) == 2
+    assert want[0]["csv"].count("\n") == 7  # batch 1's six flows, idle-expired at the pending export
+    for i, ((path, r, n_ord), w) in enumerate(zip(got, want)):
+        assert_csv_equal(open(path).read(), n_ord, w["csv"], w["n_ordered"], f"pending export {i}")
+
+
 def test_fluere_live_cli(gpu, tmp_path):
     """`fluere live --replay` (the C++ CLI over the C ABI): its CSV files equal
     the oracle's exports for the same interval batches."""
