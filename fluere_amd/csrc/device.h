@@ -276,6 +276,21 @@ __device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, 
     return dense_of_key(T, k, insert, chain_out, generic_used);
 }
 
+// Bucket of a canonical key in the exact engine's complex-flow filter (a
+// bitmap of CBITS bits, set for every flow the certificate rejects): a packet
+// whose key's bit is clear belongs to no complex flow, so the replay skips its
+// dictionary walk.
+constexpr uint32_t CBITS_LOG2 = 24;
+__device__ __forceinline__ uint32_t ckey_bucket(const uint32_t* w) {
+    uint32_t h = 0x2545F491u;
+#pragma unroll
+    for (int j = 0; j < 14; j++) {
+        h = (h ^ w[j]) * 0x9E3779B1u;
+        h ^= h >> 15;
+    }
+    return h >> (32 - CBITS_LOG2);
+}
+
 // Append one record (Mode A paths): position, updates and ended counters.
 __device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {
     const unsigned long long pos = atomicAdd(&g->n_rec, 1ull);

@@ -83,6 +83,8 @@ struct ExactJob {
     // instead of a parse of the batches.
     const ExMeta* ext_cm = nullptr;
     uint64_t ext_n = 0;
+    // Mode A: the complex-flow filter (device.h ckey_bucket), or null
+    const uint32_t* cbits = nullptr;
 };
 
 struct ExactResult {

@@ -106,7 +106,7 @@ struct ToAgg {
 
 // ---- 1. per-packet metadata of the packets to replay (one parse pass) -----
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
-                                                 ExMeta* meta, uint32_t* flag, uint64_t off) {
+                                                 const uint32_t* cbits, ExMeta* meta, uint32_t* flag, uint64_t off) {
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= B.n) return;
     Parsed P;
@@ -116,7 +116,14 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
     memset(&m, 0, sizeof m);
     if (P.cls == 0) {
         uint8_t dir;
-        const uint32_t d = flow_of(T, P, macs != 0, false, dir, nullptr, nullptr);
+        CKey k;
+        canon_key(P, macs != 0, k, dir);
+        bool maybe = true;
+        if (!all && cbits) {  // no complex flow has this key's bucket: no dictionary walk
+            const uint32_t b = ckey_bucket(k.w);
+            maybe = (cbits[b >> 5] >> (b & 31)) & 1u;
+        }
+        const uint32_t d = maybe ? dense_of_key(T, k, false, nullptr, nullptr) : FAIL;
         if (d != FAIL && d < T.fmax && (all || cplx[d])) {
             take = 1;
             m.t = P.t;
@@ -732,7 +739,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, meta, flag, off);
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, flag, off);
             off += B.n;
         }
     }
@@ -1001,7 +1008,7 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, meta, flag, off);
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, flag, off);
             off += B.n;
         }
         uint32_t last[2] = {0, 0};

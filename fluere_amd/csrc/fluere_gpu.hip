@@ -1206,6 +1206,7 @@ struct FinArgs {
     Ctl* host_ctl;   // non-null: the last workgroup writes the run counters to this pinned host copy,
     uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
     unsigned long long timeout_us;  // non-zero: skip the flows when expiries can fire (Mode B redoes every flow)
+    uint32_t* cbits = nullptr;      // the exact engine's complex-flow filter (ckey_bucket), or null
 };
 
 // A flow's order-free aggregate (the accumulators of one dense id).
@@ -1238,6 +1239,10 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
     bool certified = fc == fa && (fr == NONE64 || fr == la);
     if (!certified) {
         a.complex[d] = 1;
+        if (a.cbits) {
+            const uint32_t b = ckey_bucket(reinterpret_cast<const uint32_t*>(a.T.flow_key + (size_t)d * 56));
+            atomicOr(&a.cbits[b >> 5], 1u << (b & 31));
+        }
         cplx = true;
         cplx_pkts = v.pk[0] + v.pk[1];
         return false;
@@ -2745,6 +2750,7 @@ struct fluere_ctx {
     bool batches_dirty = true;
     uint8_t* d_flow_key = nullptr;
     uint8_t* d_complex = nullptr;
+    uint32_t* d_cbits = nullptr;   // complex-flow filter of the exact engine (1 << CBITS_LOG2 bits)
     uint8_t* d_active = nullptr;
     Batch* d_batches = nullptr;
     int d_batches_cap = 0;
@@ -2912,6 +2918,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     memset(c->h_ctl, 0, sizeof(Ctl));
     if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_cbits, (1u << CBITS_LOG2) / 8) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
         hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess ||
@@ -2929,6 +2936,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     k_fill_u32<<<grid_for(8 * F, 256), 256, 0, s>>>(c->acc.fl[0], 8 * F, 0);
     k_fill_u32<<<grid_for(F * N_TABLES, 256), 256, 0, s>>>(c->acc.slots, F * N_TABLES, NONE32);
     if (hipMemsetAsync(c->d_complex, 0, F, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    if (hipMemsetAsync(c->d_cbits, 0, (1u << CBITS_LOG2) / 8, s) != hipSuccess) return fail(FLUERE_E_HIP);
     {
         Ctl z{};
         z.g.tmin = NONE64;
@@ -2961,6 +2969,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_glob);
     hipFree(c->d_flow_key);
     hipFree(c->d_complex);
+    hipFree(c->d_cbits);
     hipFree(c->d_active);
     hipFree(c->d_batches);
     hipFree(c->d_recs);
@@ -3648,6 +3657,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
         P.fa = FinArgs{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob,
                        c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
         P.fa.timeout_us = c->timeout_ms * 1000ull;
+        P.fa.cbits = c->d_cbits;
         P.spec_ca = P.ca;
         P.spec_ca.spec = 1;
         P.spec_ca.timeout_us = c->timeout_ms * 1000ull;
@@ -4031,6 +4041,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
             ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 0, timeout_us, c->d_complex, c->d_glob,
                        &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+            J.cbits = c->d_cbits;
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
             HIPCHECK(hipEventRecord(c->ev2, s));
@@ -4108,6 +4119,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         out.sequential_mode = 2;
         }
     }
+    // the complex-flow filter is per run: clear the bits the speculative finalize set
+    if (g.n_complex) HIPCHECK(hipMemsetAsync(c->d_cbits, 0, (1u << CBITS_LOG2) / 8, s));
     c->n_ended = n_ended;
     c->have_results = true;
     float ms_parse = 0;
