@@ -11,7 +11,7 @@ xGMI, and each owner merges / finalizes its own flows (fluere_amd/dist.py).
 Weak scaling: every rank owns a fixed per-GPU shard of one global capture
 (packet-range sharding with global packet indices).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5u|tcp|tcp_t1|slow]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5u|tcp|tcp_t1|tcp_t1_backtime|slow]
   torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
 """
 from __future__ import annotations
@@ -54,6 +54,12 @@ CONFIGS = {
                           "10k flows"),
     "tcp_t1": dict(kind=4, per_gpu=10_000_000, flows=100_000, seed=0xF10E0007, use_mac=False, timeout_ms=1000,
                    workload="10M IMIX, realistic TCP (+UDP), 100k concurrent lanes, -t 1000 (expiry sweep)"),
+    # the same with 1 % of the timestamps up to 5 ms early (merged / multi-queue
+    # captures): the sweep points from the max segment tree
+    "tcp_t1_backtime": dict(kind=6, per_gpu=10_000_000, flows=100_000, seed=0xF10E0047, use_mac=False,
+                            timeout_ms=1000,
+                            workload="10M IMIX, realistic TCP (+UDP), 100k lanes, 1% timestamps up to 5 ms early, "
+                                     "-t 1000 (expiry sweep, out-of-order times)"),
 }
 BYTES_PER_PKT = 80  # algorithmic: 16 B pcap record header + min(caplen, 64) B header window
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -104,7 +110,7 @@ def main():
         ts = torch.cuda.Stream()
         torch.cuda.set_stream(ts)
         stream = ts.cuda_stream
-    max_flows = max(1 << 16, 2 * C["flows"]) if C["kind"] != 4 else n // 2
+    max_flows = max(1 << 16, 2 * C["flows"]) if C["kind"] not in (4, 6) else n // 2
     ctx = fluere_amd.FlowContext(timeout_ms=C.get("timeout_ms", 600000), use_mac=C["use_mac"], max_flows=max_flows,
                                  device=local, stream=stream)
     exchange = fdist.ShardExchange(ctx) if world > 1 else None
@@ -203,6 +209,7 @@ def main():
             # N > 1: bytes each rank sends to the others in the merge's all-to-all
             "exchange_bytes_per_rank": int(exchange.bytes_sent) if world > 1 else None,
             "sequential_mode": int(st.get("sequential_mode", 0)) if world == 1 else None,
+            "exact_passes": int(st.get("passes", 0)) if world == 1 else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, C)

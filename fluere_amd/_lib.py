@@ -51,11 +51,11 @@ class Stats(ctypes.Structure):
     _fields_ = [("packets", ctypes.c_uint64), ("valid", ctypes.c_uint64), ("updates", ctypes.c_uint64),
                 ("dropped_parse", ctypes.c_uint64), ("unsupported", ctypes.c_uint64), ("flows", ctypes.c_uint64),
                 ("complex_flows", ctypes.c_uint64), ("records", ctypes.c_uint64), ("ended", ctypes.c_uint64),
-                ("sequential_mode", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("parse_ms", ctypes.c_double),
+                ("sequential_mode", ctypes.c_uint32), ("passes", ctypes.c_uint32), ("parse_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class SynthCfg(ctypes.Structure):

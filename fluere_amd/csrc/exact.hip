@@ -86,23 +86,6 @@ struct AggOp {
         return r;
     }
 };
-struct ToAgg {
-    const ExMeta* sm;
-    __host__ __device__ Agg operator()(uint32_t p) const {
-        const ExMeta m = sm[p];
-        Agg a;
-        a.pk[0] = m.dir ? 0 : 1;
-        a.pk[1] = m.dir ? 1 : 0;
-        a.by[0] = m.dir ? 0 : m.doct;
-        a.by[1] = m.dir ? m.doct : 0;
-        a.mnp = a.mxp = m.pkt;
-        a.mnt = a.mxt = m.ttl;
-        for (int q = 0; q < 8; q++) a.fl[q] = (m.tflags >> q) & 1;
-        a.lastg = m.gidx;
-        a.lastt = m.t;
-        return a;
-    }
-};
 
 // ---- 1. per-packet metadata of the packets to replay (one parse pass) -----
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
@@ -185,7 +168,23 @@ __global__ void __launch_bounds__(256) k_ex_heads(uint64_t n, const uint32_t* hf
 // ---- 3. Mode B: timestamps non-decreasing over the valid packets? ---------
 __global__ void __launch_bounds__(256) k_ex_mono(uint64_t n, const ExMeta* cm, uint32_t* bad) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > 0 && k < n && cm[k].t < cm[k - 1].t) atomicOr(bad, 1u);
+    const bool back = k > 0 && k < n && cm[k].t < cm[k - 1].t;
+    if (__ballot(back) && (threadIdx.x & 63) == 0) *bad = 1u;  // (one store per wave, not an atomic per packet)
+}
+
+// lower_bound of t0 + b * bw over the non-decreasing times, b = 0..nb
+__global__ void __launch_bounds__(256) k_ex_tindex(uint64_t n, const ExMeta* cm, uint64_t t0, uint64_t bw, uint64_t nb,
+                                                   uint32_t* tbl) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nb) return;
+    const unsigned long long v = t0 + b * bw;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (cm[mid].t < v) lo = mid + 1;
+        else hi = mid;
+    }
+    tbl[b] = (uint32_t)lo;
 }
 
 // reversed "k if processed" for the next-processed min-scan
@@ -239,6 +238,8 @@ struct ChaseArgs {
     const unsigned long long* np_rev;  // next processed (reversed min-scan; non-decreasing times)
     const unsigned long long* tree;    // max segment tree (times that go backwards), or null
     uint64_t tree_P;
+    const uint32_t* tbl;               // non-decreasing times: lower_bound of t0 + b * bw for every bucket b
+    uint64_t t0, bw, nb;
     const unsigned long long* fext;    // sharded Mode B: sweep point of every packet (capture order), or null
     // out, indexed by the instance's first position
     uint32_t* sflag;
@@ -273,8 +274,16 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
         const uint64_t k = tree_first(a.tree, a.tree_P, k0, exp + 1);
         return k >= a.n ? NONE64 : a.cm[k].gidx;
     }
-    // non-decreasing times: lower_bound, then the next processed packet
+    // non-decreasing times: lower_bound (within the exp's time bucket), then
+    // the next processed packet
     uint64_t lo = 0, hi = a.n;
+    if (exp <= a.t0) {
+        hi = 0;
+    } else {
+        const uint64_t b = (exp - a.t0) / a.bw;
+        if (b >= a.nb) lo = a.n;
+        else { lo = a.tbl[b]; hi = a.tbl[b + 1]; }
+    }
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
         if (a.cm[mid].t < exp) lo = mid + 1;
@@ -409,23 +418,153 @@ __global__ void __launch_bounds__(256) k_ex_starts(uint64_t n, const uint32_t* s
     if (p < n && sflag[p]) ist[incl[p] - 1] = (uint32_t)p;
 }
 
-// rk[p] = instance of p (member), or a key no member has; Mode B: the
-// processed flag of each replayed packet (members are processed)
+// Mode B: the processed flag of each replayed packet (the members of an
+// instance are processed); *changed when the set moved (one store per wave:
+// an atomic per changed packet serialised on the one word)
 __global__ void __launch_bounds__(256) k_ex_members(uint64_t n, const uint32_t* incl, const uint32_t* ist,
-                                                    const uint32_t* iend, uint32_t* rk, const uint32_t* sval,
-                                                    uint8_t* pr, uint32_t* changed) {
+                                                    const uint32_t* iend, const uint32_t* sval, uint8_t* pr,
+                                                    uint32_t* changed) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const uint32_t q1 = incl[p];  // instances starting at or before p
-    const bool member = q1 > 0 && p <= iend[ist[q1 - 1]];
-    rk[p] = member ? q1 - 1 : (0x80000000u | q1);
-    if (pr) {
+    bool ch = false;
+    if (p < n) {
+        const uint32_t q1 = incl[p];  // instances starting at or before p
+        const bool member = q1 > 0 && p <= iend[ist[q1 - 1]];
         const uint8_t v = member ? 1 : 0;
         const uint32_t k = sval[p];
         if (pr[k] != v) {
             pr[k] = v;
-            atomicOr(changed, 1u);
+            ch = true;
         }
+    }
+    if (__ballot(ch) && (threadIdx.x & 63) == 0) *changed = 1u;
+}
+
+// ---- per-instance aggregates: update_flow's order-free fields over each
+// instance's packets, the contiguous sorted run [ist[q], iend[ist[q]]] ----------
+__device__ __forceinline__ void agg_clear(Agg& a) {
+    a.pk[0] = a.pk[1] = 0;
+    a.by[0] = a.by[1] = 0;
+    a.mnp = a.mnt = NONE32;
+    a.mxp = a.mxt = 0;
+    for (int q = 0; q < 8; q++) a.fl[q] = 0;
+    a.lastg = 0;
+    a.lastt = 0;
+}
+__device__ __forceinline__ void agg_add(Agg& a, const ExMeta& m) {
+    const bool r = m.dir != 0;  // (selects: a dynamic index would put the arrays in scratch)
+    a.pk[0] += r ? 0u : 1u;
+    a.pk[1] += r ? 1u : 0u;
+    a.by[0] += r ? 0ull : (unsigned long long)m.doct;
+    a.by[1] += r ? (unsigned long long)m.doct : 0ull;
+    a.mnp = min(a.mnp, m.pkt);
+    a.mxp = max(a.mxp, m.pkt);
+    a.mnt = min(a.mnt, (uint32_t)m.ttl);
+    a.mxt = max(a.mxt, (uint32_t)m.ttl);
+    for (int q = 0; q < 8; q++) a.fl[q] += (m.tflags >> q) & 1;
+    if (m.gidx >= a.lastg) {  // (the run is in index order: the last packet wins)
+        a.lastg = m.gidx;
+        a.lastt = m.t;
+    }
+}
+__device__ __forceinline__ Agg agg_shfl_xor(const Agg& a, int o) {
+    Agg b;
+    b.pk[0] = __shfl_xor(a.pk[0], o, 64);
+    b.pk[1] = __shfl_xor(a.pk[1], o, 64);
+    b.by[0] = __shfl_xor(a.by[0], o, 64);
+    b.by[1] = __shfl_xor(a.by[1], o, 64);
+    b.mnp = __shfl_xor(a.mnp, o, 64);
+    b.mxp = __shfl_xor(a.mxp, o, 64);
+    b.mnt = __shfl_xor(a.mnt, o, 64);
+    b.mxt = __shfl_xor(a.mxt, o, 64);
+    for (int q = 0; q < 8; q++) b.fl[q] = __shfl_xor(a.fl[q], o, 64);
+    b.lastg = __shfl_xor(a.lastg, o, 64);
+    b.lastt = __shfl_xor(a.lastt, o, 64);
+    return b;
+}
+__device__ __forceinline__ Agg agg_wave(Agg a) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) a = AggOp()(a, agg_shfl_xor(a, o));
+    return a;
+}
+
+constexpr uint32_t AGG_THREAD = 48;    // runs up to this long: one thread
+constexpr uint32_t AGG_WAVE = 16384;   // up to this: one wave; longer: one 1024-thread block
+
+// thread per instance; longer runs are listed for the wave / block kernels
+__global__ void __launch_bounds__(256) k_ex_agg(uint32_t n_inst, const uint32_t* ist, const uint32_t* iend,
+                                                const ExMeta* sm, Agg* aggs, uint32_t* lists, uint32_t* cnt) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    bool wide = false, huge = false;
+    if (q < n_inst) {
+        const uint32_t c = ist[q], e = iend[c];
+        const uint32_t len = e - c + 1;
+        if (len <= AGG_THREAD) {
+            Agg a;
+            agg_clear(a);
+            for (uint32_t p = c; p <= e; p++) agg_add(a, sm[p]);
+            aggs[q] = a;
+        } else {
+            wide = len <= AGG_WAVE;
+            huge = !wide;
+        }
+    }
+    // wave-aggregated appends: lists[0..] wide runs, lists[n_inst - 1 ..] (downwards) huge runs
+    const uint64_t mw = __ballot(wide), mh = __ballot(huge);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rw = __builtin_amdgcn_mbcnt_hi((uint32_t)(mw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mw, 0u));
+    const uint32_t rh = __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, 0u));
+    uint32_t bw = 0, bh = 0;
+    if (lane == 0) {
+        if (mw) bw = atomicAdd(&cnt[0], (uint32_t)__popcll(mw));
+        if (mh) bh = atomicAdd(&cnt[1], (uint32_t)__popcll(mh));
+    }
+    bw = __shfl(bw, 0, 64);
+    bh = __shfl(bh, 0, 64);
+    if (wide) lists[bw + rw] = q;
+    if (huge) lists[n_inst - 1 - (bh + rh)] = q;
+}
+
+// one wave per listed run (grid-stride over the device-side count)
+__global__ void __launch_bounds__(256) k_ex_agg_wave(uint32_t n_inst, const uint32_t* ist, const uint32_t* iend,
+                                                     const ExMeta* sm, Agg* aggs, const uint32_t* lists,
+                                                     const uint32_t* cnt) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nwide = cnt[0];
+    for (uint32_t i = w0; i < nwide; i += nw) {
+        const uint32_t q = lists[i];
+        const uint32_t c = ist[q], e = iend[c];
+        Agg a;
+        agg_clear(a);
+        for (uint32_t p = c + lane; p <= e; p += 64) agg_add(a, sm[p]);
+        a = agg_wave(a);
+        if (lane == 0) aggs[q] = a;
+    }
+}
+
+// one block per listed huge run (an elephant instance)
+__global__ void __launch_bounds__(1024) k_ex_agg_block(uint32_t n_inst, const uint32_t* ist, const uint32_t* iend,
+                                                       const ExMeta* sm, Agg* aggs, const uint32_t* lists,
+                                                       const uint32_t* cnt) {
+    __shared__ Agg part[16];
+    const uint32_t nhuge = cnt[1];
+    for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {
+        const uint32_t q = lists[n_inst - 1 - i];
+        const uint32_t c = ist[q], e = iend[c];
+        Agg a;
+        agg_clear(a);
+        for (uint32_t p = c + threadIdx.x; p <= e; p += 1024) agg_add(a, sm[p]);
+        a = agg_wave(a);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            Agg b;
+            if (threadIdx.x < 16) b = part[threadIdx.x];
+            else agg_clear(b);
+            b = agg_wave(b);
+            if (threadIdx.x == 0) aggs[q] = b;
+        }
+        __syncthreads();
     }
 }
 
@@ -434,9 +573,8 @@ struct RecArgs {
     const Batch* bs;
     int nb;
     int macs, mode_b;
-    const uint32_t* ukeys;
-    const Agg* aggs;
-    const uint32_t* nruns;
+    uint32_t n_inst;
+    const Agg* aggs;            // by instance
     const uint32_t* ist;
     const ExMeta* sm;
     const uint32_t* iend;
@@ -470,23 +608,21 @@ __device__ __forceinline__ void piece_of(const Agg& g, fluere_flow_piece& pc) {
 
 __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
     __shared__ EmitLds S;
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nr = *a.nruns;
-    const bool lane_live = r < nr && !(a.ukeys[r] & 0x80000000u);
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;  // instance (a run of the flow's packets)
+    const bool lane_live = q < a.n_inst;
     fluere_record rec;
     memset(&rec, 0, sizeof rec);
-    uint32_t q = 0;
     uint8_t kind = K_ACTIVE;
     unsigned long long cj = NONE64, cie = 0, cex = 0;
-    if (lane_live && a.shard_mode && a.irole[a.ist[a.ukeys[r]]] != R_RECORD) {
+    if (lane_live && a.shard_mode && a.irole[a.ist[q]] != R_RECORD) {
         // a piece of the flow's annex (lead / head / tail), not a record
-        const uint32_t c = a.ist[a.ukeys[r]];
+        const uint32_t c = a.ist[q];
         const ExMeta mc = a.sm[c];
         const uint8_t role = a.irole[c];
         fluere_flow_annex& ax = a.annex[a.ikey[c]];
         fluere_flow_piece pc;
         memset(&pc, 0, sizeof pc);
-        piece_of(a.aggs[r], pc);
+        piece_of(a.aggs[q], pc);
         pc.first = mc.gidx;
         pc.first_time = mc.t;
         if (role != R_LEAD) {
@@ -502,12 +638,11 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
         if (role == R_HEAD || role == R_HEAD_TAIL) ax.head = pc;
         if (role == R_TAIL) ax.tail = pc;
     }
-    const bool rec_live = lane_live && !(a.shard_mode && a.irole[a.ist[a.ukeys[r]]] != R_RECORD);
+    const bool rec_live = lane_live && !(a.shard_mode && a.irole[a.ist[q]] != R_RECORD);
     if (rec_live && a.shard_mode)  // the flow's last processed packet among its in-shard records (live mode)
-        atomicMax(reinterpret_cast<unsigned long long*>(&a.annex[a.ikey[a.ist[a.ukeys[r]]]].mid_last),
-                  (unsigned long long)a.aggs[r].lastg + 1);
+        atomicMax(reinterpret_cast<unsigned long long*>(&a.annex[a.ikey[a.ist[q]]].mid_last),
+                  (unsigned long long)a.aggs[q].lastg + 1);
     if (rec_live) {
-        q = a.ukeys[r];
         const uint32_t c = a.ist[q];
         const ExMeta mc = a.sm[c];
         if (a.seeds) {  // sharded Mode B: the creating packet is on another shard
@@ -521,7 +656,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
             parse_global(a.bs, a.nb, mc.gidx, a.macs != 0, P);
             fill_seed(rec, P);
         }
-        const Agg g = a.aggs[r];
+        const Agg g = a.aggs[q];
         const uint32_t o = mc.dir;  // orientation of the creating packet
         rec.d_pkts = g.pk[0] + g.pk[1];
         rec.d_octets = g.by[0] + g.by[1];
@@ -649,7 +784,7 @@ struct ExactSession {
     unsigned long long *hi, *lo, *ex, *hi2, *gk, *tree;
     unsigned long long nrec_new = 0;
     uint64_t tree_P = 0;
-    uint32_t *val, *sval, *hf, *hpos, *heads, *link, *plink, *sflag, *iend, *incl, *ist, *rk, *ukeys, *ctr;
+    uint32_t *val, *sval, *hf, *hpos, *heads, *link, *plink, *sflag, *iend, *incl, *ist, *alist, *ctr, *tbl;
     uint32_t *idx, *idx2, *perm, *ikey;
     uint8_t *pr, *ikind, *irole;
     Agg* aggs;
@@ -687,13 +822,14 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         add(n * 4);                                                   // plink
         add(n * 4); add(n * 4); add(n); add(n * 8); add(n * 8);       // sflag, iend, ikind, ij, iie
         add(n * 8);                                                   // iex
-        add(n * 4); add(n * 4); add(n * 4); add(n * 4);               // incl, ist, rk, ukeys
+        add(n * 4); add(n * 4); add(n * 4);                           // incl, ist, alist
         add(n * sizeof(Agg)); add(16);                                // aggs, nruns/counters
         add(n * sizeof(fluere_record)); add(n * 8); add(n * 8);       // tmp, hi, lo
         add(n * 8); add(n * 8);                                       // ex, gk
         add(n * 4); add(n * 4); add(n * 8); add(n * 4);               // idx, idx2, hi2, perm
         add(n); add(n * 4);                                           // irole, ikey
         if (J.mode_b) add(2 * P * 8);                                 // tree
+        add((n / 16 + 4) * 4);                                        // tbl
         add(tmp);
         return b;
     };
@@ -711,11 +847,6 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         tmp = std::max(tmp, t);
         (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                           hipcub::Min(), n, s);
-        tmp = std::max(tmp, t);
-        hipcub::CountingInputIterator<uint32_t> cnt(0);
-        hipcub::TransformInputIterator<Agg, ToAgg, hipcub::CountingInputIterator<uint32_t>> vit(cnt, ToAgg{nullptr});
-        (void)hipcub::DeviceReduce::ReduceByKey(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, vit, (Agg*)nullptr,
-                                          (uint32_t*)nullptr, AggOp(), n, s);
         tmp = std::max(tmp, t);
     }
     S->tmp = tmp;
@@ -771,10 +902,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     S->iex = A.take<unsigned long long>(N);
     S->incl = A.take<uint32_t>(N);
     S->ist = A.take<uint32_t>(N);
-    S->rk = A.take<uint32_t>(N);
-    S->ukeys = A.take<uint32_t>(N);
+    S->alist = A.take<uint32_t>(N);
     S->aggs = A.take<Agg>(N);
-    uint32_t* ctr = S->ctr = A.take<uint32_t>(4);  // [0] nruns, [1] non-monotonic, [2] changed
+    uint32_t* ctr = S->ctr = A.take<uint32_t>(4);  // [0..1] aggregate lists, [1] non-monotonic (begin), [2] changed
     S->tmpr = A.take<fluere_record>(N);
     S->hi = A.take<unsigned long long>(N);
     S->lo = A.take<unsigned long long>(N);
@@ -787,6 +917,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     S->irole = A.take<uint8_t>(N);
     S->ikey = A.take<uint32_t>(N);
     S->tree = J.mode_b ? A.take<unsigned long long>(2 * P) : nullptr;
+    S->tbl = A.take<uint32_t>(N / 16 + 4);
     S->tree_P = P;
     void* tp = S->tp = A.take<char>(tmp);
     uint64_t n;
@@ -848,8 +979,22 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         S->annex = *J.annex;
         S->R.annexes = S->n_keys;
     }
+    // the time-bucket index of the non-decreasing times (about 16 packets a
+    // bucket): a sweep point's lower_bound searches one bucket, not the capture
+    uint64_t t0 = 0, bw = 1, nb = 0;
+    if (J.mode_b && S->mono) {
+        unsigned long long tt[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&tt[0], &cm[0].t, 8, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipMemcpyAsync(&tt[1], &cm[n - 1].t, 8, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        t0 = tt[0];
+        nb = n / 16 + 1;
+        bw = std::max<uint64_t>(1, (tt[1] - tt[0]) / nb + 1);  // nb * bw > the span
+        k_ex_tindex<<<gridn(nb + 1, 256), 256, 0, s>>>(n, cm, t0, bw, nb, S->tbl);
+        HIPCHECK(hipGetLastError());
+    }
     S->ca = ChaseArgs{n, S->n_keys, heads, sm, sval, ne_rev, nf_rev, J.mode_b, J.timeout_us, cm, S->np_rev,
-                      (J.mode_b && !S->mono) ? S->tree : nullptr, P, nullptr,
+                      (J.mode_b && !S->mono) ? S->tree : nullptr, P, S->tbl, t0, bw, nb, nullptr,
                       S->sflag, S->iend, S->ikind, S->ij, S->iie, S->iex, S->ej, S->link, S->plink,
                       J.shard_mode, S->irole, S->ikey, S->annex, J.annex_of, J.T.flow_key};
     return FLUERE_OK;
@@ -883,8 +1028,8 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     HIPCHECK(hipcub::DeviceScan::InclusiveSum(S->tp, tb, S->sflag, S->incl, in, s));
     k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->incl, S->ist);
     HIPCHECK(hipMemsetAsync(S->ctr + 2, 0, 4, s));
-    k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->rk, S->sval,
-                                                J.mode_b ? S->pr : nullptr, S->ctr + 2);
+    if (J.mode_b)  // the processed set (Mode A needs none: every run is a record or a piece)
+        k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->sval, S->pr, S->ctr + 2);
     HIPCHECK(hipGetLastError());
     if (pr_out) HIPCHECK(hipMemcpyAsync(pr_out, S->pr, n, hipMemcpyDeviceToDevice, s));
     if (!J.mode_b) return FLUERE_OK;
@@ -920,16 +1065,18 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     hipStream_t s = S->s;
     const uint64_t n = S->n;
     if (!n) return FLUERE_OK;
-    const int in = (int)n;
     size_t tb;
     uint32_t n_inst = 0;
     HIPCHECK(hipMemcpyAsync(&n_inst, S->incl + n - 1, 4, hipMemcpyDeviceToHost, s));
-    // ---- 6. per-instance aggregates (segmented over the sorted packets)
-    hipcub::CountingInputIterator<uint32_t> cnt(0);
-    hipcub::TransformInputIterator<Agg, ToAgg, hipcub::CountingInputIterator<uint32_t>> vit(cnt, ToAgg{S->sm});
-    tb = S->tmp;
-    HIPCHECK(hipcub::DeviceReduce::ReduceByKey(S->tp, tb, S->rk, S->ukeys, vit, S->aggs, S->ctr, AggOp(), in, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    // ---- 6. per-instance aggregates over each instance's contiguous run
+    HIPCHECK(hipStreamSynchronize(s));  // (n_inst)
+    HIPCHECK(hipMemsetAsync(S->ctr, 0, 8, s));
+    if (n_inst) {
+        k_ex_agg<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
+        k_ex_agg_wave<<<1024, 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
+        k_ex_agg_block<<<256, 1024, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
+    }
+    HIPCHECK(hipGetLastError());
     S->R.instances = n_inst;
     // ---- 7. records
     Glob gh;
@@ -946,11 +1093,11 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
         *J.d_recs = nr;
         *J.d_recs_cap = want;
     }
-    RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, S->ukeys, S->aggs, S->ctr, S->ist, S->sm, S->iend, S->ikind,
+    RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, n_inst, S->aggs, S->ist, S->sm, S->iend, S->ikind,
                S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, S->tmpr, S->hi, S->lo, S->ex, S->idx,
                J.shard_mode, S->irole, S->ikey, S->annex, seeds};
     // runs <= n (every run holds a packet)
-    k_ex_records<<<gridn(n, 256), 256, 0, s>>>(ra);
+    k_ex_records<<<gridn(n_inst, 256), 256, 0, s>>>(ra);
     if (J.mode_b && n_inst) {
         // order by (closing / sweeping index, phase), then the firing entry's
         // (exp, creation): stable radix sorts from the last key to the first

@@ -4044,6 +4044,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             J.cbits = c->d_cbits;
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
+            out.passes = er.iterations;
             HIPCHECK(hipEventRecord(c->ev2, s));
             HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
             HIPCHECK(hipStreamSynchronize(s));
@@ -4067,6 +4068,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         ExactResult er{};
         rc = getenv("FLUERE_SEQ_MODE_B") ? EXACT_FALLBACK : exact_run(J, s, &er);
         if (rc < 0) return rc;
+        out.passes = er.iterations;
         if (rc == FLUERE_OK) {
             HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
             HIPCHECK(hipEventRecord(c->ev2, s));

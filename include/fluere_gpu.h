@@ -112,8 +112,9 @@ typedef struct fluere_stats {
     uint64_t complex_flows;    /* flows resolved by the exact per-flow state machine */
     uint64_t records;          /* emitted records */
     uint64_t ended;            /* records in the ended prefix */
-    uint32_t sequential_mode;  /* 0: no expiry can fire; 1: expiry sweep, parallel; 2: expiry sweep, sequential fallback */
-    uint32_t pad;
+    uint32_t sequential_mode;  /* 0: no expiry can fire; 1: expiry sweep, parallel; 2: expiry sweep, sequential
+                                  kernel (forced: FLUERE_SEQ_MODE_B) */
+    uint32_t passes;           /* passes of the exact chase (Mode B: until the processed set is stable) */
     double parse_ms;           /* device time of the fused parse+key+aggregate kernel */
     double total_ms;           /* wall time of the whole run (fluere_run: host clock, submission to results) */
 } fluere_stats;
