@@ -95,8 +95,9 @@ static int live_main(int argc, char** argv) {
         if (incl > 262144 || off + 16 + incl > data.size()) break;
         const uint64_t t = (uint64_t)rd32(&data[off], sw) * 1000000ull + (ns ? rd32(&data[off + 4], sw) / 1000 : rd32(&data[off + 4], sw));
         if (start == ~0ull) start = bstart = t;
-        if (duration && t - start >= duration * 1000) { stopped = true; break; }
-        if (interval && t - bstart >= interval * 1000 && batch.size() > 24) {
+        // signed: a timestamp that goes backwards is no elapsed interval
+        const int64_t since_start = (int64_t)(t - start), since_batch = (int64_t)(t - bstart);
+        if (interval && since_batch >= (int64_t)(interval * 1000) && batch.size() > 24) {
             fluere_record* recs = nullptr;
             uint64_t n = 0, no = 0;
             int ex = 0;
@@ -107,6 +108,8 @@ static int live_main(int argc, char** argv) {
         }
         batch.insert(batch.end(), data.begin() + off, data.begin() + off + 16 + incl);
         off += 16 + incl;
+        // the duration check runs after the packet is processed (live_fluereflow.rs:361-373)
+        if (duration && since_start >= (int64_t)(duration * 1000)) { stopped = true; break; }
     }
     if (!rc && batch.size() > 24) {
         fluere_record* recs = nullptr;

@@ -15,8 +15,11 @@
 //   * time: seconds = t / res + tsoffset, microseconds = (t % res) * 10^6 / res;
 //   * the first truncated / malformed block, unknown interface or caplen
 //     above 262144 ends the capture (pcap_next_ex fails, fluere's loop stops);
-//   * an Enhanced Packet Block's caplen is taken as written (capture tools
-//     never write more than the interface's snaplen; unpinned otherwise).
+//   * an Enhanced / obsolete Packet Block's caplen above the capture's
+//     snapshot length (the first interface's snaplen) is cut to it, like the
+//     Simple Packet Block's (unpinned: no reference fixture);
+//   * a later Section Header Block in the other byte order ends the capture
+//     (libpcap: "sections with different byte orders").
 #include "pcapng.h"
 
 #include <cstring>
@@ -76,6 +79,7 @@ int pcapng_to_pcap(const uint8_t* f, uint64_t n, std::vector<uint8_t>& out) {
     Reader R{f};
     std::vector<Iface> ifs;
     bool section = false;
+    int first_sw = -1;  // byte order of the first section
     uint64_t pos = 0;
     while (pos + 12 <= n) {
         uint32_t type;
@@ -87,6 +91,8 @@ int pcapng_to_pcap(const uint8_t* f, uint64_t n, std::vector<uint8_t>& out) {
             else if (bom == 0x4D3C2B1Au) R.sw = true;
             else break;
             if (pos + 16 > n || R.u16(pos + 12) != 1) break;
+            if (first_sw < 0) first_sw = R.sw ? 1 : 0;
+            else if (first_sw != (R.sw ? 1 : 0)) break;
             section = true;
             ifs.clear();
         } else {
@@ -140,6 +146,7 @@ int pcapng_to_pcap(const uint8_t* f, uint64_t n, std::vector<uint8_t>& out) {
                 orig = R.u32(b + 16);
                 data = b + 20;
                 if (ifid >= ifs.size() || caplen > blen - 20) break;
+                caplen = std::min<uint32_t>(caplen, ifs[0].snap);
             }
             if (caplen > kMaxSnap) break;
             const Iface& x = ifs[ifid];

@@ -530,7 +530,10 @@ static uint32_t rd32(const uint8_t* p, int swap) {
 /* pcapng (libpcap pcap-ng.c, read by pcap_open_offline at microsecond
  * precision; third-party code, restated -- SURVEY Appendix C style):
  * blocks in file order; a Section Header Block sets the byte order and
- * forgets the interfaces; Interface Description Blocks give if_tsresol
+ * forgets the interfaces (a later section in the other byte order ends the
+ * capture: "sections with different byte orders"); an Enhanced / obsolete
+ * Packet Block's caplen above the snapshot length (interface 0's snaplen) is
+ * cut to it; Interface Description Blocks give if_tsresol
  * (option 9: 10^-b, or 2^-(b & 0x7f) when the high bit is set; default 10^-6),
  * if_tsoffset (option 14, seconds) and the snaplen (0 or above 262144 ->
  * 262144); Enhanced / obsolete Packet Blocks carry (interface, 64-bit time in
@@ -548,7 +551,7 @@ static int64_t or_pcapng_index(const uint8_t* f, uint64_t n, or_pcap_rec** out) 
     uint64_t cap = 1024, cnt = 0, pos = 0;
     or_pcap_rec* r = (or_pcap_rec*)malloc(cap * sizeof *r);
     ng_if ifs[256];
-    int nif = 0, sw = 0, have_shb = 0;
+    int nif = 0, sw = 0, have_shb = 0, first_sw = -1;
     const uint32_t max_snap = 262144;
     while (pos + 12 <= n) {
         uint32_t type = rdx32(f + pos, sw);
@@ -559,6 +562,8 @@ static int64_t or_pcapng_index(const uint8_t* f, uint64_t n, or_pcap_rec** out) 
             else if (bom == 0x4D3C2B1Au) sw = 1;
             else break;
             if (pos + 16 > n || rdx16(f + pos + 12, sw) != 1) break; /* major version 1 */
+            if (first_sw < 0) first_sw = sw;
+            else if (first_sw != sw) break;
             have_shb = 1;
             nif = 0;
         } else if (!have_shb) {
@@ -616,6 +621,7 @@ static int64_t or_pcapng_index(const uint8_t* f, uint64_t n, or_pcap_rec** out) 
                     caplen = rdx32(b + 12, sw);
                     dataoff = 20;
                     if (ifid >= (uint32_t)nif || caplen > blen - 20) stop = 1;
+                    else if (caplen > ifs[0].snap) caplen = ifs[0].snap;
                 }
             }
             if (!stop && caplen > max_snap) stop = 1;

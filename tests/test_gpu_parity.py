@@ -726,6 +726,40 @@ def test_pcapng_file_ingest(gpu, tmp_path):
     assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "pcapng fluere_offline_file")
 
 
+@pytest.mark.parametrize("case", ["snaplen_clamp", "byte_order_change"])
+def test_pcapng_snaplen_and_byte_order(gpu, tmp_path, case):
+    """libpcap's pcapng reader: an Enhanced Packet Block whose caplen exceeds
+    the snapshot length (the first interface's snaplen) is cut to it; a later
+    section in the other byte order ends the capture.  Product and oracle on
+    the same bytes (parity unpinned: the reference holds no pcapng fixture)."""
+    import pktbuild as pb
+    frames = [pb.eth() + pb.ipv4("10.1.0.1", f"10.1.1.{i}", 17, pb.udp(5000 + i, 6000, b"\x11" * 40))
+              for i in range(6)]
+    if case == "snaplen_clamp":
+        items = [("shb",), ("idb", 50, None, None), ("idb", 0, None, None)]
+        items += [("epb", i % 2, 1_700_000_000_000_000 + i, f) for i, f in enumerate(frames)]
+        data = pb.pcapng(items)
+    else:
+        a = [("shb",), ("idb", 0, None, None)] + [("epb", 0, 1_700_000_000_000_000 + i, f)
+                                                  for i, f in enumerate(frames[:3])]
+        b = [("shb",), ("idb", 0, None, None)] + [("epb", 0, 1_700_000_000_000_100 + i, f)
+                                                  for i, f in enumerate(frames[3:])]
+        data = pb.pcapng(a) + pb.pcapng(b, swapped=True)
+    want = pyoracle.offline(data)
+    assert want["packets"] == (6 if case == "snaplen_clamp" else 3)
+    path = tmp_path / "cap.pcapng"
+    path.write_bytes(data)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_pcap_file(str(path))
+        assert ctx.n_packets == want["packets"]
+        ctx.run()
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], case)
+    if case == "snaplen_clamp":
+        # 50-byte frames: the UDP payload is cut, the IPv4 total length still says 68
+        assert all(int(r) == 68 for r in recs["min_pkt"])
+
+
 # ---- live mode on batched capture (fluere_amd/live.py, live_fluereflow.rs:196-376)
 LIVE_CASES = {
     # kind, packets, lanes/flows, seed, interval ms (packet clock), batch packets, timeout ms, duration_end, -M
