@@ -170,6 +170,9 @@ def lib() -> ctypes.CDLL:
                                      ctypes.POINTER(U64)]),
         "fluere_export_async": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, P]),
         "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, U64, ctypes.POINTER(Stats)]),
+        "fluere_wire_bound": (U64, [U64, U64]),
+        "fluere_wire_pack": (I, [P, P, U32, U64, U64, P, P]),
+        "fluere_wire_unpack": (I, [P, P, U32, P, U64, U64, P]),
         "fluere_sweep_pack": (I, [P, U32, P, P]),
         "fluere_sweep_load": (I, [P, P, U32, P]),
         "fluere_sweep_index": (I, [P, P, ctypes.POINTER(U64)]),

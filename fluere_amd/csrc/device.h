@@ -67,6 +67,7 @@ struct Glob {
     unsigned long long n_slow;
     unsigned long long n_spill;  // k_parse_agg: the batch's overflow-list records (cursor); next to n_slow
     unsigned long long n_dspill; // k_parse_agg: the batch's spills in owner segments; next to n_spill
+    unsigned long long n_gen;    // k_slow: the batch's general-parser list (cursor); next to n_dspill
     unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
     unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
@@ -74,8 +75,9 @@ struct Glob {
     unsigned long long clean_done;                        // k_cleanup: workgroups finished
     unsigned long long fin_done;                          // k_finalize: workgroups finished
 };
-static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16,
-              "n_slow, n_spill, n_dspill are reset together");
+static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16 &&
+                  offsetof(Glob, n_gen) == offsetof(Glob, n_slow) + 24,
+              "n_slow, n_spill, n_dspill, n_gen are reset together");
 // One device allocation holds Glob and the dictionary counters right after it
 // (n_flows, err), so a run ends with ONE small device->host copy.
 struct Ctl {
@@ -132,6 +134,13 @@ __device__ __forceinline__ void pin_win(const Win& W) {
                  "v"(W.w[16]), "v"(W.w[17]), "v"(W.w[18]), "v"(W.w[19]));
 }
 
+__device__ __forceinline__ void pin_win32(const Win32& W) {
+#pragma unroll
+    for (int k = 0; k < 32; k += 8)
+        asm volatile("" ::"v"(W.w[k]), "v"(W.w[k + 1]), "v"(W.w[k + 2]), "v"(W.w[k + 3]), "v"(W.w[k + 4]),
+                     "v"(W.w[k + 5]), "v"(W.w[k + 6]), "v"(W.w[k + 7]));
+}
+
 __device__ __forceinline__ uint64_t mac_be(const uint8_t* p) {
     uint64_t m = 0;
     for (int k = 0; k < 6; k++) m = (m << 8) | p[k];
@@ -186,6 +195,72 @@ __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const
             P.dmac = mac_be(fr + pi.frame_off);
             P.smac = mac_be(fr + pi.frame_off + 6);
         }
+    }
+}
+
+// The packets the hot parser leaves over (k_slow; k_parse_batch's production
+// mode): the record at batch offset off with its 128-byte window W loaded --
+// parse_fast, then parse_mid, then (GEN = 1) the general parser out of line;
+// GEN = 0 leaves the rest to the caller (P.cls = 2: the general parser's).
+template <int GEN>
+__device__ __forceinline__ void parse_loaded32(const Batch& B, uint32_t off, const Win32& W, bool macs, Parsed& P) {
+    const bool sw = B.flags & 1;
+    const uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
+    uint32_t L = min(incl, B.snap);
+    const uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
+    if (L > avail) L = (uint32_t)avail;
+    P.L = L;
+    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);  // time.rs:5-7
+    Win W20;
+#pragma unroll
+    for (int k = 0; k < 20; k++) W20.w[k] = W.w[k];
+    const bool fast = parse_fast(W20, L, P.pi);
+    const bool mid = !fast && parse_mid(W, L, P.pi);
+    const uint8_t* fr = B.bytes + off + 16;
+    P.smac = P.dmac = 0;
+    if (!fast && !mid) {
+        if constexpr (GEN == 0) {
+            P.cls = 2;
+            return;
+        } else {
+            PktInfo g;
+            parse_general(fr, L, g);
+            P.pi = g;
+        }
+    }
+    const PktInfo& pi = P.pi;
+    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;
+    if (macs && P.cls == 0) {
+        if (fast || mid) {
+            // the keyed frame at frame byte 0 or 50 (VXLAN inner): record bytes 16.. / 66..
+            const bool in = pi.frame_off != 0;
+            uint64_t d = 0, s = 0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) d = (d << 8) | (in ? W.b(66 + k) : W.b(16 + k));
+#pragma unroll
+            for (int k = 0; k < 6; k++) s = (s << 8) | (in ? W.b(72 + k) : W.b(22 + k));
+            P.dmac = d;
+            P.smac = s;
+        } else {
+            P.dmac = mac_be(fr + pi.frame_off);
+            P.smac = mac_be(fr + pi.frame_off + 6);
+        }
+    }
+}
+
+// The 128-byte window of the record at off: pieces 0..4 always (a batch is
+// readable 80 bytes past its end), 5..7 where they stay inside that (a record
+// short enough to need the clamp never reads them: parse_mid needs L >= 34 of
+// a whole record).
+__device__ __forceinline__ void load_win32(const Batch& B, uint32_t off, Win32& W) {
+    const uint8_t* p = B.bytes + off;
+    const uint64_t room = B.nbytes + 80 > (uint64_t)off ? B.nbytes + 80 - off : 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const uint8_t* q = (c < 5 || (uint64_t)(16 * c + 16) <= room) ? p + 16 * c : p + 64;
+        uint4 v;
+        __builtin_memcpy(&v, q, 16);
+        W.w[4 * c + 0] = v.x; W.w[4 * c + 1] = v.y; W.w[4 * c + 2] = v.z; W.w[4 * c + 3] = v.w;
     }
 }
 

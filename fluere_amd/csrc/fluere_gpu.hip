@@ -116,8 +116,11 @@ struct Stage {
                                   // stores; k_merge_partials sums them: no contended atomics at the end)
     uint32_t W;                   // sets per workgroup
     uint32_t O;                   // merge owners (k_merge_partials workgroups)
-    uint32_t n_sets;
+    uint32_t n_sets;              // sets: the hot kernel's n_hot, then k_slow's (when it runs)
     uint32_t n_wg;                // hot-kernel workgroups
+    uint32_t n_hot;               // the hot kernel's sets (n_wg * W)
+    uint32_t cap_s;               // k_slow sets: records per owner segment
+    unsigned long long slow_rec0; // k_slow sets: their segments start at this record of dspill
 };
 // per-workgroup statistics: valid, dropped, LDS-table misses, tmin, tmax, cycles total / flush / wave wait
 constexpr int WGS_N = 8;
@@ -131,10 +134,12 @@ struct AggArgs {
     uint32_t* slow;            // packets (batch-local indices) the hot parser left to the general parser:
                                // workgroup b's in slow[b * slow_region, + slow_cnt[b])
     unsigned long long* slow_n;  // their total (the merge's "any slow packet" test)
+    uint32_t* gen;             // k_slow: the slow packets parse_fast / parse_mid leave to the general parser
+                               // (batch-local indices, Glob::n_gen of them; the merge tail takes them)
     uint32_t* slow_cnt;
     uint32_t slow_region;      // packets a hot workgroup can see (its steps x BLOCK)
     int slow_abl;              // diagnostics only (FLUERE_SLOW_ABL, wrong results): 1 no dictionary, 2 no parse
-    int slow_kernel;           // the slow list is k_slow's (launched behind the merge), not the merge tail's
+    int slow_kernel;           // the slow list is k_slow's (launched before the merge), not the merge tail's
     int macs;
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
 };
@@ -200,26 +205,6 @@ __device__ __forceinline__ uint32_t hot_parse(const Batch& B, uint32_t off, cons
     const bool vlan_drop =
         whole & ((w7 & 0xFFFFu) == 0x0081u) & ((L < 32u) | ((in_et != 0x0008u) & (in_et != 0xDD86u)));
     return shape ? (ok ? HOT_OK : HOT_DROP) : (vlan_drop ? HOT_DROP : HOT_SLOW);
-}
-
-// update_flow's order-free part straight into the global accumulators
-// (flows.rs:11-42); first/last/FIN-RST positions as min/max packet indices.
-__device__ __forceinline__ void agg_global(const Acc& A, uint32_t d, uint8_t dir, const PktInfo& pi, uint64_t gi) {
-    const uint32_t tf = pi.tflags, pkt = pi.rpkt, ttl = pi.rttl;
-    atomicAdd(&A.pk[dir][d], 1u);
-    atomicAdd(&A.by[dir][d], (unsigned long long)pi.doctets);
-    if (pkt < A.mn[0][d]) atomicMin(&A.mn[0][d], pkt);  // a stale read can only skip a no-op
-    if (pkt > A.mx[0][d]) atomicMax(&A.mx[0][d], pkt);
-    if (ttl < A.mn[1][d]) atomicMin(&A.mn[1][d], ttl);
-    if (ttl > A.mx[1][d]) atomicMax(&A.mx[1][d], ttl);
-    if (tf) {
-        for (int q = 0; q < 8; q++)
-            if ((tf >> q) & 1) atomicAdd(&A.fl[q][d], 1u);
-        if (tf & 5) atomicMin(&A.fr[d], (unsigned long long)gi);
-    }
-    if (gi < A.fa[d]) atomicMin(&A.fa[d], (unsigned long long)gi);
-    if ((pi.rprot != 6 || (tf & 2)) && gi < A.fc[d]) atomicMin(&A.fc[d], (unsigned long long)gi);
-    atomicMax(&A.la[d], (unsigned long long)gi);
 }
 
 // Workgroup barrier for LDS-only hand-offs: waits for this wave's LDS
@@ -1398,7 +1383,9 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     hi = offs[(size_t)(pass ? me : me + 1) * S.n_sets + set];  // pass 1: the segment's count
                     wb = S.base[set];
                 }
-                rb = pass ? ((unsigned long long)set * S.O + me) * S.cap_o : (unsigned long long)set * NS;
+                rb = !pass ? (unsigned long long)set * NS
+                     : set < S.n_hot ? ((unsigned long long)set * S.O + me) * S.cap_o
+                                     : S.slow_rec0 + ((unsigned long long)(set - S.n_hot) * S.O + me) * S.cap_s;
                 m_lo[tid * (MCH / MB) + q] = (uint32_t)(rb + lo);
                 m_wb[tid * (MCH / MB) + q] = (uint32_t)(wb - a.B.first);
                 len[q] = hi - lo;
@@ -1624,12 +1611,16 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
     if (blockIdx.x == gridDim.x - 1 && tid < 64) reduce_stats();
-    const bool tail_slow = n_slow_all && !a.slow_kernel;
+    // k_slow ran: its general-parser list (flat); else the whole slow list
+    const unsigned long long n_gen_all =
+        a.slow_kernel ? __hip_atomic_load(&a.g->n_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const bool tail_slow = a.slow_kernel ? n_gen_all != 0 : n_slow_all != 0;
     if (tail_slow || n_spill_all) {
         // The tail: the overflow list (spills past their owner segment's
-        // capacity: full keys, no parse) and, unless k_slow takes it, the
-        // slow list (packets the hot kernel left to the general parser: IPv6,
-        // IPv4 options, ARP, VXLAN, VLAN, other IP protocols, short frames).
+        // capacity: full keys, no parse) and the packets for the general
+        // parser: the whole slow list (packets the hot kernel left over: IPv6,
+        // IPv4 options, ARP, VXLAN, VLAN, other IP protocols, short frames),
+        // or, when k_slow ran, the ones parse_fast / parse_mid left to it.
         // Each record: dense id from the dictionary, then update_flow's
         // order-free part pre-aggregated per dense id in this workgroup's LDS
         // entries (reused: the owner's flows are in the global accumulators);
@@ -1705,16 +1696,21 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             const uint32_t st0 = block_exclusive_scan(cnt, m_scan);
             if (tid < (int)nwg) m_start[tid] = st0;
             __syncthreads();
-            const unsigned long long n = m_scan[MB / 64];
+            const unsigned long long n = a.slow_kernel ? n_gen_all : (unsigned long long)m_scan[MB / 64];
             unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
             for (unsigned long long i = (unsigned long long)blockIdx.x * MB + tid; i < n; i += gstride) {
-                uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
-                while (lo_w < hi_w) {
-                    const uint32_t mid = (lo_w + hi_w + 1) >> 1;
-                    if (m_start[mid] <= i) lo_w = mid;
-                    else hi_w = mid - 1;
+                uint64_t li;
+                if (a.slow_kernel) {
+                    li = a.gen[i];
+                } else {
+                    uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
+                    while (lo_w < hi_w) {
+                        const uint32_t mid = (lo_w + hi_w + 1) >> 1;
+                        if (m_start[mid] <= i) lo_w = mid;
+                        else hi_w = mid - 1;
+                    }
+                    li = a.slow[(size_t)lo_w * a.slow_region + (i - m_start[lo_w])];
                 }
-                const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - m_start[lo_w])];
                 if (a.slow_abl == 2) { c_drop += li == NONE32; continue; }
                 Parsed P;
                 parse_record(a.B, li, macs, 1, P);
@@ -1767,39 +1763,35 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_slow: the slow list when the last run had one (the host predicts it;
-// otherwise k_merge_partials' tail takes it).  The general parser inlined
-// (out of line, every packet saved and restored the callee's registers
-// through scratch: ~2.5 KB of scratch traffic per packet), the dictionary,
-// then update_flow's order-free part pre-aggregated per dense id in LDS
-// (ST entries per workgroup, 8 probes; else the global atomics).
+// k_slow: the slow list (packets the hot parser left over) when the last run
+// had one (the host predicts it; otherwise k_merge_partials' tail takes it).
+// Runs between the hot kernel and the merge.  Workgroup b takes slow-list
+// entries [b * SLOW_SET, (b + 1) * SLOW_SET) of the hot workgroups' regions
+// flattened, as staging set n_hot + b.  Per packet: the 128-byte window,
+// parse_fast / parse_mid in registers (the rest -- ARP, VLAN, short frames,
+// drops -- go to a list for the general parser in the merge tail: inlined
+// here, its registers would cost every packet occupancy); then a spill
+// record into its merge owner's segment of the set, like the hot kernel's
+// LDS-table misses: an IPv4 key as its words (no dictionary walk here: the
+// owner resolves each key once), any other key (IPv6, -M, the raw fallback's
+// protocol 255) as its dense id from the dictionary.  k_merge_partials then
+// aggregates them with the hot kernel's partials.
 // ---------------------------------------------------------------------------
-constexpr int SB = 256;  // k_slow block
-constexpr int ST = 128;  // k_slow LDS entries
-constexpr int SSTAGE = 7;  // 16-byte pieces of a lane's staged frame (the first 112 bytes)
-__global__ void __launch_bounds__(SB, 3) k_slow(AggArgs a) {
-    __shared__ uint32_t s_key[ST], s_pk[2][ST], s_mn[2][ST], s_mx[2][ST], s_fl[8][ST];
-    __shared__ unsigned long long s_by[2][ST], s_fa[ST], s_fc[ST], s_fr[ST], s_la[ST];
+constexpr int SB = 256;                      // k_slow block
+constexpr uint32_t SLOW_SET = SPILL_WG / 4;  // slow-list entries per k_slow workgroup (one set)
+__global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
     __shared__ uint32_t s_start[MB + 1];
-    __shared__ uint4 s_stage[SB][SSTAGE];  // per lane: the packet's first 112 frame bytes
-    const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!n_slow_all) return;  // uniform
+    __shared__ uint32_t s_scnt[OWN_WORDS];  // records per owner (packed 16-bit: a set has <= SLOW_SET)
     const int tid = threadIdx.x;
     const bool macs = a.macs != 0;
-    for (int e = tid; e < ST; e += SB) {
-        s_key[e] = NONE32;
-        s_pk[0][e] = s_pk[1][e] = 0;
-        s_by[0][e] = s_by[1][e] = 0;
-        s_mn[0][e] = s_mn[1][e] = NONE32;
-        s_mx[0][e] = s_mx[1][e] = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) s_fl[q][e] = 0;
-        s_fa[e] = s_fc[e] = s_fr[e] = NONE64;
-        s_la[e] = 0;
-    }
+    const Stage& S = a.S;
+    const uint32_t O = S.O;
+    const uint32_t set = S.n_hot + blockIdx.x;
+    const int spu = spill_units(macs);
+    for (int o = tid; o < OWN_WORDS; o += SB) s_scnt[o] = 0;
     // the hot workgroups' regions, flattened (wave 0: an exclusive scan, an
     // even run of regions per lane)
-    const uint32_t nwg = a.S.n_wg;  // <= MB
+    const uint32_t nwg = S.n_wg;  // <= MB
     if (tid < 64) {
         const uint32_t per = (nwg + 63) / 64;
         uint32_t sum = 0;
@@ -1825,102 +1817,124 @@ __global__ void __launch_bounds__(SB, 3) k_slow(AggArgs a) {
     }
     __syncthreads();
     const unsigned long long n = s_start[MB];
-    unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
-    const unsigned long long stride = (unsigned long long)gridDim.x * SB;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * SB + tid; i < n; i += stride) {
-        uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
-        while (lo_w < hi_w) {
-            const uint32_t mid = (lo_w + hi_w + 1) >> 1;
-            if (s_start[mid] <= i) lo_w = mid;
-            else hi_w = mid - 1;
-        }
-        const uint64_t li = a.slow[(size_t)lo_w * a.slow_region + (i - s_start[lo_w])];
-        // the record: its header + first 64 frame bytes as the register
-        // window, its first 112 frame bytes staged in this lane's LDS slot
-        // (the batch is readable 80 bytes past its end: never past that)
-        const uint32_t off = a.B.offs[li];
-        const uint8_t* rec = a.B.bytes + off;
-        const uint64_t room = a.B.nbytes + 64 > (uint64_t)off ? a.B.nbytes + 64 - off : 0;  // readable frame bytes
-        const uint32_t nst = (uint32_t)min<uint64_t>(SSTAGE, room / 16);
-        uint4 pc[SSTAGE + 1];
-#pragma unroll
-        for (int k = 0; k < SSTAGE + 1; k++) {
-            if (k < 5 || k <= (int)nst) __builtin_memcpy(&pc[k], rec + 16 * k, 16);  // (80 bytes always readable)
-            else pc[k] = make_uint4(0, 0, 0, 0);
-        }
-        Win W;
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            W.w[4 * k + 0] = pc[k].x; W.w[4 * k + 1] = pc[k].y; W.w[4 * k + 2] = pc[k].z; W.w[4 * k + 3] = pc[k].w;
-        }
-#pragma unroll
-        for (int k = 0; k < SSTAGE; k++) s_stage[tid][k] = pc[k + 1];
+    const unsigned long long i0 = (unsigned long long)blockIdx.x * SLOW_SET;
+    const unsigned long long i1 = min(n, i0 + SLOW_SET);
+    unsigned long long c_valid = 0, c_drop = 0, c_seg = 0, tmin = NONE64, tmax = 0;
+    for (unsigned long long ib = i0; ib < i1; ib += SB) {  // (uniform)
+        const unsigned long long i = ib + tid;
+        bool rec = false, gen = false;
+        uint32_t ow = 0, gli = 0;
         Parsed P;
-        parse_loaded<true>(a.B, off, W, macs, 1, P, reinterpret_cast<const uint8_t*>(s_stage[tid]), 16 * nst);
-        if (P.cls) { c_drop++; continue; }
-        c_valid++;
-        tmin = min(tmin, (unsigned long long)P.t);
-        tmax = max(tmax, (unsigned long long)P.t);
-        uint8_t dir = 0;
-        const uint32_t d = a.slow_abl == 1 ? (P.pi.sip[3] ^ P.pi.dip[3] ^ P.pi.ksp) % 8192u  // diagnostics only
-                                           : flow_of(a.T, P, macs, true, dir, a.A.slots, &a.g->generic_used);
-        if (d == FAIL || d >= a.T.fmax) continue;
-        const unsigned long long gi = a.B.first + li;
-        uint32_t e = (d * 0x9E3779B1u) >> 25;  // 7 bits: ST == 128
-        bool in_lds = false;
-        for (int pr = 0; pr < 8; pr++) {
-            const uint32_t k = atomicCAS(&s_key[e], NONE32, d);
-            if (k == NONE32 || k == d) { in_lds = true; break; }
-            e = (e + 1) & (ST - 1);
+        uint4 wk = make_uint4(0, 0, 0, 0), wx = make_uint4(0, 0, 0, 0), wp = make_uint4(0, 0, 0, 0);
+        if (i < i1) {
+            uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
+            while (lo_w < hi_w) {
+                const uint32_t mid = (lo_w + hi_w + 1) >> 1;
+                if (s_start[mid] <= i) lo_w = mid;
+                else hi_w = mid - 1;
+            }
+            const uint32_t li = a.slow[(size_t)lo_w * a.slow_region + (i - s_start[lo_w])];
+            const uint32_t off = a.B.offs[li];
+            Win32 W;
+            load_win32(a.B, off, W);
+            pin_win32(W);
+            parse_loaded32<0>(a.B, off, W, macs, P);
+            gen = P.cls == 2;
+            if (gen) {
+                gli = li;
+            } else if (P.cls) {
+                c_drop++;
+            } else {
+                c_valid++;
+                tmin = min(tmin, (unsigned long long)P.t);
+                tmax = max(tmax, (unsigned long long)P.t);
+                const PktInfo& pi = P.pi;
+                uint8_t dir = 0;
+                CKey k;
+                canon_key(P, macs, k, dir);
+                uint32_t h;
+                if (!macs && !pi.v6 && pi.kproto != 0xFF) {
+                    // an IPv4 key: its words, as the hot kernel's spills carry them
+                    wk = make_uint4(k.w[0], k.w[4], k.w[8], (uint32_t)pi.kproto << 24);
+                    h = lt_hash(wk.x, wk.y, wk.z, wk.w);
+                    rec = true;
+                } else {
+                    const uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+                    wk = make_uint4(d, 0, 0, 0xFF000000u);
+                    h = lt_hash(d, 0, 0, 0xFF000000u);
+                    rec = d != FAIL && d < a.T.fmax;
+                }
+                const uint32_t tf = pi.tflags;
+                const bool elig = (pi.rprot != 6) | ((tf & 2u) != 0);
+                wp = make_uint4(pi.doctets, pi.rpkt | ((uint32_t)pi.rttl << 16) | ((elig ? 1u : 0u) << 24), li,
+                                tf | ((uint32_t)dir << 8));
+                wx = make_uint4(0, 0, 0, h);
+                ow = owner_of(h, O);
+            }
         }
-        if (!in_lds) { agg_global(a.A, d, dir, P.pi, gi); continue; }
-        const uint32_t tf = P.pi.tflags;
-        atomicAdd(&s_pk[dir][e], 1u);
-        atomicAdd(&s_by[dir][e], (unsigned long long)P.pi.doctets);
-        atomicMin(&s_mn[0][e], (uint32_t)P.pi.rpkt);
-        atomicMax(&s_mx[0][e], (uint32_t)P.pi.rpkt);
-        atomicMin(&s_mn[1][e], (uint32_t)P.pi.rttl);
-        atomicMax(&s_mx[1][e], (uint32_t)P.pi.rttl);
-        if (tf) {
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                if ((tf >> q) & 1) atomicAdd(&s_fl[q][e], 1u);
-            if (tf & 5) atomicMin(&s_fr[e], gi);
+        // the general parser's packets: the merge tail's list (wave-aggregated append)
+        const uint64_t gm = __ballot(gen);
+        if (gm) {
+            const uint32_t lead = __builtin_ctzll(gm);
+            unsigned long long b0 = 0;
+            if ((uint32_t)(tid & 63) == lead) b0 = atomicAdd(&a.g->n_gen, (unsigned long long)__popcll(gm));
+            b0 = __shfl(b0, lead, 64);
+            if (gen) a.gen[b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] = gli;
         }
-        atomicMin(&s_fa[e], gi);
-        if (P.pi.rprot != 6 || (tf & 2)) atomicMin(&s_fc[e], gi);
-        atomicMax(&s_la[e], gi + 1);
+        const uint32_t pos = rec ? own_add(s_scnt, ow) : 0u;
+        const bool ovf = rec && pos >= S.cap_s;
+        if (rec && !ovf) {
+            uint4* dst = reinterpret_cast<uint4*>(S.dspill) +
+                         (S.slow_rec0 + ((size_t)blockIdx.x * O + ow) * S.cap_s + pos) * (2 * spu);
+            dst[0] = wk;
+            if (macs) {
+                dst[1] = wx;
+                dst[2] = wp;
+            } else {
+                dst[1] = wp;
+            }
+            c_seg++;
+        }
+        // past the segment's capacity: the overflow list (wave-aggregated append; rare)
+        const uint64_t om = __ballot(ovf);
+        if (om) {
+            const uint32_t lead = __builtin_ctzll(om);
+            unsigned long long b0 = 0;
+            if ((uint32_t)(tid & 63) == lead) b0 = atomicAdd(&a.g->n_spill, (unsigned long long)__popcll(om));
+            b0 = __shfl(b0, lead, 64);
+            if (ovf) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u));
+                uint4* dst = reinterpret_cast<uint4*>(S.spill) + (b0 + r) * (size_t)(2 * spu);
+                wp.w |= set << 9;
+                dst[0] = wk;
+                if (macs) {
+                    dst[1] = wx;
+                    dst[2] = wp;
+                } else {
+                    dst[1] = wp;
+                }
+            }
+        }
     }
     __syncthreads();
-    for (int e = tid; e < ST; e += SB) {
-        const uint32_t d = s_key[e];
-        if (d == NONE32) continue;
-        FlowPart f;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            f.pk[q] = s_pk[q][e];
-            f.by[q] = s_by[q][e];
-            f.mn[q] = s_mn[q][e];
-            f.mx[q] = s_mx[q][e];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; q++) f.fl[q] = s_fl[q][e];
-        f.fa = s_fa[e];
-        f.fc = s_fc[e];
-        f.fr = s_fr[e];
-        f.la = s_la[e];
-        part_to_global(a.A, d, f);
+    // this set's segments: record counts, no partials, positions relative to the batch
+    for (uint32_t o = tid; o <= O; o += SB) {
+        S.off[(size_t)o * S.n_sets + set] = 0;
+        if (o < O) S.soff[(size_t)o * S.n_sets + set] = min(own_get(s_scnt, o), S.cap_s);
     }
+    if (tid == 0) S.base[set] = a.B.first;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         c_valid += __shfl_xor(c_valid, o, 64);
         c_drop += __shfl_xor(c_drop, o, 64);
+        c_seg += __shfl_xor(c_seg, o, 64);
         tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, o, 64));
         tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, o, 64));
     }
     if ((tid & 63) == 0) {
         if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
         if (c_drop) atomicAdd(&a.g->dropped, c_drop);
+        if (c_seg) atomicAdd(&a.g->n_dspill, c_seg);
     }
 }
 
@@ -2192,7 +2206,14 @@ __global__ void __launch_bounds__(256) k_parse_batch(Batch B, fluere_pkt_meta* o
     uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= B.n) return;
     Parsed P;
-    parse_record(B, li, true, mode, P);
+    if (mode == 0) {  // production: fast, middle, general (the k_slow sequence)
+        const uint32_t off = B.offs[li];
+        Win32 W;
+        load_win32(B, off, W);
+        parse_loaded32<1>(B, off, W, true, P);
+    } else {
+        parse_record(B, li, true, mode, P);
+    }
     const PktInfo& pi = P.pi;
     fluere_pkt_meta m;
     memset(&m, 0, sizeof m);
@@ -2646,6 +2667,296 @@ __global__ void __launch_bounds__(64) k_compose(MergeArgs a, const unsigned long
     }
 }
 
+// ---- the compact wire encoding of export blocks ------------------------------
+// A wide block (fluere_flow_summary, 256 B each) carries every field at full
+// width.  On the wire each summary is a variable-length record: a descriptor
+// word says which fields are present and how wide; absent fields (zero
+// counters, flag counts, a first FIN/RST, a first packet that differs from the
+// creating one, the seed of a flow with no creating packet) take no bytes, and
+// an IPv4 5-tuple key takes 12 bytes instead of 56.  Wire block of one owner:
+// the block header, a u32 offset table (one per summary, relative to the
+// records), the records (4-byte aligned), the annexes verbatim (16-byte
+// aligned).  The owner expands every received block back to the wide layout,
+// at the same positions, before fluere_merge_gathered.
+enum : uint32_t {
+    WB_PK0 = 1u << 18, WB_PK1 = 1u << 19, WB_WBY = 1u << 20, WB_WMM = 1u << 21, WB_FC = 1u << 22,
+    WB_FA = 1u << 23,  WB_FR = 1u << 24,  WB_AX = 1u << 25,  WB_DIR = 1u << 26, WB_V6 = 1u << 27,
+    WB_LADDR = 1u << 28, WB_FULLKEY = 1u << 29,
+};
+constexpr uint32_t WIRE_REC_MAX = 4 + 56 + 8 + 16 + 20 + 32 + 16 + 16 + 16 + 4 + 32 + 4;  // 224
+constexpr uint32_t WIRE_MAX_BLOCKS = 64;  // shards of one unpack (kernel-argument offsets)
+
+__device__ __forceinline__ bool wire_short_key(const fluere_flow_summary& s) {
+    uint32_t o = s.key[9] >> 10;
+#pragma unroll
+    for (int j = 0; j < 14; j++)
+        if (j != 0 && j != 4 && j != 8 && j != 9) o |= s.key[j];
+    return o == 0;
+}
+__device__ __forceinline__ bool wire_long_addr(const fluere_flow_summary& s) {
+    uint32_t o = s.first_v6;
+#pragma unroll
+    for (int k = 4; k < 16; k++) o |= s.first_src[k] | s.first_dst[k];
+    return o != 0;
+}
+__device__ __forceinline__ uint32_t wire_desc(const fluere_flow_summary& s) {
+    uint32_t fm = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) fm |= (s.flag_cnt[q] ? 1u : 0u) << q;
+    uint32_t d = (s.key[9] & 0x3FFu) | (fm << 10);
+    d |= s.pkts[0] ? WB_PK0 : 0u;
+    d |= s.pkts[1] ? WB_PK1 : 0u;
+    d |= (s.bytes[0] > 0xFFFFFFFFull || s.bytes[1] > 0xFFFFFFFFull) ? WB_WBY : 0u;
+    d |= (s.min_pkt > 0xFFFFu || s.max_pkt > 0xFFFFu || s.min_ttl > 0xFFu || s.max_ttl > 0xFFu) ? WB_WMM : 0u;
+    d |= s.first_create != NONE64 ? WB_FC : 0u;
+    d |= s.first_all != s.first_create ? WB_FA : 0u;
+    d |= s.finrst_min != NONE64 ? WB_FR : 0u;
+    d |= s.annex != NONE32 ? WB_AX : 0u;
+    d |= s.first_dir ? WB_DIR : 0u;
+    d |= s.first_v6 ? WB_V6 : 0u;
+    d |= wire_long_addr(s) ? WB_LADDR : 0u;
+    d |= wire_short_key(s) ? 0u : WB_FULLKEY;
+    return d;
+}
+__device__ __forceinline__ uint32_t wire_bytes(uint32_t d) {
+    const uint32_t by = (d & WB_WBY) ? 8u : 4u;
+    uint32_t n = 4 + ((d & WB_FULLKEY) ? 56u : 12u);
+    n += (d & WB_PK0) ? 4u + by : 0u;
+    n += (d & WB_PK1) ? 4u + by : 0u;
+    n += (d & WB_WMM) ? 20u : 8u;  // min / max pkt, ttl (+ prot, tos)
+    n += 4u * __popc((d >> 10) & 0xFFu);
+    n += 8u + 8u;  // last, last_time
+    n += (d & WB_FA) ? 8u : 0u;
+    n += (d & WB_FR) ? 8u : 0u;
+    n += (d & WB_FC) ? 8u + 8u + 4u + ((d & WB_LADDR) ? 32u : 8u) : 0u;  // first_create, first_time, ports, addresses
+    n += (d & WB_AX) ? 4u : 0u;
+    return n;
+}
+struct WirePut {
+    uint32_t* p;
+    __device__ __forceinline__ void u32(uint32_t v) { *p++ = v; }
+    __device__ __forceinline__ void u64(unsigned long long v) { p[0] = (uint32_t)v; p[1] = (uint32_t)(v >> 32); p += 2; }
+    __device__ __forceinline__ void bytes(const uint8_t* b, int n) {
+        for (int k = 0; k < n; k += 4) u32(b[k] | (b[k + 1] << 8) | (b[k + 2] << 16) | ((uint32_t)b[k + 3] << 24));
+    }
+};
+struct WireGet {
+    const uint32_t* p;
+    __device__ __forceinline__ uint32_t u32() { return *p++; }
+    __device__ __forceinline__ unsigned long long u64() {
+        const unsigned long long v = p[0] | ((unsigned long long)p[1] << 32);
+        p += 2;
+        return v;
+    }
+    __device__ __forceinline__ void bytes(uint8_t* b, int n) {
+        for (int k = 0; k < n; k += 4) {
+            const uint32_t v = u32();
+            b[k] = (uint8_t)v; b[k + 1] = (uint8_t)(v >> 8); b[k + 2] = (uint8_t)(v >> 16); b[k + 3] = (uint8_t)(v >> 24);
+        }
+    }
+};
+__device__ __forceinline__ void wire_put(const fluere_flow_summary& s, uint32_t d, uint32_t* dst) {
+    WirePut w{dst};
+    w.u32(d);
+    if (d & WB_FULLKEY) {
+#pragma unroll
+        for (int j = 0; j < 14; j++) w.u32(s.key[j]);
+    } else {
+        w.u32(s.key[0]); w.u32(s.key[4]); w.u32(s.key[8]);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+        if (d & (q ? WB_PK1 : WB_PK0)) {
+            w.u32(s.pkts[q]);
+            if (d & WB_WBY) w.u64(s.bytes[q]);
+            else w.u32((uint32_t)s.bytes[q]);
+        }
+    if (d & WB_WMM) {
+        w.u32(s.min_pkt); w.u32(s.max_pkt); w.u32(s.min_ttl); w.u32(s.max_ttl);
+        w.u32((uint32_t)s.first_prot | ((uint32_t)s.first_tos << 8));
+    } else {
+        w.u32(s.min_pkt | (s.max_pkt << 16));
+        w.u32(s.min_ttl | (s.max_ttl << 8) | ((uint32_t)s.first_prot << 16) | ((uint32_t)s.first_tos << 24));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if ((d >> (10 + q)) & 1) w.u32(s.flag_cnt[q]);
+    w.u64(s.last);
+    w.u64(s.last_time);
+    if (d & WB_FA) w.u64(s.first_all);
+    if (d & WB_FR) w.u64(s.finrst_min);
+    if (d & WB_FC) {
+        w.u64(s.first_create);
+        w.u64(s.first_time);
+        w.u32(s.first_sport | ((uint32_t)s.first_dport << 16));
+        const int na = (d & WB_LADDR) ? 16 : 4;
+        w.bytes(s.first_src, na);
+        w.bytes(s.first_dst, na);
+    }
+    if (d & WB_AX) w.u32(s.annex);
+}
+__device__ __forceinline__ void wire_get(const uint32_t* src, uint32_t shard, fluere_flow_summary& s) {
+    memset(&s, 0, sizeof s);
+    WireGet w{src};
+    const uint32_t d = w.u32();
+    if (d & WB_FULLKEY) {
+#pragma unroll
+        for (int j = 0; j < 14; j++) s.key[j] = w.u32();
+    } else {
+        s.key[0] = w.u32(); s.key[4] = w.u32(); s.key[8] = w.u32();
+        s.key[9] = d & 0x3FFu;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+        if (d & (q ? WB_PK1 : WB_PK0)) {
+            s.pkts[q] = w.u32();
+            s.bytes[q] = (d & WB_WBY) ? w.u64() : (unsigned long long)w.u32();
+        }
+    if (d & WB_WMM) {
+        s.min_pkt = w.u32(); s.max_pkt = w.u32(); s.min_ttl = w.u32(); s.max_ttl = w.u32();
+        const uint32_t x = w.u32();
+        s.first_prot = (uint8_t)x; s.first_tos = (uint8_t)(x >> 8);
+    } else {
+        const uint32_t a = w.u32(), b = w.u32();
+        s.min_pkt = a & 0xFFFFu; s.max_pkt = a >> 16;
+        s.min_ttl = b & 0xFFu; s.max_ttl = (b >> 8) & 0xFFu; s.first_prot = (uint8_t)(b >> 16); s.first_tos = (uint8_t)(b >> 24);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) s.flag_cnt[q] = ((d >> (10 + q)) & 1) ? w.u32() : 0u;
+    s.last = w.u64();
+    s.last_time = w.u64();
+    s.first_create = NONE64;
+    s.finrst_min = NONE64;
+    const unsigned long long fa = (d & WB_FA) ? w.u64() : 0ull;
+    if (d & WB_FR) s.finrst_min = w.u64();
+    if (d & WB_FC) {
+        s.first_create = w.u64();
+        s.first_time = w.u64();
+        const uint32_t pp = w.u32();
+        s.first_sport = (uint16_t)pp; s.first_dport = (uint16_t)(pp >> 16);
+        const int na = (d & WB_LADDR) ? 16 : 4;
+        w.bytes(s.first_src, na);
+        w.bytes(s.first_dst, na);
+    }
+    s.first_all = (d & WB_FA) ? fa : s.first_create;
+    s.first_dir = (d & WB_DIR) ? 1 : 0;
+    s.first_v6 = (d & WB_V6) ? 1 : 0;
+    s.annex = (d & WB_AX) ? w.u32() : NONE32;
+    s.shard = shard;
+}
+
+struct WireArgs {
+    const uint8_t* blocks;       // wide blocks (pack: the export's; unpack: the merge's)
+    uint8_t* wblocks;
+    const uint8_t* wire;
+    uint8_t* wwire;
+    uint64_t cap, cap_annex, block_bytes;
+    uint32_t n_blocks;
+    unsigned long long* sz;      // pack: [n_blocks * cap + 1] record bytes (0: absent)
+    unsigned long long* scan;    // pack: exclusive sum of sz
+    unsigned long long* woff;    // [n_blocks + 1]: offset of each wire block (device)
+    unsigned long long* sizes;   // pack: [n_blocks] bytes of each wire block (the caller's device buffer)
+    unsigned long long off_h[WIRE_MAX_BLOCKS + 1];  // unpack: offset of each received wire block, then the end
+};
+__device__ __forceinline__ uint64_t wire_table_bytes(uint64_t n) { return (4 * n + 15) & ~15ull; }
+__device__ __forceinline__ uint64_t blk_count(const uint8_t* blocks, uint64_t block_bytes, uint32_t b, uint64_t cap) {
+    return min((unsigned long long)reinterpret_cast<const fluere_shard_header*>(blocks + (size_t)b * block_bytes)->n_flows,
+               (unsigned long long)cap);
+}
+__device__ __forceinline__ uint64_t blk_acount(const uint8_t* blocks, uint64_t block_bytes, uint32_t b, uint64_t cap_annex) {
+    return min((unsigned long long)reinterpret_cast<const fluere_shard_header*>(blocks + (size_t)b * block_bytes)->n_annex,
+               (unsigned long long)cap_annex);
+}
+
+// pack 1: each summary's record bytes (0 for the absent slots past n_flows)
+__global__ void __launch_bounds__(256) k_wire_size(WireArgs a) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long n = (unsigned long long)a.n_blocks * a.cap;
+    if (i > n) return;
+    unsigned long long v = 0;
+    if (i < n) {
+        const uint32_t b = (uint32_t)(i / a.cap);
+        const uint64_t j = i % a.cap;
+        if (j < blk_count(a.blocks, a.block_bytes, b, a.cap)) {
+            const fluere_flow_summary* s = reinterpret_cast<const fluere_flow_summary*>(
+                a.blocks + (size_t)b * a.block_bytes + sizeof(fluere_shard_header)) + j;
+            v = wire_bytes(wire_desc(*s));
+        }
+    }
+    a.sz[i] = v;
+}
+// pack 2 (one thread): each wire block's size and offset
+__global__ void k_wire_offsets(WireArgs a) {
+    if (threadIdx.x || blockIdx.x) return;
+    unsigned long long off = 0;
+    for (uint32_t b = 0; b < a.n_blocks; b++) {
+        const uint64_t n = blk_count(a.blocks, a.block_bytes, b, a.cap);
+        const uint64_t na = blk_acount(a.blocks, a.block_bytes, b, a.cap_annex);
+        const uint64_t rec = a.scan[(size_t)(b + 1) * a.cap] - a.scan[(size_t)b * a.cap];
+        const uint64_t bytes = sizeof(fluere_shard_header) + wire_table_bytes(n) + ((rec + 15) & ~15ull) +
+                               na * sizeof(fluere_flow_annex);
+        a.woff[b] = off;
+        a.sizes[b] = bytes;
+        off += bytes;
+    }
+    a.woff[a.n_blocks] = off;
+}
+// pack 3: header, offset table and record of each summary (thread per summary slot)
+__global__ void __launch_bounds__(256) k_wire_pack(WireArgs a) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (unsigned long long)a.n_blocks * a.cap) return;
+    const uint32_t b = (uint32_t)(i / a.cap);
+    const uint64_t j = i % a.cap;
+    const uint8_t* wb = a.blocks + (size_t)b * a.block_bytes;
+    uint8_t* out = a.wwire + a.woff[b];
+    const uint64_t n = blk_count(a.blocks, a.block_bytes, b, a.cap);
+    if (j == 0) *reinterpret_cast<fluere_shard_header*>(out) = *reinterpret_cast<const fluere_shard_header*>(wb);
+    if (j >= n) return;
+    const uint32_t rel = (uint32_t)(a.scan[i] - a.scan[(size_t)b * a.cap]);
+    reinterpret_cast<uint32_t*>(out + sizeof(fluere_shard_header))[j] = rel;
+    const fluere_flow_summary& s = *(reinterpret_cast<const fluere_flow_summary*>(wb + sizeof(fluere_shard_header)) + j);
+    wire_put(s, wire_desc(s), reinterpret_cast<uint32_t*>(out + sizeof(fluere_shard_header) + wire_table_bytes(n) + rel));
+}
+// pack 4 / unpack 2: the annexes, verbatim (thread per 16-byte word)
+__global__ void __launch_bounds__(256) k_wire_annex(WireArgs a, int unpack) {
+    const uint32_t b = blockIdx.y;
+    const uint8_t* hdrp = unpack ? a.wire + a.off_h[b] : a.blocks + (size_t)b * a.block_bytes;
+    const fluere_shard_header& h = *reinterpret_cast<const fluere_shard_header*>(hdrp);
+    const uint64_t n = min((unsigned long long)h.n_flows, (unsigned long long)a.cap);
+    const uint64_t na = min((unsigned long long)h.n_annex, (unsigned long long)a.cap_annex);
+    const uint64_t words = na * sizeof(fluere_flow_annex) / 16;
+    const uint8_t* wide_ax = (unpack ? a.wblocks : a.blocks) + (size_t)b * a.block_bytes + sizeof(fluere_shard_header) +
+                             a.cap * sizeof(fluere_flow_summary);
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += (uint64_t)gridDim.x * blockDim.x) {
+        if (!unpack) {
+            const uint64_t rec = a.scan[(size_t)(b + 1) * a.cap] - a.scan[(size_t)b * a.cap];
+            uint8_t* wax = a.wwire + a.woff[b] + sizeof(fluere_shard_header) + wire_table_bytes(n) + ((rec + 15) & ~15ull);
+            reinterpret_cast<uint4*>(wax)[k] = reinterpret_cast<const uint4*>(wide_ax)[k];
+        } else {
+            // the received block's records end at the start of its annexes: total - annex bytes
+            const uint8_t* wax = a.wire + a.off_h[b + 1] - na * sizeof(fluere_flow_annex);
+            reinterpret_cast<uint4*>(const_cast<uint8_t*>(wide_ax))[k] = reinterpret_cast<const uint4*>(wax)[k];
+        }
+    }
+}
+// unpack 1: the wide block header and summaries (thread per summary slot)
+__global__ void __launch_bounds__(256) k_wire_unpack(WireArgs a) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (unsigned long long)a.n_blocks * a.cap) return;
+    const uint32_t b = (uint32_t)(i / a.cap);
+    const uint64_t j = i % a.cap;
+    const uint8_t* in = a.wire + a.off_h[b];
+    const fluere_shard_header& h = *reinterpret_cast<const fluere_shard_header*>(in);
+    uint8_t* wb = a.wblocks + (size_t)b * a.block_bytes;
+    if (j == 0) *reinterpret_cast<fluere_shard_header*>(wb) = h;
+    const uint64_t n = min((unsigned long long)h.n_flows, (unsigned long long)a.cap);
+    if (j >= n) return;
+    const uint32_t rel = reinterpret_cast<const uint32_t*>(in + sizeof(fluere_shard_header))[j];
+    fluere_flow_summary s;
+    wire_get(reinterpret_cast<const uint32_t*>(in + sizeof(fluere_shard_header) + wire_table_bytes(n) + rel), h.shard, s);
+    *(reinterpret_cast<fluere_flow_summary*>(wb + sizeof(fluere_shard_header)) + j) = s;
+}
+
 // test seam: insert canonical keys, return dense ids (flow dictionary checks)
 __global__ void __launch_bounds__(256) k_dense_test(TableSet T, const uint32_t* keys, unsigned long long n,
                                                     uint32_t* out, uint32_t* slots) {
@@ -2771,6 +3082,8 @@ struct fluere_ctx {
     uint64_t d_annex_cap = 0;
     uint32_t* d_annex_of = nullptr;
     uint32_t* d_sumpos = nullptr;                // [fmax] summary position of each flow in its owner's block
+    void* d_wire_tmp = nullptr;                  // fluere_wire_pack scratch (sizes, scan, offsets, scan temp)
+    size_t d_wire_tmp_bytes = 0;
     void* d_need = nullptr;
     uint64_t merge_cap = 0;                      // the last merge's block capacity and shard count
     uint32_t merge_shards = 0;
@@ -2980,6 +3293,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_annex);
     hipFree(c->d_annex_of);
     hipFree(c->d_sumpos);
+    hipFree(c->d_wire_tmp);
     hipFree(c->d_need);
     hipFree(c->d_recaux);
     sweep_free(c);
@@ -3483,6 +3797,7 @@ struct PassPlan {
     AggArgs agg[PLAN_BATCHES];
     unsigned agg_grid[PLAN_BATCHES];
     uint32_t owners[PLAN_BATCHES];
+    uint32_t slow_grid[PLAN_BATCHES];  // k_slow workgroups (its sets); 0: the merge tail takes the slow list
     int macs, abl;
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
     int spec;      // 1: k_finalize publishes the counters to the host itself, a speculative k_cleanup follows
@@ -3506,10 +3821,26 @@ static uint32_t owner_cap(size_t sets, uint32_t O) {
     return (uint32_t)cap;
 }
 
-static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n, bool macs) {
+// k_slow's sets (one per SLOW_SET slow-list entries of a batch of n packets)
+// and their owner-segment capacity, after `sets` hot sets; 0 sets when the
+// record indices would not fit u32 (the merge tail then takes the slow list).
+static void slow_shape(uint64_t n, size_t sets, uint32_t O, uint32_t& n_slow_sets, uint32_t& cap_s) {
+    n_slow_sets = (uint32_t)((n + SLOW_SET - 1) / SLOW_SET);
+    const char* force = getenv("FLUERE_OWNER_CAP");  // tests: a small capacity sends records to the overflow list
+    cap_s = force ? (uint32_t)std::max(1, atoi(force)) : SLOW_SET / O * 5 / 4 + 32;
+    const uint64_t rec0 = (uint64_t)sets * O * owner_cap(sets, O);
+    while (cap_s > 8 && rec0 + (uint64_t)n_slow_sets * O * cap_s >= (1ull << 32)) cap_s /= 2;
+    if (rec0 + (uint64_t)n_slow_sets * O * cap_s >= (1ull << 32)) n_slow_sets = 0;
+}
+
+static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, uint64_t n, bool macs, bool slow) {
+    uint32_t ns = 0, cap_s = 0;
+    if (slow) slow_shape(n, sets, O, ns, cap_s);
+    const size_t all = sets + ns;
     return cells * (sizeof(Part) + (macs ? sizeof(uint4) : 0)) +
-           (sets * O * owner_cap(sets, O) + (size_t)grid * SPILL_WG + n) * spill_units(macs) * sizeof(Spill) +
-           sets * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * sets * sizeof(uint32_t) +
+           (sets * O * owner_cap(sets, O) + (size_t)ns * O * cap_s + (size_t)grid * SPILL_WG + n) * spill_units(macs) *
+               sizeof(Spill) +
+           all * sizeof(unsigned long long) + 2 * (size_t)(O + 1) * all * sizeof(uint32_t) +
            (size_t)grid * WGS_N * sizeof(unsigned long long) + 64 + (macs ? 16 : 0);
 }
 
@@ -3553,7 +3884,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         hot_shape(hb.b.n, grid, steps);
         maxn = std::max<uint64_t>(maxn, (uint64_t)grid * steps * BLOCK);
     }
-    const uint64_t slow_words = maxn + MB;
+    const uint64_t slow_words = 2 * maxn + MB;
     if (slow_words > c->d_slow_cap) {
         hipFree(c->d_slow);
         c->d_slow = nullptr;
@@ -3562,11 +3893,12 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     }
     a.slow = c->d_slow;
     a.slow_cnt = c->d_slow + maxn;
+    a.gen = c->d_slow + maxn + MB;
     a.slow_n = &c->d_glob->n_slow;
     a.slow_abl = getenv("FLUERE_SLOW_ABL") ? atoi(getenv("FLUERE_SLOW_ABL")) : 0;
     // k_slow when the last run had slow packets (a wrong guess costs only the
     // merge tail's slower path, or an empty launch)
-    static const int slow_env = getenv("FLUERE_SLOW_KERNEL") ? atoi(getenv("FLUERE_SLOW_KERNEL")) : -1;
+    const int slow_env = getenv("FLUERE_SLOW_KERNEL") ? atoi(getenv("FLUERE_SLOW_KERNEL")) : -1;  // tests: force it
     a.slow_kernel = slow_env >= 0 ? slow_env : (c->last_n_slow > 0 ? 1 : 0);
     if (getenv("FLUERE_DEBUG")) {
         if (!g_hot_dbg && hipMalloc(&g_hot_dbg, 4096 * 8 * 8) != hipSuccess) g_hot_dbg = nullptr;
@@ -3583,7 +3915,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = merge_owners(c);
-        need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n, c->use_mac));
+        need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n, c->use_mac, a.slow_kernel != 0));
     }
     if (need_max > c->d_stage_bytes) {
         hipFree(c->d_stage);
@@ -3605,26 +3937,36 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = merge_owners(c);
         a.slow_region = (uint32_t)(steps * BLOCK);
-        Stage& S = a.S;
-        // layout (16-byte aligned pieces): parts | owner segments | spill_raw | spill | base | off | soff
+        // k_slow's sets after the hot kernel's (only when it runs)
+        uint32_t n_slow_sets = 0, cap_s = 0;
+        if (a.slow_kernel) slow_shape(hb.b.n, sets, O, n_slow_sets, cap_s);
+        AggArgs ab = a;
+        ab.slow_kernel = n_slow_sets ? a.slow_kernel : 0;
+        const size_t all = sets + n_slow_sets;
+        Stage& S = ab.S;
+        // layout (16-byte aligned pieces): parts | owner segments (hot, k_slow) | spill_raw | spill | base | off | soff
         S.part = (Part*)c->d_stage;
         S.cap_o = owner_cap(sets, O);
+        S.cap_s = cap_s;
+        S.slow_rec0 = (unsigned long long)sets * O * S.cap_o;
         S.dspill = (Spill*)(S.part + cells);
-        S.spill_raw = S.dspill + sets * O * S.cap_o * spill_units(c->use_mac);
+        S.spill_raw = S.dspill + (sets * O * S.cap_o + (size_t)n_slow_sets * O * cap_s) * spill_units(c->use_mac);
         S.spill = S.spill_raw + (size_t)grid * SPILL_WG * spill_units(c->use_mac);
         S.spill_cap = hb.b.n;  // records (32 B, or 64 B with MACs)
         S.base = (unsigned long long*)(S.spill + hb.b.n * spill_units(c->use_mac));
-        S.off = (uint32_t*)(S.base + sets);
-        S.soff = S.off + (size_t)(O + 1) * sets;
-        S.wgs = (unsigned long long*)(((uintptr_t)(S.soff + (size_t)(O + 1) * sets) + 7) & ~(uintptr_t)7);
+        S.off = (uint32_t*)(S.base + all);
+        S.soff = S.off + (size_t)(O + 1) * all;
+        S.wgs = (unsigned long long*)(((uintptr_t)(S.soff + (size_t)(O + 1) * all) + 7) & ~(uintptr_t)7);
         S.partx = c->use_mac ? (uint4*)(((uintptr_t)(S.wgs + (size_t)grid * WGS_N) + 15) & ~(uintptr_t)15) : nullptr;
         S.n_wg = grid;
         S.W = W;
         S.O = O;
-        S.n_sets = (uint32_t)sets;
+        S.n_hot = (uint32_t)sets;
+        S.n_sets = (uint32_t)all;
         if (P.nb < PLAN_BATCHES) {
-            P.agg[P.nb] = a;
+            P.agg[P.nb] = ab;
             P.agg_grid[P.nb] = grid;
+            P.slow_grid[P.nb] = n_slow_sets;
             P.owners[P.nb] = O;
         }
         P.nb++;
@@ -3676,7 +4018,7 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
     hipStream_t s = c->stream;
     for (int i = 0; i < P.nb; i++) {
         const AggArgs& a = P.agg[i];
-        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 24, s));  // n_slow, n_spill, n_dspill (k_cleanup zeroed them for batch 0)
+        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 32, s));  // n_slow, n_spill, n_dspill, n_gen (k_cleanup zeroed them for batch 0)
         const unsigned grid = P.agg_grid[i];
         const void* fn = P.macs ? (const void*)k_parse_agg<0, true>
                          : P.abl == 1 ? (const void*)k_parse_agg<1, false>
@@ -3692,9 +4034,10 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, (i == 0 && P.nb > 1) ? c->evk_first : c->evk0,
                                     c->evk1, 0));
         const auto t1 = std::chrono::steady_clock::now();
+        // the slow list into k_slow's owner segments, before the merge reads them
+        if (a.slow_kernel) k_slow<<<P.slow_grid[i], SB, 0, s>>>(a);
         // at most one merge workgroup per CU, each taking owners in turn
-        k_merge_partials<<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow takes it)
-        if (a.slow_kernel) k_slow<<<(unsigned)c->n_cu * 8, SB, 0, s>>>(a);
+        k_merge_partials<<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow took it)
         if (hostprof) {
             const auto t2 = std::chrono::steady_clock::now();
             auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
@@ -3760,7 +4103,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
             hipMemsetParams mp{};
             mp.dst = &c->d_glob->n_slow;
             mp.elementSize = 4;
-            mp.width = 6;  // n_slow, n_spill, n_dspill
+            mp.width = 8;  // n_slow, n_spill, n_dspill, n_gen
             mp.height = 1;
             mp.pitch = 16;
             mp.value = 0;
@@ -3777,8 +4120,8 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
                                              : (const void*)k_parse_agg<0, false>;
         kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
         event(c->evk1);
+        if (P.agg[i].slow_kernel) kernel((const void*)k_slow, P.slow_grid[i], SB, a_agg[i]);
         kernel((const void*)k_merge_partials, std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, a_agg[i]);
-        if (P.agg[i].slow_kernel) kernel((const void*)k_slow, (unsigned)c->n_cu * 8, SB, a_agg[i]);
     }
     void* a_fin[] = {&P.fa};
     if (P.finalize) {
@@ -4364,6 +4707,80 @@ extern "C" int fluere_export_async(fluere_ctx* c, void* d_blocks, uint32_t n_own
     // merge's wait (a spare word of the pinned control copy)
     HIPCHECK(hipMemcpyAsync(&c->h_ctl->pad[0], c->d_nflows, 4, hipMemcpyDeviceToHost, s));
     c->async_nf = true;
+    return FLUERE_OK;
+}
+
+// ---- the compact wire encoding (include/fluere_gpu.h) -------------------------
+extern "C" uint64_t fluere_wire_bound(uint64_t cap, uint64_t cap_annex) {
+    return sizeof(fluere_shard_header) + ((4 * cap + 15) & ~15ull) + ((cap * WIRE_REC_MAX + 15) & ~15ull) +
+           cap_annex * sizeof(fluere_flow_annex);
+}
+
+extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uint64_t cap, uint64_t cap_annex,
+                                void* d_wire, unsigned long long* d_sizes) {
+    if (!c || !d_blocks || !d_wire || !d_sizes || !n_owners || !cap) return FLUERE_E_ARG;
+    if (cap * WIRE_REC_MAX >= (1ull << 32)) return FLUERE_E_ARG;  // u32 record offsets within a block
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t n = (uint64_t)n_owners * cap;
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                           (int)(n + 1), s);
+    const size_t need = 2 * (n + 1) * 8 + (size_t)(n_owners + 1) * 8 + ((tb + 255) & ~(size_t)255);
+    if (need > c->d_wire_tmp_bytes) {
+        hipFree(c->d_wire_tmp);
+        c->d_wire_tmp = nullptr;
+        c->d_wire_tmp_bytes = 0;
+        if (hipMalloc(&c->d_wire_tmp, need) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_wire_tmp_bytes = need;
+    }
+    WireArgs a{};
+    a.blocks = (const uint8_t*)d_blocks;
+    a.wwire = (uint8_t*)d_wire;
+    a.cap = cap;
+    a.cap_annex = cap_annex;
+    a.block_bytes = fluere_shard_block_bytes(cap, cap_annex);
+    a.n_blocks = n_owners;
+    char* t = (char*)c->d_wire_tmp;
+    void* tmp = t;
+    a.sz = (unsigned long long*)(t + ((tb + 255) & ~(size_t)255));
+    a.scan = a.sz + (n + 1);
+    a.woff = a.scan + (n + 1);
+    a.sizes = d_sizes;
+    k_wire_size<<<grid_for(n + 1, 256), 256, 0, s>>>(a);
+    HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.sz, a.scan, (int)(n + 1), s));
+    k_wire_offsets<<<1, 64, 0, s>>>(a);
+    k_wire_pack<<<grid_for(n, 256), 256, 0, s>>>(a);
+    const unsigned ax = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(64, cap_annex * 32 / 256));
+    k_wire_annex<<<dim3(ax, n_owners), 256, 0, s>>>(a, 0);
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_wire_unpack(fluere_ctx* c, const void* d_wire, uint32_t n_shards, const uint64_t* sizes,
+                                  uint64_t cap, uint64_t cap_annex, void* d_blocks) {
+    if (!c || !d_wire || !d_blocks || !sizes || !n_shards || n_shards > WIRE_MAX_BLOCKS || !cap) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    WireArgs a{};
+    a.wire = (const uint8_t*)d_wire;
+    a.wblocks = (uint8_t*)d_blocks;
+    a.cap = cap;
+    a.cap_annex = cap_annex;
+    a.block_bytes = fluere_shard_block_bytes(cap, cap_annex);
+    a.n_blocks = n_shards;
+    unsigned long long off = 0;
+    for (uint32_t b = 0; b < n_shards; b++) {
+        if (sizes[b] < sizeof(fluere_shard_header)) return FLUERE_E_ARG;
+        a.off_h[b] = off;
+        off += sizes[b];
+    }
+    a.off_h[n_shards] = off;
+    const uint64_t n = (uint64_t)n_shards * cap;
+    k_wire_unpack<<<grid_for(n, 256), 256, 0, s>>>(a);
+    const unsigned ax = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(64, cap_annex * 32 / 256));
+    k_wire_annex<<<dim3(ax, n_shards), 256, 0, s>>>(a, 1);
+    HIPCHECK(hipGetLastError());
     return FLUERE_OK;
 }
 

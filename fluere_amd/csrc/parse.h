@@ -125,6 +125,152 @@ __device__ __forceinline__ bool parse_fast(const Win& W, uint32_t L, PktInfo& o)
 }
 
 // ---------------------------------------------------------------------------
+// Middle path over a 128-byte register window (record bytes 0..127): the
+// classes the hot parser leaves to k_slow that still have every field inside
+// the window, parsed with selects instead of byte-serial reads:
+//   * IPv4 with options (ihl 6..15), any IP protocol;
+//   * IPv6 (no VXLAN prefix), any next header;
+//   * VXLAN: outer Ethernet / IPv4 (ihl 5) / VXLAN header (keys.rs:186-200,
+//     fluereflows.rs:100-110), inner Ethernet / IPv4 (ihl 5), any protocol.
+// It computes exactly what parse_general computes for these packets, and only
+// for valid ones: anything else (a drop, an empty UDP payload, a VXLAN prefix
+// elsewhere, other ethertypes) returns false and takes parse_general.  Every
+// byte it reads lies inside a span whose length it has checked, so bytes past
+// the caplen (the next record) never decide a result.
+// ---------------------------------------------------------------------------
+struct Win32 {
+    uint32_t w[32];
+    __device__ __forceinline__ uint32_t b(int k) const { return (w[k >> 2] >> (8 * (k & 3))) & 0xFF; }
+    __device__ __forceinline__ uint32_t be16(int k) const { return (b(k) << 8) | b(k + 1); }
+    __device__ __forceinline__ uint32_t be32(int k) const { return (be16(k) << 16) | be16(k + 2); }
+};
+
+// byte k (< 16) / big-endian pair at k of a 16-byte view held as 4 little-endian words
+__device__ __forceinline__ uint32_t view_b(const uint32_t (&v)[4], int k) { return (v[k >> 2] >> (8 * (k & 3))) & 0xFF; }
+__device__ __forceinline__ uint32_t view_be16(const uint32_t (&v)[4], int k) { return (view_b(v, k) << 8) | view_b(v, k + 1); }
+
+__device__ __forceinline__ bool parse_mid(const Win32& W, uint32_t L, PktInfo& o) {
+    constexpr int F = 16;
+    if (L < 34) return false;
+    const uint32_t et = W.be16(F + 12);
+    uint32_t v[4];  // the keyed L4 view: its first 16 bytes
+    uint32_t pll, proto, doct, rpkt, ttl, tosb, frame_off = 0;
+    uint32_t sip[4] = {0, 0, 0, 0}, dip[4] = {0, 0, 0, 0};
+    bool v6 = false;
+    if (et == 0x0800) {
+        const uint32_t ihl = W.b(F + 14) & 0x0F;
+        if (ihl < 5) return false;
+        const uint32_t h = 4 * ihl, tl = W.be16(F + 16), plen = tl > h ? tl - h : 0, Pl = L - 14;
+        const uint32_t pl0 = Pl <= h ? 0 : min(h + plen, Pl) - h;  // Ipv4Packet::payload() (v4_payload)
+        // L4 bytes 0..15 at record byte 30 + h = 50 + 4s (s option words): words 12 + s .. 16 + s, shifted
+        const uint32_t s = ihl - 5;
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = 0;
+#pragma unroll
+        for (uint32_t c = 0; c <= 10; c++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                v[j] = s == c ? __builtin_amdgcn_alignbit(W.w[13 + c + j], W.w[12 + c + j], 16) : v[j];
+        if (pl0 == 8) return false;  // empty "UDP" payload: EmptyPacket (keys.rs:182-184)
+        const bool vx = pl0 >= 16 && v[2] == 0x00000008u && v[3] == 0x00640000u;  // is_vxlan (keys.rs:188)
+        if (vx) {
+            if (ihl != 5) return false;
+            // inner Ethernet frame at frame byte 50, pl0 - 16 bytes long
+            const uint32_t inl = pl0 - 16;
+            if (inl < 14 || W.be16(F + 62) != 0x0800) return false;
+            const uint32_t P2 = inl - 14;
+            if (P2 < 20 || (W.b(F + 64) & 0x0F) != 5) return false;
+            const uint32_t tl2 = W.be16(F + 66), plen2 = tl2 > 20 ? tl2 - 20 : 0;
+            pll = P2 <= 20 ? 0 : min(20 + plen2, P2) - 20;
+            proto = W.b(F + 73);
+            ttl = W.b(F + 72);
+            tosb = W.b(F + 65);
+            sip[0] = W.be32(F + 76);
+            dip[0] = W.be32(F + 80);
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = W.w[25 + j];  // inner L4 at record byte 100
+            doct = 20 + plen2;  // v4_size
+            rpkt = tl2;
+            frame_off = 50;
+        } else {
+            pll = pl0;
+            proto = W.b(F + 23);
+            ttl = W.b(F + 22);
+            tosb = W.b(F + 15);
+            sip[0] = W.be32(F + 26);
+            dip[0] = W.be32(F + 30);
+            doct = h + plen;  // v4_size: 20 + options + (tl - h)
+            rpkt = tl;
+        }
+    } else if (et == 0x86DD) {
+        if (L < 54) return false;
+        const uint32_t plf = W.be16(F + 18), Pl = L - 14;
+        pll = Pl <= 40 ? 0 : min(40 + plf, Pl) - 40;  // v6_payload
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = __builtin_amdgcn_alignbit(W.w[18 + j], W.w[17 + j], 16);  // record byte 70
+        if (pll == 8) return false;
+        if (pll >= 16 && v[2] == 0x00000008u && v[3] == 0x00640000u) return false;
+        v6 = true;
+        proto = W.b(F + 20);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            sip[k] = W.be32(F + 22 + 4 * k);
+            dip[k] = W.be32(F + 38 + 4 * k);
+        }
+        doct = 40 + plf;
+        rpkt = plf;
+        ttl = 0;
+        tosb = (((W.b(F + 14) & 0x0F) << 4) | (W.b(F + 15) >> 4));  // traffic class
+    } else {
+        return false;
+    }
+    // parse_ports (ports.rs:7-58) over the L4 view
+    const uint32_t p01 = view_be16(v, 0), p23 = view_be16(v, 2);
+    uint32_t sp = 0, dp = 0;
+    switch (proto) {
+    case 0: case 1: case 2: case 4: case 47: case 50: case 51: case 58: break;
+    case 6: if (pll < 20) return false; sp = p01; dp = p23; break;
+    case 17: if (pll < 8) return false; sp = p01; dp = p23; break;
+    case 53: if (pll >= 8) { sp = p01; dp = p23; } else { sp = dp = 53; } break;
+    default:
+        if (pll >= 4) {
+            if (pll < 8 && proto == 0x36) { sp = view_b(v, 0); dp = view_b(v, 1); }
+            else { sp = p01; dp = p23; }
+        }
+    }
+    o.kst = ST_OK;
+    o.fst = ST_OK;
+    o.raw = 0;
+    o.frame_off = frame_off;
+    o.v6 = v6 ? 1 : 0;
+    o.rv6 = o.v6;
+    o.kproto = (uint8_t)proto;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        o.sip[k] = o.rsip[k] = sip[k];
+        o.dip[k] = o.rdip[k] = dip[k];
+    }
+    o.ksp = (uint16_t)sp;
+    o.kdp = (uint16_t)dp;
+    if (!v6 && proto == 47 && pll >= 4) { o.ksp = (uint16_t)p23; o.kdp = 0; }                        // keys.rs:367-379
+    if (v6 && proto == 58 && pll >= 4) { o.ksp = (uint16_t)view_b(v, 0); o.kdp = (uint16_t)view_b(v, 1); }  // keys.rs:403-409
+    o.doctets = doct;
+    o.rttl = (uint8_t)ttl;
+    if (!v6 && proto == 17 && pll >= 8 && (p23 == 53 || p01 == 53)) {  // DNS (fluereflows.rs:255-291)
+        o.rsp = (uint16_t)p01; o.rdp = (uint16_t)p23;
+        o.rpkt = pll;
+        o.rprot = 17; o.rtos = 0; o.tflags = 0;
+        return true;
+    }
+    o.rsp = (uint16_t)sp; o.rdp = (uint16_t)dp;
+    o.rpkt = rpkt;
+    o.rprot = (uint8_t)proto;
+    o.rtos = dscp_to_tos(tosb >> 2);
+    o.tflags = (proto == 6 && pll >= 20) ? (uint8_t)view_b(v, 13) : 0;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // General path: byte reads from global memory.  d = frame start, L = caplen.
 // ---------------------------------------------------------------------------
 // d: the frame in global memory.  s / sn: an optional staged copy of its

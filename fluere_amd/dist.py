@@ -36,6 +36,10 @@ from ._lib import RECORD_DTYPE, Stats, check
 
 NONE64 = (1 << 64) - 1
 SPAN_BIAS = 1 << 62  # fluere_export_async d_info[4] = SPAN_BIAS - earliest valid time
+# wide blocks of at least this many bytes travel in the compact wire encoding
+# (fluere_wire_pack / fluere_wire_unpack): variable-length summaries, split
+# sizes exact per owner; smaller ones go as equal wide blocks (one fewer pass)
+WIRE_MIN_BLOCK = 1 << 20
 
 
 def shard_range(n_packets: int, rank: int, world: int):
@@ -79,6 +83,26 @@ def exchange_blocks(send, recv, group=None):
         recv.copy_(r_h)
     else:
         dist.all_to_all_single(recv, send, group=group)
+
+
+def exchange_known(send, send_counts, recv_counts, group=None):
+    """All-to-all of byte runs whose sizes every rank already knows (the
+    gathered wire sizes): send_counts[o] bytes for rank o, recv_counts[s]
+    bytes from rank s, both in rank order.  Returns the received bytes."""
+    import torch
+    import torch.distributed as dist
+    ins = [int(x) for x in send_counts]
+    outs = [int(x) for x in recv_counts]
+    n_out = sum(outs)
+    recv = torch.empty(max(1, n_out), dtype=torch.uint8, device=send.device)
+    if dist.get_backend(group) == "gloo":
+        s_h = send[: sum(ins)].cpu() if send.is_cuda else send[: sum(ins)]
+        r_h = torch.empty(n_out, dtype=torch.uint8)
+        dist.all_to_all_single(r_h, s_h, outs, ins, group=group)
+        recv[:n_out].copy_(r_h)
+    else:
+        dist.all_to_all_single(recv[:n_out], send[: sum(ins)], outs, ins, group=group)
+    return recv
 
 
 def exchange_var(send, send_counts, elem: int, group=None):
@@ -146,6 +170,28 @@ class _DistComm:
         self._after()
         return np.asarray(x.tolist(), dtype=np.int64)
 
+    def allgather_dev(self, tensors):
+        """Every rank's device vector -> (world, k) on the host (one read)."""
+        import torch
+        import torch.distributed as dist
+        (t,) = tensors
+        self._before()
+        x = t.cpu() if self.gloo else t
+        out = torch.empty((self.world, x.numel()), dtype=x.dtype, device=x.device)
+        if self.gloo:
+            dist.all_gather(list(out.unbind(0)), x, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, x, group=self.group)
+        self._after()
+        return np.asarray(out.tolist(), dtype=np.int64)
+
+    def all_to_all_known(self, sends, send_counts, recv_counts):
+        (s,), (sc,), (rc,) = sends, send_counts, recv_counts
+        self._before()
+        r = exchange_known(s, sc, rc, self.group)
+        self._after()
+        return [r]
+
     def allreduce_max(self, arrays):
         import torch
         import torch.distributed as dist
@@ -194,6 +240,14 @@ class _LocalComm:
     def allreduce_max_dev(self, tensors):
         self._sync()
         return np.max(np.stack([np.asarray(t.tolist(), dtype=np.int64) for t in tensors]), axis=0)
+
+    def allgather_dev(self, tensors):
+        self._sync()
+        return np.stack([np.asarray(t.tolist(), dtype=np.int64) for t in tensors])
+
+    def all_to_all_known(self, sends, send_counts, recv_counts):
+        recvs, _ = self.all_to_all_v(sends, send_counts, 1)
+        return recvs
 
     def allreduce_max(self, arrays):
         return np.max(np.stack([np.asarray(a, dtype=np.int64) for a in arrays]), axis=0)
@@ -346,12 +400,16 @@ def _sweep_compose(comm, ctxs, rank_first, counts, sends):
 
 
 class _StepState:
-    def __init__(self, cap, cap_annex):
+    def __init__(self, cap, cap_annex, wire=None):
         self.cap, self.cap_annex = max(1, int(cap)), max(1, int(cap_annex))
         self.sends = self.recvs = None
         self.blk = 0
         self.infos = None
-        self.bytes_sent = 0  # per local context, last step: the blocks' bytes for other ranks
+        self.wsends = None
+        self.wbound = 0
+        self.wire = wire  # None: by block size (WIRE_MIN_BLOCK); True / False: always / never
+        self.bytes_sent = 0  # per local context, last step: the bytes it sent to other ranks
+        self.wire_used = False
 
 
 def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
@@ -364,21 +422,35 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
     W = comm.world
     for c in ctxs:
         c.parse_aggregate()
-    if S.infos is None or len(S.infos) != len(ctxs):
-        S.infos = [torch.zeros(6, dtype=torch.int64, device="cuda") for _ in ctxs]
     annexes = expiry = False
     timeout_us = int(ctxs[0].timeout_ms) * 1000
+    sizes = None  # wire: (world, W) bytes of every rank's block for every owner
     while True:
         blk = int(L.fluere_shard_block_bytes(S.cap, S.cap_annex))
+        wire = (blk >= WIRE_MIN_BLOCK) if S.wire is None else bool(S.wire)  # (the same on every rank)
         if S.sends is None or S.blk != blk or len(S.sends) != len(ctxs):
             S.sends = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in ctxs]
             S.recvs = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in ctxs]
             S.blk = blk
+        if wire:
+            wb = int(L.fluere_wire_bound(S.cap, S.cap_annex))
+            if S.wsends is None or S.wbound != wb or len(S.wsends) != len(ctxs):
+                S.wsends = [torch.empty(W * wb, dtype=torch.uint8, device="cuda") for _ in ctxs]
+                S.wbound = wb
+        nk = 6 + (W if wire else 0)
+        if S.infos is None or len(S.infos) != len(ctxs) or S.infos[0].numel() != nk:
+            S.infos = [torch.zeros(nk, dtype=torch.int64, device="cuda") for _ in ctxs]
         if not annexes:
-            for c, rk, s, info in zip(ctxs, comm.ranks, S.sends, S.infos):
+            for c, rk, s, info, ws in zip(ctxs, comm.ranks, S.sends, S.infos, S.wsends if wire else S.sends):
                 check(L.fluere_export_async(c._h, s.data_ptr(), W, rk, S.cap, S.cap_annex, info.data_ptr()),
                       "fluere_export_async")
-            n0, n1, n_cplx, _, span0, span1 = (int(x) for x in comm.allreduce_max_dev(S.infos))
+                if wire:  # the wire sizes ride in the same gathered vector
+                    check(L.fluere_wire_pack(c._h, s.data_ptr(), W, S.cap, S.cap_annex, ws.data_ptr(),
+                                             info.data_ptr() + 48), "fluere_wire_pack")
+            g = comm.allgather_dev(S.infos)
+            n0, n1, n_cplx = (int(x) for x in g[:, :3].max(axis=0))
+            span0, span1 = int(g[:, 4].max()), int(g[:, 5].max())
+            sizes = g[:, 6:6 + W] if wire else None
             expiry = span0 > 0 and span1 - (SPAN_BIAS - span0) >= timeout_us
             if n_cplx and not expiry:
                 annexes = True  # some rank has order-dependent flows: export with annexes
@@ -392,14 +464,30 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
                                              ctypes.byref(need_a)), "fluere_export_device")
                 needs.append(np.array([need.value, need_a.value], dtype=np.int64))
             n0, n1 = (int(x) for x in comm.allreduce_max(needs))
+            if wire and n0 <= S.cap and n1 <= S.cap_annex:
+                for c, s, ws, info in zip(ctxs, S.sends, S.wsends, S.infos):
+                    check(L.fluere_wire_pack(c._h, s.data_ptr(), W, S.cap, S.cap_annex, ws.data_ptr(),
+                                             info.data_ptr() + 48), "fluere_wire_pack")
+                sizes = comm.allgather_dev(S.infos)[:, 6:6 + W]
         if n0 <= S.cap and n1 <= S.cap_annex:
             break
         # a shard had more flows for some owner: grow the blocks, export again
         S.cap = _pow2_at_least(n0, S.cap)
         S.cap_annex = _pow2_at_least(n1, S.cap_annex)
-    S.bytes_sent = (W - 1) * blk
     packed = _sweep_pack(comm, ctxs) if expiry else None
-    comm.all_to_all_equal(S.sends, S.recvs)
+    S.wire_used = wire
+    if wire:
+        sizes = np.asarray(sizes, dtype=np.int64)  # sizes[r][o]: rank r's block for owner o
+        rks = comm.ranks
+        wrecv = comm.all_to_all_known(S.wsends, [sizes[rk] for rk in rks], [sizes[:, rk] for rk in rks])
+        for c, rk, wr, r in zip(ctxs, rks, wrecv, S.recvs):
+            rs = np.ascontiguousarray(sizes[:, rk].astype(np.uint64))
+            check(L.fluere_wire_unpack(c._h, wr.data_ptr(), W, _arr(rs), S.cap, S.cap_annex, r.data_ptr()),
+                  "fluere_wire_unpack")
+        S.bytes_sent = int(sizes[rks[0]].sum() - sizes[rks[0], rks[0]])
+    else:
+        S.bytes_sent = (W - 1) * blk
+        comm.all_to_all_equal(S.sends, S.recvs)
     stats, rcs = [], []
     for c, r in zip(ctxs, S.recvs):
         st = Stats()
@@ -433,9 +521,9 @@ class ShardExchange:
     the collectives after the export without host waits; a context on a
     stream of its own is synchronised around every collective instead."""
 
-    def __init__(self, ctx, cap: int = 64, cap_annex: int = 16, group=None):
+    def __init__(self, ctx, cap: int = 64, cap_annex: int = 16, group=None, wire=None):
         self.ctx, self.group = ctx, group
-        self._S = _StepState(cap, cap_annex)
+        self._S = _StepState(cap, cap_annex, wire)
         self._comm = None
         self._rank_first = None
 
@@ -451,6 +539,11 @@ class ShardExchange:
     def bytes_sent(self):
         """Bytes this rank's last step sent to other ranks in the merge's all-to-all."""
         return self._S.bytes_sent
+
+    @property
+    def wire_used(self):
+        """The last step moved the compact wire encoding (else equal wide blocks)."""
+        return self._S.wire_used
 
     def _rank_first_fn(self):
         if self._rank_first is None:
@@ -503,9 +596,9 @@ class LogicalShards:
     with every collective done by device copies (SURVEY.md section 8e "testing
     without 8 GPUs"): contexts[r] holds packets [first_r, first_r + n_r)."""
 
-    def __init__(self, contexts, cap: int = 1024, cap_annex: int = 256):
+    def __init__(self, contexts, cap: int = 1024, cap_annex: int = 256, wire=None):
         self.ctxs = contexts
-        self._S = _StepState(cap, cap_annex)
+        self._S = _StepState(cap, cap_annex, wire)
         self._comm = _LocalComm(len(contexts))
 
     @property
@@ -515,6 +608,15 @@ class LogicalShards:
     @property
     def cap_annex(self):
         return self._S.cap_annex
+
+    @property
+    def bytes_sent(self):
+        """Bytes shard 0 sent to the other shards in the last step's all-to-all."""
+        return self._S.bytes_sent
+
+    @property
+    def wire_used(self):
+        return self._S.wire_used
 
     def _rank_first(self):
         first = [int(getattr(c, "index_base", 0)) for c in self.ctxs]

@@ -292,6 +292,26 @@ int fluere_export_async(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint
 int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
                           uint64_t cap_annex, fluere_stats* stats);
 
+/* The compact wire encoding of the blocks (what the all-to-all moves): each
+ * summary as a variable-length record that leaves out absent and zero fields
+ * (an IPv4 5-tuple key in 12 bytes; no seed for a flow without a creating
+ * packet; only the non-zero flag counts), behind a u32 offset table; annexes
+ * verbatim.  A flow of the C4 recipe takes ~90-110 bytes instead of 256.
+ * fluere_wire_bound: the largest wire block of one owner.
+ * fluere_wire_pack (exporting side, after the export, enqueued on the context
+ * stream): the n_owners blocks at d_blocks -> their wire blocks, contiguous in
+ * owner order, at d_wire (n_owners * fluere_wire_bound bytes); d_sizes (device,
+ * n_owners x uint64) receives each wire block's bytes -- the all-to-all's split
+ * sizes.  fluere_wire_unpack (owner side, before fluere_merge_gathered): the
+ * n_shards (<= 64) received wire blocks, contiguous in shard order with
+ * sizes[s] (host) bytes each, -> the wide blocks at d_blocks (n_shards *
+ * fluere_shard_block_bytes), every summary at its exported position. */
+uint64_t fluere_wire_bound(uint64_t cap, uint64_t cap_annex);
+int fluere_wire_pack(fluere_ctx* ctx, const void* d_blocks, uint32_t n_owners, uint64_t cap, uint64_t cap_annex,
+                     void* d_wire, unsigned long long* d_sizes);
+int fluere_wire_unpack(fluere_ctx* ctx, const void* d_wire, uint32_t n_shards, const uint64_t* sizes, uint64_t cap,
+                       uint64_t cap_annex, void* d_blocks);
+
 /* ---- the hard-timeout sweep across shards (offline_fluereflows.rs:103-119,
  * 161-175): an expiry entry pushed at a flow's creation fires at the first
  * processed packet of the WHOLE capture with t >= exp, so shards are coupled.

@@ -112,7 +112,12 @@ def _var_worker(rank, world, port, q):
         comm.same_stream = True
         g = comm.allgather([np.array([rank, 10 * rank], dtype=np.int64)])
         m = comm.allreduce_max([np.array([rank, -rank], dtype=np.int64)])
-        q.put((rank, recv[:n].numpy().tobytes(), [int(x) for x in rc], g.tolist(), m.tolist()))
+        # the wire path: sizes every rank knows from one gather of a vector
+        gd = comm.allgather_dev([torch.tensor([rank, 7] + [int(c) * 3 for c in counts], dtype=torch.int64)])
+        sizes = gd[:, 2:]
+        (rk,) = comm.all_to_all_known([send], [sizes[rank]], [sizes[:, rank]])
+        q.put((rank, recv[:n].numpy().tobytes(), [int(x) for x in rc], g.tolist(), m.tolist(), gd.tolist(),
+               rk[:int(sizes[:, rank].sum())].numpy().tobytes()))
     finally:
         dist.destroy_process_group()
 
@@ -130,12 +135,14 @@ def test_exchange_var_gloo(world):
         p.join(timeout=120)
         assert p.exitcode == 0
     for o in range(world):
-        raw, rc, g, m = got[o]
+        raw, rc, g, m, gd, rk = got[o]
         assert rc == [(r + 1) * (o + 1) for r in range(world)]
         want = b"".join(bytes([16 * r + o]) * (3 * (r + 1) * (o + 1)) for r in range(world))
         assert raw == want
+        assert rk == want  # exchange_known with the gathered sizes moves the same bytes
         assert g == [[r, 10 * r] for r in range(world)]
         assert m == [world - 1, 0]
+        assert gd == [[r, 7] + [3 * (r + 1) * (x + 1) for x in range(world)] for r in range(world)]
 
 
 

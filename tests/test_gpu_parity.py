@@ -56,6 +56,60 @@ def test_parse_batch_matches_oracle(gpu, name, general):
     _check_meta(got, pyoracle.parse_batch(data), name)
 
 
+def _mutated_pcap(data, seed, n_mut=3):
+    """Every record of a classic pcap with a few header bytes changed (frame
+    bytes 12..119: ethertypes, IHL, lengths, protocols, ports, the VXLAN
+    header) and some caplens cut short: the parser classes' boundaries."""
+    rng = np.random.default_rng(seed)
+    vals = [0, 1, 4, 5, 6, 8, 0x11, 0x2F, 0x35, 0x3A, 0x45, 0x46, 0x4F, 0x64, 0x86, 0xDD, 0xFF]
+    out = [data[:24]]
+    off = 24
+    while off + 16 <= len(data):
+        incl = int.from_bytes(data[off + 8:off + 12], "little")
+        hdr = bytearray(data[off:off + 16])
+        fr = bytearray(data[off + 16:off + 16 + incl])
+        for _ in range(int(rng.integers(0, n_mut + 1))):
+            k = int(rng.integers(12, 120))
+            if k < len(fr):
+                fr[k] = vals[int(rng.integers(0, len(vals)))] if rng.random() < 0.8 else int(rng.integers(0, 256))
+        if rng.random() < 0.1:  # a shorter caplen (orig_len stays)
+            fr = fr[:int(rng.integers(0, len(fr) + 1))]
+            hdr[8:12] = len(fr).to_bytes(4, "little")
+        out += [bytes(hdr), bytes(fr)]
+        off += 16 + incl
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_parse_middle_path_matches_oracle(gpu, seed):
+    """parse_mid (IPv6, IPv4 options, VXLAN in a 128-byte register window) and
+    its hand-off to the general parser, on the general-parser classes with
+    random header bytes changed and caplens cut: the production sequence
+    (fast, middle, general) and the general parser alone both equal the oracle."""
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_SLOW, 20_000, 500, 0xF10E0100 + seed))
+    data = _mutated_pcap(data, seed)
+    want = pyoracle.parse_batch(data)
+    with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+        ctx.add_host_pcap(data)
+        for general in (False, True):
+            _check_meta(ctx.parse_batch(general_only=general), want, f"mutated seed {seed} general={general}")
+
+
+@pytest.mark.parametrize("name", ["slow_small", "slow_mac"])
+@pytest.mark.parametrize("cap", ["3", ""])
+def test_slow_kernel_first_run(gpu, name, cap, monkeypatch):
+    """k_slow forced on the first run (FLUERE_SLOW_KERNEL=1); with owner
+    segments of 3 records nearly every slow record goes to the overflow list."""
+    monkeypatch.setenv("FLUERE_SLOW_KERNEL", "1")
+    if cap:
+        monkeypatch.setenv("FLUERE_OWNER_CAP", cap)
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = _mutated_pcap(fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed)), 7, 1)
+    want = pyoracle.offline(data, use_mac=use_mac)
+    csv, ne, st = _gpu_csv(data, use_mac=use_mac, max_flows=max(1 << 16, 4 * f))
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
+
+
 @pytest.mark.parametrize("name", sorted(manifest()))
 def test_fixture_csv_matches_golden(gpu, name):
     m = manifest()[name]
@@ -113,8 +167,9 @@ def test_spill_overflow_list(gpu, name, monkeypatch):
 @pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small"])
 def test_second_run_takes_slow_kernel(gpu, name):
     """The first run of a context leaves the slow list to the merge kernel's
-    tail; a run after one that had slow packets gives it to k_slow (inlined
-    general parser, per-id LDS pre-aggregation).  Both equal the oracle."""
+    tail; a run after one that had slow packets gives it to k_slow (register
+    parsers, spill records into the merge owners' segments; the general
+    parser's packets to the merge tail).  Both equal the oracle."""
     kind, n, f, seed, use_mac = SYNTH[name]
     data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
     want = pyoracle.offline(data, use_mac=use_mac)
@@ -184,7 +239,7 @@ def test_rerun_is_idempotent(gpu):
     assert outs[0] == outs[1] == outs[2]
 
 
-def _logical_shards(cfg, G, use_mac=False, max_flows=1 << 16, cap=1024, cap_annex=256, timeout_ms=600000):
+def _logical_shards(cfg, G, use_mac=False, max_flows=1 << 16, cap=1024, cap_annex=256, timeout_ms=600000, wire=None):
     """G shards of one synthetic capture on one device through the multi-GPU
     export / owner merge (the all-to-all done by device copies)."""
     ctxs = []
@@ -196,32 +251,36 @@ def _logical_shards(cfg, G, use_mac=False, max_flows=1 << 16, cap=1024, cap_anne
             ctx.add_device_batch(b, nbytes, o, nb)
         ctxs.append(ctx)
     torch.cuda.synchronize()
-    ls = fluere_amd.dist.LogicalShards(ctxs, cap, cap_annex)
+    ls = fluere_amd.dist.LogicalShards(ctxs, cap, cap_annex, wire=wire)
     return ls, ctxs
 
 
+@pytest.mark.parametrize("wire", [False, True])
 @pytest.mark.parametrize("G", [1, 2, 4])
-def test_sharded_merge_equals_single(gpu, G):
+def test_sharded_merge_equals_single(gpu, G, wire):
     """G logical shards on one device through the export / all-to-all / owner
-    merge path: every record equals the oracle's on the whole capture."""
+    merge path (equal wide blocks, or the compact wire encoding): every record
+    equals the oracle's on the whole capture."""
     cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
-    ls, ctxs = _logical_shards(cfg, G, cap=64, cap_annex=8)  # small blocks: the capacity retry runs
+    ls, ctxs = _logical_shards(cfg, G, cap=64, cap_annex=8, wire=wire)  # small blocks: the capacity retry runs
     ls.run()
+    assert ls.wire_used == wire
     recs, ne = ls.records()
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"sharded G={G}")
     for c in ctxs:
         c.close()
 
 
+@pytest.mark.parametrize("wire", [False, True])
 @pytest.mark.parametrize("G", [2, 3, 8])
-def test_sharded_realistic_tcp(gpu, G):
+def test_sharded_realistic_tcp(gpu, G, wire):
     """Realistic TCP split into shards: FIN handshakes, SYN-gated peers,
     reopened keys and elephants cross shard boundaries; the owners compose the
     shards' pieces of the state machine (annexes) in shard order."""
     cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 400_000, 4_000, 0xF10E0017)
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
-    ls, ctxs = _logical_shards(cfg, G, max_flows=1 << 18)
+    ls, ctxs = _logical_shards(cfg, G, max_flows=1 << 18, wire=wire)
     st = ls.run()
     assert sum(x["complex_flows"] for x in st) > 0
     recs, ne = ls.records()
@@ -268,7 +327,7 @@ SWEEP_SHARDS = {
 
 @pytest.mark.parametrize("G", [2, 3, 8])
 @pytest.mark.parametrize("name", sorted(SWEEP_SHARDS))
-def test_sharded_expiry_sweep(gpu, name, G):
+def test_sharded_expiry_sweep(gpu, name, G):  # (1024-summary blocks of 256 KiB: the wide exchange)
     """A capture whose span reaches the timeout over G logical shards: the
     shards ship their packets to the keys' owners, compute sweep points over
     their own processed packets (later shards answer the rest), and the owners
@@ -620,6 +679,11 @@ def test_c4_recipe_8_shards_1m_flows(gpu):
     recs, ne = ls.records()
     for c in ctxs:
         c.close()
+    # the compact wire encoding (32 MiB blocks): at least 2.5x fewer bytes than
+    # the equal wide blocks would move
+    wide = 7 * _lib.lib().fluere_shard_block_bytes(ls.cap, ls.cap_annex)
+    print(f"c4 recipe: shard 0 sent {ls.bytes_sent} B (wide blocks: {wide} B, {wide / ls.bytes_sent:.2f}x)")
+    assert ls.wire_used and ls.bytes_sent * 2.5 <= wide
     assert len(recs) == 1_000_000
     assert int(recs["d_pkts"].sum()) == cfg.n_packets
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
@@ -634,6 +698,9 @@ EXCHANGE_CASES = {
     # span >= timeout: the sweep composition over the process group
     "tcp_sweep": (_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037, 10),
     "backtime_sweep": (_lib.SYNTH_TCP_BACKTIME, 300_000, 3_000, 0xF10E0047, 10),
+    # the compact wire encoding (variable-size all-to-all, gathered split sizes)
+    "tcp_wire": (_lib.SYNTH_TCP, 300_000, 3_000, 0xF10E0037, 600000),
+    "udp_wire": (_lib.SYNTH_UDP64, 400_000, 2_000, 0xF10E0038, 600000),
 }
 
 
@@ -655,7 +722,7 @@ def _shard_exchange_rank(rank, world, port, q, case):
         for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, first, n):
             ctx.add_device_batch(b, nbytes, o, nb)
         torch.cuda.synchronize()
-        ex = fluere_amd.dist.ShardExchange(ctx, cap=128, cap_annex=16)
+        ex = fluere_amd.dist.ShardExchange(ctx, cap=128, cap_annex=16, wire=case.endswith("_wire") or None)
         for _ in range(2):  # the first step grows the blocks, the second reuses them
             ex.step()
         got = ex.gather_records()
