@@ -164,6 +164,8 @@ def lib() -> ctypes.CDLL:
         "fluere_live_close": (I, [P]),
         "fluere_live_batch": (I, [P, P, U64, I, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64),
                                   ctypes.POINTER(I)]),
+        "fluere_live_batch_indexed": (I, [P, P, U64, P, U64, I, ctypes.POINTER(P), ctypes.POINTER(U64),
+                                          ctypes.POINTER(U64), ctypes.POINTER(I)]),
         "fluere_live_finish": (I, [P, I, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "fluere_shard_block_bytes": (U64, [U64, U64]),
         "fluere_export_device": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.POINTER(U64),

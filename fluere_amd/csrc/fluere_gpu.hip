@@ -125,6 +125,53 @@ struct Stage {
 // per-workgroup statistics: valid, dropped, LDS-table misses, tmin, tmax, cycles total / flush / wave wait
 constexpr int WGS_N = 8;
 
+// IPv6 address ids (k_slow): each distinct address of a pass gets an id from
+// a write-once chain of three 64-bit levels (the protocol of flow_table.h's
+// dictionary): A[addr words 0,1] -> sa, B[sa << 32 | word 2] -> sb,
+// C[sb << 32 | word 3] -> id; the level-C inserter writes addr_of[id].  An
+// IPv6 5-tuple then travels like an IPv4 one, as three words (id of the lower
+// address, id of the higher, ports) with bit 0 of its tag set, through the
+// merge owners' segments and LDS tables; the owner rebuilds the full key once
+// per flow (a later launch reads addr_of).  Cleared before every pass that
+// uses it; a full chain falls back to the dictionary walk per packet.
+struct V6Map {
+    unsigned long long* tab[3];  // (C + 1) keys each (slot C: the word EMPTY)
+    uint4* addr_of;              // [C + 1]
+    uint32_t C;                  // power of two; 0: no map
+};
+constexpr uint32_t V6_TAG = 1u;  // tag bit 0: the key words are (address id, address id, ports)
+
+__device__ __forceinline__ uint32_t v6_level(unsigned long long* keys, uint32_t C, uint64_t w, bool& fresh) {
+    fresh = false;
+    if (w == EMPTY) return C;
+    uint32_t h = (uint32_t)mix64(w) & (C - 1);
+    for (int p = 0; p < 64; p++) {
+        const unsigned long long k = keys[h];  // (a stale load shows EMPTY for a filled slot, never another key)
+        if (k == w) return h;
+        if (k == EMPTY) {
+            const unsigned long long old = atomicCAS(&keys[h], EMPTY, (unsigned long long)w);
+            if (old == EMPTY) { fresh = true; return h; }
+            if (old == w) return h;
+        }
+        h = (h + 1) & (C - 1);
+    }
+    return FAIL;
+}
+// ids of two addresses, their levels interleaved (two lookups per round trip)
+__device__ __forceinline__ void v6_ids(const V6Map& M, const uint32_t* a, const uint32_t* b, uint32_t& ia, uint32_t& ib) {
+    bool fa, fb;
+    uint32_t sa = v6_level(M.tab[0], M.C, ((uint64_t)a[0] << 32) | a[1], fa);
+    uint32_t sb = v6_level(M.tab[0], M.C, ((uint64_t)b[0] << 32) | b[1], fb);
+    if (sa != FAIL) sa = v6_level(M.tab[1], M.C, ((uint64_t)sa << 32) | a[2], fa);
+    if (sb != FAIL) sb = v6_level(M.tab[1], M.C, ((uint64_t)sb << 32) | b[2], fb);
+    if (sa != FAIL) sa = v6_level(M.tab[2], M.C, ((uint64_t)sa << 32) | a[3], fa);
+    if (sb != FAIL) sb = v6_level(M.tab[2], M.C, ((uint64_t)sb << 32) | b[3], fb);
+    if (sa != FAIL && fa) M.addr_of[sa] = make_uint4(a[0], a[1], a[2], a[3]);
+    if (sb != FAIL && fb) M.addr_of[sb] = make_uint4(b[0], b[1], b[2], b[3]);
+    ia = sa;
+    ib = sb;
+}
+
 struct AggArgs {
     Batch B;
     TableSet T;
@@ -134,11 +181,13 @@ struct AggArgs {
     uint32_t* slow;            // packets (batch-local indices) the hot parser left to the general parser:
                                // workgroup b's in slow[b * slow_region, + slow_cnt[b])
     unsigned long long* slow_n;  // their total (the merge's "any slow packet" test)
+    V6Map v6;                  // k_slow's IPv6 address ids (C = 0: none)
     uint32_t* gen;             // k_slow: the slow packets parse_fast / parse_mid leave to the general parser
                                // (batch-local indices, Glob::n_gen of them; the merge tail takes them)
     uint32_t* slow_cnt;
     uint32_t slow_region;      // packets a hot workgroup can see (its steps x BLOCK)
-    int slow_abl;              // diagnostics only (FLUERE_SLOW_ABL, wrong results): 1 no dictionary, 2 no parse
+    int slow_abl;              // diagnostics only (FLUERE_SLOW_ABL, wrong results): 1 no dictionary, 2 no parse,
+                               // 3 no spill records (k_slow)
     int slow_kernel;           // the slow list is k_slow's (launched before the merge), not the merge tail's
     int macs;
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
@@ -1124,11 +1173,27 @@ __device__ __forceinline__ void pkt_to_part(const PktInfo& pi, uint8_t dir, unsi
     f.la = gi + 1;
 }
 
-// Dense id of a staged key (flow_table.h dictionary; tag 0xFF: the key is the id).
-__device__ __forceinline__ uint32_t staged_id(const TableSet& T, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag,
-                                              uint32_t* slots) {
-    if (tag == 0xFF000000u) return k0;
+// The canonical key of an IPv6 5-tuple staged as address ids (V6Map).
+__device__ __forceinline__ void v6_ckey(const V6Map& M, uint32_t ia, uint32_t ib, uint32_t ports, uint32_t tag, CKey& k) {
+    const uint4 a = M.addr_of[ia], b = M.addr_of[ib];
+#pragma unroll
+    for (int j = 0; j < 14; j++) k.w[j] = 0;
+    k.w[0] = a.x; k.w[1] = a.y; k.w[2] = a.z; k.w[3] = a.w;
+    k.w[4] = b.x; k.w[5] = b.y; k.w[6] = b.z; k.w[7] = b.w;
+    k.w[8] = ports;
+    k.w[9] = (1u << 8) | (tag >> 24);
+}
+
+// Dense id of a staged key (flow_table.h dictionary; tag 0xFF: the key is the
+// id; tag bit 0: an IPv6 5-tuple as address ids).
+__device__ __forceinline__ uint32_t staged_id(const TableSet& T, const V6Map& M, uint32_t k0, uint32_t k1, uint32_t k2,
+                                              uint32_t tag, uint32_t* slots) {
     CKey k;
+    if (tag & V6_TAG) {
+        v6_ckey(M, k0, k1, k2, tag, k);
+        return dense_of_key(T, k, true, slots, nullptr);
+    }
+    if (tag == 0xFF000000u) return k0;
 #pragma unroll
     for (int j = 0; j < 14; j++) k.w[j] = 0;
     k.w[0] = k0;
@@ -1503,7 +1568,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                         mac_ckey(k0, k1, k2, tag, x0, x1, x2, ck);
                         d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
                     } else {
-                        d = staged_id(a.T, k0, k1, k2, tag, a.A.slots);
+                        d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
                     }
                     if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
                 }
@@ -1527,7 +1592,11 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         bool claimed = false, wait = false;
         unsigned long long* val = nullptr;
         if (have) {
-            if (tag == 0xFF000000u) {
+            if (kk.w & V6_TAG) {  // an IPv6 5-tuple from k_slow: the full key from the address ids
+                CKey ck;
+                v6_ckey(a.v6, kk.x, kk.y, kk.z, tag, ck);
+                d = dense_of_key(a.T, ck, true, a.A.slots, &a.g->generic_used);
+            } else if (tag == 0xFF000000u) {
                 d = kk.x;  // MAC kernels' partials carry dense ids
             } else if (macs) {  // a spilled MAC-kernel key: one dictionary walk per flow and owner
                 const uint4 xx = m_kx[e];
@@ -1685,7 +1754,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 mac_ckey(v0.x, v0.y, v0.z, v0.w, x0, x1, x2, ck);
                 d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
             } else {
-                d = staged_id(a.T, v0.x, v0.y, v0.z, v0.w, a.A.slots);
+                d = staged_id(a.T, a.v6, v0.x, v0.y, v0.z, v0.w, a.A.slots);
             }
             if (d != FAIL && d < a.T.fmax) put(d, f);
         }
@@ -1838,7 +1907,17 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             Win32 W;
             load_win32(a.B, off, W);
             pin_win32(W);
-            parse_loaded32<0>(a.B, off, W, macs, P);
+            if (a.slow_abl == 2) {  // diagnostics: no parse (wrong results)
+                P.cls = 0;
+                P.t = W.w[0];
+                P.pi.v6 = 0; P.pi.kproto = 17; P.pi.sip[0] = W.w[9] & 0xF; P.pi.dip[0] = W.w[10] & 0xF;
+                P.pi.sip[1] = P.pi.sip[2] = P.pi.sip[3] = P.pi.dip[1] = P.pi.dip[2] = P.pi.dip[3] = 0;
+                P.pi.ksp = (uint16_t)(W.w[11] & 7); P.pi.kdp = (uint16_t)(W.w[12] & 7);
+                P.pi.tflags = 0; P.pi.rprot = 17; P.pi.doctets = W.w[13] & 0xFFFF; P.pi.rpkt = W.w[14] & 0xFFFF; P.pi.rttl = 1;
+                P.smac = P.dmac = 0;
+            } else {
+                parse_loaded32<0>(a.B, off, W, macs, P);
+            }
             gen = P.cls == 2;
             if (gen) {
                 gli = li;
@@ -1853,13 +1932,21 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
                 CKey k;
                 canon_key(P, macs, k, dir);
                 uint32_t h;
+                uint32_t ia = FAIL, ib = FAIL;
+                if (!macs && pi.v6 && a.v6.C) v6_ids(a.v6, &k.w[0], &k.w[4], ia, ib);
                 if (!macs && !pi.v6 && pi.kproto != 0xFF) {
                     // an IPv4 key: its words, as the hot kernel's spills carry them
                     wk = make_uint4(k.w[0], k.w[4], k.w[8], (uint32_t)pi.kproto << 24);
                     h = lt_hash(wk.x, wk.y, wk.z, wk.w);
                     rec = true;
+                } else if (ia != FAIL && ib != FAIL) {
+                    // an IPv6 key: the ids of its two addresses (no dictionary walk here)
+                    wk = make_uint4(ia, ib, k.w[8], ((uint32_t)pi.kproto << 24) | V6_TAG);
+                    h = lt_hash(wk.x, wk.y, wk.z, wk.w);
+                    rec = true;
                 } else {
-                    const uint32_t d = dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
+                    const uint32_t d = a.slow_abl == 1 ? (k.w[3] ^ k.w[7] ^ k.w[8]) % 8192u  // diagnostics: no dictionary
+                                                       : dense_of_key(a.T, k, true, a.A.slots, &a.g->generic_used);
                     wk = make_uint4(d, 0, 0, 0xFF000000u);
                     h = lt_hash(d, 0, 0, 0xFF000000u);
                     rec = d != FAIL && d < a.T.fmax;
@@ -1881,6 +1968,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             b0 = __shfl(b0, lead, 64);
             if (gen) a.gen[b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] = gli;
         }
+        if (a.slow_abl == 3) rec = false;  // diagnostics: no spill records
         const uint32_t pos = rec ? own_add(s_scnt, ow) : 0u;
         const bool ovf = rec && pos >= S.cap_s;
         if (rec && !ovf) {
@@ -3044,6 +3132,16 @@ struct fluere_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    // Ingest arena (live sessions: a batch per call): the device image, its
+    // record offsets and the pinned staging chunks are kept and reused instead
+    // of allocated per batch (hipHostMalloc of the staging alone cost ms)
+    bool reuse_ingest = false;
+    uint8_t* ar_d = nullptr;
+    uint64_t ar_d_cap = 0;
+    uint32_t* ar_offs = nullptr;
+    uint64_t ar_offs_cap = 0;
+    uint8_t* ar_pin[8] = {};
+    hipEvent_t ar_ev[8] = {};
     uint64_t timeout_ms = 600000;
     int use_mac = 0;
     uint32_t C = 0, fmax = 0;
@@ -3082,6 +3180,8 @@ struct fluere_ctx {
     uint64_t d_annex_cap = 0;
     uint32_t* d_annex_of = nullptr;
     uint32_t* d_sumpos = nullptr;                // [fmax] summary position of each flow in its owner's block
+    void* d_v6map = nullptr;                     // k_slow's IPv6 address-id map (V6Map: 3 key levels, addr_of)
+    uint32_t v6C = 0;
     void* d_wire_tmp = nullptr;                  // fluere_wire_pack scratch (sizes, scan, offsets, scan temp)
     size_t d_wire_tmp_bytes = 0;
     void* d_need = nullptr;
@@ -3294,6 +3394,13 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_annex_of);
     hipFree(c->d_sumpos);
     hipFree(c->d_wire_tmp);
+    hipFree(c->d_v6map);
+    hipFree(c->ar_d);
+    hipFree(c->ar_offs);
+    for (int i = 0; i < 8; i++) {
+        if (c->ar_pin[i]) hipHostFree(c->ar_pin[i]);
+        if (c->ar_ev[i]) hipEventDestroy(c->ar_ev[i]);
+    }
     hipFree(c->d_need);
     hipFree(c->d_recaux);
     sweep_free(c);
@@ -3483,11 +3590,18 @@ struct Ingest {
     std::vector<uint64_t> offs;      // absolute record offsets
     std::vector<size_t> cut;         // first record of each batch
     std::vector<uint64_t> cut_base;  // byte offset of each batch
+    // the capture side's record offsets (fluere_live_batch_indexed): the
+    // chunks are only copied; finish() checks the records against them in
+    // the source image (independent loads, not the walk's pointer chase)
+    const uint8_t* src = nullptr;
+    const uint64_t* given = nullptr;
+    uint64_t given_n = 0;
 
     explicit Ingest(fluere_ctx* cc) : c(cc) {}
     ~Ingest() {
         for (int i = 0; i < kIngestSlots; i++)
             if (busy[i]) hipEventSynchronize(ev[i]);  // no copy may read a freed staging chunk
+        if (c->reuse_ingest) return;  // the arena keeps them
         for (int i = 0; i < kIngestSlots; i++) {
             if (ev[i]) hipEventDestroy(ev[i]);
             if (pin[i]) hipHostFree(pin[i]);
@@ -3497,10 +3611,31 @@ struct Ingest {
     int begin(uint64_t nbytes) {
         if (nbytes < 24) return FLUERE_E_PCAP;
         size = nbytes;
-        if (hipMalloc(&d, nbytes + 256) != hipSuccess) return FLUERE_E_NOMEM;
         nslots = ingest_slots();
         const int ns_ = (int)std::min<uint64_t>(nslots, (nbytes + kIngestChunk - 1) / kIngestChunk);
         const auto ta = std::chrono::steady_clock::now();
+        if (c->reuse_ingest) {
+            static_assert(kIngestSlots == 8, "arena slots");
+            if (nbytes + 256 > c->ar_d_cap) {
+                const uint64_t cap = std::max<uint64_t>(nbytes + 256, c->ar_d_cap * 3 / 2);
+                hipFree(c->ar_d);
+                c->ar_d = nullptr;
+                c->ar_d_cap = 0;
+                if (hipMalloc(&c->ar_d, cap) != hipSuccess) return FLUERE_E_NOMEM;
+                c->ar_d_cap = cap;
+            }
+            d = c->ar_d;
+            for (int i = 0; i < ns_; i++) {
+                if (!c->ar_pin[i] && hipHostMalloc(&c->ar_pin[i], kIngestChunk, hipHostMallocDefault) != hipSuccess)
+                    return FLUERE_E_NOMEM;
+                if (!c->ar_ev[i] && hipEventCreateWithFlags(&c->ar_ev[i], hipEventDisableTiming) != hipSuccess)
+                    return FLUERE_E_HIP;
+                pin[i] = c->ar_pin[i];
+                ev[i] = c->ar_ev[i];
+            }
+            return FLUERE_OK;
+        }
+        if (hipMalloc(&d, nbytes + 256) != hipSuccess) return FLUERE_E_NOMEM;
         for (int i = 0; i < ns_; i++) {
             if (hipHostMalloc(&pin[i], kIngestChunk, hipHostMallocDefault) != hipSuccess) return FLUERE_E_NOMEM;
             if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return FLUERE_E_HIP;
@@ -3600,7 +3735,7 @@ struct Ingest {
         }
         const uint64_t ce = cs + len;
         uint8_t h[16];
-        while (!stopped && pos + 16 <= ce) {
+        while (!given && !stopped && pos + 16 <= ce) {
             const uint8_t* hp;
             if (pos >= cs) {
                 hp = b + (pos - cs);
@@ -3632,12 +3767,41 @@ struct Ingest {
         busy[i] = true;
         return FLUERE_OK;
     }
+    // libpcap's walk over the given offsets: the same stop rules, every
+    // record where the previous one ended
+    void walk_given() {
+        pos = 24;
+        for (uint64_t i = 0; i < given_n; i++) {
+            if (given[i] != pos || pos + 16 > size) break;
+            const uint32_t incl = rd32(src + pos + 8);
+            if (incl > kSnapMax || pos + 16 + (uint64_t)incl > size) break;
+            if (pos + 16 + incl - cut_base.back() > kMaxBatch) {
+                cut.push_back(offs.size());
+                cut_base.push_back(pos);
+            }
+            offs.push_back(pos);
+            pos += 16 + (uint64_t)incl;
+        }
+    }
     // the index as batches of the context (device bytes handed over)
     int finish() {
+        if (given && !cut.empty()) walk_given();
         HIPCHECK(hipMemsetAsync(d + size, 0, 256, c->stream));
         const size_t n = offs.size();
         uint32_t* d_offs = nullptr;
-        if (hipMalloc(&d_offs, std::max<size_t>(n, 1) * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        if (c->reuse_ingest) {
+            if (std::max<size_t>(n, 1) > c->ar_offs_cap) {
+                const uint64_t cap = std::max<uint64_t>(std::max<size_t>(n, 1), c->ar_offs_cap * 3 / 2);
+                hipFree(c->ar_offs);
+                c->ar_offs = nullptr;
+                c->ar_offs_cap = 0;
+                if (hipMalloc(&c->ar_offs, cap * 4) != hipSuccess) return FLUERE_E_NOMEM;
+                c->ar_offs_cap = cap;
+            }
+            d_offs = c->ar_offs;
+        } else if (hipMalloc(&d_offs, std::max<size_t>(n, 1) * 4) != hipSuccess) {
+            return FLUERE_E_NOMEM;
+        }
         std::vector<uint32_t> rel(std::max<size_t>(n, 1));
         for (size_t q = 0; q < cut.size(); q++) {
             const size_t i0 = cut[q], i1 = q + 1 < cut.size() ? cut[q + 1] : n;
@@ -3656,8 +3820,8 @@ struct Ingest {
             // part of any batch (and cannot push it past the 4 GiB offset range)
             const uint64_t endb = q + 1 < cut.size() ? cut_base[q + 1] : pos;
             HostBatch hb;
-            hb.own_bytes = first ? d : nullptr;  // one allocation for every batch
-            hb.own_offs = first ? d_offs : nullptr;
+            hb.own_bytes = first && !c->reuse_ingest ? d : nullptr;  // one allocation for every batch
+            hb.own_offs = first && !c->reuse_ingest ? d_offs : nullptr;
             first = false;
             hb.b.bytes = d + base;
             hb.b.offs = d_offs + i0;
@@ -3670,7 +3834,9 @@ struct Ingest {
             c->batches_dirty = true;
             c->n_total += hb.b.n;
         }
-        if (first) {  // no records: nothing attached
+        if (c->reuse_ingest) {
+            d = nullptr;  // the arena's
+        } else if (first) {  // no records: nothing attached
             hipFree(d_offs);
         } else {
             d = nullptr;  // owned by the first batch now
@@ -3679,6 +3845,22 @@ struct Ingest {
         return FLUERE_OK;
     }
 };
+
+// A classic pcap image with its record offsets known (live batches).
+static int add_host_pcap_indexed(fluere_ctx* c, const uint8_t* file, uint64_t nbytes, const uint64_t* rec_off,
+                                 uint64_t n_recs) {
+    Ingest in(c);
+    in.src = file;
+    in.given = rec_off;
+    in.given_n = n_recs;
+    int rc = in.begin(nbytes);
+    if (rc) return rc;
+    rc = in.run(nbytes, [&](uint8_t* dst, uint64_t cs, uint64_t len) {
+        memcpy(dst, file + cs, len);
+        return true;
+    });
+    return rc ? rc : in.finish();
+}
 
 extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t nbytes) {
     if (!c || !file) return FLUERE_E_ARG;
@@ -3900,6 +4082,24 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     // merge tail's slower path, or an empty launch)
     const int slow_env = getenv("FLUERE_SLOW_KERNEL") ? atoi(getenv("FLUERE_SLOW_KERNEL")) : -1;  // tests: force it
     a.slow_kernel = slow_env >= 0 ? slow_env : (c->last_n_slow > 0 ? 1 : 0);
+    // k_slow's IPv6 address ids (non-MAC runs): 4 slots per flow of capacity, at most 2^20
+    if (a.slow_kernel && !c->use_mac) {
+        uint32_t C = 1u << 12;
+        while (C < (1u << 20) && C < 4ull * c->fmax) C <<= 1;
+        if (C != c->v6C) {
+            hipFree(c->d_v6map);
+            c->d_v6map = nullptr;
+            c->v6C = 0;
+            if (hipMalloc(&c->d_v6map, (size_t)(C + 1) * (3 * 8 + 16) + 16) != hipSuccess) return FLUERE_E_NOMEM;
+            c->v6C = C;
+        }
+        unsigned long long* k = (unsigned long long*)c->d_v6map;
+        a.v6.tab[0] = k;
+        a.v6.tab[1] = k + (C + 1);
+        a.v6.tab[2] = k + 2 * (size_t)(C + 1);
+        a.v6.addr_of = (uint4*)(k + ((3 * (size_t)(C + 1) + 1) & ~(size_t)1));  // (16-byte aligned)
+        a.v6.C = C;
+    }
     if (getenv("FLUERE_DEBUG")) {
         if (!g_hot_dbg && hipMalloc(&g_hot_dbg, 4096 * 8 * 8) != hipSuccess) g_hot_dbg = nullptr;
         a.dbg = g_hot_dbg;
@@ -4035,7 +4235,10 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
                                     c->evk1, 0));
         const auto t1 = std::chrono::steady_clock::now();
         // the slow list into k_slow's owner segments, before the merge reads them
-        if (a.slow_kernel) k_slow<<<P.slow_grid[i], SB, 0, s>>>(a);
+        if (a.slow_kernel) {
+            if (a.v6.C) HIPCHECK(hipMemsetAsync(a.v6.tab[0], 0xFF, (size_t)(a.v6.C + 1) * 3 * 8, s));  // every key EMPTY
+            k_slow<<<P.slow_grid[i], SB, 0, s>>>(a);
+        }
         // at most one merge workgroup per CU, each taking owners in turn
         k_merge_partials<<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow took it)
         if (hostprof) {
@@ -4120,6 +4323,17 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
                                              : (const void*)k_parse_agg<0, false>;
         kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
         event(c->evk1);
+        if (P.agg[i].slow_kernel && P.agg[i].v6.C && ok) {
+            hipMemsetParams mp{};
+            mp.dst = P.agg[i].v6.tab[0];
+            mp.elementSize = 4;
+            mp.width = (size_t)(P.agg[i].v6.C + 1) * 3 * 2;
+            mp.height = 1;
+            mp.pitch = 0;
+            mp.value = 0xFFFFFFFFu;
+            ok = hipGraphAddMemsetNode(&n, g, &prev, 1, &mp) == hipSuccess;
+            prev = n;
+        }
         if (P.agg[i].slow_kernel) kernel((const void*)k_slow, P.slow_grid[i], SB, a_agg[i]);
         kernel((const void*)k_merge_partials, std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, a_agg[i]);
     }
@@ -4729,6 +4943,13 @@ extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_
     const size_t need = 2 * (n + 1) * 8 + (size_t)(n_owners + 1) * 8 + ((tb + 255) & ~(size_t)255);
     if (need > c->d_wire_tmp_bytes) {
         hipFree(c->d_wire_tmp);
+    hipFree(c->d_v6map);
+    hipFree(c->ar_d);
+    hipFree(c->ar_offs);
+    for (int i = 0; i < 8; i++) {
+        if (c->ar_pin[i]) hipHostFree(c->ar_pin[i]);
+        if (c->ar_ev[i]) hipEventDestroy(c->ar_ev[i]);
+    }
         c->d_wire_tmp = nullptr;
         c->d_wire_tmp_bytes = 0;
         if (hipMalloc(&c->d_wire_tmp, need) != hipSuccess) return FLUERE_E_NOMEM;
@@ -5602,6 +5823,7 @@ extern "C" int fluere_live_open(const fluere_opts* o, fluere_live** out) {
     fluere_live* lv = new (std::nothrow) fluere_live();
     if (!lv) return FLUERE_E_NOMEM;
     int rc = fluere_open(o, &lv->batch);
+    if (!rc) lv->batch->reuse_ingest = true;  // one batch per call: keep the ingest buffers
     if (!rc) rc = fluere_open(o, &lv->persist);
     const uint64_t pmax = lv->persist ? lv->persist->fmax : 0;
     if (!rc && (hipMalloc(&lv->P, pmax * sizeof(fluere_flow_piece)) != hipSuccess ||
@@ -5717,8 +5939,24 @@ static int live_compact(fluere_live* lv) {
     return FLUERE_OK;
 }
 
+static int live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, const uint64_t* rec_off, uint64_t n_recs,
+                      int do_export, fluere_record** recs, uint64_t* n, uint64_t* n_ordered, int* exported);
+
 extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, int do_export,
                                  fluere_record** recs, uint64_t* n, uint64_t* n_ordered, int* exported) {
+    return live_batch(lv, pcap, nbytes, nullptr, 0, do_export, recs, n, n_ordered, exported);
+}
+
+extern "C" int fluere_live_batch_indexed(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, const uint64_t* rec_off,
+                                         uint64_t n_recs, int do_export, fluere_record** recs, uint64_t* n,
+                                         uint64_t* n_ordered, int* exported) {
+    if (!rec_off && n_recs) return FLUERE_E_ARG;
+    return live_batch(lv, pcap, nbytes, rec_off ? rec_off : (const uint64_t*)"", n_recs, do_export, recs, n, n_ordered,
+                      exported);
+}
+
+static int live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, const uint64_t* rec_off, uint64_t n_recs,
+                      int do_export, fluere_record** recs, uint64_t* n, uint64_t* n_ordered, int* exported) {
     if (!lv || !pcap || !recs || !n) return FLUERE_E_ARG;
     *recs = nullptr;
     *n = 0;
@@ -5728,13 +5966,23 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
+    static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    const auto t0 = now();
+    auto t1 = t0, t2 = t0, t3 = t0, t4 = t0;
     if ((rc = fluere_reset(c))) return rc;
     if ((rc = fluere_set_index_base(c, lv->base))) return rc;
-    if ((rc = fluere_add_host_pcap(c, pcap, nbytes))) return rc;
+    if (rec_off && !is_pcapng(pcap, nbytes)) rc = add_host_pcap_indexed(c, pcap, nbytes, rec_off, n_recs);
+    else rc = fluere_add_host_pcap(c, pcap, nbytes);
+    if (rc) return rc;
     lv->base += c->n_total;
     lv->last_have = false;
     if (c->n_total) {
+        t1 = now();
         if ((rc = fluere_parse_aggregate(c))) return rc;
+        if (hostprof) HIPCHECK(hipStreamSynchronize(s));
+        t2 = now();
         uint64_t need_nf = 0;
         for (;;) {  // one owner: the whole batch
             const uint64_t bb = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
@@ -5759,6 +6007,7 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
             HIPCHECK(hipMemcpyAsync(lv->pending.data() + at, c->d_recs, c->local_n_rec * sizeof(fluere_record),
                                     hipMemcpyDeviceToHost, s));
         c->local_n_rec = c->local_updates = c->local_ended = 0;
+        t3 = now();
         // room for the batch's flows in the session dictionary (need: the
         // batch's flow count, one owner): compact it first when short
         if (lv->persist_nf + need_nf > lv->persist->fmax) {
@@ -5784,6 +6033,10 @@ extern "C" int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t 
             HIPCHECK(hipStreamSynchronize(s));
             lv->last_have = true;
         }
+        t4 = now();
+        if (hostprof)
+            fprintf(stderr, "[fluere] live batch: ingest %.2f parse+aggregate %.2f export %.2f compose+take %.2f ms\n",
+                    ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
     }
     // the interval check runs after a processed packet: an interval that
     // elapsed in a batch without one exports at the next batch with one

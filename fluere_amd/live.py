@@ -65,15 +65,24 @@ class LiveSession:
         finally:
             _lib.lib().fluere_records_free(p)
 
-    def batch(self, pcap: bytes, export: bool):
-        """One batch; (records, n_ordered) when the interval export ran, else None."""
+    def batch(self, pcap: bytes, export: bool, offsets=None):
+        """One batch; (records, n_ordered) when the interval export ran, else
+        None.  offsets (optional, uint64): each record's header offset in the
+        image, as the capture side delivered them (fluere_live_batch_indexed:
+        no host walk over the headers)."""
         if isinstance(pcap, bytes):  # the bytes object's own buffer (no host copy)
             buf = ctypes.cast(ctypes.c_char_p(pcap), ctypes.POINTER(ctypes.c_uint8))
         else:
             buf = (ctypes.c_uint8 * max(len(pcap), 1)).from_buffer_copy(pcap)
         p, n, no, ex = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
-        check(self._L.fluere_live_batch(self._h, buf, len(pcap), 1 if export else 0, ctypes.byref(p), ctypes.byref(n),
-                                        ctypes.byref(no), ctypes.byref(ex)), "fluere_live_batch")
+        if offsets is not None:
+            offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+            check(self._L.fluere_live_batch_indexed(self._h, buf, len(pcap), offs.ctypes.data_as(ctypes.c_void_p),
+                                                    len(offs), 1 if export else 0, ctypes.byref(p), ctypes.byref(n),
+                                                    ctypes.byref(no), ctypes.byref(ex)), "fluere_live_batch_indexed")
+        else:
+            check(self._L.fluere_live_batch(self._h, buf, len(pcap), 1 if export else 0, ctypes.byref(p),
+                                            ctypes.byref(n), ctypes.byref(no), ctypes.byref(ex)), "fluere_live_batch")
         recs = self._take(p, n) if p.value else None
         return (recs, no.value) if ex.value else None
 
@@ -108,26 +117,32 @@ def pcap_records(data: bytes) -> Iterator[Tuple[int, int, int]]:
         off += 16 + incl
 
 
-def replay_batches(data: bytes, interval_ms: int, batch_packets: int = 0) -> Iterator[Tuple[bytes, bool]]:
+def _batch_offsets(cur):
+    """Header offsets of the records of one batch image (24-byte file header first)."""
+    lens = np.fromiter((len(x) for x in cur), dtype=np.uint64, count=len(cur))
+    return 24 + np.concatenate([np.zeros(1, np.uint64), np.cumsum(lens)[:-1]]).astype(np.uint64)
+
+
+def replay_batches(data: bytes, interval_ms: int, batch_packets: int = 0) -> Iterator[Tuple[bytes, bool, np.ndarray]]:
     """A capture file as the batches a ring would deliver: a batch ends where
     the packets' own clock crosses the next interval boundary (its export flag
     set), or every batch_packets packets without an export in between.
-    Yields (classic pcap image, export)."""
+    Yields (classic pcap image, export, record header offsets)."""
     hdr = data[:24]
     cur, start, n = [], None, 0
     for off, ln, t in pcap_records(data):
         if start is None:
             start = t
         if interval_ms and t - start >= interval_ms * 1000 and cur:
-            yield hdr + b"".join(cur), True
+            yield hdr + b"".join(cur), True, _batch_offsets(cur)
             cur, start, n = [], t, 0
         cur.append(data[off:off + ln])
         n += 1
         if batch_packets and n >= batch_packets:
-            yield hdr + b"".join(cur), False
+            yield hdr + b"".join(cur), False, _batch_offsets(cur)
             cur, n = [], 0
     if cur:
-        yield hdr + b"".join(cur), False
+        yield hdr + b"".join(cur), False, _batch_offsets(cur)
 
 
 def packet_capture(args, batches: Iterable[Tuple[bytes, bool]], out_dir: str = "./output", plugins=(),
@@ -151,8 +166,8 @@ def packet_capture(args, batches: Iterable[Tuple[bytes, bool]], out_dir: str = "
         exports.append((path, recs, n_ordered))
 
     with LiveSession(int(args.parameters.timeout), bool(args.parameters.use_mac), max_flows) as s:
-        for pcap, export in batches:
-            got = s.batch(pcap, export)
+        for item in batches:  # (pcap, export[, record offsets])
+            got = s.batch(*item)
             if got is not None:
                 write(*got)
         write(*s.finish(duration_end))

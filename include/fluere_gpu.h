@@ -389,6 +389,18 @@ int fluere_live_close(fluere_live* lv);
 int fluere_live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, int do_export, fluere_record** recs,
                       uint64_t* n, uint64_t* n_ordered, int* exported);
 int fluere_live_finish(fluere_live* lv, int duration_end, fluere_record** recs, uint64_t* n, uint64_t* n_ordered);
+/* fluere_live_batch for a batch whose record offsets the capture side already
+ * holds (a capture ring hands over packets one by one, headers included):
+ * rec_off[i] = byte offset of record i's 16-byte header in pcap.  The host
+ * then skips libpcap's walk over the headers, a pointer chase that costs one
+ * memory latency per record (~0.1 us for IMIX-sized records, the live-mode
+ * ingest bound); the records are checked against the offsets with independent
+ * loads instead.  Same result as fluere_live_batch: the batch ends at the
+ * first record that does not start where the previous one ended, or whose
+ * caplen the walk would refuse. */
+int fluere_live_batch_indexed(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, const uint64_t* rec_off,
+                              uint64_t n_recs, int do_export, fluere_record** recs, uint64_t* n, uint64_t* n_ordered,
+                              int* exported);
 
 /* Test seam: insert n canonical keys (14 u32 words each, device memory) into
  * the flow dictionary and write each key's dense flow id. */

@@ -837,20 +837,24 @@ LIVE_CASES = {
 }
 
 
+@pytest.mark.parametrize("indexed", [True, False])
 @pytest.mark.parametrize("name", sorted(LIVE_CASES))
-def test_live_matches_oracle(gpu, name, tmp_path):
+def test_live_matches_oracle(gpu, name, indexed, tmp_path):
     """Every export (CSV file / plugin hand-off batch) of the live mode equals
     the oracle's: the FIN/RST-closed records in order, the idle-timeout,
-    duration and final-flush records as a multiset (HashMap order)."""
+    duration and final-flush records as a multiset (HashMap order).  Batches
+    with their record offsets (fluere_live_batch_indexed) or without."""
     from fluere_amd import live
     kind, n, f, seed, interval, bp, timeout, dur, mac = LIVE_CASES[name]
     data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
     batches = list(live.replay_batches(data, interval, bp))
+    if not indexed:
+        batches = [(img, e) for img, e, _ in batches]
     ends, k = [], 0
-    for img, _ in batches:
+    for img, *_ in batches:
         k += sum(1 for _ in live.pcap_records(img))
         ends.append(k)
-    want = pyoracle.live(data, ends, [e for _, e in batches], timeout, mac, dur)
+    want = pyoracle.live(data, ends, [b[1] for b in batches], timeout, mac, dur)
 
     class Plugin:  # fluere-plugin's process_data(table) (lib.rs:228-276)
         def __init__(self):
@@ -878,10 +882,10 @@ def test_live_session_reclaims_closed_flows(gpu, tmp_path):
     data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 600_000, 1_000, 0xF10E0097))
     batches = list(live.replay_batches(data, 20, 20_000))
     ends, k = [], 0
-    for img, _ in batches:
+    for img, *_ in batches:
         k += sum(1 for _ in live.pcap_records(img))
         ends.append(k)
-    want = pyoracle.live(data, ends, [e for _, e in batches], 10, False, True)
+    want = pyoracle.live(data, ends, [b[1] for b in batches], 10, False, True)
     n_keys = sum(w["csv"].count("\n") - 1 for w in want)
     assert n_keys > 3 * 4096  # records (one per flow instance) far beyond the dictionary
     args = fluere_amd.Args(fluere_amd.Files(csv="live"), fluere_amd.Parameters(use_mac=False, timeout=10))
@@ -917,6 +921,29 @@ def test_live_export_waits_for_a_processed_packet(gpu, tmp_path):
         assert_csv_equal(open(path).read(), n_ord, w["csv"], w["n_ordered"], f"pending export {i}")
 
 
+def test_live_indexed_offsets_cut_the_batch(gpu):
+    """Record offsets that stop following the records (a ring that handed
+    over fewer packets than the image holds, or a bad header): the indexed
+    batch ends where the offsets stop matching libpcap's walk, and equals the
+    same batch cut there."""
+    from fluere_amd import live
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 30_000, 300, 0xF10E00A7))
+    offs = np.array([o for o, _, _ in live.pcap_records(data)], dtype=np.uint64)
+    cut = 17_000
+    bad = offs.copy()
+    bad[cut] += 4  # record `cut` does not start where the previous one ended
+    cut_img = data[:int(offs[cut])]
+    results = []
+    for img, o in ((data, bad), (data, offs[:cut]), (cut_img, None)):
+        with live.LiveSession(1000, False, max_flows=1 << 16) as s:
+            s.batch(img, False, o)
+            recs, no = s.finish(False)
+        results.append((fluere_amd.format_csv(recs), no))
+    assert results[0][1] == results[2][1] and results[1][1] == results[2][1]
+    assert_csv_equal(results[0][0], results[0][1], results[2][0], results[2][1], "bad offset")
+    assert_csv_equal(results[1][0], results[1][1], results[2][0], results[2][1], "short offset list")
+
+
 def test_fluere_live_cli(gpu, tmp_path):
     """`fluere live --replay` (the C++ CLI over the C ABI): its CSV files equal
     the oracle's exports for the same interval batches."""
@@ -930,10 +957,10 @@ def test_fluere_live_cli(gpu, tmp_path):
                    check=True, capture_output=True)
     batches = list(live.replay_batches(data, 15))
     ends, k = [], 0
-    for img, _ in batches:
+    for img, *_ in batches:
         k += sum(1 for _ in live.pcap_records(img))
         ends.append(k)
-    want = pyoracle.live(data, ends, [e for _, e in batches], 10, False, False)
+    want = pyoracle.live(data, ends, [b[1] for b in batches], 10, False, False)
     files = sorted(out.glob("lv_*.csv"), key=lambda p: int(p.stem.split("_")[1]))
     assert len(files) == len(want)
     for f, w in zip(files, want):

@@ -29,32 +29,41 @@ def main():
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--export-every", type=int, default=5)
     ap.add_argument("--timeout-ms", type=int, default=600000)
+    ap.add_argument("--indexed", type=int, default=1, help="1: batches carry their record offsets")
     args = ap.parse_args()
     import fluere_amd
     from fluere_amd.live import LiveSession, pcap_records
 
     kind, flows, seed = CONFIGS[args.config]
     data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, args.packets, flows, seed))
+    import numpy as np
     hdr = data[:24]
     batches, cur, n = [], [], 0
+
+    def close(cur):
+        # the image and its record offsets, as a capture ring hands them over
+        lens = np.array([ln for _, ln in cur], dtype=np.uint64)
+        offs = 24 + np.concatenate([np.zeros(1, np.uint64), np.cumsum(lens)[:-1]]).astype(np.uint64)
+        batches.append((hdr + b"".join(data[o:o + l] for o, l in cur), offs if args.indexed else None))
+
     for off, ln, _ in pcap_records(data):
         cur.append((off, ln))
         if len(cur) == args.batch:
-            batches.append(hdr + b"".join(data[o:o + l] for o, l in cur))
+            close(cur)
             cur = []
     if cur:
-        batches.append(hdr + b"".join(data[o:o + l] for o, l in cur))
+        close(cur)
     del data
     res = {"config": args.config, "packets": args.packets, "batch_packets": args.batch, "batches": len(batches),
-           "export_every": args.export_every}
+           "export_every": args.export_every, "indexed": bool(args.indexed), "timeout_ms": args.timeout_ms}
     with LiveSession(args.timeout_ms, False, max_flows=MAX_FLOWS[args.config]) as s:
-        s.batch(batches[0], False)  # warm-up (the runtime, the session buffers)
+        s.batch(batches[0][0], False, batches[0][1])  # warm-up (the runtime, the session buffers)
     times, exported = [], 0
     with LiveSession(args.timeout_ms, False, max_flows=MAX_FLOWS[args.config]) as s:
         t_all = time.perf_counter()
-        for k, b in enumerate(batches):
+        for k, (b, o) in enumerate(batches):
             t0 = time.perf_counter()
-            got = s.batch(b, (k + 1) % args.export_every == 0)
+            got = s.batch(b, (k + 1) % args.export_every == 0, o)
             times.append(time.perf_counter() - t0)
             if got is not None:
                 exported += len(got[0])

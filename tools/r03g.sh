@@ -3,7 +3,7 @@
 set -eo pipefail
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
-for A in 0 1 2; do
+for A in 2 3; do
   O=$R/gpurun_out/r03g/abl$A; mkdir -p $O
   FLUERE_SLOW_ABL=$A timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
     python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --config slow > $O/trace.log 2>&1
