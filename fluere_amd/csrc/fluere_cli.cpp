@@ -88,6 +88,7 @@ static int live_main(int argc, char** argv) {
         return w;
     };
     std::vector<uint8_t> batch(data.begin(), data.begin() + 24);
+    std::vector<uint64_t> boff;  // the batch's record offsets (the ring hands them over with the packets)
     uint64_t off = 24, start = ~0ull, bstart = ~0ull;
     bool stopped = false;
     while (!rc && off + 16 <= data.size()) {
@@ -101,11 +102,14 @@ static int live_main(int argc, char** argv) {
             fluere_record* recs = nullptr;
             uint64_t n = 0, no = 0;
             int ex = 0;
-            rc = fluere_live_batch(lv, batch.data(), batch.size(), 1, &recs, &n, &no, &ex);
+            rc = fluere_live_batch_indexed(lv, batch.data(), batch.size(), boff.data(), boff.size(), 1, &recs, &n, &no,
+                                           &ex);
             if (!rc && ex) rc = write(recs, n);
             batch.resize(24);
+            boff.clear();
             bstart = t;
         }
+        boff.push_back(batch.size());
         batch.insert(batch.end(), data.begin() + off, data.begin() + off + 16 + incl);
         off += 16 + incl;
         // the duration check runs after the packet is processed (live_fluereflow.rs:361-373)
@@ -115,7 +119,7 @@ static int live_main(int argc, char** argv) {
         fluere_record* recs = nullptr;
         uint64_t n = 0, no = 0;
         int ex = 0;
-        rc = fluere_live_batch(lv, batch.data(), batch.size(), 0, &recs, &n, &no, &ex);
+        rc = fluere_live_batch_indexed(lv, batch.data(), batch.size(), boff.data(), boff.size(), 0, &recs, &n, &no, &ex);
         if (!rc && ex) rc = write(recs, n);
     }
     if (!rc) {

@@ -3767,20 +3767,53 @@ struct Ingest {
         busy[i] = true;
         return FLUERE_OK;
     }
-    // libpcap's walk over the given offsets: the same stop rules, every
-    // record where the previous one ended
+    // libpcap's walk over the given offsets, the same stop rules: record i is
+    // taken while it starts where record i - 1 ended and its caplen is one the
+    // walk takes.  Each record's test needs only its own header and the one
+    // before, so threads test ranges of records at once (independent loads);
+    // the first failing record ends the batch.
     void walk_given() {
-        pos = 24;
-        for (uint64_t i = 0; i < given_n; i++) {
-            if (given[i] != pos || pos + 16 > size) break;
-            const uint32_t incl = rd32(src + pos + 8);
-            if (incl > kSnapMax || pos + 16 + (uint64_t)incl > size) break;
-            if (pos + 16 + incl - cut_base.back() > kMaxBatch) {
-                cut.push_back(offs.size());
-                cut_base.push_back(pos);
+        const uint64_t n = given_n;
+        auto incl_of = [&](uint64_t i) -> uint64_t {
+            const uint64_t o = given[i];
+            return o + 16 <= size ? rd32(src + o + 8) : ~0ull;
+        };
+        auto ok = [&](uint64_t i, uint64_t prev_end) {
+            const uint64_t o = given[i], incl = incl_of(i);
+            return o == prev_end && o + 16 <= size && incl <= kSnapMax && o + 16 + incl <= size;
+        };
+        const int T = n >= (1u << 16) ? 8 : 1;
+        std::vector<uint64_t> first_bad(T, n);
+        auto part = [&](int t) {
+            const uint64_t i0 = n * t / T, i1 = n * (t + 1) / T;
+            uint64_t prev_end = 24;
+            if (i0 > 0) {
+                const uint64_t pi = incl_of(i0 - 1);
+                prev_end = pi == ~0ull ? ~0ull : given[i0 - 1] + 16 + pi;
             }
-            offs.push_back(pos);
-            pos += 16 + (uint64_t)incl;
+            for (uint64_t i = i0; i < i1; i++) {
+                if (i + 32 < i1 && given[i + 32] + 16 <= size) __builtin_prefetch(src + given[i + 32]);
+                if (!ok(i, prev_end)) { first_bad[t] = i; return; }
+                prev_end = given[i] + 16 + incl_of(i);
+            }
+        };
+        if (T == 1) {
+            part(0);
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < T; t++) th.emplace_back(part, t);
+            for (auto& x : th) x.join();
+        }
+        const uint64_t m = *std::min_element(first_bad.begin(), first_bad.end());
+        pos = 24;
+        for (uint64_t i = 0; i < m; i++) {
+            const uint64_t end = i + 1 < m ? given[i + 1] : given[i] + 16 + incl_of(i);
+            if (end - cut_base.back() > kMaxBatch) {
+                cut.push_back(offs.size());
+                cut_base.push_back(given[i]);
+            }
+            offs.push_back(given[i]);
+            pos = end;
         }
     }
     // the index as batches of the context (device bytes handed over)
@@ -6044,6 +6077,7 @@ static int live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, con
     if (!lv->export_due || !lv->last_have) return FLUERE_OK;
     lv->export_due = false;
     std::vector<fluere_record> scan;
+    const auto t5 = now();
     if (lv->timeout_ms > 0) {
         LiveArgs a = live_args(lv);
         a.block_bytes = fluere_shard_block_bytes(lv->cap, lv->cap_annex);
@@ -6052,7 +6086,12 @@ static int live_batch(fluere_live* lv, const uint8_t* pcap, uint64_t nbytes, con
         if ((rc = live_take(lv, scan))) return rc;
     }
     if (exported) *exported = 1;
-    return live_export(lv, scan, recs, n, n_ordered);
+    const auto t6 = now();
+    rc = live_export(lv, scan, recs, n, n_ordered);
+    if (hostprof)
+        fprintf(stderr, "[fluere] live export: scan+take %.2f (%zu records) order+copy %.2f ms (%llu records)\n",
+                ms(t5, t6), scan.size(), ms(t6, now()), (unsigned long long)*n);
+    return rc;
 }
 
 extern "C" int fluere_live_finish(fluere_live* lv, int duration_end, fluere_record** recs, uint64_t* n,
