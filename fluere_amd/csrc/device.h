@@ -74,6 +74,7 @@ struct Glob {
     unsigned long long cyc_m_scan, cyc_m_ids;             // diagnostics: k_merge_partials phases
     unsigned long long clean_done;                        // k_cleanup: workgroups finished
     unsigned long long fin_done;                          // k_finalize: workgroups finished
+    unsigned long long n_fdefer;                          // k_finalize: certified flows left to k_finalize_gen
 };
 static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16 &&
                   offsetof(Glob, n_gen) == offsetof(Glob, n_slow) + 24,
@@ -195,6 +196,33 @@ __device__ __forceinline__ void parse_loaded(const Batch& B, uint32_t off, const
             P.dmac = mac_be(fr + pi.frame_off);
             P.smac = mac_be(fr + pi.frame_off + 6);
         }
+    }
+}
+
+// The record at batch offset off through the register parser alone (no
+// general parser in the caller's code: its registers and stack would cost the
+// whole kernel occupancy); P.cls = 2 when parse_fast declines the packet.
+__device__ __forceinline__ void parse_loaded_fast(const Batch& B, uint32_t off, const Win& W, bool macs, Parsed& P) {
+    const bool sw = B.flags & 1;
+    const uint32_t sec = hdr_word(W.w[0], sw), frac = hdr_word(W.w[1], sw), incl = hdr_word(W.w[2], sw);
+    uint32_t L = min(incl, B.snap);
+    const uint64_t avail = B.nbytes > (uint64_t)off + 16 ? B.nbytes - off - 16 : 0;
+    if (L > avail) L = (uint32_t)avail;
+    P.L = L;
+    P.t = (uint64_t)sec * 1000000ull + ((B.flags & 2) ? frac / 1000u : frac);  // time.rs:5-7
+    P.smac = P.dmac = 0;
+    if (!parse_fast(W, L, P.pi)) {
+        P.cls = 2;
+        return;
+    }
+    const PktInfo& pi = P.pi;
+    P.cls = (pi.kst != ST_OK || pi.fst != ST_OK) ? 1 : 0;
+    if (macs && P.cls == 0) {  // frame bytes 0..12 = record bytes 16..28
+        uint64_t d = 0, s = 0;
+        for (int k = 0; k < 6; k++) d = (d << 8) | W.b(16 + k);
+        for (int k = 0; k < 6; k++) s = (s << 8) | W.b(22 + k);
+        P.dmac = d;
+        P.smac = s;
     }
 }
 
@@ -396,6 +424,15 @@ __device__ __forceinline__ void parse_global(const Batch* bs, int nb, uint64_t g
     int b = find_batch(bs, nb, gi);
     parse_record(bs[b], gi - bs[b].first, macs, 0, P);
 }
+// The register parser alone (parse_loaded_fast): P.cls = 2 when it declines.
+__device__ __forceinline__ void parse_global_fast(const Batch* bs, int nb, uint64_t gi, bool macs, Parsed& P) {
+    const int b = find_batch(bs, nb, gi);
+    const Batch& B = bs[b];
+    const uint32_t off = B.offs[gi - B.first];
+    Win W;
+    load_win(B, off, W);
+    parse_loaded_fast(B, off, W, macs, P);
+}
 
 // parse_microseconds (time.rs:5-7) of the record at batch offset off: the
 // record header alone (a record's `last` needs no parse of its frame).
@@ -449,9 +486,14 @@ struct EmitLds {
     unsigned long long w[EMIT_BLOCK / 64][3];  // per wave: records (-> exclusive prefix), updates, ended
     unsigned long long base, n;
     fluere_record rec[EMIT_BLOCK];
+    uint16_t slot[EMIT_BLOCK];                 // emit_inplace_block: the k-th record's thread
 };
+// aux (optional): two order words per record, written beside it (Mode B:
+// {0 for a FIN/RST close, else exp + 1; the firing entry's creation}).
 __device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_record* out, uint64_t cap,
-                                                  const fluere_record& r, bool want) {
+                                                  const fluere_record& r, bool want,
+                                                  unsigned long long* aux = nullptr, unsigned long long a0 = 0,
+                                                  unsigned long long a1 = 0) {
     static_assert(sizeof(fluere_record) % 8 == 0, "records are whole 8-byte words");
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t m = __ballot(want), em = __ballot(want && r.order_key != NONE64);
@@ -477,8 +519,12 @@ __device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_re
         if (t[2]) atomicAdd(&g->n_ended, t[2]);
     }
     __syncthreads();
-    if (want)
-        S.rec[S.w[w][0] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = r;
+    if (want) {
+        const uint32_t i = S.w[w][0] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        S.rec[i] = r;
+        if (aux && S.base + i < cap)
+            *reinterpret_cast<ulonglong2*>(aux + 2 * (S.base + i)) = make_ulonglong2(a0, a1);
+    }
     __syncthreads();
     const unsigned long long base = S.base;
     const unsigned long long n = base < cap ? min(S.n, cap - base) : 0ull;  // (records past the capacity: counted only)
@@ -487,6 +533,54 @@ __device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_re
     uint2* dst = reinterpret_cast<uint2*>(out + base);
     for (uint32_t i = threadIdx.x; i < n * RW; i += EMIT_BLOCK) dst[i] = src[i];
     __syncthreads();  // S is rewritten by the next call
+}
+
+// emit_record_block for records built in place, thread t's in S.rec[t] (a
+// kernel that builds its record field by field in LDS holds no 38-word record
+// in registers): the copy gathers the wanted slots in thread order.
+__device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_record* out, uint64_t cap, bool want,
+                                                   uint32_t d_pkts, bool ended, unsigned long long* aux = nullptr,
+                                                   unsigned long long a0 = 0, unsigned long long a1 = 0) {
+    const uint32_t w = threadIdx.x >> 6;
+    const uint64_t m = __ballot(want), em = __ballot(want && ended);
+    const unsigned long long upd = wave_sum(want ? (unsigned long long)d_pkts : 0ull);
+    if ((threadIdx.x & 63) == 0) {
+        S.w[w][0] = __popcll(m);
+        S.w[w][1] = upd;
+        S.w[w][2] = __popcll(em);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t[3] = {0, 0, 0};
+        for (int k = 0; k < EMIT_BLOCK / 64; k++) {
+            const unsigned long long nk = S.w[k][0];
+            t[1] += S.w[k][1];
+            t[2] += S.w[k][2];
+            S.w[k][0] = t[0];
+            t[0] += nk;
+        }
+        S.base = t[0] ? atomicAdd(&g->n_rec, t[0]) : 0ull;
+        S.n = t[0];
+        if (t[1]) atomicAdd(&g->n_updates, t[1]);
+        if (t[2]) atomicAdd(&g->n_ended, t[2]);
+    }
+    __syncthreads();
+    if (want) {
+        const uint32_t i = S.w[w][0] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        S.slot[i] = (uint16_t)threadIdx.x;
+        if (aux && S.base + i < cap)
+            *reinterpret_cast<ulonglong2*>(aux + 2 * (S.base + i)) = make_ulonglong2(a0, a1);
+    }
+    __syncthreads();
+    const unsigned long long base = S.base;
+    const unsigned long long n = base < cap ? min(S.n, cap - base) : 0ull;
+    constexpr uint32_t RW = sizeof(fluere_record) / 8;
+    uint2* dst = reinterpret_cast<uint2*>(out + base);
+    for (uint32_t i = threadIdx.x; i < n * RW; i += EMIT_BLOCK) {
+        const uint32_t k = i / RW, wd = i - k * RW;
+        dst[i] = reinterpret_cast<const uint2*>(&S.rec[S.slot[k]])[wd];
+    }
+    __syncthreads();
 }
 
 __device__ __forceinline__ void update_flow(fluere_record& r, bool rev, const PktInfo& pi, uint64_t t) {

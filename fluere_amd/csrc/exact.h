@@ -56,6 +56,21 @@ __device__ __forceinline__ uint64_t tree_first(const unsigned long long* tree, u
     }
 }
 
+// A pinned host mailbox for the few device scalars a run needs on the host
+// (counts that size the next launches): one wave copies them in and then
+// writes seq; the host spins on seq.  A hipMemcpyAsync + hipStreamSynchronize
+// round trip costs a copy kernel and the blocking wake-up (measured 20-45 us
+// of idle GPU per round trip on MI355X in the exact engine's timeline).
+struct alignas(64) HostMail {
+    uint32_t seq;       // written by the device last
+    uint32_t host_seq;  // the host's last request (never written by the device)
+    unsigned long long v[14];
+};
+constexpr int MAIL_MAX = 14;
+// out[i] = the `bytes[i]`-byte (1, 4 or 8) value at device address src[i],
+// stream-ordered after the work enqueued on s; m null: copies + a stream sync.
+int mail_fetch(HostMail* m, hipStream_t s, int n, const void* const* src, const int* bytes, unsigned long long* out);
+
 struct ExactJob {
     const Batch* d_batches;  // device copy of the batches
     const Batch* h_batches;  // host copy (per-batch launches)
@@ -85,6 +100,12 @@ struct ExactJob {
     uint64_t ext_n = 0;
     // Mode A: the complex-flow filter (device.h ckey_bucket), or null
     const uint32_t* cbits = nullptr;
+    // pinned mailbox for the host's scalar reads (null: copies + stream syncs)
+    HostMail* mail = nullptr;
+    // Mode B without a caller-provided aux_out (one GPU): the records' order
+    // words, grown to the record count (records already there keep zeros)
+    unsigned long long** recaux = nullptr;
+    uint64_t* recaux_cap = nullptr;
 };
 
 struct ExactResult {

@@ -53,7 +53,6 @@ namespace fl {
 namespace {
 
 constexpr uint64_t M40 = (1ull << 40) - 1;
-constexpr uint64_t HI_ACTIVE = (1ull << 41) - 1;  // Mode B order key of an active record (after every ended one)
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr int MAX_PASSES = 32;
 enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2, K_LEAD = 3 };
@@ -583,13 +582,16 @@ struct RecArgs {
     const unsigned long long* iie;
     const unsigned long long* iex;
     Glob* g;
-    fluere_record* out;      // Mode A: the run's records (appended)
+    fluere_record* out;      // the run's records (appended)
     uint64_t out_cap;
-    fluere_record* tmp;      // Mode B: by instance, ordered afterwards
-    unsigned long long* hi;  // Mode B order: (sweeping / closing index, phase)
-    unsigned long long* lo;  //               (the firing entry's creation index)
-    unsigned long long* ex;  //               (the firing entry's exp; between hi and lo)
-    uint32_t* idx;
+    // Mode B: two order words beside each record (indexed like out): {0 for a
+    // FIN/RST close, else the firing entry's exp + 1; its creation index}.
+    // With order_key = the ending packet's index they give the reference's
+    // emission order (by ending packet, FIN/RST before the sweep, sweeps by
+    // (exp, push order); offline_fluereflows.rs:152-175); fetch_records sorts by them.
+    unsigned long long* aux;
+    uint32_t* defer;         // k_ex_records_t<false> -> <true>: instances for the general parser
+    uint32_t* n_defer;       //   (their count, device)
     int shard_mode;
     const uint8_t* irole;
     const uint32_t* ikey;
@@ -606,132 +608,125 @@ __device__ __forceinline__ void piece_of(const Agg& g, fluere_flow_piece& pc) {
     pc.last_time = g.lastt;
 }
 
-__global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records(RecArgs a) {
-    __shared__ EmitLds S;
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;  // instance (a run of the flow's packets)
-    const bool lane_live = q < a.n_inst;
-    fluere_record rec;
-    memset(&rec, 0, sizeof rec);
-    uint8_t kind = K_ACTIVE;
-    unsigned long long cj = NONE64, cie = 0, cex = 0;
-    if (lane_live && a.shard_mode && a.irole[a.ist[q]] != R_RECORD) {
-        // a piece of the flow's annex (lead / head / tail), not a record
-        const uint32_t c = a.ist[q];
-        const ExMeta mc = a.sm[c];
-        const uint8_t role = a.irole[c];
-        fluere_flow_annex& ax = a.annex[a.ikey[c]];
-        fluere_flow_piece pc;
-        memset(&pc, 0, sizeof pc);
-        piece_of(a.aggs[q], pc);
-        pc.first = mc.gidx;
-        pc.first_time = mc.t;
-        if (role != R_LEAD) {
-            Parsed P;
-            parse_global(a.bs, a.nb, mc.gidx, a.macs != 0, P);
-            fluere_record sd;
-            fill_seed(sd, P);
-            for (int k = 0; k < 16; k++) { pc.src[k] = sd.source[k]; pc.dst[k] = sd.destination[k]; }
-            pc.v6 = sd.src_v6; pc.prot = sd.prot; pc.tos = sd.tos; pc.dir = mc.dir;
-            pc.src_port = sd.src_port; pc.dst_port = sd.dst_port;
-        }
-        if (role == R_LEAD) ax.lead = pc;
-        if (role == R_HEAD || role == R_HEAD_TAIL) ax.head = pc;
-        if (role == R_TAIL) ax.tail = pc;
-    }
-    const bool rec_live = lane_live && !(a.shard_mode && a.irole[a.ist[q]] != R_RECORD);
-    if (rec_live && a.shard_mode)  // the flow's last processed packet among its in-shard records (live mode)
-        atomicMax(reinterpret_cast<unsigned long long*>(&a.annex[a.ikey[a.ist[q]]].mid_last),
-                  (unsigned long long)a.aggs[q].lastg + 1);
-    if (rec_live) {
-        const uint32_t c = a.ist[q];
-        const ExMeta mc = a.sm[c];
-        if (a.seeds) {  // sharded Mode B: the creating packet is on another shard
-            const Seed sd = a.seeds[q];
-            for (int k = 0; k < 16; k++) { rec.source[k] = sd.src[k]; rec.destination[k] = sd.dst[k]; }
-            rec.src_v6 = rec.dst_v6 = sd.v6;
-            rec.prot = sd.prot; rec.tos = sd.tos; rec.src_port = sd.sp; rec.dst_port = sd.dp;
-            rec.first = mc.t;
-        } else {
-            Parsed P;
-            parse_global(a.bs, a.nb, mc.gidx, a.macs != 0, P);
-            fill_seed(rec, P);
-        }
-        const Agg g = a.aggs[q];
-        const uint32_t o = mc.dir;  // orientation of the creating packet
-        rec.d_pkts = g.pk[0] + g.pk[1];
-        rec.d_octets = g.by[0] + g.by[1];
-        rec.out_pkts = g.pk[o];
-        rec.in_pkts = g.pk[1 - o];
-        rec.out_bytes = g.by[o];
-        rec.in_bytes = g.by[1 - o];
-        rec.min_pkt = g.mnp;
-        rec.max_pkt = g.mxp;
-        rec.min_ttl = (uint8_t)g.mnt;
-        rec.max_ttl = (uint8_t)g.mxt;
-        for (int k = 0; k < 8; k++) rec.cnt[k] = g.fl[k];
-        rec.cnt[8] = 0;
-        rec.last = g.lastt;
-        kind = a.ikind[c];
-        cj = a.ij[c];
-        cie = a.iie[c];
-        cex = a.iex[c];
-        rec.order_key = kind == K_ACTIVE ? NONE64 : cj;
-    }
-    if (!a.mode_b) {  // (uniform: every thread of the block emits)
-        emit_record_block(S, a.g, a.out, a.out_cap, rec, rec_live);
-        return;
-    }
-    if (rec_live) {
-        a.tmp[q] = rec;
-        a.hi[q] = kind == K_ACTIVE ? HI_ACTIVE : (cj << 1) | (kind == K_SWEEP ? 1ull : 0ull);
-        a.lo[q] = kind == K_SWEEP ? cie : 0ull;
-        a.ex[q] = kind == K_SWEEP ? cex : 0ull;
-        a.idx[q] = q;
-    }
+// The creating packet's parse: the register parser alone in the fast
+// kernel (P.cls = 2: the instance is listed for the general one).
+template <bool GEN>
+__device__ __forceinline__ void ex_parse(const RecArgs& a, uint64_t gi, Parsed& P) {
+    if constexpr (GEN) parse_global(a.bs, a.nb, gi, a.macs != 0, P);
+    else parse_global_fast(a.bs, a.nb, gi, a.macs != 0, P);
 }
 
-// Mode B: records in the reference's emission order; order_key = rank
-__global__ void __launch_bounds__(EMIT_BLOCK) k_ex_emit_sorted(uint32_t n_inst, const uint32_t* perm, const fluere_record* tmp,
-                                                               Glob* g, fluere_record* out, uint64_t cap) {
+// Records (and, in shard mode, annex pieces) of the instances.  GEN false:
+// instance q = the thread's index, the register parser only, instances whose
+// creating packet it declines listed in a.defer; GEN true: the listed ones,
+// with the general parser.  Each thread builds its record in place in the
+// block's LDS staging (S.rec[thread]): held in registers, the record and the
+// general parser took the kernel to 178 VGPRs (2 waves per SIMD).
+template <bool GEN>
+__global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records_t(RecArgs a) {
     __shared__ EmitLds S;
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    fluere_record rec;
-    const bool live = r < n_inst;
-    if (live) {
-        rec = tmp[perm[r]];
-        if (rec.order_key != NONE64) rec.order_key = r;
-    } else {
-        memset(&rec, 0, sizeof rec);
-    }
-    emit_record_block(S, g, out, cap, rec, live);
-}
-
-// sharded Mode B: records in the reference's order at fixed positions; the
-// order stays global (order_key = the ending packet's index, aux = {0 for a
-// FIN/RST close, else exp + 1; the firing entry's creation}) so the records of
-// every owner merge by (order_key, aux) (fluere_get_record_order)
-__global__ void __launch_bounds__(256) k_ex_emit_owner(uint32_t n_inst, const uint32_t* perm, const fluere_record* tmp,
-                                                       const unsigned long long* hi, const unsigned long long* ex,
-                                                       const unsigned long long* lo, Glob* g, fluere_record* out,
-                                                       unsigned long long* aux) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = r < n_inst;
-    unsigned long long upd = 0, ended = 0;
-    if (live) {
-        const uint32_t q = perm[r];
-        const fluere_record rec = tmp[q];
-        out[r] = rec;
-        const unsigned long long h = hi[q];
-        aux[2 * r] = h == HI_ACTIVE ? 0ull : ((h & 1) ? ex[q] + 1 : 0ull);
-        aux[2 * r + 1] = h == HI_ACTIVE ? 0ull : lo[q];
-        upd = rec.d_pkts;
-        ended = rec.order_key != NONE64;
-    }
-    upd = wave_sum(upd);
-    ended = wave_sum(ended);
-    if ((threadIdx.x & 63) == 0) {
-        if (upd) atomicAdd(&g->n_updates, upd);
-        if (ended) atomicAdd(&g->n_ended, ended);
+    const uint32_t n_items = GEN ? min(*a.n_defer, a.n_inst) : a.n_inst;
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n_items; i0 += gridDim.x * blockDim.x) {  // (uniform)
+        const uint32_t i = i0 + threadIdx.x;
+        const bool lane_live = i < n_items;
+        const uint32_t q = lane_live ? (GEN ? a.defer[i] : i) : 0u;  // instance (a run of the flow's packets)
+        fluere_record& rec = S.rec[threadIdx.x];
+        uint8_t kind = K_ACTIVE;
+        unsigned long long cie = 0, cex = 0;
+        bool defer = false, rec_live = false;
+        const uint32_t c = lane_live ? a.ist[q] : 0u;
+        const uint8_t role = (lane_live && a.shard_mode) ? a.irole[c] : (uint8_t)R_RECORD;
+        if (lane_live && role != R_RECORD) {
+            // a piece of the flow's annex (lead / head / tail), not a record:
+            // built in this thread's (unused) record slot, then copied out
+            const ExMeta mc = a.sm[c];
+            fluere_flow_piece& pc = *reinterpret_cast<fluere_flow_piece*>(&S.rec[threadIdx.x]);
+            Parsed P;
+            if (role != R_LEAD) {
+                ex_parse<GEN>(a, mc.gidx, P);
+                defer = !GEN && P.cls == 2;
+            }
+            if (!defer) {
+                memset(&pc, 0, sizeof pc);
+                piece_of(a.aggs[q], pc);
+                pc.first = mc.gidx;
+                pc.first_time = mc.t;
+                if (role != R_LEAD) {  // fill_seed's fields (device.h)
+                    const PktInfo& pi = P.pi;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            pc.src[4 * k + b] = (uint8_t)(pi.rsip[k] >> (24 - 8 * b));
+                            pc.dst[4 * k + b] = (uint8_t)(pi.rdip[k] >> (24 - 8 * b));
+                        }
+                    pc.v6 = pi.rv6; pc.prot = pi.rprot; pc.tos = pi.rtos; pc.dir = mc.dir;
+                    pc.src_port = pi.rsp; pc.dst_port = pi.rdp;
+                }
+                fluere_flow_annex& ax = a.annex[a.ikey[c]];
+                if (role == R_LEAD) ax.lead = pc;
+                if (role == R_HEAD || role == R_HEAD_TAIL) ax.head = pc;
+                if (role == R_TAIL) ax.tail = pc;
+            }
+        } else if (lane_live) {
+            const ExMeta mc = a.sm[c];
+            if (a.seeds) {  // sharded Mode B: the creating packet is on another shard
+                const Seed sd = a.seeds[q];
+                memset(&rec, 0, sizeof rec);
+#pragma unroll
+                for (int k = 0; k < 16; k++) { rec.source[k] = sd.src[k]; rec.destination[k] = sd.dst[k]; }
+                rec.src_v6 = rec.dst_v6 = sd.v6;
+                rec.prot = sd.prot; rec.tos = sd.tos; rec.src_port = sd.sp; rec.dst_port = sd.dp;
+                rec.first = mc.t;
+            } else {
+                Parsed P;
+                ex_parse<GEN>(a, mc.gidx, P);
+                defer = !GEN && P.cls == 2;
+                if (!defer) fill_seed(rec, P);
+            }
+            if (!defer) {
+                rec_live = true;
+                if (a.shard_mode)  // the flow's last processed packet among its in-shard records (live mode)
+                    atomicMax(reinterpret_cast<unsigned long long*>(&a.annex[a.ikey[c]].mid_last),
+                              (unsigned long long)a.aggs[q].lastg + 1);
+                const Agg g = a.aggs[q];
+                const bool o = mc.dir != 0;  // orientation of the creating packet (selects: no indexed copy of g)
+                const uint32_t p0 = g.pk[0], p1 = g.pk[1];
+                const unsigned long long b0 = g.by[0], b1 = g.by[1];
+                rec.d_pkts = p0 + p1;
+                rec.d_octets = b0 + b1;
+                rec.out_pkts = o ? p1 : p0;
+                rec.in_pkts = o ? p0 : p1;
+                rec.out_bytes = o ? b1 : b0;
+                rec.in_bytes = o ? b0 : b1;
+                rec.min_pkt = g.mnp;
+                rec.max_pkt = g.mxp;
+                rec.min_ttl = (uint8_t)g.mnt;
+                rec.max_ttl = (uint8_t)g.mxt;
+                for (int k = 0; k < 8; k++) rec.cnt[k] = g.fl[k];
+                rec.cnt[8] = 0;
+                rec.last = g.lastt;
+                kind = a.ikind[c];
+                cie = a.iie[c];
+                cex = a.iex[c];
+                rec.order_key = kind == K_ACTIVE ? NONE64 : a.ij[c];
+            }
+        }
+        if (!GEN) {  // instances for the general parser: listed (wave-aggregated append)
+            const uint64_t dm = __ballot(defer);
+            if (dm) {
+                const uint32_t lead = __builtin_ctzll(dm);
+                uint32_t b0 = 0;
+                if ((uint32_t)(threadIdx.x & 63) == lead) b0 = atomicAdd(a.n_defer, (uint32_t)__popcll(dm));
+                b0 = __shfl(b0, lead, 64);
+                if (defer)
+                    a.defer[b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] = q;
+            }
+        }
+        // (uniform: every thread of the block emits)
+        emit_inplace_block(S, a.g, a.out, a.out_cap, rec_live, rec_live ? rec.d_pkts : 0u,
+                           rec_live && rec.order_key != NONE64, a.mode_b ? a.aux : nullptr,
+                           kind == K_SWEEP ? cex + 1 : 0ull, kind == K_SWEEP ? cie : 0ull);
     }
 }
 
@@ -744,13 +739,26 @@ __global__ void __launch_bounds__(256) k_ex_seed_req(uint32_t n_inst, const uint
     }
 }
 
-__global__ void __launch_bounds__(256) k_ex_gather_u64(uint32_t m, const uint32_t* id, const unsigned long long* h,
-                                                       unsigned long long* out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) out[i] = h[id[i]];
-}
-
 unsigned gridn(uint64_t n, unsigned b) { return (unsigned)std::max<uint64_t>(1, (n + b - 1) / b); }
+
+struct MailSrc {
+    const void* p[MAIL_MAX];
+    int bytes[MAIL_MAX];
+    int n;
+};
+// One wave: the values, then (after the wave's system-scope fence) seq.
+__global__ void __launch_bounds__(64) k_mail(MailSrc a, HostMail* m, uint32_t seq) {
+    const int l = threadIdx.x;
+    if (l < a.n) {
+        const int b = a.bytes[l];
+        const unsigned long long v = b == 8 ? *static_cast<const unsigned long long*>(a.p[l])
+                                     : b == 4 ? (unsigned long long)*static_cast<const uint32_t*>(a.p[l])
+                                              : (unsigned long long)*static_cast<const uint8_t*>(a.p[l]);
+        __hip_atomic_store(&m->v[l], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __threadfence_system();
+    if (l == 0) __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // bump allocator over the scratch arena (256-byte aligned pieces)
 struct Arena {
@@ -767,6 +775,39 @@ struct Arena {
 
 }  // namespace
 
+int mail_fetch(HostMail* m, hipStream_t s, int n, const void* const* src, const int* bytes, unsigned long long* out) {
+    if (n < 0 || n > MAIL_MAX) return FLUERE_E_ARG;
+    if (!m) {  // no mailbox: one copy per value, then a stream sync
+        for (int i = 0; i < n; i++) {
+            out[i] = 0;
+            HIPCHECK(hipMemcpyAsync(&out[i], src[i], bytes[i], hipMemcpyDeviceToHost, s));
+        }
+        HIPCHECK(hipStreamSynchronize(s));
+        return FLUERE_OK;
+    }
+    MailSrc a{};
+    a.n = n;
+    for (int i = 0; i < n; i++) {
+        a.p[i] = src[i];
+        a.bytes[i] = bytes[i];
+    }
+    const uint32_t seq = ++m->host_seq ? m->host_seq : ++m->host_seq;  // never 0 (the initial value)
+    k_mail<<<1, 64, 0, s>>>(a, m, seq);
+    HIPCHECK(hipGetLastError());
+    for (uint32_t spin = 1;; spin++) {
+        if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) == seq) break;
+        if ((spin & 1023) == 0) {  // now and then: did the stream fail instead?
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) == seq) break;
+            HIPCHECK(q);
+            return FLUERE_E_HIP;  // the stream finished without writing seq: cannot happen
+        }
+    }
+    for (int i = 0; i < n; i++) out[i] = __atomic_load_n(&m->v[i], __ATOMIC_RELAXED);
+    return FLUERE_OK;
+}
+
 // One exact run, in phases (exact.h): the arena views and the host state
 // between them.
 struct ExactSession {
@@ -781,14 +822,12 @@ struct ExactSession {
     ExMeta *cm, *sm;
     uint32_t *key, *skey;
     unsigned long long *re, *rf, *ne_rev, *nf_rev, *npr, *np_rev, *ej, *ij, *iie, *iex;
-    unsigned long long *hi, *lo, *ex, *hi2, *gk, *tree;
-    unsigned long long nrec_new = 0;
+    unsigned long long *hi2, *tree;
     uint64_t tree_P = 0;
     uint32_t *val, *sval, *hf, *hpos, *heads, *link, *plink, *sflag, *iend, *incl, *ist, *alist, *ctr, *tbl;
-    uint32_t *idx, *idx2, *perm, *ikey;
+    uint32_t *idx, *ikey;
     uint8_t *pr, *ikind, *irole;
     Agg* aggs;
-    fluere_record* tmpr;
     fluere_flow_annex* annex = nullptr;
     ChaseArgs ca;
 };
@@ -824,9 +863,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         add(n * 8);                                                   // iex
         add(n * 4); add(n * 4); add(n * 4);                           // incl, ist, alist
         add(n * sizeof(Agg)); add(16);                                // aggs, nruns/counters
-        add(n * sizeof(fluere_record)); add(n * 8); add(n * 8);       // tmp, hi, lo
-        add(n * 8); add(n * 8);                                       // ex, gk
-        add(n * 4); add(n * 4); add(n * 8); add(n * 4);               // idx, idx2, hi2, perm
+        add(n * 4); add(n * 8);                                       // idx, hi2 (seed requests)
         add(n); add(n * 4);                                           // irole, ikey
         if (J.mode_b) add(2 * P * 8);                                 // tree
         add((n / 16 + 4) * 4);                                        // tbl
@@ -904,16 +941,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     S->ist = A.take<uint32_t>(N);
     S->alist = A.take<uint32_t>(N);
     S->aggs = A.take<Agg>(N);
-    uint32_t* ctr = S->ctr = A.take<uint32_t>(4);  // [0..1] aggregate lists, [1] non-monotonic (begin), [2] changed
-    S->tmpr = A.take<fluere_record>(N);
-    S->hi = A.take<unsigned long long>(N);
-    S->lo = A.take<unsigned long long>(N);
-    S->ex = A.take<unsigned long long>(N);
-    S->gk = A.take<unsigned long long>(N);
+    uint32_t* ctr = S->ctr = A.take<uint32_t>(4);  // [0..1] aggregate lists, [1] non-monotonic (begin), [2] changed, [3] deferred records
     S->idx = A.take<uint32_t>(N);
-    S->idx2 = A.take<uint32_t>(N);
     S->hi2 = A.take<unsigned long long>(N);
-    S->perm = A.take<uint32_t>(N);
     S->irole = A.take<uint8_t>(N);
     S->ikey = A.take<uint32_t>(N);
     S->tree = J.mode_b ? A.take<unsigned long long>(2 * P) : nullptr;
@@ -928,11 +958,12 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     } else {
         const int iN = (int)N;
         HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, iN, s));
-        uint32_t last[2] = {0, 0};
-        HIPCHECK(hipMemcpyAsync(&last[0], pos + N - 1, 4, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipMemcpyAsync(&last[1], flag + N - 1, 4, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
-        n = (uint64_t)last[0] + last[1];
+        unsigned long long last[2] = {0, 0};
+        const void* src[2] = {pos + N - 1, flag + N - 1};
+        const int by[2] = {4, 4};
+        int rc = mail_fetch(J.mail, s, 2, src, by, last);
+        if (rc) return rc;
+        n = last[0] + last[1];
         if (n) k_ex_compact<<<gridn(N, 256), 256, 0, s>>>(meta, flag, pos, N, cm, key, val);
     }
     S->n = n;
@@ -954,20 +985,22 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     tb = tmp;
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, hf, hpos, in, s));
     k_ex_heads<<<gridn(n, 256), 256, 0, s>>>(n, hf, hpos, heads);
-    uint32_t last[2] = {0, 0};
-    HIPCHECK(hipMemcpyAsync(&last[0], hpos + n - 1, 4, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(&last[1], hf + n - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipMemsetAsync(ctr, 0, 16, s));
     if (J.mode_b) {
         k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1);
         HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed
     }
-    uint32_t mono_bad = 0;
-    HIPCHECK(hipMemcpyAsync(&mono_bad, ctr + 1, 4, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    S->n_keys = last[0] + last[1];
+    // one host read: key count, monotonicity, the first and last times
+    unsigned long long hv[5] = {0, 0, 0, 0, 0};
+    {
+        const void* src[5] = {hpos + n - 1, hf + n - 1, ctr + 1, &cm[0].t, &cm[n - 1].t};
+        const int by[5] = {4, 4, 4, 8, 8};
+        int rc = mail_fetch(J.mail, s, J.mode_b ? 5 : 2, src, by, hv);
+        if (rc) return rc;
+    }
+    S->n_keys = (uint32_t)(hv[0] + hv[1]);
     S->R.keys = S->n_keys;
-    S->mono = !mono_bad;
+    S->mono = !hv[2];
     if (J.shard_mode) {
         if (S->n_keys > *J.annex_cap) {
             hipFree(*J.annex);
@@ -983,10 +1016,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     // bucket): a sweep point's lower_bound searches one bucket, not the capture
     uint64_t t0 = 0, bw = 1, nb = 0;
     if (J.mode_b && S->mono) {
-        unsigned long long tt[2] = {0, 0};
-        HIPCHECK(hipMemcpyAsync(&tt[0], &cm[0].t, 8, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipMemcpyAsync(&tt[1], &cm[n - 1].t, 8, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        const unsigned long long tt[2] = {hv[3], hv[4]};
         t0 = tt[0];
         nb = n / 16 + 1;
         bw = std::max<uint64_t>(1, (tt[1] - tt[0]) / nb + 1);  // nb * bw > the span
@@ -1033,9 +1063,11 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     HIPCHECK(hipGetLastError());
     if (pr_out) HIPCHECK(hipMemcpyAsync(pr_out, S->pr, n, hipMemcpyDeviceToDevice, s));
     if (!J.mode_b) return FLUERE_OK;
-    uint32_t ch = 0;
-    HIPCHECK(hipMemcpyAsync(&ch, S->ctr + 2, 4, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    unsigned long long ch = 0;
+    const void* src[1] = {S->ctr + 2};
+    const int by[1] = {4};
+    int rc = mail_fetch(J.mail, s, 1, src, by, &ch);
+    if (rc) return rc;
     if (changed) *changed = ch != 0;
     return FLUERE_OK;
 }
@@ -1065,11 +1097,17 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     hipStream_t s = S->s;
     const uint64_t n = S->n;
     if (!n) return FLUERE_OK;
-    size_t tb;
-    uint32_t n_inst = 0;
-    HIPCHECK(hipMemcpyAsync(&n_inst, S->incl + n - 1, 4, hipMemcpyDeviceToHost, s));
+    // one host read: the instance count and the records already emitted
+    unsigned long long hv[2] = {0, 0};
+    {
+        const void* src[2] = {S->incl + n - 1, reinterpret_cast<const char*>(J.g) + offsetof(Glob, n_rec)};
+        const int by[2] = {4, 8};
+        int rc = mail_fetch(J.mail, s, 2, src, by, hv);
+        if (rc) return rc;
+    }
+    const uint32_t n_inst = (uint32_t)hv[0];
+    const uint64_t n_rec0 = hv[1];
     // ---- 6. per-instance aggregates over each instance's contiguous run
-    HIPCHECK(hipStreamSynchronize(s));  // (n_inst)
     HIPCHECK(hipMemsetAsync(S->ctr, 0, 8, s));
     if (n_inst) {
         k_ex_agg<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
@@ -1079,55 +1117,51 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     HIPCHECK(hipGetLastError());
     S->R.instances = n_inst;
     // ---- 7. records
-    Glob gh;
-    HIPCHECK(hipMemcpyAsync(&gh, J.g, sizeof gh, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    const uint64_t want = gh.n_rec + n_inst;
+    const uint64_t want = n_rec0 + n_inst;
     if (want > *J.d_recs_cap) {  // grow, keeping the records already there
         fluere_record* nr = nullptr;
         if (hipMalloc(&nr, want * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
-        if (gh.n_rec)
-            HIPCHECK(hipMemcpyAsync(nr, *J.d_recs, gh.n_rec * sizeof(fluere_record), hipMemcpyDeviceToDevice, s));
+        if (n_rec0)
+            HIPCHECK(hipMemcpyAsync(nr, *J.d_recs, n_rec0 * sizeof(fluere_record), hipMemcpyDeviceToDevice, s));
         HIPCHECK(hipStreamSynchronize(s));
         hipFree(*J.d_recs);
         *J.d_recs = nr;
         *J.d_recs_cap = want;
     }
-    RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, n_inst, S->aggs, S->ist, S->sm, S->iend, S->ikind,
-               S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, S->tmpr, S->hi, S->lo, S->ex, S->idx,
-               J.shard_mode, S->irole, S->ikey, S->annex, seeds};
-    // runs <= n (every run holds a packet)
-    k_ex_records<<<gridn(n_inst, 256), 256, 0, s>>>(ra);
-    if (J.mode_b && n_inst) {
-        // order by (closing / sweeping index, phase), then the firing entry's
-        // (exp, creation): stable radix sorts from the last key to the first
-        const int ni = (int)n_inst;
-        uint32_t* cur = S->idx;   // permutation so far (k_ex_records: the identity)
-        uint32_t* nxt = S->idx2;
-        tb = S->tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->lo, S->hi2, cur, nxt, ni, 0, 40, s));
-        std::swap(cur, nxt);
-        if (!S->mono) {  // exp order differs from creation order only when times go backwards
-            k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, cur, S->ex, S->gk);
-            tb = S->tmp;
-            HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->gk, S->hi2, cur, nxt, ni, 0, 64, s));
-            std::swap(cur, nxt);
-        }
-        k_ex_gather_u64<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, cur, S->hi, S->gk);
-        tb = S->tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->gk, S->hi2, cur, S->perm, ni, 0, 41, s));
+    // Mode B: the order words beside the records (indexed like them); the
+    // caller's aux_out is the slot of record n_rec0
+    unsigned long long* aux = nullptr;
+    if (J.mode_b) {
         if (aux_out) {
-            k_ex_emit_owner<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->perm, S->tmpr, S->hi, S->ex, S->lo,
-                                                               J.g, *J.d_recs + gh.n_rec, aux_out);
-            S->nrec_new = gh.n_rec + n_inst;
-            HIPCHECK(hipMemcpyAsync(reinterpret_cast<char*>(J.g) + offsetof(Glob, n_rec), &S->nrec_new, 8,
-                                    hipMemcpyHostToDevice, s));
+            aux = aux_out - 2 * n_rec0;
         } else {
-            k_ex_emit_sorted<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->perm, S->tmpr, J.g, *J.d_recs, *J.d_recs_cap);
+            if (!J.recaux || !J.recaux_cap) return FLUERE_E_ARG;
+            if (want > *J.recaux_cap) {
+                HIPCHECK(hipStreamSynchronize(s));  // (the old buffer may still be in use)
+                hipFree(*J.recaux);
+                *J.recaux = nullptr;
+                *J.recaux_cap = 0;
+                if (hipMalloc(J.recaux, std::max<uint64_t>(want, 1) * 16) != hipSuccess) return FLUERE_E_NOMEM;
+                *J.recaux_cap = std::max<uint64_t>(want, 1);
+            }
+            if (n_rec0) HIPCHECK(hipMemsetAsync(*J.recaux, 0, n_rec0 * 16, s));
+            aux = *J.recaux;
         }
     }
+    RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, n_inst, S->aggs, S->ist, S->sm, S->iend, S->ikind,
+               S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, aux, S->idx, S->ctr + 3,
+               J.shard_mode, S->irole, S->ikey, S->annex, seeds};
+    // runs <= n (every run holds a packet); records appended per block, Mode B
+    // with their order words (fetch_records orders them: no device sort).
+    // The instances whose creating packet needs the general parser are listed
+    // by the first kernel and done by the second (grid-stride over the count).
+    if (n_inst) {
+        HIPCHECK(hipMemsetAsync(S->ctr + 3, 0, 4, s));
+        k_ex_records_t<false><<<gridn(n_inst, 256), 256, 0, s>>>(ra);
+        k_ex_records_t<true><<<std::min<unsigned>(gridn(n_inst, 256), 64), 256, 0, s>>>(ra);
+    }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(s));
+    // (every caller reads the run counters back with a stream-ordered copy)
     return FLUERE_OK;
 }
 

@@ -1257,6 +1257,8 @@ struct FinArgs {
     uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
     unsigned long long timeout_us;  // non-zero: skip the flows when expiries can fire (Mode B redoes every flow)
     uint32_t* cbits = nullptr;      // the exact engine's complex-flow filter (ckey_bucket), or null
+    uint32_t* defer = nullptr;      // k_finalize: certified flows whose first packet needs the general
+                                    // parser (Glob::n_fdefer of them), finalized by k_finalize_gen
 };
 
 // A flow's order-free aggregate (the accumulators of one dense id).
@@ -1281,7 +1283,10 @@ __device__ __forceinline__ void load_acc(const Acc& A, uint32_t d, AccVals& v) {
 }
 
 // Certified flow d -> its record; false when d has no record here (TCP flow
-// without a SYN: dropped; complex: marked for the per-flow state machine).
+// without a SYN: dropped; complex: marked for the per-flow state machine;
+// GEN false: a first packet the register parser declines is listed for
+// k_finalize_gen, whose general parser would cost k_finalize its occupancy).
+template <bool GEN>
 __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, const AccVals& v, fluere_record& r,
                                               bool& cplx, unsigned long long& cplx_pkts) {
     const unsigned long long fa = v.fa, fc = v.fc, fr = v.fr, la = v.la;
@@ -1308,7 +1313,15 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
     const uint64_t t_last = record_time(BQ, oq);  // the last packet: its time only
     pin_win(WP);
     Parsed P;
-    parse_loaded(BP, op, WP, macs, 0, P);
+    if constexpr (GEN) {
+        parse_loaded(BP, op, WP, macs, 0, P);
+    } else {
+        parse_loaded_fast(BP, op, WP, macs, P);
+        if (P.cls == 2) {
+            a.defer[atomicAdd(&a.g->n_fdefer, 1ull)] = d;
+            return false;
+        }
+    }
     const uint8_t cd = canon_dir(P, macs);
     fill_seed(r, P);
     const uint32_t p0 = v.pk[0], p1 = v.pk[1];
@@ -1326,11 +1339,12 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
     return true;
 }
 
+template <bool GEN>
 __device__ __forceinline__ bool finalize_one(const FinArgs& a, uint32_t d, fluere_record& r, bool& cplx,
                                              unsigned long long& cplx_pkts) {
     AccVals v;
     load_acc(a.A, d, v);
-    return finalize_vals(a, d, v, r, cplx, cplx_pkts);
+    return finalize_vals<GEN>(a, d, v, r, cplx, cplx_pkts);
 }
 
 // emit + complex-flow counters of one wave's flows (every lane of the wave)
@@ -2056,6 +2070,8 @@ __device__ void publish_ctl(Glob* g, unsigned long long* done, Ctl* host_ctl, ui
 
 // k_finalize: one thread per flow (grid-stride); records appended per
 // workgroup (emit_record_block).
+// The record is built in place in the block's LDS staging (S.rec[thread]):
+// held in registers it took the kernel to 250 VGPRs (2 waves per SIMD).
 __global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
     const Glob& gg = *a.g;
     const bool mode_b = a.timeout_us && gg.valid && gg.tmax - gg.tmin >= a.timeout_us;
@@ -2063,13 +2079,36 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
     __shared__ EmitLds S;
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
         const uint32_t d = d0 + threadIdx.x;
+        fluere_record& r = S.rec[threadIdx.x];
+        bool cplx = false;
+        unsigned long long cplx_pkts = 0;
+        const bool want = d < nf && finalize_one<false>(a, d, r, cplx, cplx_pkts);
+        emit_inplace_block(S, a.g, a.out, a.out_cap, want, want ? r.d_pkts : 0u, want && r.order_key != NONE64);
+        const uint64_t cm = __ballot(cplx);
+        if (cm) {
+            const unsigned long long pk = wave_sum(cplx_pkts);
+            if ((uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm)) {
+                atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
+                atomicAdd(&a.g->n_complex_pkts, pk);
+            }
+        }
+    }
+    if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
+}
+
+// k_finalize_gen: the flows k_finalize listed (first packet outside the
+// register parser's classes), with the general parser.
+__global__ void __launch_bounds__(EMIT_BLOCK) k_finalize_gen(FinArgs a) {
+    const uint32_t n = (uint32_t)min(a.g->n_fdefer, (unsigned long long)a.T.fmax);
+    __shared__ EmitLds S;
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
         fluere_record r;
         bool cplx = false;
         unsigned long long cplx_pkts = 0;
-        const bool want = d < nf && finalize_one(a, d, r, cplx, cplx_pkts);
+        const bool want = i < n && finalize_one<true>(a, a.defer[i], r, cplx, cplx_pkts);
         finalize_emit(S, a, r, want, cplx, cplx_pkts);
     }
-    if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -2215,12 +2254,14 @@ struct CleanArgs {
     // fluere_run takes the same decision on the host from the copied counters.
     int spec;
     unsigned long long timeout_us, recs_cap;
+    int abl = 0;  // diagnostics only (FLUERE_CLEAN_ABL, wrong results): 1 no table clears, 2 no accumulator clears
 };
 
 __device__ __host__ __forceinline__ bool run_complete(const Glob& g, uint32_t err, unsigned long long timeout_us,
                                                       unsigned long long recs_cap) {
     const bool modeB = g.valid && (g.tmax - g.tmin) >= timeout_us;
-    return !(err & (ERR_TABLE_FULL | ERR_SPIN | ERR_FLOWS_FULL)) && !modeB && g.n_complex == 0 && g.n_rec <= recs_cap;
+    return !(err & (ERR_TABLE_FULL | ERR_SPIN | ERR_FLOWS_FULL)) && !modeB && g.n_complex == 0 && g.n_rec <= recs_cap &&
+           g.n_fdefer == 0;
 }
 
 __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool tables) {
@@ -2234,10 +2275,11 @@ __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool
 #pragma unroll
     for (int t = 0; t < N_TABLES / 2; t++) {
         const uint32_t s0 = sv[t].x, s1 = sv[t].y;
-        if (tables && s0 != NONE32) { a.T.tab[2 * t][2 * s0] = EMPTY; a.T.tab[2 * t][2 * s0 + 1] = EMPTY; }
-        if (tables && s1 != NONE32) { a.T.tab[2 * t + 1][2 * s1] = EMPTY; a.T.tab[2 * t + 1][2 * s1 + 1] = EMPTY; }
+        if (tables && !(a.abl & 1) && s0 != NONE32) { a.T.tab[2 * t][2 * s0] = EMPTY; a.T.tab[2 * t][2 * s0 + 1] = EMPTY; }
+        if (tables && !(a.abl & 1) && s1 != NONE32) { a.T.tab[2 * t + 1][2 * s1] = EMPTY; a.T.tab[2 * t + 1][2 * s1 + 1] = EMPTY; }
         if ((s0 & s1) != NONE32) row[t] = make_uint2(NONE32, NONE32);
     }
+    if (a.abl & 2) return;
     a.A.pk[0][d] = a.A.pk[1][d] = 0;
     a.A.by[0][d] = a.A.by[1][d] = 0;
     a.A.mn[0][d] = a.A.mn[1][d] = NONE32;
@@ -3156,9 +3198,11 @@ struct fluere_ctx {
     uint32_t* d_nflows = nullptr;  // [0] n_flows, [1] err (inside the d_glob allocation: Ctl)
     Glob* d_glob = nullptr;        // Ctl
     Ctl* h_ctl = nullptr;          // pinned host copy
+    HostMail* h_mail = nullptr;    // pinned mailbox of the exact engine's host reads (exact.h)
     bool batches_dirty = true;
     uint8_t* d_flow_key = nullptr;
     uint8_t* d_complex = nullptr;
+    uint32_t* d_fdefer = nullptr;  // k_finalize -> k_finalize_gen: flows for the general parser [fmax]
     uint32_t* d_cbits = nullptr;   // complex-flow filter of the exact engine (1 << CBITS_LOG2 bits)
     uint8_t* d_active = nullptr;
     Batch* d_batches = nullptr;
@@ -3223,7 +3267,8 @@ struct fluere_ctx {
 static void reset_record_counters(fluere_ctx* c) {
     char* g = (char*)c->d_glob;
     for (size_t off : {offsetof(Glob, n_rec), offsetof(Glob, n_complex), offsetof(Glob, n_complex_pkts),
-                       offsetof(Glob, n_heads), offsetof(Glob, n_updates), offsetof(Glob, n_ended)})
+                       offsetof(Glob, n_heads), offsetof(Glob, n_updates), offsetof(Glob, n_ended),
+                       offsetof(Glob, n_fdefer)})
         hipMemsetAsync(g + off, 0, 8, c->stream);
 }
 
@@ -3329,8 +3374,11 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     c->d_nflows = &reinterpret_cast<Ctl*>(c->d_glob)->n_flows;
     if (hipHostMalloc(&c->h_ctl, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     memset(c->h_ctl, 0, sizeof(Ctl));
+    if (hipHostMalloc(&c->h_mail, sizeof(HostMail)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    memset(c->h_mail, 0, sizeof(HostMail));
     if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_fdefer, F * 4) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_cbits, (1u << CBITS_LOG2) / 8) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
@@ -3379,9 +3427,11 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_tab);
     hipFree(c->d_acc);
     if (c->h_ctl) hipHostFree(c->h_ctl);
+    if (c->h_mail) hipHostFree(c->h_mail);
     hipFree(c->d_glob);
     hipFree(c->d_flow_key);
     hipFree(c->d_complex);
+    hipFree(c->d_fdefer);
     hipFree(c->d_cbits);
     hipFree(c->d_active);
     hipFree(c->d_batches);
@@ -3432,6 +3482,8 @@ static int clear_flows(fluere_ctx* c) {
     hipStream_t s = c->stream;
     (void)hipGetLastError();
     CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
+    static const int clean_abl = getenv("FLUERE_CLEAN_ABL") ? atoi(getenv("FLUERE_CLEAN_ABL")) : 0;
+    a.abl = clean_abl;
     // grid: the last fetched run's flow count when known (k_cleanup is
     // grid-stride over the device count, so any grid is correct)
     const unsigned g = c->prev_nf == ~0ull ? flow_grid(c)
@@ -3439,18 +3491,6 @@ static int clear_flows(fluere_ctx* c) {
     k_cleanup<<<g, 256, 0, s>>>(a, (size_t)N_TABLES * 2 * (c->C + 1));
     c->prev_nf = ~0ull;
     HIPCHECK(hipGetLastError());
-    return FLUERE_OK;
-}
-
-// Glob + n_flows + err of the stream's last results: one pinned copy.
-static int fetch_ctl(fluere_ctx* c, Glob& g, uint32_t (&nf_err)[2]) {
-    HIPCHECK(hipMemcpyAsync(c->h_ctl, c->d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    g = c->h_ctl->g;
-    nf_err[0] = c->h_ctl->n_flows;
-    nf_err[1] = c->h_ctl->err;
-    // a failed run clears every table word: keep the full cleanup grid then
-    c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
     return FLUERE_OK;
 }
 
@@ -3473,6 +3513,27 @@ static int wait_published(fluere_ctx* c, uint32_t seq, Glob& g, uint32_t (&nf_er
     nf_err[1] = c->h_ctl->err;
     c->prev_nf = (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) ? ~0ull : nf_err[0];
     return FLUERE_OK;
+}
+
+// The run counters to the pinned host copy, stream-ordered (one wave: the
+// words, the wave's system-scope fence, then seq), read by polling: no copy
+// kernel and no blocking stream sync on the way back.
+__global__ void __launch_bounds__(64) k_publish(const Glob* g, Ctl* host_ctl, uint32_t seq) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(host_ctl);
+    constexpr uint32_t nw = offsetof(Ctl, seq) / 4;
+    for (uint32_t i = threadIdx.x; i < nw; i += 64)
+        __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    if (threadIdx.x == 0) __hip_atomic_store(&host_ctl->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static int read_glob(fluere_ctx* c, Glob& g) {
+    const uint32_t seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0
+    k_publish<<<1, 64, 0, c->stream>>>(c->d_glob, c->h_ctl, seq);
+    HIPCHECK(hipGetLastError());
+    uint32_t nf_err[2];
+    return wait_published(c, seq, g, nf_err);
 }
 
 extern "C" int fluere_reset(fluere_ctx* c) {
@@ -4212,6 +4273,8 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     int rc;
     if ((rc = upload_batches(c))) return rc;  // host -> device, only when the batches changed
     P.ca = CleanArgs{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
+    static const int clean_abl = getenv("FLUERE_CLEAN_ABL") ? atoi(getenv("FLUERE_CLEAN_ABL")) : 0;
+    P.ca.abl = clean_abl;
     // cleanup grid: the last fetched run's flow count when known (k_cleanup is
     // grid-stride over the device count, so any grid is correct)
     P.clean_grid = c->prev_nf == ~0ull
@@ -4233,6 +4296,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
                        c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
         P.fa.timeout_us = c->timeout_ms * 1000ull;
         P.fa.cbits = c->d_cbits;
+        P.fa.defer = c->d_fdefer;
         P.spec_ca = P.ca;
         P.spec_ca.spec = 1;
         P.spec_ca.timeout_us = c->timeout_ms * 1000ull;
@@ -4614,16 +4678,23 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     uint64_t n_ended = 0, n_rec = 0, updates = 0;
     fluere_stats out{};
     if (!modeB) {
-        if (g.n_rec > c->d_recs_cap) {  // more flows than the record buffer: grow and finalize again
+        const uint64_t n_defer = g.n_fdefer;
+        if (g.n_rec + n_defer > c->d_recs_cap) {  // more flows than the record buffer: grow and finalize again
             reset_record_counters(c);
             if ((rc = ensure_recs(c, nf))) return rc;
             fa.out = c->d_recs;
             fa.out_cap = c->d_recs_cap;
             k_finalize<<<flow_grid(c), 256, 0, s>>>(fa);
             HIPCHECK(hipGetLastError());
+        }
+        // certified flows whose first packet needs the general parser
+        // (IPv6, VXLAN, IPv4 options, ...): k_finalize listed them
+        if (n_defer)
+            k_finalize_gen<<<(unsigned)std::min<uint64_t>(flow_grid(c), grid_for(n_defer, 256)), 256, 0, s>>>(fa);
+        if (n_defer || g.n_rec > c->d_recs_cap) {
+            HIPCHECK(hipGetLastError());
             HIPCHECK(hipEventRecord(c->ev2, s));
-            HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-            HIPCHECK(hipStreamSynchronize(s));
+            if ((rc = read_glob(c, g))) return rc;
         }
         if (g.n_complex) {
             // flows the certificate rejected: the exact state machine (exact.hip)
@@ -4632,12 +4703,12 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 0, timeout_us, c->d_complex, c->d_glob,
                        &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
             J.cbits = c->d_cbits;
+            J.mail = c->h_mail;
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
             out.passes = er.iterations;
             HIPCHECK(hipEventRecord(c->ev2, s));
-            HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-            HIPCHECK(hipStreamSynchronize(s));
+            if ((rc = read_glob(c, g))) return rc;
         }
         // records stay on the device; fluere_get_records copies and orders them
         n_rec = g.n_rec;
@@ -4655,14 +4726,17 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
         ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 1, timeout_us, c->d_complex, c->d_glob,
                    &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+        J.mail = c->h_mail;
+        J.recaux = &c->d_recaux;  // the records' order words (fetch_records orders by them)
+        J.recaux_cap = &c->d_recaux_cap;
         ExactResult er{};
         rc = getenv("FLUERE_SEQ_MODE_B") ? EXACT_FALLBACK : exact_run(J, s, &er);
         if (rc < 0) return rc;
         out.passes = er.iterations;
         if (rc == FLUERE_OK) {
-            HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
             HIPCHECK(hipEventRecord(c->ev2, s));
-            HIPCHECK(hipStreamSynchronize(s));
+            if ((rc = read_glob(c, g))) return rc;
+            c->has_aux = er.replayed != 0;
             n_rec = g.n_rec;
             n_ended = g.n_ended;
             updates = g.n_updates;
@@ -4906,6 +4980,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
         ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 0, c->timeout_ms * 1000ull, c->d_complex, c->d_glob,
                    &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes,
                    1, &c->d_annex, &c->d_annex_cap, c->d_annex_of};
+        J.mail = c->h_mail;
         ExactResult er{};
         if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
         if ((rc = enqueue_export(true))) return rc;
@@ -5463,6 +5538,7 @@ extern "C" int fluere_sweep_load(fluere_ctx* c, const void* d_recv, uint32_t n_s
                nullptr, c->d_glob, &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
     J.ext_cm = w->ocm;
     J.ext_n = n;
+    J.mail = c->h_mail;
     ExactSession* es = nullptr;
     int rc = exact_begin(J, s, &es);
     w->es = es;
