@@ -87,12 +87,19 @@ struct AggOp {
 };
 
 // ---- 1. per-packet metadata of the packets to replay (one parse pass) -----
+// The taken packets of each 256-packet block go to the block's region of
+// meta_blk in capture order (block-local compaction, one ballot per wave), the
+// block's count to bcount[blk0 + block]; k_ex_compact concatenates the
+// regions after a scan over the block counts (a scan over every packet's flag
+// and a sparse write per taken packet before).
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
-                                                 const uint32_t* cbits, ExMeta* meta, uint32_t* flag, uint64_t off) {
+                                                 const uint32_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
+                                                 uint64_t blk0) {
+    __shared__ uint32_t s_w[4];
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= B.n) return;
     Parsed P;
-    parse_record(B, li, macs != 0, 0, P);
+    if (li < B.n) parse_record(B, li, macs != 0, 0, P);
+    else P.cls = 1;
     uint32_t take = 0;
     ExMeta m;
     memset(&m, 0, sizeof m);
@@ -119,17 +126,26 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
             m.bits = ((P.pi.rprot != 6 || (P.pi.tflags & 2)) ? 1 : 0) | ((P.pi.tflags & 5) ? 2 : 0);
         }
     }
-    flag[off + li] = take;
-    if (take) meta[off + li] = m;  // (k_ex_compact reads the taken ones only)
+    const uint64_t bal = __ballot(take != 0);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_w[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < w; k++) before += s_w[k];
+    if (take)
+        meta_blk[(blk0 + blockIdx.x) * 256 + before +
+                 __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = m;
+    if (threadIdx.x == 0) bcount[blk0 + blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
-// compaction in capture order: cm[k] = the k-th replayed packet; sort keys (key, index)
-__global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta, const uint32_t* flag, const uint32_t* pos,
-                                                    uint64_t n, ExMeta* cm, uint32_t* key, uint32_t* val) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    const uint32_t k = pos[i];
-    const ExMeta m = meta[i];
+// compaction in capture order: cm[k] = the k-th replayed packet; sort keys
+// (key, index).  Block b of k_ex_meta's regions -> positions bpos[b] ...
+__global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta_blk, const uint32_t* bcount, const uint32_t* bpos,
+                                                    ExMeta* cm, uint32_t* key, uint32_t* val) {
+    const uint32_t b = blockIdx.x, c = bcount[b];
+    if (threadIdx.x >= c) return;
+    const uint32_t k = bpos[b] + threadIdx.x;
+    const ExMeta m = meta_blk[(uint64_t)b * 256 + threadIdx.x];
     cm[k] = m;
     key[k] = m.d;  // (a stable sort by flow keeps capture order within a flow)
     val[k] = k;
@@ -777,7 +793,8 @@ struct Arena {
 
 int mail_fetch(HostMail* m, hipStream_t s, int n, const void* const* src, const int* bytes, unsigned long long* out) {
     if (n < 0 || n > MAIL_MAX) return FLUERE_E_ARG;
-    if (!m) {  // no mailbox: one copy per value, then a stream sync
+    static const bool no_mail = getenv("FLUERE_NO_MAIL") != nullptr;  // diagnostics: the copy + sync path
+    if (!m || no_mail) {  // no mailbox: one copy per value, then a stream sync
         for (int i = 0; i < n; i++) {
             out[i] = 0;
             HIPCHECK(hipMemcpyAsync(&out[i], src[i], bytes[i], hipMemcpyDeviceToHost, s));
@@ -796,7 +813,7 @@ int mail_fetch(HostMail* m, hipStream_t s, int n, const void* const* src, const 
     HIPCHECK(hipGetLastError());
     for (uint32_t spin = 1;; spin++) {
         if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) == seq) break;
-        if ((spin & 1023) == 0) {  // now and then: did the stream fail instead?
+        if ((spin & 65535) == 0) {  // now and then (~ms): did the stream fail instead?
             const hipError_t q = hipStreamQuery(s);
             if (q == hipErrorNotReady) continue;
             if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) == seq) break;
@@ -852,7 +869,8 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     auto bytes_for = [&](uint64_t n_all, uint64_t n, size_t tmp) {
         size_t b = 0;
         auto add = [&](size_t x) { b += ((x + 255) & ~(size_t)255) + 256; };
-        add(n_all * sizeof(ExMeta)); add(n_all * 4); add(n_all * 4);  // meta, flag, pos
+        add((n_all + 256 * (size_t)J.nb) * sizeof(ExMeta));          // meta_blk (k_ex_meta's block regions)
+        add(4 * (n_all / 256 + J.nb + 1)); add(4 * (n_all / 256 + J.nb + 1));  // bcount, bpos
         add(n * sizeof(ExMeta)); add(n * 4); add(n * 4);              // cm, key, val
         add(n * 4); add(n * 4); add(n * sizeof(ExMeta));              // skey, sval, sm
         add(n * 4); add(n * 4); add(n * 4);                           // hf, hpos, heads
@@ -898,17 +916,20 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     Arena A;
     A.base = (char*)*J.scratch;
     A.cap = need;
-    ExMeta* meta = A.take<ExMeta>(N);
-    uint32_t* flag = A.take<uint32_t>(N);
-    uint32_t* pos = A.take<uint32_t>(N);
+    uint64_t nblk = 0;  // k_ex_meta blocks over every batch
+    if (!J.ext_cm)
+        for (int b = 0; b < J.nb; b++) nblk += J.h_batches[b].n ? gridn(J.h_batches[b].n, 256) : 0;
+    ExMeta* meta = A.take<ExMeta>(nblk * 256);
+    uint32_t* bcount = A.take<uint32_t>(nblk + 1);
+    uint32_t* bpos = A.take<uint32_t>(nblk + 1);
     // ---- 1. metadata of every packet to replay, compacted in capture order
     if (!J.ext_cm) {
-        uint64_t off = 0;
+        uint64_t blk = 0;
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, flag, off);
-            off += B.n;
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk);
+            blk += gridn(B.n, 256);
         }
     }
     size_t tb = tmp;
@@ -956,15 +977,14 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         HIPCHECK(hipMemcpyAsync(cm, J.ext_cm, n * sizeof(ExMeta), hipMemcpyDeviceToDevice, s));
         k_ex_keys<<<gridn(n, 256), 256, 0, s>>>(n, cm, key, val);
     } else {
-        const int iN = (int)N;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, iN, s));
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, bcount, bpos, (int)nblk, s));
         unsigned long long last[2] = {0, 0};
-        const void* src[2] = {pos + N - 1, flag + N - 1};
+        const void* src[2] = {bpos + nblk - 1, bcount + nblk - 1};
         const int by[2] = {4, 4};
         int rc = mail_fetch(J.mail, s, 2, src, by, last);
         if (rc) return rc;
         n = last[0] + last[1];
-        if (n) k_ex_compact<<<gridn(N, 256), 256, 0, s>>>(meta, flag, pos, N, cm, key, val);
+        if (n) k_ex_compact<<<(unsigned)nblk, 256, 0, s>>>(meta, bcount, bpos, cm, key, val);
     }
     S->n = n;
     S->R.replayed = n;
@@ -1169,41 +1189,43 @@ const ExactResult& exact_result(const ExactSession* S) { return S->R; }
 
 int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out) {
     *n_out = 0;
-    uint64_t N = 0;
-    for (int b = 0; b < J.nb; b++) N += J.h_batches[b].n;
-    if (!N) return FLUERE_OK;
+    uint64_t nblk = 0;
+    for (int b = 0; b < J.nb; b++) nblk += J.h_batches[b].n ? gridn(J.h_batches[b].n, 256) : 0;
+    if (!nblk) return FLUERE_OK;
     ExMeta* meta = nullptr;
-    uint32_t *flag = nullptr, *pos = nullptr;
+    uint32_t *bcount = nullptr, *bpos = nullptr;
     uint32_t* key = nullptr;
     uint32_t* val = nullptr;
     void* tp = nullptr;
     size_t tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)N, s);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, bcount, bpos, (int)nblk, s);
     int rc = FLUERE_OK;
-    if (hipMalloc(&meta, N * sizeof(ExMeta)) != hipSuccess || hipMalloc(&flag, N * 4) != hipSuccess ||
-        hipMalloc(&pos, N * 4) != hipSuccess || hipMalloc(&key, N * 4) != hipSuccess ||
+    const uint64_t N = nblk * 256;
+    if (hipMalloc(&meta, N * sizeof(ExMeta)) != hipSuccess || hipMalloc(&bcount, nblk * 4) != hipSuccess ||
+        hipMalloc(&bpos, nblk * 4) != hipSuccess || hipMalloc(&key, N * 4) != hipSuccess ||
         hipMalloc(&val, N * 4) != hipSuccess || hipMalloc(&tp, std::max<size_t>(tb, 16)) != hipSuccess)
         rc = FLUERE_E_NOMEM;
     if (rc == FLUERE_OK) {
-        uint64_t off = 0;
+        uint64_t blk = 0;
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, flag, off);
-            off += B.n;
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk);
+            blk += gridn(B.n, 256);
         }
-        uint32_t last[2] = {0, 0};
-        if (hipcub::DeviceScan::ExclusiveSum(tp, tb, flag, pos, (int)N, s) != hipSuccess ||
-            hipMemcpyAsync(&last[0], pos + N - 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(&last[1], flag + N - 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        unsigned long long last[2] = {0, 0};
+        const void* src[2] = {bpos + nblk - 1, bcount + nblk - 1};
+        const int by[2] = {4, 4};
+        if (hipcub::DeviceScan::ExclusiveSum(tp, tb, bcount, bpos, (int)nblk, s) != hipSuccess ||
+            mail_fetch(J.mail, s, 2, src, by, last) != FLUERE_OK)
             rc = FLUERE_E_HIP;
         else {
-            k_ex_compact<<<gridn(N, 256), 256, 0, s>>>(meta, flag, pos, N, cm, key, val);
+            k_ex_compact<<<(unsigned)nblk, 256, 0, s>>>(meta, bcount, bpos, cm, key, val);
             if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) rc = FLUERE_E_HIP;
-            *n_out = (uint64_t)last[0] + last[1];
+            *n_out = last[0] + last[1];
         }
     }
-    hipFree(meta); hipFree(flag); hipFree(pos); hipFree(key); hipFree(val); hipFree(tp);
+    hipFree(meta); hipFree(bcount); hipFree(bpos); hipFree(key); hipFree(val); hipFree(tp);
     return rc;
 }
 

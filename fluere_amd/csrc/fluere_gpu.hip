@@ -35,6 +35,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -356,7 +357,12 @@ __device__ __forceinline__ void mac_ckey(uint32_t k0, uint32_t k1, uint32_t k2, 
     k.w[13] = m1 << 16;
 }
 
-// ABL (diagnostics only): 0 full kernel; 1 parse + canonical key only; 2 + LDS key
+// ABL (diagnostics only): 5 every LDS-table miss written to its lane's own
+// contiguous run (4 consecutive misses of a lane fill one 128-B line; wrong
+// results: the merge never sees them) -- the store pattern of per-owner bins;
+// 4 every LDS-table miss appended to the workgroup's
+// raw buffer (coalesced, wave-aggregated) instead of its owner segment (still
+// correct: the overflow list); 0 full kernel; 1 parse + canonical key only; 2 + LDS key
 // table, no aggregation; 3 aggregation into hashed slots without the key table
 template <int ABL, bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
@@ -413,6 +419,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     const uint64_t end = FLUERE_HOT_ORDER ? n : min(n, beg + per);
     unsigned long long c_valid = 0, c_drop = 0, c_miss = 0, tmin = NONE64, tmax = 0;
     uint32_t d_loops = 0, d_iters = 0;  // diagnostics (per wave, uniform)
+    uint32_t d_abl5 = 0;                // diagnostics (ABL 5): this lane's misses
     const uint64_t nsteps = end > beg ? (end - beg + stride - 1) / stride : 0;
     uint64_t wbase = beg;
     uint32_t win = 0;  // this workgroup's window (set blockIdx.x * W + win)
@@ -619,8 +626,13 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 const uint4 w_pay = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), loc,
                                                h.tf | (q[u].dir << 8));
                 const uint32_t ow = owner_of(hk[u], a.S.O);
-                const uint32_t pos = own_add(s_scnt, ow);
-                if (pos < a.S.cap_o) {
+                const uint32_t pos = ABL == 4 ? 0xFFFFFFFFu : ABL == 5 ? 0u : own_add(s_scnt, ow);
+                if (ABL == 5) {
+                    uint4* dst = reinterpret_cast<uint4*>(a.S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2 +
+                                 ((size_t)threadIdx.x * WIN_ITERS + (d_abl5++ % WIN_ITERS)) * 2;
+                    dst[0] = w_key;
+                    dst[1] = w_pay;
+                } else if (pos < a.S.cap_o) {
                     uint4* dst = reinterpret_cast<uint4*>(a.S.dspill) +
                                  (((size_t)(blockIdx.x * a.S.W + win) * a.S.O + ow) * a.S.cap_o + pos) * (2 * SPU);
                     dst[0] = w_key;
@@ -1085,6 +1097,270 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_parse_spill: the hot pass for captures with many flows per window (the
+// last run sent more than half of its packets past k_parse_agg's LDS table:
+// C3/C4-like IMIX with 100k-1M flows).  No key table: every valid packet
+// becomes a 32-byte record for its merge owner, staged in an LDS bin per
+// owner (O x BIN records, 128 KiB); a full bin leaves as one contiguous run
+// of its owner's segment, written cooperatively by the wave that completed
+// it (2*BIN lanes per bin: 16-byte pieces, whole lines per instruction).
+// k_parse_agg's scattered per-packet 32-byte stores into the owner segments
+// were ~90 us of C3's 0.44-ms kernel (ablation: the same stores coalesced).
+// The merge, the segments and the sets are k_parse_agg's (no partials).
+// ---------------------------------------------------------------------------
+constexpr int SPB_WORDS = 8192;  // LDS bins: 16-byte words (128 KiB), 2 per record
+__device__ __forceinline__ uint32_t own_add_n(uint32_t* arr, uint32_t o, uint32_t n) {
+    return (atomicAdd(&arr[o >> 1], n << ((o & 1) * 16)) >> ((o & 1) * 16)) & 0xFFFFu;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
+    __shared__ uint4 s_bin[SPB_WORDS];
+    __shared__ uint32_t s_cl[MAX_OWNERS], s_wr[MAX_OWNERS];  // per bin: slots claimed / records written
+    __shared__ uint32_t s_scnt[OWN_WORDS];                   // per owner: records in its segment (packed)
+    __shared__ uint32_t s_chunk, s_nspill, s_slow;
+    __shared__ unsigned long long s_sbase, s_cnt[3], s_tmin, s_tmax;
+    const int tid = threadIdx.x;
+    const Stage& S = a.S;
+    const Batch& B = a.B;
+    const uint32_t O = S.O;
+    const uint32_t BIN = (uint32_t)(SPB_WORDS / 2) / O;  // records per bin: 16 (256 owners) .. 2 (2048)
+    const uint32_t PPB = 2 * BIN;                         // 16-byte pieces per bin
+    for (uint32_t o = tid; o < MAX_OWNERS; o += BLOCK) s_cl[o] = s_wr[o] = 0;
+    for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
+    if (tid < 3) s_cnt[tid] = 0;
+    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; s_chunk = 0; s_nspill = 0; s_slow = 0; }
+    __syncthreads();
+    const uint64_t n = B.n, G = gridDim.x, stride = G * BLOCK, beg = (uint64_t)blockIdx.x * BLOCK;
+    const uint64_t nsteps = n > beg ? (n - beg + stride - 1) / stride : 0;
+    const uint64_t lastp = n - 1;
+    const uint32_t lane = tid & 63;
+    constexpr uint32_t WAVES = BLOCK / 64;
+    unsigned long long c_valid = 0, c_drop = 0, tmin = NONE64, tmax = 0;
+    uint64_t wbase = beg;
+    uint32_t win = 0, ovf_total = 0;
+    const unsigned long long rt_start = wall_clock64();
+    // a lane's overflow record (its owner segment is full): the workgroup's
+    // raw buffer, listed at the window flush (k_parse_agg's overflow list)
+    auto overflow = [&](uint32_t q, uint32_t h, uint4 v) {
+        uint4* dst = reinterpret_cast<uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2 + (size_t)h * SPILL_WG + q;
+        *dst = v;
+    };
+    for (uint64_t ws = 0; ws < nsteps; ws += WIN_ITERS) {
+        const uint32_t set = blockIdx.x * S.W + win;
+        const uint32_t nch = (uint32_t)min<uint64_t>(WIN_ITERS, nsteps - ws) * WAVES;
+        uint4* seg0 = reinterpret_cast<uint4*>(S.dspill) + (size_t)set * O * S.cap_o * 2;
+        auto li_of = [&](uint32_t c) -> uint64_t {
+            return beg + (ws + c / WAVES) * stride + (uint64_t)(c % WAVES) * 64 + lane;
+        };
+        // the record offset of this lane's packet of chunk c (dense chunks: computed)
+        auto off_of = [&](uint32_t c) -> uint32_t {
+            const uint64_t li = min(li_of(c), lastp);
+            const uint64_t ch = (li_of(c) - lane) >> 6;
+            uint2 d = make_uint2(0, 0);
+            if (ch < B.n_desc) d = B.desc[ch];
+            return d.y ? d.x + lane * d.y : B.offs[li];
+        };
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(&s_chunk, 1u);
+        c = __builtin_amdgcn_readfirstlane(c);
+        uint32_t off = c < nch ? off_of(c) : 0u;
+        while (c < nch) {
+            uint32_t cn = 0;
+            if (lane == 0) cn = atomicAdd(&s_chunk, 1u);
+            cn = __builtin_amdgcn_readfirstlane(cn);
+            const uint64_t li = li_of(c);
+            const bool live = li < n;
+            Win W;
+            {
+                const uint8_t* p = B.bytes + off;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    uint4 q;
+                    __builtin_memcpy(&q, p + 16 * k, 16);
+                    W.w[4 * k + 0] = q.x; W.w[4 * k + 1] = q.y; W.w[4 * k + 2] = q.z; W.w[4 * k + 3] = q.w;
+                }
+                W.w[16] = W.w[17] = W.w[18] = W.w[19] = 0u;
+            }
+            const uint32_t off_n = cn < nch ? off_of(cn) : 0u;  // the next chunk's offset, in flight
+            pin_win(W);
+            Hot h;
+            const uint32_t cls = live ? hot_parse(B, off, W, h) : HOT_DROP;
+            c_drop += (live & (cls == HOT_DROP)) ? 1 : 0;
+            const bool valid = live & (cls == HOT_OK);
+            const bool slow = live & (cls == HOT_SLOW);
+            // canonical key (lower endpoint first, flow_table.h)
+            const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
+            const bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
+            const uint4 w_key = make_uint4(gt ? h.dip : h.sip, gt ? h.sip : h.dip,
+                                           gt ? __builtin_amdgcn_alignbit(h.ports, h.ports, 16) : h.ports, h.proto << 24);
+            const bool elig = (h.proto != 6u) | ((h.tf & 2u) != 0);
+            const uint4 w_pay = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), (uint32_t)(li - wbase),
+                                           h.tf | ((gt ? 1u : 0u) << 8));
+            const uint32_t o = owner_of(lt_hash(w_key.x, w_key.y, w_key.z, w_key.w), O);
+            if (valid) {
+                c_valid++;
+                tmin = min(tmin, (unsigned long long)h.t);
+                tmax = max(tmax, (unsigned long long)h.t);
+            }
+            // claim a bin slot, write the record, count it written; a lane whose
+            // bin is full retries once the bin's completer has flushed it
+            bool pend = valid;
+            for (int it = 0; it < (1 << 16); it++) {
+                if (__ballot(pend) == 0) break;
+                uint32_t done = NONE32;
+                if (pend) {
+                    const uint32_t slot = atomicAdd(&s_cl[o], 1u);
+                    if (slot < BIN) {
+                        uint4* b = &s_bin[(o * BIN + slot) * 2];
+                        b[0] = w_key;
+                        b[1] = w_pay;
+                        __threadfence_block();
+                        if (atomicAdd(&s_wr[o], 1u) + 1 == BIN) done = o;
+                        pend = false;
+                    }
+                }
+                // the bins completed this round: their segment positions, then
+                // the wave writes them out, 2*BIN lanes per bin
+                uint32_t pos = 0;
+                if (done != NONE32) pos = own_add_n(s_scnt, done, BIN);
+                uint64_t fm = __ballot(done != NONE32);
+                while (fm) {
+                    const uint32_t j = lane / PPB, pc = lane % PPB;  // this lane: piece pc of the j-th bin of the group
+                    uint64_t m = fm;
+                    for (uint32_t k = 0; k < j && m; k++) m &= m - 1;
+                    const bool act = m != 0;
+                    const uint32_t src = act ? (uint32_t)__builtin_ctzll(m) : 0u;
+                    const uint32_t bo = __shfl(done, src, 64), bp = __shfl(pos, src, 64);
+                    if (act) {
+                        const uint32_t r = pc >> 1, hh = pc & 1;
+                        const uint4 v = s_bin[(bo * BIN + r) * 2 + hh];
+                        if (bp + r < S.cap_o) {
+                            seg0[((size_t)bo * S.cap_o + bp + r) * 2 + hh] = v;
+                        } else {  // past the segment's capacity: the overflow list
+                            uint32_t q = 0;
+                            if (hh == 0) q = atomicAdd(&s_nspill, 1u);
+                            q = __shfl(q, lane & ~1u, 64);
+                            overflow(q, hh, v);
+                        }
+                    }
+                    // drop the group's bins (the first 64 / PPB set bits)
+                    for (uint32_t k = 0; k < 64 / PPB && fm; k++) fm &= fm - 1;
+                }
+                if (done != NONE32) {  // (the wave's reads of the bin come first: LDS order)
+                    atomicExch(&s_wr[done], 0u);
+                    atomicExch(&s_cl[done], 0u);
+                }
+                if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
+            }
+            if (pend) atomicOr(a.T.err, ERR_SPIN);  // (cannot happen: a full bin's completer flushes it)
+            // slow list: wave-aggregated append into this workgroup's region
+            const uint64_t sm = __ballot(slow);
+            if (sm) {
+                const uint32_t lead = __builtin_ctzll(sm);
+                uint32_t b0 = 0;
+                if (lane == lead) b0 = atomicAdd(&s_slow, (uint32_t)__popcll(sm));
+                b0 = __shfl(b0, lead, 64);
+                if (slow)
+                    a.slow[(size_t)blockIdx.x * a.slow_region + b0 +
+                           __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] = (uint32_t)li;
+            }
+            c = cn;
+            off = off_n;
+        }
+        // ---- window flush: the partly filled bins, then the set's segment counts
+        __syncthreads();
+        for (uint32_t o = tid; o < O; o += BLOCK) {
+            const uint32_t k = s_wr[o];
+            if (!k) continue;
+            const uint32_t p0 = own_add_n(s_scnt, o, k);
+            for (uint32_t r = 0; r < k; r++) {
+                const uint4 v0 = s_bin[(o * BIN + r) * 2], v1 = s_bin[(o * BIN + r) * 2 + 1];
+                if (p0 + r < S.cap_o) {
+                    uint4* d = seg0 + ((size_t)o * S.cap_o + p0 + r) * 2;
+                    d[0] = v0;
+                    d[1] = v1;
+                } else {
+                    const uint32_t q = atomicAdd(&s_nspill, 1u);
+                    overflow(q, 0, v0);
+                    overflow(q, 1, v1);
+                }
+            }
+            s_cl[o] = s_wr[o] = 0;
+        }
+        __syncthreads();  // (every overflow record written before the list copy below)
+        const uint32_t nsp = s_nspill;
+        if (tid == 128) s_sbase = nsp ? atomicAdd(&a.g->n_spill, (unsigned long long)nsp) : 0ull;
+        if (tid == 0) { ovf_total += nsp; S.base[set] = B.first + wbase; s_chunk = 0; }
+        for (uint32_t o = tid; o <= O; o += BLOCK) {
+            S.off[(size_t)o * S.n_sets + set] = 0;  // no partials
+            if (o < O) S.soff[(size_t)o * S.n_sets + set] = min(own_get(s_scnt, o), S.cap_o);
+        }
+        __syncthreads();
+        if (nsp) {  // overflow records -> the overflow list (the set in fl's high bits)
+            const uint4* raw = reinterpret_cast<const uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2;
+            const unsigned long long sb = s_sbase;
+            for (uint32_t i = tid; i < nsp; i += BLOCK) {
+                // (written by other waves of this workgroup: nontemporal loads bypass the CU's L1)
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 k0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(raw + i));
+                const u32x4 k1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(raw + SPILL_WG + i));
+                uint4* dst = reinterpret_cast<uint4*>(S.spill) + (sb + i) * 2;
+                dst[0] = make_uint4(k0.x, k0.y, k0.z, k0.w);
+                dst[1] = make_uint4(k1.x, k1.y, k1.z, k1.w | (set << 9));
+            }
+        }
+        for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
+        if (tid == 0) s_nspill = 0;
+        __syncthreads();
+        wbase += stride * WIN_ITERS;
+        win++;
+    }
+    // sets of windows this workgroup did not have: empty segments
+    for (uint32_t w = win; w < S.W; w++) {
+        const uint32_t set = blockIdx.x * S.W + w;
+        for (uint32_t oo = tid; oo <= O; oo += BLOCK) {
+            S.off[(size_t)oo * S.n_sets + set] = 0;
+            if (oo < O) S.soff[(size_t)oo * S.n_sets + set] = 0;
+        }
+    }
+    // statistics (k_parse_agg's per-workgroup record; every valid packet is a "miss")
+    {
+        uint32_t cv = (uint32_t)c_valid, cd = (uint32_t)c_drop;
+        unsigned long long tn = tmin, tx = tmax;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            cv += __shfl_xor(cv, o, 64);
+            cd += __shfl_xor(cd, o, 64);
+            tn = min(tn, (unsigned long long)__shfl_xor(tn, o, 64));
+            tx = max(tx, (unsigned long long)__shfl_xor(tx, o, 64));
+        }
+        if (lane == 0) {
+            if (cv) atomicAdd(&s_cnt[0], (unsigned long long)cv);
+            if (cd) atomicAdd(&s_cnt[1], (unsigned long long)cd);
+            if (cv) { atomicMin(&s_tmin, tn); atomicMax(&s_tmax, tx); }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long* st = S.wgs + (size_t)blockIdx.x * WGS_N;
+        st[0] = s_cnt[0];
+        st[1] = s_cnt[1];
+        st[2] = s_cnt[0];
+        st[3] = s_cnt[0] ? s_tmin : NONE64;
+        st[4] = s_cnt[0] ? s_tmax : 0;
+        st[5] = st[6] = st[7] = 0;
+        a.slow_cnt[blockIdx.x] = s_slow;
+        if (s_slow) atomicAdd(a.slow_n, (unsigned long long)s_slow);
+        if (s_cnt[0] > ovf_total) atomicAdd(&a.g->n_dspill, s_cnt[0] - ovf_total);
+        if (a.dbg) {
+            a.dbg[blockIdx.x * 8 + 0] = rt_start;
+            a.dbg[blockIdx.x * 8 + 1] = a.dbg[blockIdx.x * 8 + 2] = a.dbg[blockIdx.x * 8 + 3] = wall_clock64();
+            a.dbg[blockIdx.x * 8 + 7] = 0;
+        }
+    }
+}
+
 // One flow's merged update_flow aggregate -> the global accumulators of dense
 // id d (flows.rs:11-42).  Positions are global packet indices.
 struct FlowPart {
@@ -1212,6 +1488,9 @@ __device__ __forceinline__ uint32_t staged_id(const TableSet& T, const V6Map& M,
 constexpr int MB = 1024;   // merge kernel block
 constexpr int MT = 1024;   // merge table entries (120 B each)
 constexpr int MCH = 1024;  // sets per scan chunk
+#ifndef FLUERE_MERGE_U
+#define FLUERE_MERGE_U 1  // spilled packets per lane per round in the merge's record loop
+#endif
 #ifndef FLUERE_MERGE_GUARD
 #define FLUERE_MERGE_GUARD 1  // read-before-atomic for min / max / positions (0: unconditional)
 #endif
@@ -1317,7 +1596,12 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
         parse_loaded(BP, op, WP, macs, 0, P);
     } else {
         parse_loaded_fast(BP, op, WP, macs, P);
-        if (P.cls == 2) {
+        if (P.cls == 2) {  // IPv6, VXLAN, IPv4 options: parse_mid over the 128-byte window
+            Win32 W32;
+            load_win32(BP, op, W32);
+            parse_loaded32<0>(BP, op, W32, macs, P);
+        }
+        if (P.cls == 2) {  // the general parser's classes (ARP, VLAN, raw fallback ...)
             a.defer[atomicAdd(&a.g->n_fdefer, 1ull)] = d;
             return false;
         }
@@ -1479,6 +1763,115 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             __syncthreads();
             const uint32_t total = m_scan[MB / 64];
             if (a.dbg && tid == 0 && c0s == 0 && pass == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 2] = wall_clock64();
+            // one record (a staged partial or a spilled packet): find or claim
+            // its merge entry, then the update (or the global path)
+            auto merge_rec = [&](uint32_t h, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag, uint32_t x0,
+                                 uint32_t x1, uint32_t x2, const FlowPart& f) {
+                    // find or claim the merge entry (same protocol as the hot kernel)
+                    uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
+                    int state = 0, probes = 0;
+                    for (int it = 0; it < 128; it++) {
+                        if (state == 0) {
+                            const uint4 kk = m_key[e];
+                            bool xm = true;
+                            if (macs) {  // MAC words
+                                const uint4 xx = m_kx[e];
+                                xm = xx.w == 1u && xx.x == x0 && xx.y == x1 && xx.z == x2;
+                            }
+                            if (kk.w & LT_READY) {
+                                if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2 && xm) state = 1;
+                                else if (++probes == 64) state = 2;
+                                else e = (e + 1) & (MT - 1);
+                            } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
+                                m_key[e].x = k0;
+                                m_key[e].y = k1;
+                                m_key[e].z = k2;
+                                if (macs) m_kx[e] = make_uint4(x0, x1, x2, 1u);
+                                __threadfence_block();
+                                atomicExch(&m_key[e].w, tag | LT_READY);
+                                state = 1;
+                            }
+                        }
+                        if (__ballot(state == 0) == 0) break;
+                    }
+                    if (state == 1) {
+                        // Many records land on one entry (a flow's partials from every
+                        // set, its spilled packets), and LDS atomics on one address
+                        // serialise: min / max and first / last positions are read
+                        // first and written only where the record moves them (values
+                        // move monotonically, so a stale read costs at most a
+                        // redundant atomic).
+    #if FLUERE_MERGE_GUARD
+                        const uint32_t gmn0 = m_mn[0][e], gmn1 = m_mn[1][e], gmx0 = m_mx[0][e], gmx1 = m_mx[1][e];
+                        const unsigned long long gfa = m_fa[e], gfc = m_fc[e], gla = m_la[e];
+    #else
+                        const uint32_t gmn0 = NONE32, gmn1 = NONE32, gmx0 = 0, gmx1 = 0;
+                        const unsigned long long gfa = NONE64, gfc = NONE64, gla = 0;
+    #endif
+    #pragma unroll
+                        for (int q = 0; q < 2; q++) {
+                            if (f.pk[q]) {
+                                atomicAdd(&m_pk[q][e], f.pk[q]);
+                                atomicAdd(&m_by[q][e], f.by[q]);
+                            }
+                            if (f.mn[q] < (q ? gmn1 : gmn0) || !FLUERE_MERGE_GUARD) atomicMin(&m_mn[q][e], f.mn[q]);
+                            if (f.mx[q] > (q ? gmx1 : gmx0) || !FLUERE_MERGE_GUARD) atomicMax(&m_mx[q][e], f.mx[q]);
+                        }
+    #pragma unroll
+                        for (int q = 0; q < 8; q++)
+                            if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
+                        if (f.fa != NONE64 && f.fa < gfa) atomicMin(&m_fa[e], f.fa);
+                        if (f.fc != NONE64 && f.fc < gfc) atomicMin(&m_fc[e], f.fc);
+                        if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
+                        if (f.la && (f.la > gla || !FLUERE_MERGE_GUARD)) atomicMax(&m_la[e], f.la);
+                    } else {
+                        uint32_t d;
+                        if (macs && tag != 0xFF000000u) {
+                            CKey ck;
+                            mac_ckey(k0, k1, k2, tag, x0, x1, x2, ck);
+                            d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+                        } else {
+                            d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
+                        }
+                        if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
+                    }
+            };
+#if FLUERE_MERGE_U > 1
+            if (pass == 1 && !macs) {
+                // spilled packets, FLUERE_MERGE_U per lane per round: every
+                // record's set search and loads issued before the first update
+                constexpr int U = FLUERE_MERGE_U;
+                for (uint32_t i0 = tid; i0 < total; i0 += MB * U) {
+                    uint4 v0[U], v1[U];
+                    uint32_t wbv[U];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t idx = min(i0 + u * MB, total - 1);
+                        uint32_t lo_i = 0, hi_i = nset - 1;
+                        while (lo_i < hi_i) {
+                            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                            if (m_start[mid] <= idx) lo_i = mid;
+                            else hi_i = mid - 1;
+                        }
+                        wbv[u] = m_wb[lo_i];
+                        const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
+                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * 2;
+                        v0[u] = src[0];
+                        v1[u] = src[1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        if (i0 + u * MB >= total) break;
+                        FlowPart f;
+                        spill_to_part(v1[u].x, v1[u].y, v1[u].z, v1[u].w, a.B.first + wbv[u], f);
+                        merge_rec(lt_hash(v0[u].x, v0[u].y, v0[u].z, v0[u].w), v0[u].x, v0[u].y, v0[u].z, v0[u].w, 0u,
+                                  0u, 0u, f);
+                    }
+                }
+                __syncthreads();
+                continue;
+            }
+#endif
             for (uint32_t idx = tid; idx < total; idx += MB) {
                 uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
                 while (lo_i < hi_i) {
@@ -1518,74 +1911,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                         spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
                     }
                 }
-                // find or claim the merge entry (same protocol as the hot kernel)
-                uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
-                int state = 0, probes = 0;
-                for (int it = 0; it < 128; it++) {
-                    if (state == 0) {
-                        const uint4 kk = m_key[e];
-                        bool xm = true;
-                        if (macs) {  // MAC words
-                            const uint4 xx = m_kx[e];
-                            xm = xx.w == 1u && xx.x == x0 && xx.y == x1 && xx.z == x2;
-                        }
-                        if (kk.w & LT_READY) {
-                            if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2 && xm) state = 1;
-                            else if (++probes == 64) state = 2;
-                            else e = (e + 1) & (MT - 1);
-                        } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
-                            m_key[e].x = k0;
-                            m_key[e].y = k1;
-                            m_key[e].z = k2;
-                            if (macs) m_kx[e] = make_uint4(x0, x1, x2, 1u);
-                            __threadfence_block();
-                            atomicExch(&m_key[e].w, tag | LT_READY);
-                            state = 1;
-                        }
-                    }
-                    if (__ballot(state == 0) == 0) break;
-                }
-                if (state == 1) {
-                    // Many records land on one entry (a flow's partials from every
-                    // set, its spilled packets), and LDS atomics on one address
-                    // serialise: min / max and first / last positions are read
-                    // first and written only where the record moves them (values
-                    // move monotonically, so a stale read costs at most a
-                    // redundant atomic).
-    #if FLUERE_MERGE_GUARD
-                    const uint32_t gmn0 = m_mn[0][e], gmn1 = m_mn[1][e], gmx0 = m_mx[0][e], gmx1 = m_mx[1][e];
-                    const unsigned long long gfa = m_fa[e], gfc = m_fc[e], gla = m_la[e];
-    #else
-                    const uint32_t gmn0 = NONE32, gmn1 = NONE32, gmx0 = 0, gmx1 = 0;
-                    const unsigned long long gfa = NONE64, gfc = NONE64, gla = 0;
-    #endif
-    #pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        if (f.pk[q]) {
-                            atomicAdd(&m_pk[q][e], f.pk[q]);
-                            atomicAdd(&m_by[q][e], f.by[q]);
-                        }
-                        if (f.mn[q] < (q ? gmn1 : gmn0) || !FLUERE_MERGE_GUARD) atomicMin(&m_mn[q][e], f.mn[q]);
-                        if (f.mx[q] > (q ? gmx1 : gmx0) || !FLUERE_MERGE_GUARD) atomicMax(&m_mx[q][e], f.mx[q]);
-                    }
-    #pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (f.fl[q]) atomicAdd(&m_fl[q][e], f.fl[q]);
-                    if (f.fa != NONE64 && f.fa < gfa) atomicMin(&m_fa[e], f.fa);
-                    if (f.fc != NONE64 && f.fc < gfc) atomicMin(&m_fc[e], f.fc);
-                    if (f.fr != NONE64) atomicMin(&m_fr[e], f.fr);
-                    if (f.la && (f.la > gla || !FLUERE_MERGE_GUARD)) atomicMax(&m_la[e], f.la);
-                } else {
-                    uint32_t d;
-                    if (macs && tag != 0xFF000000u) {
-                        CKey ck;
-                        mac_ckey(k0, k1, k2, tag, x0, x1, x2, ck);
-                        d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
-                    } else {
-                        d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
-                    }
-                    if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
-                }
+                merge_rec(h, k0, k1, k2, tag, x0, x1, x2, f);
             }
             __syncthreads();
         }
@@ -3498,9 +3824,10 @@ static int clear_flows(fluere_ctx* c) {
 // (publish_ctl); now and then ask whether the stream failed instead.
 static int wait_published(fluere_ctx* c, uint32_t seq, Glob& g, uint32_t (&nf_err)[2]) {
     volatile uint32_t* seqp = &c->h_ctl->seq;
+    static const uint32_t qmask = getenv("FLUERE_QUERY_MASK") ? (uint32_t)atoi(getenv("FLUERE_QUERY_MASK")) : 65535u;
     for (uint32_t spin = 1;; spin++) {
         if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == seq) break;
-        if ((spin & 1023) == 0) {
+        if ((spin & qmask) == 0) {  // now and then (~ms): did the stream fail instead?
             const hipError_t q = hipStreamQuery(c->stream);
             if (q == hipErrorNotReady) continue;
             if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == seq) break;
@@ -4075,6 +4402,7 @@ struct PassPlan {
     uint32_t owners[PLAN_BATCHES];
     uint32_t slow_grid[PLAN_BATCHES];  // k_slow workgroups (its sets); 0: the merge tail takes the slow list
     int macs, abl;
+    int spill;     // 1: the hot pass is k_parse_spill (many flows per window), not k_parse_agg
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
     int spec;      // 1: k_finalize publishes the counters to the host itself, a speculative k_cleanup follows
     CleanArgs spec_ca;
@@ -4268,6 +4596,23 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     return FLUERE_OK;
 }
 
+// k_parse_spill when the last run's flows would overflow k_parse_agg's LDS
+// table in most windows: the distinct keys a workgroup window of w packets
+// sees out of F flows, F (1 - e^(-w/F)), above twice the table's slots
+// (C3/C4-like captures: ~45k-60k keys per window, 92-95 % of the packets
+// past the table).  A prediction from the last run: either kernel is exact.
+static int spill_mode(const fluere_ctx* c) {
+    const int env = getenv("FLUERE_SPILL_MODE") ? atoi(getenv("FLUERE_SPILL_MODE")) : -1;  // tests: force either kernel
+    if (c->use_mac) return 0;
+    if (env >= 0) return env;
+    const double F = (double)c->last_nf;
+    if (F <= 0) return 0;
+    uint64_t nmax = 0;
+    for (auto& hb : c->batches) nmax = std::max<uint64_t>(nmax, hb.b.n);
+    const double w = std::min<double>((double)WIN_ITERS * BLOCK, (double)nmax / std::max(1, c->n_cu));
+    return F * (1.0 - std::exp(-w / F)) > 2.0 * NS ? 1 : 0;
+}
+
 static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     memset(&P, 0, sizeof P);  // byte-comparable (padding included)
     int rc;
@@ -4286,6 +4631,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
     P.macs = c->use_mac;
     P.abl = abl;
+    P.spill = spill_mode(c);
     P.finalize = finalize ? 1 : 0;
     P.h_ctl = c->h_ctl;
     P.d_glob = c->d_glob;
@@ -4317,10 +4663,13 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         const AggArgs& a = P.agg[i];
         if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 32, s));  // n_slow, n_spill, n_dspill, n_gen (k_cleanup zeroed them for batch 0)
         const unsigned grid = P.agg_grid[i];
-        const void* fn = P.macs ? (const void*)k_parse_agg<0, true>
+        const void* fn = P.spill ? (const void*)k_parse_spill
+                       : P.macs ? (const void*)k_parse_agg<0, true>
                          : P.abl == 1 ? (const void*)k_parse_agg<1, false>
                          : P.abl == 2 ? (const void*)k_parse_agg<2, false>
                          : P.abl == 3 ? (const void*)k_parse_agg<3, false>
+                         : P.abl == 4 ? (const void*)k_parse_agg<4, false>
+                         : P.abl == 5 ? (const void*)k_parse_agg<5, false>
                                       : (const void*)k_parse_agg<0, false>;
         // HIP events carried by the dispatch itself (start / stop timestamps of
         // the hot kernel): separate event markers would each add a gap to the
@@ -4413,10 +4762,13 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
         if (i == 0 && P.nb > 1) event(c->evk_first);
         event(c->evk0);
         a_agg[i][0] = &P.agg[i];
-        const void* fn = P.macs ? (const void*)k_parse_agg<0, true>
+        const void* fn = P.spill ? (const void*)k_parse_spill
+                       : P.macs ? (const void*)k_parse_agg<0, true>
                                 : P.abl == 1 ? (const void*)k_parse_agg<1, false>
                                 : P.abl == 2 ? (const void*)k_parse_agg<2, false>
                                 : P.abl == 3 ? (const void*)k_parse_agg<3, false>
+                                : P.abl == 4 ? (const void*)k_parse_agg<4, false>
+                                : P.abl == 5 ? (const void*)k_parse_agg<5, false>
                                              : (const void*)k_parse_agg<0, false>;
         kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
         event(c->evk1);
@@ -4540,6 +4892,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
     P.macs = c->use_mac;
     P.abl = abl;
+    P.spill = spill_mode(c);
     c->plan_nb = P.nb;
     c->precleaned = false;
     rc = enqueue_batches(c, P);
@@ -4615,6 +4968,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             memset(&Q, 0, sizeof Q);
             Q.macs = P.macs;
             Q.abl = P.abl;
+            Q.spill = P.spill;
             rc = plan_batches(c, Q);
             if (!rc) rc = enqueue_batches(c, Q);
             if (rc) break;

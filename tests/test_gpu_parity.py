@@ -164,6 +164,49 @@ def test_spill_overflow_list(gpu, name, monkeypatch):
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
 
 
+@pytest.mark.parametrize("name", ["c1_udp64_1flow", "c2_udp64_small", "c3_imix_small", "many_flows", "slow_small",
+                                  "slow_many_flows", "c3_imix_2m"])
+@pytest.mark.parametrize("cap", [None, "3"])
+def test_spill_kernel_matches_oracle(gpu, name, cap, monkeypatch):
+    """k_parse_spill (the hot pass for many flows per window: every valid
+    packet through the per-owner LDS bins into its owner's segment, full bins
+    written out by the wave) forced on every capture kind, also with owner
+    segments of 3 records (nearly every record through the overflow list)."""
+    monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
+    if cap:
+        monkeypatch.setenv("FLUERE_OWNER_CAP", cap)
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=use_mac)
+    csv, ne, st = _gpu_csv(data, use_mac=use_mac, max_flows=max(1 << 16, 2 * f))
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
+
+
+@pytest.mark.parametrize("t", [600000, 1000])
+def test_spill_kernel_realistic_tcp(gpu, t, monkeypatch):
+    """Realistic TCP through k_parse_spill: the exact engine and the sweep
+    over its owner segments."""
+    monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007))
+    want = pyoracle.offline(data, t)
+    csv, ne, st = _gpu_csv(data, t, max_flows=1 << 20)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp spill t={t}")
+
+
+def test_spill_kernel_chosen_on_rerun(gpu):
+    """A context whose last run had ~50k flows per window takes k_parse_spill
+    on the next run (the prediction from the last flow count); the runs agree."""
+    kind, n, f, seed, use_mac = SYNTH["c3_imix_2m"]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data)
+    with fluere_amd.FlowContext(max_flows=1 << 18) as ctx:
+        ctx.add_host_pcap(data)
+        for run in range(3):
+            ctx.run()
+            recs, ne = ctx.records()
+            assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"run {run}")
+
+
 @pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small"])
 def test_second_run_takes_slow_kernel(gpu, name):
     """The first run of a context leaves the slow list to the merge kernel's
