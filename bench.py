@@ -197,7 +197,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          # also against the measured copy rate (MI355X_MICROARCH.md)
                          "frac_vs_copy_6290": round(achieved / HBM_COPY_GBS, 4),
-                         "kernel": "k_parse_agg", "kernel_ms": round(kernel_avg, 4),
+                         "kernel": ctx.last_hot_kernel(), "kernel_ms": round(kernel_avg, 4),
                          # > 1: kernel_ms spans the first launch's start to the last one's end
                          "launches_per_step": len(batches),
                          "algorithmic_bytes_per_launch": BYTES_PER_PKT * n},

@@ -2601,8 +2601,12 @@ __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool
 #pragma unroll
     for (int t = 0; t < N_TABLES / 2; t++) {
         const uint32_t s0 = sv[t].x, s1 = sv[t].y;
-        if (tables && !(a.abl & 1) && s0 != NONE32) { a.T.tab[2 * t][2 * s0] = EMPTY; a.T.tab[2 * t][2 * s0 + 1] = EMPTY; }
-        if (tables && !(a.abl & 1) && s1 != NONE32) { a.T.tab[2 * t + 1][2 * s1] = EMPTY; a.T.tab[2 * t + 1][2 * s1 + 1] = EMPTY; }
+        // one 16-byte store per entry {key, value} (two 8-byte stores were two
+        // partial writes of the same random line)
+        if (tables && !(a.abl & 1) && s0 != NONE32)
+            *reinterpret_cast<ulonglong2*>(&a.T.tab[2 * t][2 * s0]) = make_ulonglong2(EMPTY, EMPTY);
+        if (tables && !(a.abl & 1) && s1 != NONE32)
+            *reinterpret_cast<ulonglong2*>(&a.T.tab[2 * t + 1][2 * s1]) = make_ulonglong2(EMPTY, EMPTY);
         if ((s0 & s1) != NONE32) row[t] = make_uint2(NONE32, NONE32);
     }
     if (a.abl & 2) return;
@@ -3576,6 +3580,7 @@ struct fluere_ctx {
     bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
     uint32_t run_seq = 0;                       // number of the last run that publishes its counters (Ctl::seq)
     int plan_nb = 0;                            // batches of the last pass
+    int plan_spill = 0;                         // the last pass's hot kernel was k_parse_spill
     double last_run_ms = 0;                     // host wall time of the last fluere_run
     // hipGraph of the last fluere_run pass, replayed while the plan is unchanged
     hipGraphExec_t graph = nullptr;
@@ -4894,10 +4899,15 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     P.abl = abl;
     P.spill = spill_mode(c);
     c->plan_nb = P.nb;
+    c->plan_spill = P.spill;
     c->precleaned = false;
     rc = enqueue_batches(c, P);
     debug_counters(c);
     return rc;
+}
+
+extern "C" const char* fluere_last_hot_kernel(fluere_ctx* c) {
+    return c && c->plan_spill ? "k_parse_spill" : "k_parse_agg";
 }
 
 // Duration of the last k_parse_agg launch (HIP events on the context stream).
@@ -4953,6 +4963,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     PassPlan P;
     if ((rc = plan_pass(c, P, true))) return rc;
     c->plan_nb = P.nb;
+    c->plan_spill = P.spill;
     const auto t_plan = std::chrono::steady_clock::now();
     // hipGraph replay is opt-in (FLUERE_GRAPH=1): measured on MI355X / ROCm 7.2
     // it is slower than these few direct launches (C2 step 0.264 vs 0.257 ms)

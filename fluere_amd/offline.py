@@ -95,6 +95,10 @@ class FlowContext:
         """HIP-event time of the last k_parse_agg launch (the roofline kernel)."""
         return float(self._L.fluere_last_kernel_ms(self._h))
 
+    def last_hot_kernel(self) -> str:
+        """Name of the last pass's hot kernel (k_parse_agg or k_parse_spill)."""
+        return self._L.fluere_last_hot_kernel(self._h).decode()
+
     def last_pass_ms(self) -> float:
         """HIP-event time of the whole last parse+key+aggregate pass."""
         return float(self._L.fluere_last_pass_ms(self._h))

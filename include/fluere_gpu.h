@@ -177,6 +177,10 @@ double fluere_last_kernel_ms(fluere_ctx* ctx);
 /* After fluere_run: its host wall time (submission to results), ms.  After
  * fluere_parse_aggregate: device time of the hot kernel + merge, ms. */
 double fluere_last_pass_ms(fluere_ctx* ctx);
+/* The hot kernel of the last pass: "k_parse_agg" (LDS flow table) or
+ * "k_parse_spill" (many flows per window: per-owner LDS bins), chosen from
+ * the previous run's flow count.  Static string. */
+const char* fluere_last_hot_kernel(fluere_ctx* ctx);
 
 /* Records of the last fluere_run, host memory, ended prefix first (in the
  * reference's emission order), then active flows.  Caller frees with
