@@ -68,6 +68,7 @@ struct Glob {
     unsigned long long n_spill;  // k_parse_agg: the batch's overflow-list records (cursor); next to n_slow
     unsigned long long n_dspill; // k_parse_agg: the batch's spills in owner segments; next to n_spill
     unsigned long long n_gen;    // k_slow: the batch's general-parser list (cursor); next to n_dspill
+    unsigned long long n_owner;  // k_merge_partials: owners claimed by its workgroups; next to n_gen
     unsigned long long n_updates, n_ended;  // over emitted records: sum of d_pkts, ended (order_key set)
     unsigned long long n_kc_miss;  // diagnostics: hot-kernel packets that found no LDS table entry
     unsigned long long cyc_total, cyc_flush, cyc_flush0;  // diagnostics: thread-0 clock sums over workgroups
@@ -77,8 +78,8 @@ struct Glob {
     unsigned long long n_fdefer;                          // k_finalize: certified flows left to k_finalize_gen
 };
 static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16 &&
-                  offsetof(Glob, n_gen) == offsetof(Glob, n_slow) + 24,
-              "n_slow, n_spill, n_dspill, n_gen are reset together");
+                  offsetof(Glob, n_gen) == offsetof(Glob, n_slow) + 24 && offsetof(Glob, n_owner) == offsetof(Glob, n_slow) + 32,
+              "n_slow, n_spill, n_dspill, n_gen, n_owner are reset together");
 // One device allocation holds Glob and the dictionary counters right after it
 // (n_flows, err), so a run ends with ONE small device->host copy.
 struct Ctl {

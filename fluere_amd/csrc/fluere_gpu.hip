@@ -1488,9 +1488,6 @@ __device__ __forceinline__ uint32_t staged_id(const TableSet& T, const V6Map& M,
 constexpr int MB = 1024;   // merge kernel block
 constexpr int MT = 1024;   // merge table entries (120 B each)
 constexpr int MCH = 1024;  // sets per scan chunk
-#ifndef FLUERE_MERGE_U
-#define FLUERE_MERGE_U 1  // spilled packets per lane per round in the merge's record loop
-#endif
 #ifndef FLUERE_MERGE_GUARD
 #define FLUERE_MERGE_GUARD 1  // read-before-atomic for min / max / positions (0: unconditional)
 #endif
@@ -1694,7 +1691,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // Owners o = blockIdx.x, + gridDim.x, ...: the grid is at most one workgroup
     // per CU (one merge table fills a CU's LDS), so a workgroup merges several
     // owners in turn rather than being dispatched again for each.
-    for (uint32_t me = blockIdx.x; me < S.O; me += gridDim.x) {
+    // Owner blockIdx.x first; with more owners than workgroups the rest are
+    // claimed from a counter (Glob::n_owner), so a workgroup that finishes
+    // early takes the next one (owners' record phases spread, e.g. C3 99-199
+    // us).  No counter when every workgroup has one owner.
+    __shared__ uint32_t s_me;
+    if (tid == 0) s_me = blockIdx.x;
+    __syncthreads();
+    for (uint32_t me = s_me; me < S.O; me = s_me) {
         uint32_t pre_lo[MCH / MB], pre_hi[MCH / MB];
         unsigned long long pre_wb[MCH / MB];
     #pragma unroll
@@ -1836,42 +1840,75 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                         if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
                     }
             };
-#if FLUERE_MERGE_U > 1
             if (pass == 1 && !macs) {
-                // spilled packets, FLUERE_MERGE_U per lane per round: every
-                // record's set search and loads issued before the first update
-                constexpr int U = FLUERE_MERGE_U;
-                for (uint32_t i0 = tid; i0 < total; i0 += MB * U) {
-                    uint4 v0[U], v1[U];
-                    uint32_t wbv[U];
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        const uint32_t idx = min(i0 + u * MB, total - 1);
-                        uint32_t lo_i = 0, hi_i = nset - 1;
-                        while (lo_i < hi_i) {
-                            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-                            if (m_start[mid] <= idx) lo_i = mid;
-                            else hi_i = mid - 1;
-                        }
-                        wbv[u] = m_wb[lo_i];
-                        const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * 2;
-                        v0[u] = src[0];
-                        v1[u] = src[1];
+                // Spilled packets (no MACs), the lean path: the merge is
+                // instruction-bound (PMC on C3: 28 % of wave time issuing at
+                // 4 waves per SIMD, 14k VALU + 7k SALU instructions per wave),
+                // so no binary search per record (the wave's first index is
+                // searched once, each lane steps forward over the few sets
+                // its index is past) and update_flow of one packet written
+                // out directly instead of through a FlowPart.
+                for (uint32_t idx = tid; idx < total; idx += MB) {
+                    const uint32_t iw = __builtin_amdgcn_readfirstlane(idx);  // the wave's smallest index
+                    uint32_t lo_i = 0, hi_i = nset - 1;
+                    while (lo_i < hi_i) {
+                        const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                        if (m_start[mid] <= iw) lo_i = mid;
+                        else hi_i = mid - 1;
                     }
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        if (i0 + u * MB >= total) break;
+                    while (lo_i + 1 < nset && m_start[lo_i + 1] <= idx) lo_i++;
+                    const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
+                    const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * 2;
+                    const uint4 v0 = src[0], v1 = src[1];
+                    const unsigned long long gi = a.B.first + m_wb[lo_i] + v1.z;
+                    const uint32_t k0 = v0.x, k1 = v0.y, k2 = v0.z, tag = v0.w;
+                    const uint32_t h = lt_hash(k0, k1, k2, tag);
+                    uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
+                    int state = 0, probes = 0;
+                    for (int it = 0; it < 128; it++) {  // find or claim (the hot kernel's protocol)
+                        if (state == 0) {
+                            const uint4 kk = m_key[e];
+                            if (kk.w & LT_READY) {
+                                if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2) state = 1;
+                                else if (++probes == 64) state = 2;
+                                else e = (e + 1) & (MT - 1);
+                            } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
+                                m_key[e].x = k0;
+                                m_key[e].y = k1;
+                                m_key[e].z = k2;
+                                __threadfence_block();
+                                atomicExch(&m_key[e].w, tag | LT_READY);
+                                state = 1;
+                            }
+                        }
+                        if (__ballot(state == 0) == 0) break;
+                    }
+                    const uint32_t dir = (v1.w >> 8) & 1u, tf = v1.w & 0xFFu;
+                    const uint32_t pkt = v1.y & 0xFFFFu, ttl = (v1.y >> 16) & 0xFFu;
+                    if (state == 1) {  // update_flow of one packet (flows.rs:11-42), order-free part
+                        atomicAdd(&m_pk[dir][e], 1u);
+                        atomicAdd(&m_by[dir][e], (unsigned long long)v1.x);
+                        const uint32_t gmn0 = m_mn[0][e], gmn1 = m_mn[1][e], gmx0 = m_mx[0][e], gmx1 = m_mx[1][e];
+                        const unsigned long long gfa = m_fa[e], gfc = m_fc[e], gla = m_la[e];
+                        if (pkt < gmn0) atomicMin(&m_mn[0][e], pkt);
+                        if (ttl < gmn1) atomicMin(&m_mn[1][e], ttl);
+                        if (pkt > gmx0) atomicMax(&m_mx[0][e], pkt);
+                        if (ttl > gmx1) atomicMax(&m_mx[1][e], ttl);
+                        for (uint32_t t = tf; t; t &= t - 1) atomicAdd(&m_fl[__builtin_ctz(t)][e], 1u);
+                        if (gi < gfa) atomicMin(&m_fa[e], gi);
+                        if (((v1.y >> 24) & 1u) && gi < gfc) atomicMin(&m_fc[e], gi);
+                        if (tf & 5u) atomicMin(&m_fr[e], gi);
+                        if (gi + 1 > gla) atomicMax(&m_la[e], gi + 1);
+                    } else {  // no entry within 64 probes: the global path
                         FlowPart f;
-                        spill_to_part(v1[u].x, v1[u].y, v1[u].z, v1[u].w, a.B.first + wbv[u], f);
-                        merge_rec(lt_hash(v0[u].x, v0[u].y, v0[u].z, v0[u].w), v0[u].x, v0[u].y, v0[u].z, v0[u].w, 0u,
-                                  0u, 0u, f);
+                        spill_to_part(v1.x, v1.y, v1.z, v1.w, a.B.first + m_wb[lo_i], f);
+                        const uint32_t d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
+                        if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
                     }
                 }
                 __syncthreads();
                 continue;
             }
-#endif
             for (uint32_t idx = tid; idx < total; idx += MB) {
                 uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
                 while (lo_i < hi_i) {
@@ -2016,6 +2053,8 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
         }
         __syncthreads();  // (the next owner re-initialises the table)
+        if (tid == 0) s_me = S.O > gridDim.x ? gridDim.x + (uint32_t)atomicAdd(&a.g->n_owner, 1ull) : S.O;
+        __syncthreads();
     }
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
     // of the last workgroup, off the other owners' critical path)
@@ -2373,11 +2412,15 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
 // polls it: no copy kernel, no event on the way back).
 __device__ void publish_ctl(Glob* g, unsigned long long* done, Ctl* host_ctl, uint32_t seq) {
     __shared__ unsigned long long p_rank;
+    // Every wave waits for its own counter atomics to be performed (they are
+    // device-scope: at the coherence point once acknowledged), then the
+    // workgroup counts itself done.  No agent-scope fence per workgroup: it
+    // writes back the XCD's L2 (the records just stored) and ~1-4k
+    // workgroups serialised on it (C4 k_finalize 327 -> 192 us with the grid
+    // capped; the records reach later kernels at the launch boundary).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        p_rank = atomicAdd(done, 1ull);
-    }
+    if (threadIdx.x == 0) p_rank = atomicAdd(done, 1ull);
     __syncthreads();
     if (p_rank != gridDim.x - 1) return;
     __threadfence();
@@ -2581,6 +2624,9 @@ struct CleanArgs {
     int spec;
     unsigned long long timeout_us, recs_cap;
     int abl = 0;  // diagnostics only (FLUERE_CLEAN_ABL, wrong results): 1 no table clears, 2 no accumulator clears
+    // 1: tables 0 and 1 (the IPv4 chain) are cleared whole, sequentially,
+    // instead of two random 16-byte entries per flow (runs with many flows)
+    int bulk = 0;
 };
 
 __device__ __host__ __forceinline__ bool run_complete(const Glob& g, uint32_t err, unsigned long long timeout_us,
@@ -2597,7 +2643,7 @@ __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool
     static_assert(N_TABLES % 2 == 0, "slot rows are whole 8-byte pairs");
     uint2 sv[N_TABLES / 2];
 #pragma unroll
-    for (int t = 0; t < N_TABLES / 2; t++) sv[t] = row[t];
+    for (int t = 0; t < N_TABLES / 2; t++) sv[t] = (a.bulk && t == 0) ? make_uint2(NONE32, NONE32) : row[t];
 #pragma unroll
     for (int t = 0; t < N_TABLES / 2; t++) {
         const uint32_t s0 = sv[t].x, s1 = sv[t].y;
@@ -2607,7 +2653,7 @@ __device__ __forceinline__ void cleanup_one(const CleanArgs& a, uint32_t d, bool
             *reinterpret_cast<ulonglong2*>(&a.T.tab[2 * t][2 * s0]) = make_ulonglong2(EMPTY, EMPTY);
         if (tables && !(a.abl & 1) && s1 != NONE32)
             *reinterpret_cast<ulonglong2*>(&a.T.tab[2 * t + 1][2 * s1]) = make_ulonglong2(EMPTY, EMPTY);
-        if ((s0 & s1) != NONE32) row[t] = make_uint2(NONE32, NONE32);
+        if (!a.bulk && (s0 & s1) != NONE32) row[t] = make_uint2(NONE32, NONE32);  // (bulk: every claim rewrites its row)
     }
     if (a.abl & 2) return;
     a.A.pk[0][d] = a.A.pk[1][d] = 0;
@@ -2635,12 +2681,16 @@ __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words) 
     for (size_t d = t0; d < nf; d += stride) cleanup_one(a, (uint32_t)d, !failed);
     if (failed)
         for (size_t w = t0; w < tab_words; w += stride) a.T.tab[0][w] = EMPTY;  // tables are contiguous
+    else if (a.bulk)  // tables 0 and 1: 2 (C + 1) entries of 16 bytes
+        for (size_t w = t0; w < 2 * ((size_t)a.T.C + 1); w += stride)
+            reinterpret_cast<ulonglong2*>(a.T.tab[0])[w] = make_ulonglong2(EMPTY, EMPTY);
     __shared__ unsigned long long s_rank;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        s_rank = atomicAdd(&a.g->clean_done, 1ull);
-    }
+    // (no fence: what the last workgroup resets, every workgroup read before
+    // its work, and its count comes after that work; the stores reach the
+    // next kernel at the launch boundary.  A per-workgroup agent-scope fence
+    // writes back the XCD's L2 and serialised thousands of workgroups.)
+    if (threadIdx.x == 0) s_rank = atomicAdd(&a.g->clean_done, 1ull);
     __syncthreads();
     if (s_rank != gridDim.x - 1) return;
     __threadfence();
@@ -3806,6 +3856,21 @@ extern "C" int fluere_close(fluere_ctx* c) {
 static unsigned flow_grid(fluere_ctx* c) {
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(c->fmax, 256), (uint64_t)c->n_cu * 16));
 }
+// Grid of the per-flow kernels that end on a done-counter (k_cleanup,
+// k_finalize): grid-stride over n flows with at most 4 workgroups per CU, so
+// a million-flow run counts ~1k workgroups done on the one word, not ~4k.
+static unsigned done_grid(fluere_ctx* c, uint64_t n) {
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->n_cu * 4));
+}
+
+// Sequential clear of the IPv4 chain's tables when the flows to clear would
+// cost more as random 16-byte writes (two per flow) than 32 (C + 1) bytes
+// written in order: more than (C + 1) / 16 flows.
+static int bulk_clean(const fluere_ctx* c, uint64_t nf) {
+    static const int env = getenv("FLUERE_BULK_CLEAN") ? atoi(getenv("FLUERE_BULK_CLEAN")) : -1;
+    if (env >= 0) return env;
+    return nf != ~0ull && nf > ((uint64_t)c->C + 1) / 16 ? 1 : 0;
+}
 
 // Clears the flows of the last run and re-initialises every run counter
 // (one launch; see k_cleanup).
@@ -3815,10 +3880,10 @@ static int clear_flows(fluere_ctx* c) {
     CleanArgs a{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
     static const int clean_abl = getenv("FLUERE_CLEAN_ABL") ? atoi(getenv("FLUERE_CLEAN_ABL")) : 0;
     a.abl = clean_abl;
+    a.bulk = bulk_clean(c, c->prev_nf == ~0ull ? c->last_nf : c->prev_nf);
     // grid: the last fetched run's flow count when known (k_cleanup is
     // grid-stride over the device count, so any grid is correct)
-    const unsigned g = c->prev_nf == ~0ull ? flow_grid(c)
-                                           : (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(1, grid_for(c->prev_nf, 256)));
+    const unsigned g = done_grid(c, c->prev_nf == ~0ull ? c->fmax : c->prev_nf);
     k_cleanup<<<g, 256, 0, s>>>(a, (size_t)N_TABLES * 2 * (c->C + 1));
     c->prev_nf = ~0ull;
     HIPCHECK(hipGetLastError());
@@ -4464,7 +4529,8 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     // enough owners that each one's share of the flows (the last run's count
     // as the estimate) fits its merge workgroup's 1024-entry LDS table at ~60 %
     // load; at least one per CU
-    uint32_t o = 256;
+    static const uint32_t o_min = getenv("FLUERE_MIN_OWNERS") ? (uint32_t)atoi(getenv("FLUERE_MIN_OWNERS")) : 256u;
+    uint32_t o = o_min;
     while (o < (uint32_t)MAX_OWNERS && c->last_nf > 640ull * o) o *= 2;
     const int cap = c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS;
     return (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
@@ -4625,11 +4691,10 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     P.ca = CleanArgs{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
     static const int clean_abl = getenv("FLUERE_CLEAN_ABL") ? atoi(getenv("FLUERE_CLEAN_ABL")) : 0;
     P.ca.abl = clean_abl;
+    P.ca.bulk = bulk_clean(c, c->prev_nf == ~0ull ? c->last_nf : c->prev_nf);
     // cleanup grid: the last fetched run's flow count when known (k_cleanup is
     // grid-stride over the device count, so any grid is correct)
-    P.clean_grid = c->prev_nf == ~0ull
-                       ? flow_grid(c)
-                       : (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(1, grid_for(c->prev_nf, 256)));
+    P.clean_grid = done_grid(c, c->prev_nf == ~0ull ? c->fmax : c->prev_nf);
     P.tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
     P.clean = c->precleaned ? 0 : 1;
     if ((rc = plan_batches(c, P))) return rc;
@@ -4650,13 +4715,14 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
         P.fa.defer = c->d_fdefer;
         P.spec_ca = P.ca;
         P.spec_ca.spec = 1;
+        P.spec_ca.bulk = bulk_clean(c, c->last_nf);  // (this run's flows: the last run's count as the guess)
         P.spec_ca.timeout_us = c->timeout_ms * 1000ull;
         P.spec_ca.recs_cap = c->d_recs_cap;
         // grid-stride over the device flow count: any grid is correct; size
         // them for the last known flow count (k_finalize's workgroups also
         // count themselves done on one counter before the last one publishes)
         const uint64_t guess = c->last_nf ? c->last_nf : c->fmax;
-        P.fin_grid = (unsigned)std::min<uint64_t>(flow_grid(c), std::max<uint64_t>(8, grid_for(guess, 256)));
+        P.fin_grid = std::max(8u, done_grid(c, guess));
         P.spec_grid = P.fin_grid;
     }
     return FLUERE_OK;
@@ -4666,7 +4732,7 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
     hipStream_t s = c->stream;
     for (int i = 0; i < P.nb; i++) {
         const AggArgs& a = P.agg[i];
-        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 32, s));  // n_slow, n_spill, n_dspill, n_gen (k_cleanup zeroed them for batch 0)
+        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 40, s));  // n_slow, n_spill, n_dspill, n_gen, n_owner (k_cleanup zeroed them for batch 0)
         const unsigned grid = P.agg_grid[i];
         const void* fn = P.spill ? (const void*)k_parse_spill
                        : P.macs ? (const void*)k_parse_agg<0, true>
@@ -4757,7 +4823,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
             hipMemsetParams mp{};
             mp.dst = &c->d_glob->n_slow;
             mp.elementSize = 4;
-            mp.width = 8;  // n_slow, n_spill, n_dspill, n_gen
+            mp.width = 10;  // n_slow, n_spill, n_dspill, n_gen, n_owner
             mp.height = 1;
             mp.pitch = 16;
             mp.value = 0;
@@ -4846,6 +4912,13 @@ static void debug_counters(fluere_ctx* c, const Glob* have = nullptr) {
                             ph[k] += (m[b * 8 + k] - m0) / 100.0 / 256;
                             mx[k] = std::max(mx[k], (m[b * 8 + k] - m0) / 100.0);
                         }
+                    {  // the spread of the owners' record phase over the workgroups (the kernel waits for the slowest)
+                        std::vector<double> pr;
+                        for (int b = 0; b < 256; b++) pr.push_back((m[b * 8 + 3] - m[b * 8 + 2]) / 100.0);
+                        std::sort(pr.begin(), pr.end());
+                        fprintf(stderr, "[fluere] merge record phase per workgroup (us): min %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f\n",
+                                pr[0], pr[25], pr[128], pr[230], pr[253], pr[255]);
+                    }
                     fprintf(stderr, "[fluere] merge phases (mean/max us): init %.1f/%.1f offs+scan %.1f/%.1f parts %.1f/%.1f "
                             "claims %.1f/%.1f n_flows %.1f/%.1f ids %.1f/%.1f global %.1f/%.1f\n",
                             ph[1], mx[1], ph[2], mx[2], ph[3], mx[3], ph[7], mx[7], ph[6], mx[6], ph[4], mx[4], ph[5], mx[5]);
