@@ -384,7 +384,7 @@ __device__ __forceinline__ uint32_t flow_of(const TableSet& T, const Parsed& P, 
 // bitmap of CBITS bits, set for every flow the certificate rejects): a packet
 // whose key's bit is clear belongs to no complex flow, so the replay skips its
 // dictionary walk.
-constexpr uint32_t CBITS_LOG2 = 24;
+constexpr uint32_t CBITS_LOG2 = 22;  // complex-flow filter: one byte per bucket (plain stores, no atomics)
 __device__ __forceinline__ uint32_t ckey_bucket(const uint32_t* w) {
     uint32_t h = 0x2545F491u;
 #pragma unroll
@@ -539,9 +539,13 @@ __device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_re
 // emit_record_block for records built in place, thread t's in S.rec[t] (a
 // kernel that builds its record field by field in LDS holds no 38-word record
 // in registers): the copy gathers the wanted slots in thread order.
+// tot (optional): thread 0 adds the block's updates / ended counts there
+// instead of one pair of global atomics per call (the caller adds its totals
+// once: thousands of blocks on two words serialised k_finalize).
 __device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_record* out, uint64_t cap, bool want,
                                                    uint32_t d_pkts, bool ended, unsigned long long* aux = nullptr,
-                                                   unsigned long long a0 = 0, unsigned long long a1 = 0) {
+                                                   unsigned long long a0 = 0, unsigned long long a1 = 0,
+                                                   unsigned long long* tot = nullptr) {
     const uint32_t w = threadIdx.x >> 6;
     const uint64_t m = __ballot(want), em = __ballot(want && ended);
     const unsigned long long upd = wave_sum(want ? (unsigned long long)d_pkts : 0ull);
@@ -562,8 +566,13 @@ __device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_r
         }
         S.base = t[0] ? atomicAdd(&g->n_rec, t[0]) : 0ull;
         S.n = t[0];
-        if (t[1]) atomicAdd(&g->n_updates, t[1]);
-        if (t[2]) atomicAdd(&g->n_ended, t[2]);
+        if (tot) {
+            tot[0] += t[1];
+            tot[1] += t[2];
+        } else {
+            if (t[1]) atomicAdd(&g->n_updates, t[1]);
+            if (t[2]) atomicAdd(&g->n_ended, t[2]);
+        }
     }
     __syncthreads();
     if (want) {

@@ -99,7 +99,7 @@ struct ExactJob {
     const ExMeta* ext_cm = nullptr;
     uint64_t ext_n = 0;
     // Mode A: the complex-flow filter (device.h ckey_bucket), or null
-    const uint32_t* cbits = nullptr;
+    const uint8_t* cbits = nullptr;
     // pinned mailbox for the host's scalar reads (null: copies + stream syncs)
     HostMail* mail = nullptr;
     // Mode B without a caller-provided aux_out (one GPU): the records' order

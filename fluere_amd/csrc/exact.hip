@@ -93,7 +93,7 @@ struct AggOp {
 // regions after a scan over the block counts (a scan over every packet's flag
 // and a sparse write per taken packet before).
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
-                                                 const uint32_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
+                                                 const uint8_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
                                                  uint64_t blk0) {
     __shared__ uint32_t s_w[4];
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
         bool maybe = true;
         if (!all && cbits) {  // no complex flow has this key's bucket: no dictionary walk
             const uint32_t b = ckey_bucket(k.w);
-            maybe = (cbits[b >> 5] >> (b & 31)) & 1u;
+            maybe = cbits[b] != 0;
         }
         const uint32_t d = maybe ? dense_of_key(T, k, false, nullptr, nullptr) : FAIL;
         if (d != FAIL && d < T.fmax && (all || cplx[d])) {
@@ -641,6 +641,7 @@ __device__ __forceinline__ void ex_parse(const RecArgs& a, uint64_t gi, Parsed& 
 template <bool GEN>
 __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records_t(RecArgs a) {
     __shared__ EmitLds S;
+    unsigned long long tot[2] = {0, 0};  // thread 0: the workgroup's updates / ended (one atomic pair at the end)
     const uint32_t n_items = GEN ? min(*a.n_defer, a.n_inst) : a.n_inst;
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n_items; i0 += gridDim.x * blockDim.x) {  // (uniform)
         const uint32_t i = i0 + threadIdx.x;
@@ -742,7 +743,11 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records_t(RecArgs a) {
         // (uniform: every thread of the block emits)
         emit_inplace_block(S, a.g, a.out, a.out_cap, rec_live, rec_live ? rec.d_pkts : 0u,
                            rec_live && rec.order_key != NONE64, a.mode_b ? a.aux : nullptr,
-                           kind == K_SWEEP ? cex + 1 : 0ull, kind == K_SWEEP ? cie : 0ull);
+                           kind == K_SWEEP ? cex + 1 : 0ull, kind == K_SWEEP ? cie : 0ull, tot);
+    }
+    if (threadIdx.x == 0) {
+        if (tot[0]) atomicAdd(&a.g->n_updates, tot[0]);
+        if (tot[1]) atomicAdd(&a.g->n_ended, tot[1]);
     }
 }
 
@@ -1177,7 +1182,7 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     // by the first kernel and done by the second (grid-stride over the count).
     if (n_inst) {
         HIPCHECK(hipMemsetAsync(S->ctr + 3, 0, 4, s));
-        k_ex_records_t<false><<<gridn(n_inst, 256), 256, 0, s>>>(ra);
+        k_ex_records_t<false><<<std::min<unsigned>(gridn(n_inst, 256), 1024), 256, 0, s>>>(ra);
         k_ex_records_t<true><<<std::min<unsigned>(gridn(n_inst, 256), 64), 256, 0, s>>>(ra);
     }
     HIPCHECK(hipGetLastError());

@@ -1532,7 +1532,7 @@ struct FinArgs {
     Ctl* host_ctl;   // non-null: the last workgroup writes the run counters to this pinned host copy,
     uint32_t seq;    // then host_ctl->seq = seq (the host polls it: no copy, no event on the way back)
     unsigned long long timeout_us;  // non-zero: skip the flows when expiries can fire (Mode B redoes every flow)
-    uint32_t* cbits = nullptr;      // the exact engine's complex-flow filter (ckey_bucket), or null
+    uint8_t* cbits = nullptr;       // the exact engine's complex-flow filter (ckey_bucket: a byte per bucket), or null
     uint32_t* defer = nullptr;      // k_finalize: certified flows whose first packet needs the general
                                     // parser (Glob::n_fdefer of them), finalized by k_finalize_gen
 };
@@ -1572,7 +1572,7 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
         a.complex[d] = 1;
         if (a.cbits) {
             const uint32_t b = ckey_bucket(reinterpret_cast<const uint32_t*>(a.T.flow_key + (size_t)d * 56));
-            atomicOr(&a.cbits[b >> 5], 1u << (b & 31));
+            a.cbits[b] = 1;
         }
         cplx = true;
         cplx_pkts = v.pk[0] + v.pk[1];
@@ -2446,20 +2446,39 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
     const bool mode_b = a.timeout_us && gg.valid && gg.tmax - gg.tmin >= a.timeout_us;
     const uint32_t nf = mode_b ? 0u : min(*a.T.n_flows, a.T.fmax);
     __shared__ EmitLds S;
+    __shared__ unsigned long long s_tot[4];  // updates, ended, complex flows, their packets (this workgroup)
+    if (threadIdx.x < 4) s_tot[threadIdx.x] = 0;
+    unsigned long long tot[2] = {0, 0}, n_cplx = 0, cplx_all = 0;  // (thread 0's totals: updates, ended)
     for (uint32_t d0 = blockIdx.x * blockDim.x; d0 < nf; d0 += gridDim.x * blockDim.x) {
         const uint32_t d = d0 + threadIdx.x;
         fluere_record& r = S.rec[threadIdx.x];
         bool cplx = false;
         unsigned long long cplx_pkts = 0;
         const bool want = d < nf && finalize_one<false>(a, d, r, cplx, cplx_pkts);
-        emit_inplace_block(S, a.g, a.out, a.out_cap, want, want ? r.d_pkts : 0u, want && r.order_key != NONE64);
-        const uint64_t cm = __ballot(cplx);
-        if (cm) {
-            const unsigned long long pk = wave_sum(cplx_pkts);
-            if ((uint32_t)(threadIdx.x & 63) == (uint32_t)__builtin_ctzll(cm)) {
-                atomicAdd(&a.g->n_complex, (unsigned long long)__popcll(cm));
-                atomicAdd(&a.g->n_complex_pkts, pk);
-            }
+        emit_inplace_block(S, a.g, a.out, a.out_cap, want, want ? r.d_pkts : 0u, want && r.order_key != NONE64, nullptr, 0,
+                           0, tot);
+        n_cplx += cplx ? 1 : 0;
+        cplx_all += cplx_pkts;
+    }
+    // the workgroup's counters: one set of global atomics (per-block or
+    // per-wave atomics on these few words serialised a million-flow run)
+    n_cplx = wave_sum(n_cplx);
+    cplx_all = wave_sum(cplx_all);
+    if ((threadIdx.x & 63) == 0 && n_cplx) {
+        atomicAdd(&s_tot[2], n_cplx);
+        atomicAdd(&s_tot[3], cplx_all);
+    }
+    if (threadIdx.x == 0) {
+        s_tot[0] = tot[0];
+        s_tot[1] = tot[1];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_tot[0]) atomicAdd(&a.g->n_updates, s_tot[0]);
+        if (s_tot[1]) atomicAdd(&a.g->n_ended, s_tot[1]);
+        if (s_tot[2]) {
+            atomicAdd(&a.g->n_complex, s_tot[2]);
+            atomicAdd(&a.g->n_complex_pkts, s_tot[3]);
         }
     }
     if (a.host_ctl) publish_ctl(a.g, &a.g->fin_done, a.host_ctl, a.seq);
@@ -3583,7 +3602,7 @@ struct fluere_ctx {
     uint8_t* d_flow_key = nullptr;
     uint8_t* d_complex = nullptr;
     uint32_t* d_fdefer = nullptr;  // k_finalize -> k_finalize_gen: flows for the general parser [fmax]
-    uint32_t* d_cbits = nullptr;   // complex-flow filter of the exact engine (1 << CBITS_LOG2 bits)
+    uint8_t* d_cbits = nullptr;    // complex-flow filter of the exact engine (1 << CBITS_LOG2 bytes)
     uint8_t* d_active = nullptr;
     Batch* d_batches = nullptr;
     int d_batches_cap = 0;
@@ -3760,7 +3779,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipMalloc(&c->d_fdefer, F * 4) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    if (hipMalloc(&c->d_cbits, (1u << CBITS_LOG2) / 8) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_cbits, 1u << CBITS_LOG2) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
         hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess ||
@@ -3778,7 +3797,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     k_fill_u32<<<grid_for(8 * F, 256), 256, 0, s>>>(c->acc.fl[0], 8 * F, 0);
     k_fill_u32<<<grid_for(F * N_TABLES, 256), 256, 0, s>>>(c->acc.slots, F * N_TABLES, NONE32);
     if (hipMemsetAsync(c->d_complex, 0, F, s) != hipSuccess) return fail(FLUERE_E_HIP);
-    if (hipMemsetAsync(c->d_cbits, 0, (1u << CBITS_LOG2) / 8, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    if (hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s) != hipSuccess) return fail(FLUERE_E_HIP);
     {
         Ctl z{};
         z.g.tmin = NONE64;
@@ -5224,7 +5243,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         }
     }
     // the complex-flow filter is per run: clear the bits the speculative finalize set
-    if (g.n_complex) HIPCHECK(hipMemsetAsync(c->d_cbits, 0, (1u << CBITS_LOG2) / 8, s));
+    if (g.n_complex) HIPCHECK(hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s));
     c->n_ended = n_ended;
     c->have_results = true;
     float ms_parse = 0;
