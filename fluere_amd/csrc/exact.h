@@ -106,6 +106,9 @@ struct ExactJob {
     // words, grown to the record count (records already there keep zeros)
     unsigned long long** recaux = nullptr;
     uint64_t* recaux_cap = nullptr;
+    // Mode A: the records already emitted (the caller's fresh counters), or ~0
+    // (exact_finish reads them): lets exact_finish skip its host read
+    uint64_t n_rec_known = ~0ull;
 };
 
 struct ExactResult {

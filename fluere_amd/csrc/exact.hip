@@ -180,6 +180,10 @@ __global__ void __launch_bounds__(256) k_ex_heads(uint64_t n, const uint32_t* hf
     if (p < n && hf[p]) heads[hpos[p]] = (uint32_t)p;
 }
 
+__global__ void k_ex_nkeys(const uint32_t* hpos_last, const uint32_t* hf_last, uint32_t* out) {
+    if (threadIdx.x == 0) *out = *hpos_last + *hf_last;
+}
+
 // ---- 3. Mode B: timestamps non-decreasing over the valid packets? ---------
 __global__ void __launch_bounds__(256) k_ex_mono(uint64_t n, const ExMeta* cm, uint32_t* bad) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -241,7 +245,7 @@ namespace {
 // ---- 4. the chase: one thread per key ----------------------------------------
 struct ChaseArgs {
     uint64_t n;
-    uint32_t n_keys;
+    uint32_t n_keys;         // (d_nkeys non-null: the count is on the device, the grid covers n)
     const uint32_t* heads;
     const ExMeta* sm;   // sorted by (key, index)
     const uint32_t* sval;  // sorted position -> capture-order index k (Mode B: into cm)
@@ -273,6 +277,7 @@ struct ChaseArgs {
     fluere_flow_annex* annex;
     uint32_t* annex_of;
     const uint8_t* flow_key;  // TableSet::flow_key (56-byte canonical keys by dense id)
+    const uint32_t* d_nkeys = nullptr;  // Mode A: the key count, written on the device (no host read)
 };
 
 __device__ __forceinline__ unsigned long long exp_of(uint64_t t, uint64_t timeout_us) {
@@ -312,9 +317,10 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
 
 __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= a.n_keys) return;
+    const uint32_t n_keys = a.d_nkeys ? *a.d_nkeys : a.n_keys;
+    if (q >= n_keys) return;
     const uint32_t p0 = a.heads[q];
-    const uint32_t pend = q + 1 < a.n_keys ? a.heads[q + 1] : (uint32_t)a.n;
+    const uint32_t pend = q + 1 < n_keys ? a.heads[q + 1] : (uint32_t)a.n;
     // pending expiry entries per orientation, sorted by (sweep point, exp,
     // creation): the BTreeMap's pop order among the entries that can evict
     // this orientation's flow (offline_fluereflows.rs:161-175)
@@ -506,8 +512,12 @@ constexpr uint32_t AGG_THREAD = 48;    // runs up to this long: one thread
 constexpr uint32_t AGG_WAVE = 16384;   // up to this: one wave; longer: one 1024-thread block
 
 // thread per instance; longer runs are listed for the wave / block kernels
+// p_ninst (these three kernels and k_ex_records_t): the instance count on
+// the device (Mode A: no host read; the grid covers an upper bound)
 __global__ void __launch_bounds__(256) k_ex_agg(uint32_t n_inst, const uint32_t* ist, const uint32_t* iend,
-                                                const ExMeta* sm, Agg* aggs, uint32_t* lists, uint32_t* cnt) {
+                                                const ExMeta* sm, Agg* aggs, uint32_t* lists, uint32_t* cnt,
+                                                const uint32_t* p_ninst) {
+    if (p_ninst) n_inst = *p_ninst;
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     bool wide = false, huge = false;
     if (q < n_inst) {
@@ -542,7 +552,8 @@ __global__ void __launch_bounds__(256) k_ex_agg(uint32_t n_inst, const uint32_t*
 // one wave per listed run (grid-stride over the device-side count)
 __global__ void __launch_bounds__(256) k_ex_agg_wave(uint32_t n_inst, const uint32_t* ist, const uint32_t* iend,
                                                      const ExMeta* sm, Agg* aggs, const uint32_t* lists,
-                                                     const uint32_t* cnt) {
+                                                     const uint32_t* cnt, const uint32_t* p_ninst) {
+    if (p_ninst) n_inst = *p_ninst;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     const uint32_t nwide = cnt[0];
@@ -560,8 +571,9 @@ __global__ void __launch_bounds__(256) k_ex_agg_wave(uint32_t n_inst, const uint
 // one block per listed huge run (an elephant instance)
 __global__ void __launch_bounds__(1024) k_ex_agg_block(uint32_t n_inst, const uint32_t* ist, const uint32_t* iend,
                                                        const ExMeta* sm, Agg* aggs, const uint32_t* lists,
-                                                       const uint32_t* cnt) {
+                                                       const uint32_t* cnt, const uint32_t* p_ninst) {
     __shared__ Agg part[16];
+    if (p_ninst) n_inst = *p_ninst;
     const uint32_t nhuge = cnt[1];
     for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {
         const uint32_t q = lists[n_inst - 1 - i];
@@ -606,6 +618,7 @@ struct RecArgs {
     // emission order (by ending packet, FIN/RST before the sweep, sweeps by
     // (exp, push order); offline_fluereflows.rs:152-175); fetch_records sorts by them.
     unsigned long long* aux;
+    const uint32_t* p_ninst; // the instance count on the device, or null (n_inst)
     uint32_t* defer;         // k_ex_records_t<false> -> <true>: instances for the general parser
     uint32_t* n_defer;       //   (their count, device)
     int shard_mode;
@@ -642,7 +655,8 @@ template <bool GEN>
 __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records_t(RecArgs a) {
     __shared__ EmitLds S;
     unsigned long long tot[2] = {0, 0};  // thread 0: the workgroup's updates / ended (one atomic pair at the end)
-    const uint32_t n_items = GEN ? min(*a.n_defer, a.n_inst) : a.n_inst;
+    const uint32_t n_inst = a.p_ninst ? *a.p_ninst : a.n_inst;
+    const uint32_t n_items = GEN ? min(*a.n_defer, n_inst) : n_inst;
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n_items; i0 += gridDim.x * blockDim.x) {  // (uniform)
         const uint32_t i = i0 + threadIdx.x;
         const bool lane_live = i < n_items;
@@ -1015,9 +1029,16 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1);
         HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed
     }
-    // one host read: key count, monotonicity, the first and last times
+    // one host read: key count, monotonicity, the first and last times.  Mode
+    // A (not shard mode) needs none of them on the host: the key count stays
+    // on the device and the chase's grid covers the replayed packets (every
+    // host round trip leaves the GPU idle for ~50-60 us: the wait, then the
+    // next submission on an idle queue)
     unsigned long long hv[5] = {0, 0, 0, 0, 0};
-    {
+    const bool dev_keys = !J.mode_b && !J.shard_mode;
+    if (dev_keys) {
+        k_ex_nkeys<<<1, 64, 0, s>>>(hpos + n - 1, hf + n - 1, ctr + 3);
+    } else {
         const void* src[5] = {hpos + n - 1, hf + n - 1, ctr + 1, &cm[0].t, &cm[n - 1].t};
         const int by[5] = {4, 4, 4, 8, 8};
         int rc = mail_fetch(J.mail, s, J.mode_b ? 5 : 2, src, by, hv);
@@ -1052,6 +1073,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
                       (J.mode_b && !S->mono) ? S->tree : nullptr, P, S->tbl, t0, bw, nb, nullptr,
                       S->sflag, S->iend, S->ikind, S->ij, S->iie, S->iex, S->ej, S->link, S->plink,
                       J.shard_mode, S->irole, S->ikey, S->annex, J.annex_of, J.T.flow_key};
+    if (dev_keys) S->ca.d_nkeys = ctr + 3;  // (ctr[3] is the records' defer count only after the chase)
     return FLUERE_OK;
 }
 
@@ -1078,7 +1100,7 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
         }
     }
     HIPCHECK(hipMemsetAsync(S->sflag, 0, n * 4, s));
-    k_ex_chase<<<gridn(S->n_keys, 64), 64, 0, s>>>(S->ca);
+    k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
     tb = S->tmp;
     HIPCHECK(hipcub::DeviceScan::InclusiveSum(S->tp, tb, S->sflag, S->incl, in, s));
     k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->incl, S->ist);
@@ -1122,9 +1144,19 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     hipStream_t s = S->s;
     const uint64_t n = S->n;
     if (!n) return FLUERE_OK;
-    // one host read: the instance count and the records already emitted
+    // the instance count and the records already emitted: one host read, or
+    // (Mode A with the record count known to the caller) none -- the
+    // kernels read the count on the device and their grids cover n
     unsigned long long hv[2] = {0, 0};
-    {
+    // (the record buffer is grown to the bound, kept below 4 GiB of HBM)
+    const bool dev_inst = !J.mode_b && !J.shard_mode && !seeds && !aux_out && J.n_rec_known != ~0ull &&
+                          (J.n_rec_known + n <= *J.d_recs_cap ||
+                           (J.n_rec_known + n) * sizeof(fluere_record) <= (4ull << 30));
+    const uint32_t* p_ninst = dev_inst ? S->incl + n - 1 : nullptr;
+    if (dev_inst) {
+        hv[0] = n;  // (an upper bound: every instance holds a packet)
+        hv[1] = J.n_rec_known;
+    } else {
         const void* src[2] = {S->incl + n - 1, reinterpret_cast<const char*>(J.g) + offsetof(Glob, n_rec)};
         const int by[2] = {4, 8};
         int rc = mail_fetch(J.mail, s, 2, src, by, hv);
@@ -1135,12 +1167,12 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     // ---- 6. per-instance aggregates over each instance's contiguous run
     HIPCHECK(hipMemsetAsync(S->ctr, 0, 8, s));
     if (n_inst) {
-        k_ex_agg<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
-        k_ex_agg_wave<<<1024, 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
-        k_ex_agg_block<<<256, 1024, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr);
+        k_ex_agg<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
+        k_ex_agg_wave<<<1024, 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
+        k_ex_agg_block<<<256, 1024, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
     }
     HIPCHECK(hipGetLastError());
-    S->R.instances = n_inst;
+    S->R.instances = dev_inst ? 0 : n_inst;
     // ---- 7. records
     const uint64_t want = n_rec0 + n_inst;
     if (want > *J.d_recs_cap) {  // grow, keeping the records already there
@@ -1174,7 +1206,7 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
         }
     }
     RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, n_inst, S->aggs, S->ist, S->sm, S->iend, S->ikind,
-               S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, aux, S->idx, S->ctr + 3,
+               S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, aux, p_ninst, S->idx, S->ctr + 3,
                J.shard_mode, S->irole, S->ikey, S->annex, seeds};
     // runs <= n (every run holds a packet); records appended per block, Mode B
     // with their order words (fetch_records orders them: no device sort).

@@ -5161,6 +5161,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
                        &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
             J.cbits = c->d_cbits;
             J.mail = c->h_mail;
+            J.n_rec_known = g.n_rec;  // (g: this run's counters after finalize)
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
             out.passes = er.iterations;
