@@ -395,6 +395,17 @@ __device__ __forceinline__ uint32_t ckey_bucket(const uint32_t* w) {
     return h >> (32 - CBITS_LOG2);
 }
 
+// ckey_bucket of an IPv4 non-MAC canonical key (the hot kernels' key words:
+// lower ip, higher ip, lower port << 16 | higher port, protocol)
+__device__ __forceinline__ uint32_t ckey_bucket_v4(uint32_t lo, uint32_t hi, uint32_t ports, uint32_t proto) {
+    const uint32_t w[14] = {lo, 0, 0, 0, hi, 0, 0, 0, ports, proto, 0, 0, 0, 0};
+    return ckey_bucket(w);
+}
+// Per-packet filter words of the hot pass (AggArgs::phash): the packet's
+// ckey_bucket, or PH_PARSE (the hot parser did not key it: the exact engine
+// parses the packet itself).
+constexpr uint32_t PH_PARSE = 0xFFFFFFFFu;
+
 // Append one record (Mode A paths): position, updates and ended counters.
 __device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {
     const unsigned long long pos = atomicAdd(&g->n_rec, 1ull);

@@ -109,6 +109,10 @@ struct ExactJob {
     // Mode A: the records already emitted (the caller's fresh counters), or ~0
     // (exact_finish reads them): lets exact_finish skip its host read
     uint64_t n_rec_known = ~0ull;
+    // Mode A: the hot pass's per-packet filter words (AggArgs::phash), packet
+    // B.first - phash_base of each batch first, or null
+    const uint32_t* phash = nullptr;
+    uint64_t phash_base = 0;
 };
 
 struct ExactResult {

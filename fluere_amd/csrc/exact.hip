@@ -94,11 +94,18 @@ struct AggOp {
 // and a sparse write per taken packet before).
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
                                                  const uint8_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
-                                                 uint64_t blk0) {
+                                                 uint64_t blk0, const uint32_t* phash) {
     __shared__ uint32_t s_w[4];
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the hot pass's filter word: a keyed packet whose bucket holds no complex
+    // flow is skipped without its parse (PH_PARSE: parse it here)
+    bool skip = li >= B.n;
+    if (!skip && phash && !all && cbits) {
+        const uint32_t hb = phash[li];
+        skip = hb != PH_PARSE && cbits[hb & ((1u << CBITS_LOG2) - 1)] == 0;
+    }
     Parsed P;
-    if (li < B.n) parse_record(B, li, macs != 0, 0, P);
+    if (!skip) parse_record(B, li, macs != 0, 0, P);
     else P.cls = 1;
     uint32_t take = 0;
     ExMeta m;
@@ -947,7 +954,8 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk);
+            const uint32_t* ph = J.phash && !J.mode_b ? J.phash + (B.first - J.phash_base) : nullptr;
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk, ph);
             blk += gridn(B.n, 256);
         }
     }
@@ -1247,7 +1255,7 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk);
+            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk, nullptr);
             blk += gridn(B.n, 256);
         }
         unsigned long long last[2] = {0, 0};

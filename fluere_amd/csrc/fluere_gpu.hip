@@ -192,6 +192,8 @@ struct AggArgs {
     int slow_kernel;           // the slow list is k_slow's (launched before the merge), not the merge tail's
     int macs;
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
+    uint32_t* phash;           // or null: per packet of the batch, its ckey_bucket or PH_PARSE (device.h), for
+                               // the exact engine's filter (k_ex_meta reads it instead of parsing every packet)
 };
 
 // Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
@@ -467,6 +469,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             q[u].k1 = q[u].hi_ip;
             q[u].k2 = q[u].kports;
             q[u].tag = h.proto << 24;
+            if (!MACS && a.phash && live[u])
+                a.phash[li[u]] = q[u].valid ? ckey_bucket_v4(q[u].k0, q[u].k1, q[u].k2, h.proto) : PH_PARSE;
             q[u].m0 = q[u].m1 = q[u].m2 = 0;
             if (MACS) {  // the MAC pair joins the key (the dictionary is walked once per slot, at the flush)
                 const uint64_t lom = gt ? dmac : smac, him = gt ? smac : dmac;
@@ -1198,6 +1202,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
             const uint4 w_pay = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), (uint32_t)(li - wbase),
                                            h.tf | ((gt ? 1u : 0u) << 8));
             const uint32_t o = owner_of(lt_hash(w_key.x, w_key.y, w_key.z, w_key.w), O);
+            if (a.phash && live) a.phash[li] = valid ? ckey_bucket_v4(w_key.x, w_key.y, w_key.z, h.proto) : PH_PARSE;
             if (valid) {
                 c_valid++;
                 tmin = min(tmin, (unsigned long long)h.t);
@@ -3644,6 +3649,10 @@ struct fluere_ctx {
     hipEvent_t ev_ctl = nullptr;                // after a run's counter copy (the speculative cleanup follows)
     uint64_t last_nf = 0;                       // flows of the last completed run (sizing only)
     uint64_t last_n_slow = 0;                   // slow-list packets of the last run (k_slow prediction)
+    uint64_t last_n_complex = 0;                // complex flows of the last run, and whether it was Mode B:
+    int last_mode_b = 0;                        //   the phash prediction (the exact engine's Mode A filter)
+    uint32_t* d_phash = nullptr;                // per packet: ckey_bucket or PH_PARSE (AggArgs::phash)
+    uint64_t phash_cap = 0;
     bool async_nf = false;                      // fluere_export_async left the shard's flow count in h_ctl->pad[0]
     bool pass_in_run = false;
     bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
@@ -3833,6 +3842,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_complex);
     hipFree(c->d_fdefer);
     hipFree(c->d_cbits);
+    hipFree(c->d_phash);
     hipFree(c->d_active);
     hipFree(c->d_batches);
     hipFree(c->d_recs);
@@ -4492,6 +4502,7 @@ struct PassPlan {
     uint32_t slow_grid[PLAN_BATCHES];  // k_slow workgroups (its sets); 0: the merge tail takes the slow list
     int macs, abl;
     int spill;     // 1: the hot pass is k_parse_spill (many flows per window), not k_parse_agg
+    int phash;     // 1: the hot pass writes the per-packet filter words (AggArgs::phash)
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
     int spec;      // 1: k_finalize publishes the counters to the host itself, a speculative k_cleanup follows
     CleanArgs spec_ca;
@@ -4612,6 +4623,18 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         a.v6.addr_of = (uint4*)(k + ((3 * (size_t)(C + 1) + 1) & ~(size_t)1));  // (16-byte aligned)
         a.v6.C = C;
     }
+    // per-packet filter words for the exact engine when the last run replayed
+    // complex flows in Mode A (a prediction: without them k_ex_meta parses
+    // every packet; 4 bytes per packet written by the hot pass)
+    static const int phash_env = getenv("FLUERE_PHASH") ? atoi(getenv("FLUERE_PHASH")) : -1;  // tests / A/B
+    P.phash = !c->use_mac && (phash_env >= 0 ? phash_env : (c->last_n_complex > 0 && !c->last_mode_b)) ? 1 : 0;
+    if (P.phash && c->n_total > c->phash_cap) {
+        hipFree(c->d_phash);
+        c->d_phash = nullptr;
+        c->phash_cap = 0;
+        if (hipMalloc(&c->d_phash, c->n_total * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        c->phash_cap = c->n_total;
+    }
     if (getenv("FLUERE_DEBUG")) {
         if (!g_hot_dbg && hipMalloc(&g_hot_dbg, 4096 * 8 * 8) != hipSuccess) g_hot_dbg = nullptr;
         a.dbg = g_hot_dbg;
@@ -4654,6 +4677,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         if (a.slow_kernel) slow_shape(hb.b.n, sets, O, n_slow_sets, cap_s);
         AggArgs ab = a;
         ab.slow_kernel = n_slow_sets ? a.slow_kernel : 0;
+        ab.phash = P.phash ? c->d_phash + (hb.b.first - c->index_base) : nullptr;
         const size_t all = sets + n_slow_sets;
         Stage& S = ab.S;
         // layout (16-byte aligned pieces): parts | owner segments (hot, k_slow) | spill_raw | spill | base | off | soff
@@ -5162,6 +5186,10 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             J.cbits = c->d_cbits;
             J.mail = c->h_mail;
             J.n_rec_known = g.n_rec;  // (g: this run's counters after finalize)
+            if (P.phash) {
+                J.phash = c->d_phash;
+                J.phash_base = c->index_base;
+            }
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
             out.passes = er.iterations;
@@ -5245,6 +5273,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     }
     // the complex-flow filter is per run: clear the bits the speculative finalize set
     if (g.n_complex) HIPCHECK(hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s));
+    c->last_n_complex = g.n_complex;
+    c->last_mode_b = modeB ? 1 : 0;
     c->n_ended = n_ended;
     c->have_results = true;
     float ms_parse = 0;

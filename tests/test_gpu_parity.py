@@ -193,6 +193,37 @@ def test_spill_kernel_realistic_tcp(gpu, t, monkeypatch):
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp spill t={t}")
 
 
+@pytest.mark.parametrize("spill", ["0", "1"])
+@pytest.mark.parametrize("t", [600000, 1000])
+@pytest.mark.parametrize("mutate", [False, True])
+def test_phash_filter_realistic_tcp(gpu, spill, t, mutate, monkeypatch):
+    """The hot pass's per-packet filter words (FLUERE_PHASH=1 forced on the
+    first run): the exact engine's k_ex_meta skips the keyed packets whose
+    bucket holds no complex flow and parses the rest (PH_PARSE: drops, slow
+    packets -- the mutated capture has both inside TCP flows)."""
+    monkeypatch.setenv("FLUERE_PHASH", "1")
+    monkeypatch.setenv("FLUERE_SPILL_MODE", spill)
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 1_000_000, 10_000, 0xF10E0017))
+    if mutate:
+        data = _mutated_pcap(data, 11, 1)
+    want = pyoracle.offline(data, t)
+    csv, ne, st = _gpu_csv(data, t, max_flows=1 << 20)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp phash spill={spill} t={t} mutate={mutate}")
+
+
+def test_phash_chosen_on_rerun(gpu):
+    """A context whose last run replayed complex flows in Mode A writes the
+    filter words on the next runs (the prediction); every run equals the oracle."""
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 1_000_000, 10_000, 0xF10E0027))
+    want = pyoracle.offline(data)
+    with fluere_amd.FlowContext(max_flows=1 << 20) as ctx:
+        ctx.add_host_pcap(data)
+        for run in range(3):
+            st = ctx.run()
+            recs, ne = ctx.records()
+            assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"run {run}")
+
+
 def test_spill_kernel_chosen_on_rerun(gpu):
     """A context whose last run had ~50k flows per window takes k_parse_spill
     on the next run (the prediction from the last flow count); the runs agree."""
