@@ -87,62 +87,97 @@ struct AggOp {
 };
 
 // ---- 1. per-packet metadata of the packets to replay (one parse pass) -----
-// The taken packets of each 256-packet block go to the block's region of
-// meta_blk in capture order (block-local compaction, one ballot per wave), the
-// block's count to bcount[blk0 + block]; k_ex_compact concatenates the
-// regions after a scan over the block counts (a scan over every packet's flag
-// and a sparse write per taken packet before).
+// A block takes EXM_PKTS consecutive packets in two phases:
+//  1. candidates: every live packet, or (the hot pass's filter words) those
+//     whose bucket may hold a complex flow, listed in LDS in capture order
+//     (coalesced 4-byte reads; the skipped packets are not parsed);
+//  2. the candidates, 256 at a time (full waves however sparse they are):
+//     parse, dictionary walk, the taken ones to the block's region of meta_blk
+//     in capture order (one ballot per wave), the block's count to
+//     bcount[blk0 + block].
+// k_ex_compact concatenates the regions after a scan over the block counts.
+constexpr uint32_t EXM_PKTS = 1024;
+constexpr int EXM_R = EXM_PKTS / 256;
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
                                                  const uint8_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
                                                  uint64_t blk0, const uint32_t* phash) {
-    __shared__ uint32_t s_w[4];
-    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the hot pass's filter word: a keyed packet whose bucket holds no complex
-    // flow is skipped without its parse (PH_PARSE: parse it here)
-    bool skip = li >= B.n;
-    if (!skip && phash && !all && cbits) {
-        const uint32_t hb = phash[li];
-        skip = hb != PH_PARSE && cbits[hb & ((1u << CBITS_LOG2) - 1)] == 0;
+    __shared__ uint32_t s_c[EXM_PKTS];
+    __shared__ uint32_t s_w[2][4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * EXM_PKTS;
+    const bool filt = phash && !all && cbits;
+    // phase 1 (the filter words' loads, then their buckets' bytes, all in flight)
+    bool cand[EXM_R];
+    uint32_t hw[EXM_R];
+#pragma unroll
+    for (int r = 0; r < EXM_R; r++) {
+        const uint64_t li = base + r * 256 + tid;
+        cand[r] = li < B.n;
+        hw[r] = (filt && cand[r]) ? phash[li] : PH_PARSE;
     }
-    Parsed P;
-    if (!skip) parse_record(B, li, macs != 0, 0, P);
-    else P.cls = 1;
-    uint32_t take = 0;
-    ExMeta m;
-    memset(&m, 0, sizeof m);
-    if (P.cls == 0) {
-        uint8_t dir;
-        CKey k;
-        canon_key(P, macs != 0, k, dir);
-        bool maybe = true;
-        if (!all && cbits) {  // no complex flow has this key's bucket: no dictionary walk
-            const uint32_t b = ckey_bucket(k.w);
-            maybe = cbits[b] != 0;
-        }
-        const uint32_t d = maybe ? dense_of_key(T, k, false, nullptr, nullptr) : FAIL;
-        if (d != FAIL && d < T.fmax && (all || cplx[d])) {
-            take = 1;
-            m.t = P.t;
-            m.gidx = B.first + li;
-            m.d = d;
-            m.pkt = P.pi.rpkt;
-            m.doct = P.pi.doctets;
-            m.dir = dir;
-            m.tflags = P.pi.tflags;
-            m.ttl = P.pi.rttl;
-            m.bits = ((P.pi.rprot != 6 || (P.pi.tflags & 2)) ? 1 : 0) | ((P.pi.tflags & 5) ? 2 : 0);
-        }
+#pragma unroll
+    for (int r = 0; r < EXM_R; r++)
+        if (hw[r] != PH_PARSE) cand[r] = cbits[hw[r] & ((1u << CBITS_LOG2) - 1)] != 0;
+    uint32_t nc = 0;
+#pragma unroll
+    for (int r = 0; r < EXM_R; r++) {
+        const uint64_t bal = __ballot(cand[r]);
+        if (lane == 0) s_w[r & 1][w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = nc;
+        for (uint32_t k = 0; k < w; k++) before += s_w[r & 1][k];
+        if (cand[r])
+            s_c[before + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] =
+                (uint32_t)(r * 256 + tid);
+        nc += s_w[r & 1][0] + s_w[r & 1][1] + s_w[r & 1][2] + s_w[r & 1][3];
     }
-    const uint64_t bal = __ballot(take != 0);
-    const uint32_t w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) s_w[w] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t k = 0; k < w; k++) before += s_w[k];
-    if (take)
-        meta_blk[(blk0 + blockIdx.x) * 256 + before +
-                 __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = m;
-    if (threadIdx.x == 0) bcount[blk0 + blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();  // (every candidate listed)
+    // phase 2
+    uint32_t nt = 0;
+    ExMeta* region = meta_blk + (blk0 + blockIdx.x) * EXM_PKTS;
+    for (uint32_t j = 0, r = 0; j < nc; j += 256, r++) {
+        const uint32_t i = j + tid;
+        uint32_t take = 0;
+        ExMeta m;
+        memset(&m, 0, sizeof m);
+        if (i < nc) {
+            const uint64_t li = base + s_c[i];
+            Parsed P;
+            parse_record(B, li, macs != 0, 0, P);
+            if (P.cls == 0) {
+                uint8_t dir;
+                CKey k;
+                canon_key(P, macs != 0, k, dir);
+                bool maybe = true;
+                if (!all && cbits) {  // no complex flow has this key's bucket: no dictionary walk
+                    const uint32_t b = ckey_bucket(k.w);
+                    maybe = cbits[b] != 0;
+                }
+                const uint32_t d = maybe ? dense_of_key(T, k, false, nullptr, nullptr) : FAIL;
+                if (d != FAIL && d < T.fmax && (all || cplx[d])) {
+                    take = 1;
+                    m.t = P.t;
+                    m.gidx = B.first + li;
+                    m.d = d;
+                    m.pkt = P.pi.rpkt;
+                    m.doct = P.pi.doctets;
+                    m.dir = dir;
+                    m.tflags = P.pi.tflags;
+                    m.ttl = P.pi.rttl;
+                    m.bits = ((P.pi.rprot != 6 || (P.pi.tflags & 2)) ? 1 : 0) | ((P.pi.tflags & 5) ? 2 : 0);
+                }
+            }
+        }
+        const uint64_t bal = __ballot(take != 0);
+        if (lane == 0) s_w[r & 1][w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = nt;
+        for (uint32_t k = 0; k < w; k++) before += s_w[r & 1][k];
+        if (take)
+            region[before + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = m;
+        nt += s_w[r & 1][0] + s_w[r & 1][1] + s_w[r & 1][2] + s_w[r & 1][3];
+    }
+    if (tid == 0) bcount[blk0 + blockIdx.x] = nt;
 }
 
 // compaction in capture order: cm[k] = the k-th replayed packet; sort keys
@@ -150,12 +185,13 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
 __global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta_blk, const uint32_t* bcount, const uint32_t* bpos,
                                                     ExMeta* cm, uint32_t* key, uint32_t* val) {
     const uint32_t b = blockIdx.x, c = bcount[b];
-    if (threadIdx.x >= c) return;
-    const uint32_t k = bpos[b] + threadIdx.x;
-    const ExMeta m = meta_blk[(uint64_t)b * 256 + threadIdx.x];
-    cm[k] = m;
-    key[k] = m.d;  // (a stable sort by flow keeps capture order within a flow)
-    val[k] = k;
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+        const uint32_t k = bpos[b] + i;
+        const ExMeta m = meta_blk[(uint64_t)b * EXM_PKTS + i];
+        cm[k] = m;
+        key[k] = m.d;  // (a stable sort by flow keeps capture order within a flow)
+        val[k] = k;
+    }
 }
 
 // sharded Mode B owner: sort keys of the shards' packets (capture order)
@@ -895,7 +931,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     auto bytes_for = [&](uint64_t n_all, uint64_t n, size_t tmp) {
         size_t b = 0;
         auto add = [&](size_t x) { b += ((x + 255) & ~(size_t)255) + 256; };
-        add((n_all + 256 * (size_t)J.nb) * sizeof(ExMeta));          // meta_blk (k_ex_meta's block regions)
+        add((n_all + EXM_PKTS * (size_t)J.nb) * sizeof(ExMeta));     // meta_blk (k_ex_meta's block regions)
         add(4 * (n_all / 256 + J.nb + 1)); add(4 * (n_all / 256 + J.nb + 1));  // bcount, bpos
         add(n * sizeof(ExMeta)); add(n * 4); add(n * 4);              // cm, key, val
         add(n * 4); add(n * 4); add(n * sizeof(ExMeta));              // skey, sval, sm
@@ -944,8 +980,8 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     A.cap = need;
     uint64_t nblk = 0;  // k_ex_meta blocks over every batch
     if (!J.ext_cm)
-        for (int b = 0; b < J.nb; b++) nblk += J.h_batches[b].n ? gridn(J.h_batches[b].n, 256) : 0;
-    ExMeta* meta = A.take<ExMeta>(nblk * 256);
+        for (int b = 0; b < J.nb; b++) nblk += J.h_batches[b].n ? gridn(J.h_batches[b].n, EXM_PKTS) : 0;
+    ExMeta* meta = A.take<ExMeta>(nblk * EXM_PKTS);
     uint32_t* bcount = A.take<uint32_t>(nblk + 1);
     uint32_t* bpos = A.take<uint32_t>(nblk + 1);
     // ---- 1. metadata of every packet to replay, compacted in capture order
@@ -955,8 +991,8 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
             const uint32_t* ph = J.phash && !J.mode_b ? J.phash + (B.first - J.phash_base) : nullptr;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk, ph);
-            blk += gridn(B.n, 256);
+            k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk, ph);
+            blk += gridn(B.n, EXM_PKTS);
         }
     }
     size_t tb = tmp;
@@ -1235,7 +1271,7 @@ const ExactResult& exact_result(const ExactSession* S) { return S->R; }
 int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out) {
     *n_out = 0;
     uint64_t nblk = 0;
-    for (int b = 0; b < J.nb; b++) nblk += J.h_batches[b].n ? gridn(J.h_batches[b].n, 256) : 0;
+    for (int b = 0; b < J.nb; b++) nblk += J.h_batches[b].n ? gridn(J.h_batches[b].n, EXM_PKTS) : 0;
     if (!nblk) return FLUERE_OK;
     ExMeta* meta = nullptr;
     uint32_t *bcount = nullptr, *bpos = nullptr;
@@ -1245,7 +1281,7 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, bcount, bpos, (int)nblk, s);
     int rc = FLUERE_OK;
-    const uint64_t N = nblk * 256;
+    const uint64_t N = nblk * EXM_PKTS;
     if (hipMalloc(&meta, N * sizeof(ExMeta)) != hipSuccess || hipMalloc(&bcount, nblk * 4) != hipSuccess ||
         hipMalloc(&bpos, nblk * 4) != hipSuccess || hipMalloc(&key, N * 4) != hipSuccess ||
         hipMalloc(&val, N * 4) != hipSuccess || hipMalloc(&tp, std::max<size_t>(tb, 16)) != hipSuccess)
@@ -1255,8 +1291,8 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, 256), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk, nullptr);
-            blk += gridn(B.n, 256);
+            k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk, nullptr);
+            blk += gridn(B.n, EXM_PKTS);
         }
         unsigned long long last[2] = {0, 0};
         const void* src[2] = {bpos + nblk - 1, bcount + nblk - 1};

@@ -4557,12 +4557,17 @@ static size_t stage_bytes(size_t cells, size_t sets, uint32_t O, unsigned grid, 
 #endif
 static uint32_t merge_owners(const fluere_ctx* c) {
     // enough owners that each one's share of the flows (the last run's count
-    // as the estimate) fits its merge workgroup's 1024-entry LDS table at ~60 %
-    // load; at least one per CU
+    // as the estimate) fits its merge workgroup's 1024-entry LDS table at
+    // <= 85 % load; at least one per CU.  No more than that: k_parse_spill's
+    // per-owner LDS bins shrink as owners grow (BIN = 4096 / O records), and
+    // at 2048 owners the 2-record bins cost realistic TCP (847k flows) 85 us of
+    // hot kernel over 1024 owners (827 flows each); 1M flows at 1024 owners
+    // (977 each) overflow the merge tables and cost 0.5 ms (r03ah)
     static const uint32_t o_min = getenv("FLUERE_MIN_OWNERS") ? (uint32_t)atoi(getenv("FLUERE_MIN_OWNERS")) : 256u;
     uint32_t o = o_min;
-    while (o < (uint32_t)MAX_OWNERS && c->last_nf > 640ull * o) o *= 2;
-    const int cap = c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS;
+    while (o < (uint32_t)MAX_OWNERS && c->last_nf > 870ull * o) o *= 2;
+    static const int o_max = getenv("FLUERE_MAX_OWNERS") ? atoi(getenv("FLUERE_MAX_OWNERS")) : MAX_OWNERS;  // diagnostics
+    const int cap = std::min(o_max, c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS);
     return (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
 }
 
