@@ -171,8 +171,9 @@ int fluere_run(fluere_ctx* ctx, fluere_stats* stats);
  * then k_merge_partials, which also runs the general parser over the packets
  * the hot kernel left to it); leaves the flow table populated. Asynchronous. */
 int fluere_parse_aggregate(fluere_ctx* ctx);
-/* Device time (HIP events on the ctx stream) of the last k_parse_agg launch
- * (the roofline kernel) of the last fluere_run / fluere_parse_aggregate, ms. */
+/* Device time (HIP events on the ctx stream) of the last hot-kernel launch
+ * (k_parse_agg or k_parse_spill, the roofline kernel) of the last fluere_run /
+ * fluere_parse_aggregate, ms. */
 double fluere_last_kernel_ms(fluere_ctx* ctx);
 /* After fluere_run: its host wall time (submission to results), ms.  After
  * fluere_parse_aggregate: device time of the hot kernel + merge, ms. */
