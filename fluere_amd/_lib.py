@@ -159,6 +159,7 @@ def lib() -> ctypes.CDLL:
         "fluere_last_kernel_ms": (ctypes.c_double, [P]),
         "fluere_last_hot_kernel": (ctypes.c_char_p, [P]),
         "fluere_last_pass_ms": (ctypes.c_double, [P]),
+        "fluere_last_census": (I, [P, P, I]),
         "fluere_debug_dense_ids": (I, [P, P, U64, P]),
         "fluere_debug_raw": (I, [I, P, P, P, P, U64, P, P]),
         "fluere_live_open": (I, [ctypes.POINTER(Opts), ctypes.POINTER(P)]),

@@ -128,6 +128,9 @@ struct ExactResult {
 // within the pass limit): the caller runs the sequential kernel; else FLUERE_E_*.
 constexpr int EXACT_FALLBACK = 1;
 int exact_run(const ExactJob& job, hipStream_t s, ExactResult* res);
+// Grow the job's scratch arena (J.scratch) to what exact_begin lays out for
+// it, ahead of the run (host-side allocation while the GPU works).
+int exact_reserve(const ExactJob& job, hipStream_t s);
 
 // exact_run in phases, for the sharded Mode B owner, whose sweep points and
 // seeds come from the shards between the phases:

@@ -913,19 +913,9 @@ struct ExactSession {
 
 void exact_free(ExactSession* S) { delete S; }
 
-int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
-    *out = nullptr;
-    uint64_t N = 0;
-    if (J.ext_cm) N = J.ext_n;
-    else
-        for (int b = 0; b < J.nb; b++) N += J.h_batches[b].n;
-    ExactSession* S = new (std::nothrow) ExactSession();
-    if (!S) return FLUERE_E_NOMEM;
-    S->J = J;
-    S->s = s;
-    S->N = N;
-    *out = S;
-    if (!N) return FLUERE_OK;
+// The arena exact_begin lays out for a job: phase 1 over every packet, phase
+// 2 over at most every packet, and the hipCUB temp storage at that size.
+static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* tmp_out) {
     const uint64_t P = J.mode_b ? tree_leaves(N) : 1;
     // ---- arena sizing: phase 1 (all packets) + phase 2 (replayed packets, at most N)
     auto bytes_for = [&](uint64_t n_all, uint64_t n, size_t tmp) {
@@ -966,8 +956,47 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
                                           hipcub::Min(), n, s);
         tmp = std::max(tmp, t);
     }
+    if (tmp_out) *tmp_out = tmp;
+    return bytes_for(N, N, tmp);
+}
+
+static uint64_t job_packets(const ExactJob& J) {
+    uint64_t N = 0;
+    if (J.ext_cm) N = J.ext_n;
+    else
+        for (int b = 0; b < J.nb; b++) N += J.h_batches[b].n;
+    return N;
+}
+
+int exact_reserve(const ExactJob& J, hipStream_t s) {
+    const uint64_t N = job_packets(J);
+    if (!N) return FLUERE_OK;
+    const size_t need = arena_bytes(J, N, s, nullptr);
+    if (need <= *J.scratch_bytes) return FLUERE_OK;
+    if (*J.scratch) {  // (the old arena may still be in use: hipFree waits for the device)
+        hipFree(*J.scratch);
+        *J.scratch = nullptr;
+        *J.scratch_bytes = 0;
+    }
+    if (hipMalloc(J.scratch, need) != hipSuccess) return FLUERE_E_NOMEM;
+    *J.scratch_bytes = need;
+    return FLUERE_OK;
+}
+
+int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
+    *out = nullptr;
+    const uint64_t N = job_packets(J);
+    ExactSession* S = new (std::nothrow) ExactSession();
+    if (!S) return FLUERE_E_NOMEM;
+    S->J = J;
+    S->s = s;
+    S->N = N;
+    *out = S;
+    if (!N) return FLUERE_OK;
+    const uint64_t P = J.mode_b ? tree_leaves(N) : 1;
+    size_t tmp = 0;
+    const size_t need = arena_bytes(J, N, s, &tmp);
     S->tmp = tmp;
-    const size_t need = bytes_for(N, N, tmp);
     if (need > *J.scratch_bytes) {
         hipFree(*J.scratch);
         *J.scratch = nullptr;

@@ -98,7 +98,15 @@ static int live_main(int argc, char** argv) {
         if (start == ~0ull) start = bstart = t;
         // signed: a timestamp that goes backwards is no elapsed interval
         const int64_t since_start = (int64_t)(t - start), since_batch = (int64_t)(t - bstart);
-        if (interval && since_batch >= (int64_t)(interval * 1000) && batch.size() > 24) {
+        boff.push_back(batch.size());
+        batch.insert(batch.end(), data.begin() + off, data.begin() + off + 16 + incl);
+        off += 16 + incl;
+        // both checks follow the packet, the interval export first
+        // (live_fluereflow.rs:303-306, then :361-373): the crossing packet
+        // belongs to the interval it closes.  (The reference skips both checks
+        // after a packet that fails parse_keys / parse_fluereflow; the session
+        // runs a due export after the next processed packet, the same point.)
+        if (interval && since_batch >= (int64_t)(interval * 1000)) {
             fluere_record* recs = nullptr;
             uint64_t n = 0, no = 0;
             int ex = 0;
@@ -109,10 +117,6 @@ static int live_main(int argc, char** argv) {
             boff.clear();
             bstart = t;
         }
-        boff.push_back(batch.size());
-        batch.insert(batch.end(), data.begin() + off, data.begin() + off + 16 + incl);
-        off += 16 + incl;
-        // the duration check runs after the packet is processed (live_fluereflow.rs:361-373)
         if (duration && since_start >= (int64_t)(duration * 1000)) { stopped = true; break; }
     }
     if (!rc && batch.size() > 24) {

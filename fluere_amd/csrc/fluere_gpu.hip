@@ -1234,7 +1234,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                     const uint32_t j = lane / PPB, pc = lane % PPB;  // this lane: piece pc of the j-th bin of the group
                     uint64_t m = fm;
                     for (uint32_t k = 0; k < j && m; k++) m &= m - 1;
-                    const bool act = m != 0;
+                    const bool act = m != 0 && j < 64 / PPB;  // (64 % PPB != 0: the spare lanes idle)
                     const uint32_t src = act ? (uint32_t)__builtin_ctzll(m) : 0u;
                     const uint32_t bo = __shfl(done, src, 64), bp = __shfl(pos, src, 64);
                     if (act) {
@@ -3562,6 +3562,104 @@ __global__ void __launch_bounds__(256) k_chunk_desc(const uint32_t* offs, uint64
     if (lane == 0) desc[ch] = make_uint2(base, dense ? S : 0u);
 }
 
+// ---------------------------------------------------------------------------
+// k_census: the shape of a newly attached capture, from a sample, for the
+// choices its first run makes before any count exists (the hot kernel, the
+// merge owner count, k_slow, the exact engine's filter words).  Reruns of the
+// same batches use the last run's exact counts instead.
+//   sample: one packet per stratum of n / s_n consecutive packets, at a hashed
+//   position inside it (no aliasing with periodic flow assignments);
+//   per sampled packet the hot parser, and for a keyed packet a 64-bit
+//   fingerprint of its canonical key counted in an open-addressing table, so
+//   the sample's distinct keys D and the keys seen once (f1) and twice (f2)
+//   are maintained on the fly (count 0 -> 1: D, f1 up; 1 -> 2: f1 down, f2
+//   up; 2 -> 3: f2 down).  The host extrapolates the capture's flow count
+//   from them (census_flows).
+// ---------------------------------------------------------------------------
+struct CensusOut {
+    unsigned long long seen, valid, slow, tcp, d, f1, f2, tmin, tmax;
+};
+constexpr uint32_t CENSUS_TBITS = 21;  // fingerprint table: 2^21 slots, >= 2x the largest sample
+constexpr uint64_t CENSUS_MAX = 1ull << 20;
+struct CensusArgs {
+    Batch B;
+    uint64_t s_n;  // samples of this batch
+    unsigned long long* fp;
+    uint32_t* cnt;
+    CensusOut* out;
+    int macs;
+};
+__global__ void __launch_bounds__(256) k_census(CensusArgs a) {
+    __shared__ unsigned long long s_c[7], s_tmin, s_tmax;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 7) s_c[tid] = 0;
+    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; }
+    __syncthreads();
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + tid;
+    const Batch& B = a.B;
+    if (j < a.s_n) {
+        const uint64_t lo = j * B.n / a.s_n, hi = (j + 1) * B.n / a.s_n;
+        uint32_t r = (uint32_t)(j * 0x9E3779B97F4A7C15ull >> 32);
+        r ^= r >> 15; r *= 0x2C1B3C6Du; r ^= r >> 12;
+        const uint64_t li = lo + (hi > lo ? r % (uint32_t)(hi - lo) : 0u);
+        const uint32_t off = B.offs[li];
+        Win W;
+        const uint8_t* p = B.bytes + off;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint4 q;
+            __builtin_memcpy(&q, p + 16 * k, 16);
+            W.w[4 * k + 0] = q.x; W.w[4 * k + 1] = q.y; W.w[4 * k + 2] = q.z; W.w[4 * k + 3] = q.w;
+        }
+        W.w[16] = W.w[17] = W.w[18] = W.w[19] = 0u;
+        Hot h;
+        const uint32_t cls = hot_parse(B, off, W, h);
+        atomicAdd(&s_c[0], 1ull);
+        if (cls == HOT_SLOW) atomicAdd(&s_c[2], 1ull);
+        if (cls == HOT_OK) {
+            atomicAdd(&s_c[1], 1ull);
+            if (h.proto == 6u) atomicAdd(&s_c[3], 1ull);
+            atomicMin(&s_tmin, (unsigned long long)h.t);
+            atomicMax(&s_tmax, (unsigned long long)h.t);
+            const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
+            bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
+            uint64_t mx = 0;
+            if (a.macs) {  // the MAC pair joins the key (canonical order as in k_parse_agg<MACS>)
+                const uint64_t dm = ((uint64_t)__builtin_amdgcn_perm(W.w[5], W.w[4], 0x00010203u) << 16) |
+                                    __builtin_amdgcn_perm(W.w[5], W.w[4], 0x0C0C0405u);
+                const uint64_t sm = ((uint64_t)__builtin_amdgcn_perm(W.w[6], W.w[5], 0x02030405u) << 16) |
+                                    __builtin_amdgcn_perm(W.w[6], W.w[5], 0x0C0C0607u);
+                if ((h.sip == h.dip) & (sp == dp)) gt = sm > dm;
+                mx = (gt ? dm : sm) * 0xFF51AFD7ED558CCDull ^ (gt ? sm : dm);
+            }
+            const uint32_t k0 = gt ? h.dip : h.sip, k1 = gt ? h.sip : h.dip;
+            const uint32_t k2 = gt ? __builtin_amdgcn_alignbit(h.ports, h.ports, 16) : h.ports;
+            uint64_t f = ((uint64_t)k0 << 32 | k1) * 0x9E3779B97F4A7C15ull;
+            f ^= ((uint64_t)k2 << 8 | h.proto) * 0xC2B2AE3D27D4EB4Full;
+            f ^= mx * 0x165667B19E3779F9ull;
+            f ^= f >> 29; f *= 0xBF58476D1CE4E5B9ull; f ^= f >> 32;
+            f |= 1ull;  // (0 marks an empty slot)
+            const uint32_t mask = (1u << CENSUS_TBITS) - 1;
+            uint32_t e = (uint32_t)(f >> 40) & mask;
+            for (int probe = 0; probe < 256; probe++) {
+                const unsigned long long v = atomicCAS(&a.fp[e], 0ull, (unsigned long long)f);
+                if (v == 0ull || v == f) {
+                    const uint32_t old = atomicAdd(&a.cnt[e], 1u);
+                    if (old == 0) { atomicAdd(&s_c[4], 1ull); atomicAdd(&s_c[5], 1ull); }
+                    else if (old == 1) { atomicAdd(&s_c[5], ~0ull); atomicAdd(&s_c[6], 1ull); }
+                    else if (old == 2) atomicAdd(&s_c[6], ~0ull);
+                    break;
+                }
+                e = (e + 1) & mask;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 7 && s_c[tid]) atomicAdd(&a.out->seen + tid, s_c[tid]);
+    if (tid == 7 && s_tmin != NONE64) atomicMin(&a.out->tmin, s_tmin);
+    if (tid == 8 && s_tmax) atomicMax(&a.out->tmax, s_tmax);
+}
+
 // ===========================================================================
 // host side
 // ===========================================================================
@@ -3660,6 +3758,13 @@ struct fluere_ctx {
     int plan_nb = 0;                            // batches of the last pass
     int plan_spill = 0;                         // the last pass's hot kernel was k_parse_spill
     double last_run_ms = 0;                     // host wall time of the last fluere_run
+    // census of a newly attached capture (k_census): due when batches were
+    // attached since the last pass; its sample counts and flow estimate
+    bool census_due = false;
+    uint64_t runs = 0;                          // passes run on this context
+    void* d_census = nullptr;                   // fingerprint table, counts, CensusOut
+    unsigned long long census_v[10] = {};       // CensusOut + the flow estimate (fluere_last_census)
+    int census_ran = 0;
     // hipGraph of the last fluere_run pass, replayed while the plan is unchanged
     hipGraphExec_t graph = nullptr;
     void* graph_plan = nullptr;                 // PassPlan the graph was captured from
@@ -3671,6 +3776,16 @@ struct fluere_ctx {
     bool have_results = false;
     bool host_recs = false;          // recs holds the last results
     uint64_t dev_n_rec = 0;          // records of the last results in d_recs (Mode A / merge order: by order_key)
+    // the device ordered the ended prefix (order_records): [ended, in the
+    // reference's order][active]; the second buffers are the scatter targets
+    bool dev_ordered = false;
+    uint64_t dev_ordered_ended = 0;
+    fluere_record* d_recs2 = nullptr;
+    uint64_t d_recs2_cap = 0;
+    unsigned long long* d_recaux2 = nullptr;
+    uint64_t d_recaux2_cap = 0;
+    void* d_ord = nullptr;           // order_records scratch
+    size_t d_ord_bytes = 0;
 };
 
 static void reset_record_counters(fluere_ctx* c) {
@@ -3683,7 +3798,11 @@ static void reset_record_counters(fluere_ctx* c) {
 
 // Host copy of device-resident records, ended prefix first in emission order
 // (order_key: global index of the closing packet; with order words, sharded
-// Mode B: then aux[0], aux[1]), then active flows.
+// Mode B: then aux[0], aux[1]), then active flows.  After a one-GPU run the
+// device has ordered the ended prefix already (order_records): only the
+// active flows are sorted here, by first packet -- the reference emits them
+// after its loop (offline_fluereflows.rs:182-191) in HashMap order, so any
+// order is the reference's; this one is deterministic.
 static int fetch_records(fluere_ctx* c) {
     if (c->host_recs) return FLUERE_OK;
     hipStream_t s = c->stream;
@@ -3695,6 +3814,24 @@ static int fetch_records(fluere_ctx* c) {
     if (n && c->has_aux)
         HIPCHECK(hipMemcpyAsync(c->aux.data(), c->d_recaux, 2 * n * 8, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
+    if (c->dev_ordered) {
+        const uint64_t ne = std::min<uint64_t>(c->dev_ordered_ended, n);
+        auto& R = c->recs;
+        std::vector<uint64_t> ix(n - ne);
+        for (uint64_t i = 0; i < n - ne; i++) ix[i] = ne + i;
+        std::stable_sort(ix.begin(), ix.end(), [&](uint64_t a, uint64_t b) { return R[a].first < R[b].first; });
+        std::vector<fluere_record> act(n - ne);
+        for (uint64_t i = 0; i < n - ne; i++) act[i] = R[ix[i]];
+        std::copy(act.begin(), act.end(), R.begin() + ne);
+        if (c->has_aux) {
+            std::vector<unsigned long long> xa(2 * (n - ne));
+            for (uint64_t i = 0; i < n - ne; i++) { xa[2 * i] = c->aux[2 * ix[i]]; xa[2 * i + 1] = c->aux[2 * ix[i] + 1]; }
+            std::copy(xa.begin(), xa.end(), c->aux.begin() + 2 * ne);
+        }
+        c->n_ended = ne;
+        c->host_recs = true;
+        return FLUERE_OK;
+    }
     std::vector<uint64_t> ix(n);
     for (uint64_t i = 0; i < n; i++) ix[i] = i;
     const auto& R = c->recs;
@@ -3813,6 +3950,9 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
         if (hipMemcpyAsync(c->d_glob, &z, sizeof z, hipMemcpyHostToDevice, s) != hipSuccess) return fail(FLUERE_E_HIP);
     }
     if (hipStreamSynchronize(s) != hipSuccess) return fail(FLUERE_E_HIP);
+    // the state above is what k_cleanup leaves: the first pass needs none
+    c->precleaned = true;
+    c->prev_nf = 0;
     (void)rc;
     *out = c;
     return FLUERE_OK;
@@ -3827,6 +3967,7 @@ static void free_batches(fluere_ctx* c) {
     c->batches.clear();
     c->n_total = 0;
     c->batches_dirty = true;
+    c->census_due = true;
 }
 
 extern "C" int fluere_close(fluere_ctx* c) {
@@ -3862,6 +4003,10 @@ extern "C" int fluere_close(fluere_ctx* c) {
         if (c->ar_ev[i]) hipEventDestroy(c->ar_ev[i]);
     }
     hipFree(c->d_need);
+    hipFree(c->d_census);
+    hipFree(c->d_recs2);
+    hipFree(c->d_recaux2);
+    hipFree(c->d_ord);
     hipFree(c->d_recaux);
     sweep_free(c);
     hipFree(c->d_sd);
@@ -3988,6 +4133,7 @@ extern "C" int fluere_add_device_batch(fluere_ctx* c, const uint8_t* d_bytes, ui
     hb.b.flags = (swapped ? 1u : 0u) | (nsec_ts ? 2u : 0u);
     c->batches.push_back(hb);
     c->batches_dirty = true;
+    c->census_due = true;
     c->n_total += n;
     c->have_results = false;
     return FLUERE_OK;
@@ -4352,6 +4498,7 @@ struct Ingest {
             hb.b.flags = (sw ? 1u : 0u) | (ns ? 2u : 0u);
             c->batches.push_back(hb);
             c->batches_dirty = true;
+            c->census_due = true;
             c->n_total += hb.b.n;
         }
         if (c->reuse_ingest) {
@@ -4470,6 +4617,79 @@ static int upload_batches(fluere_ctx* c) {
     return FLUERE_OK;
 }
 
+// The capture's flow count from the census sample: D distinct keys among s of
+// its N packets, f1 / f2 of them seen once / twice.  Chao's estimator for a
+// sample drawn without replacement (q = s / N): F = D + f1^2 / (2 f2 s / (s - 1)
+// + f1 q / (1 - q)); the whole capture (q = 1) gives D itself.
+static uint64_t census_flows(uint64_t s, uint64_t N, double D, double f1, double f2) {
+    if (s >= N || s < 2) return (uint64_t)D;
+    const double q = (double)s / (double)N;
+    const double den = 2.0 * f2 * (double)s / (double)(s - 1) + f1 * q / (1.0 - q);
+    const double F = D + (den > 0 ? f1 * f1 / den : 0.0);
+    return (uint64_t)std::min<double>(F + 0.5, (double)N);
+}
+
+// Census of newly attached batches (k_census; one host round trip, first pass
+// after an attach only): sets the predictions a pass plans with -- the flow
+// count (hot kernel, owners, grids), slow packets (k_slow), TCP in Mode A (the
+// exact engine's filter words).  Live sessions keep the last batch's counts.
+// FLUERE_CENSUS=0 disables it (A/B), =1 runs it before every pass (tests).
+static int census(fluere_ctx* c) {
+    static const int env = getenv("FLUERE_CENSUS") ? atoi(getenv("FLUERE_CENSUS")) : -1;
+    if (env == 1) c->census_due = true;
+    if (!c->census_due || env == 0) return FLUERE_OK;
+    c->census_due = false;
+    if (c->reuse_ingest && c->runs > 0 && env != 1) return FLUERE_OK;
+    const uint64_t N = c->n_total;
+    if (!N) return FLUERE_OK;
+    const uint64_t S = std::min<uint64_t>(N, CENSUS_MAX);
+    hipStream_t s = c->stream;
+    const size_t T = (size_t)1 << CENSUS_TBITS;
+    if (!c->d_census && hipMalloc(&c->d_census, T * 12 + sizeof(CensusOut) + 64) != hipSuccess) return FLUERE_E_NOMEM;
+    CensusArgs a{};
+    a.fp = (unsigned long long*)c->d_census;
+    a.cnt = (uint32_t*)(a.fp + T);
+    a.out = (CensusOut*)(a.cnt + T);
+    a.macs = c->use_mac;
+    HIPCHECK(hipMemsetAsync(c->d_census, 0, T * 12 + sizeof(CensusOut), s));
+    HIPCHECK(hipMemsetAsync(&a.out->tmin, 0xFF, 8, s));
+    uint64_t done = 0, seen_n = 0;
+    for (size_t i = 0; i < c->batches.size(); i++) {
+        const Batch& B = c->batches[i].b;
+        if (!B.n) continue;
+        seen_n += B.n;
+        const uint64_t upto = seen_n == N ? S : (uint64_t)((double)S * seen_n / N);
+        a.B = B;
+        a.s_n = std::min<uint64_t>(B.n, upto > done ? upto - done : 0);
+        done += a.s_n;
+        if (a.s_n) k_census<<<grid_for(a.s_n, 256), 256, 0, s>>>(a);
+    }
+    HIPCHECK(hipGetLastError());
+    const void* src[9];
+    int by[9];
+    for (int k = 0; k < 9; k++) { src[k] = &a.out->seen + k; by[k] = 8; }
+    unsigned long long v[9] = {};
+    int rc = mail_fetch(c->h_mail, s, 9, src, by, v);
+    if (rc) return rc;
+    const uint64_t s_seen = v[0];
+    const uint64_t F = census_flows(s_seen, N, (double)v[4], (double)v[5], (double)v[6]);
+    for (int k = 0; k < 9; k++) c->census_v[k] = v[k];
+    c->census_v[9] = F;
+    c->census_ran++;
+    // the predictions (the same fields a finished run sets)
+    c->last_nf = std::min<uint64_t>(F, c->fmax);
+    c->last_n_slow = v[2] ? std::max<uint64_t>(1, v[2] * N / std::max<uint64_t>(1, s_seen)) : 0;
+    c->last_mode_b = (v[1] && v[8] >= v[7] && v[8] - v[7] >= c->timeout_ms * 1000ull) ? 1 : 0;
+    c->last_n_complex = v[3] ? 1 : 0;  // TCP keys: flows the certificate may reject (filter words, 4 B/packet)
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_last_census(fluere_ctx* c, uint64_t* out, int n) {
+    if (!c || !out || n < 0) return FLUERE_E_ARG;
+    for (int k = 0; k < n && k < 10; k++) out[k] = c->census_v[k];
+    return c->census_ran;
+}
+
 extern "C" int fluere_parse_batch(fluere_ctx* c, fluere_pkt_meta* d_out, uint64_t cap) {
     if (!c || !d_out || cap < c->n_total) return FLUERE_E_ARG;
     HIPCHECK(hipSetDevice(c->device));
@@ -4568,7 +4788,11 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     while (o < (uint32_t)MAX_OWNERS && c->last_nf > 870ull * o) o *= 2;
     static const int o_max = getenv("FLUERE_MAX_OWNERS") ? atoi(getenv("FLUERE_MAX_OWNERS")) : MAX_OWNERS;  // diagnostics
     const int cap = std::min(o_max, c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS);
-    return (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
+    // a power of two: k_parse_spill writes a wave's completed bins in groups of
+    // 64 / (2 * BIN) lanes with BIN = 4096 / O (a CU count such as 304 rounds up)
+    uint32_t r = (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
+    while (r & (r - 1)) r += r & (~r + 1);
+    return std::min<uint32_t>(r, (uint32_t)MAX_OWNERS);
 }
 
 static int plan_batches(fluere_ctx* c, PassPlan& P) {
@@ -4723,6 +4947,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
 static int spill_mode(const fluere_ctx* c) {
     const int env = getenv("FLUERE_SPILL_MODE") ? atoi(getenv("FLUERE_SPILL_MODE")) : -1;  // tests: force either kernel
     if (c->use_mac) return 0;
+    if (merge_owners(c) < 128) return 0;  // bins of more than 32 records: more than a wave per bin
     if (env >= 0) return env;
     const double F = (double)c->last_nf;
     if (F <= 0) return 0;
@@ -4736,6 +4961,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     memset(&P, 0, sizeof P);  // byte-comparable (padding included)
     int rc;
     if ((rc = upload_batches(c))) return rc;  // host -> device, only when the batches changed
+    if ((rc = census(c))) return rc;          // a new capture: its shape from a sample
     P.ca = CleanArgs{tables_of(c), c->acc, c->d_complex, c->d_active, c->d_glob};
     static const int clean_abl = getenv("FLUERE_CLEAN_ABL") ? atoi(getenv("FLUERE_CLEAN_ABL")) : 0;
     P.ca.abl = clean_abl;
@@ -4755,7 +4981,10 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     P.d_glob = c->d_glob;
     if (finalize) {
         // speculative Mode A finalize over the device-side flow count
-        if ((rc = ensure_recs(c, std::max<uint64_t>(c->d_recs_cap, std::min<uint64_t>(c->fmax, 1u << 16))))) return rc;
+        // (sized for the expected flows: a speculative finalize past the
+        // buffer runs again after growing it)
+        const uint64_t want = std::max<uint64_t>(1u << 16, c->last_nf + c->last_nf / 4);
+        if ((rc = ensure_recs(c, std::max<uint64_t>(c->d_recs_cap, std::min<uint64_t>(c->fmax, want))))) return rc;
         P.fa = FinArgs{c->d_batches, (int)c->batches.size(), tables_of(c), c->acc, c->d_glob,
                        c->d_recs,    c->d_complex,           c->use_mac,   c->d_recs_cap};
         P.fa.timeout_us = c->timeout_ms * 1000ull;
@@ -5013,6 +5242,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     PassPlan P;
     memset(&P, 0, sizeof P);
     if ((rc = upload_batches(c))) return rc;
+    if ((rc = census(c))) return rc;
     if ((rc = plan_batches(c, P))) return rc;
     if (P.nb > PLAN_BATCHES) return FLUERE_E_ARG;
     static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
@@ -5022,6 +5252,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     c->plan_nb = P.nb;
     c->plan_spill = P.spill;
     c->precleaned = false;
+    c->runs++;
     rc = enqueue_batches(c, P);
     debug_counters(c);
     return rc;
@@ -5052,6 +5283,187 @@ extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
     return ms;
 }
 
+// ---------------------------------------------------------------------------
+// Ended-record order on the device, inside the run.  The reference appends a
+// record when its flow ends, in packet order (offline_fluereflows.rs:155,171,
+// inside the "Converted in" window :49-178), and its active flows after the
+// loop (:182-191) in HashMap order.  The run's records leave as [ended, in
+// the reference's order][active, any order]:
+//  * Mode A: an ended record's order_key (its closing packet's index) is
+//    unique -- a packet closes at most one instance of its key -- so its
+//    place is the count of ended keys below it: one bit per packet, a
+//    popcount scan, one scatter;
+//  * Mode B: a sweep ends several flows at one packet, in the BTreeMap's pop
+//    order (exp, then push order) after a FIN/RST close (order words aux):
+//    stable radix sorts by the packed order words, then by order_key, and a
+//    gather of the records and their words.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_ord_mark(const fluere_record* r, uint64_t n, uint64_t base, uint32_t* bits) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t k = r[i].order_key;
+        if (k != NONE64) atomicOr(&bits[(k - base) >> 5], 1u << ((k - base) & 31));
+    }
+}
+__global__ void __launch_bounds__(256) k_ord_popc(const uint32_t* bits, uint64_t nw, uint32_t* pc) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w < nw) pc[w] = __popc(bits[w]);
+}
+__device__ __forceinline__ void copy_record(fluere_record* dst, const fluere_record* src) {
+    const uint2* a = reinterpret_cast<const uint2*>(src);
+    uint2* b = reinterpret_cast<uint2*>(dst);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(fluere_record) / 8); k++) b[k] = a[k];
+}
+__global__ void __launch_bounds__(256) k_ord_place(const fluere_record* r, uint64_t n, uint64_t base, const uint32_t* bits,
+                                                   const uint32_t* pre, uint64_t n_ended, fluere_record* out,
+                                                   unsigned long long* act) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = i < n;
+    const uint64_t k = live ? r[i].order_key : NONE64;
+    const bool ended = k != NONE64;
+    uint64_t pos = 0;
+    if (ended) {
+        const uint64_t q = k - base;
+        pos = pre[q >> 5] + __popc(bits[q >> 5] & ((1u << (q & 31)) - 1u));
+    }
+    // the active records after the ended prefix (wave-aggregated append)
+    const uint64_t m = __ballot(live && !ended);
+    if (m) {
+        const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+        unsigned long long b0 = 0;
+        if (lane == lead) b0 = atomicAdd(act, (unsigned long long)__popcll(m));
+        b0 = __shfl(b0, lead, 64);
+        if (live && !ended)
+            pos = n_ended + b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    if (live) copy_record(out + pos, r + i);
+}
+// Mode B: key1 = (exp + 1 - t0) << b1 | creation index (FIN/RST closes: 0),
+// then key2 = order_key - base (active records: all ones, last)
+__global__ void __launch_bounds__(256) k_ordb_key1(const fluere_record* r, const unsigned long long* aux, uint64_t n,
+                                                   unsigned long long t0, uint64_t base, int b1,
+                                                   unsigned long long* key, uint32_t* idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long k = 0;
+    if (r[i].order_key != NONE64) {
+        const unsigned long long a0 = aux[2 * i], a1 = aux[2 * i + 1];
+        k = a0 ? (((a0 - t0) << b1) | (a1 - base)) : 0ull;
+    }
+    key[i] = k;
+    idx[i] = (uint32_t)i;
+}
+__global__ void __launch_bounds__(256) k_ordb_key2(const fluere_record* r, const uint32_t* idx, uint64_t n, uint64_t base,
+                                                   unsigned long long none, unsigned long long* key) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t k = r[idx[j]].order_key;
+    key[j] = k == NONE64 ? none : k - base;
+}
+__global__ void __launch_bounds__(256) k_ordb_gather(const fluere_record* r, const unsigned long long* aux,
+                                                     const uint32_t* idx, uint64_t n, fluere_record* out,
+                                                     unsigned long long* aux_out) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = idx[j];
+    copy_record(out + j, r + i);
+    aux_out[2 * j] = aux[2 * i];
+    aux_out[2 * j + 1] = aux[2 * i + 1];
+}
+
+static int bits_of(uint64_t v) {  // bits to hold the values 0..v
+    int b = 1;
+    while (b < 64 && (v >> b)) b++;
+    return b;
+}
+
+static int ord_scratch(fluere_ctx* c, size_t need) {
+    if (need <= c->d_ord_bytes) return FLUERE_OK;
+    hipFree(c->d_ord);
+    c->d_ord = nullptr;
+    c->d_ord_bytes = 0;
+    if (hipMalloc(&c->d_ord, need) != hipSuccess) return FLUERE_E_NOMEM;
+    c->d_ord_bytes = need;
+    return FLUERE_OK;
+}
+
+// Orders the run's n records in d_recs (n_ended of them ended) as
+// [ended][active]; Mode B with the order words in d_recaux.  Stream-ordered,
+// no host wait.  tmin / tmax: the capture's valid times (Mode B key width).
+static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint64_t tmin, uint64_t tmax) {
+    c->dev_ordered = false;
+    if (!n || !n_ended) return FLUERE_OK;
+    hipStream_t s = c->stream;
+    const uint64_t base = c->index_base, N = std::max<uint64_t>(c->n_total, 1);
+    if (c->d_recs2_cap < c->d_recs_cap) {
+        hipFree(c->d_recs2);
+        c->d_recs2 = nullptr;
+        c->d_recs2_cap = 0;
+        if (hipMalloc(&c->d_recs2, c->d_recs_cap * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
+        c->d_recs2_cap = c->d_recs_cap;
+    }
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    if (!mode_b) {
+        const uint64_t nw = N / 32 + 1;
+        size_t tb = 0;
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nw, s);
+        int rc = ord_scratch(c, 3 * al(nw * 4) + al(8) + al(tb));
+        if (rc) return rc;
+        char* p = (char*)c->d_ord;
+        uint32_t* bits = (uint32_t*)p;
+        uint32_t* pc = (uint32_t*)(p + al(nw * 4));
+        uint32_t* pre = (uint32_t*)(p + 2 * al(nw * 4));
+        unsigned long long* act = (unsigned long long*)(p + 3 * al(nw * 4));
+        void* tmp = p + 3 * al(nw * 4) + al(8);
+        HIPCHECK(hipMemsetAsync(bits, 0, nw * 4, s));
+        HIPCHECK(hipMemsetAsync(act, 0, 8, s));
+        k_ord_mark<<<(unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->n_cu * 8), 256, 0, s>>>(c->d_recs, n, base, bits);
+        k_ord_popc<<<grid_for(nw, 256), 256, 0, s>>>(bits, nw, pc);
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, pc, pre, (int)nw, s));
+        k_ord_place<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, n, base, bits, pre, n_ended, c->d_recs2, act);
+    } else {
+        if (!c->d_recaux) return FLUERE_OK;
+        const unsigned long long t0 = tmin + c->timeout_ms * 1000ull;  // exp + 1 > t0 for every sweep close
+        const int b1 = bits_of(N), b0 = bits_of(tmax >= tmin ? tmax - tmin + 2 : 2);
+        const int bk = bits_of(N);  // order_key - base < N; actives: all ones
+        if (b0 + b1 > 64) return FLUERE_OK;  // (a span past 2^40 us at 2^24 packets: the host orders them)
+        if (c->d_recaux2_cap < c->d_recaux_cap) {
+            hipFree(c->d_recaux2);
+            c->d_recaux2 = nullptr;
+            c->d_recaux2_cap = 0;
+            if (hipMalloc(&c->d_recaux2, c->d_recaux_cap * 16) != hipSuccess) return FLUERE_E_NOMEM;
+            c->d_recaux2_cap = c->d_recaux_cap;
+        }
+        size_t tb = 0;
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                                 (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64, s);
+        int rc = ord_scratch(c, 2 * al(n * 8) + 3 * al(n * 4) + al(tb));
+        if (rc) return rc;
+        char* p = (char*)c->d_ord;
+        unsigned long long* ka = (unsigned long long*)p;
+        unsigned long long* kb = (unsigned long long*)(p + al(n * 8));
+        uint32_t* ia = (uint32_t*)(p + 2 * al(n * 8));
+        uint32_t* ib = (uint32_t*)(p + 2 * al(n * 8) + al(n * 4));
+        uint32_t* ic = (uint32_t*)(p + 2 * al(n * 8) + 2 * al(n * 4));
+        void* tmp = p + 2 * al(n * 8) + 3 * al(n * 4);
+        k_ordb_key1<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, c->d_recaux, n, t0, base, b1, ka, ia);
+        size_t t = tb;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp, t, ka, kb, ia, ib, (int)n, 0, b0 + b1, s));
+        k_ordb_key2<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, ib, n, base, (1ull << bk) - 1, ka);
+        t = tb;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp, t, ka, kb, ib, ic, (int)n, 0, bk, s));
+        k_ordb_gather<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, c->d_recaux, ic, n, c->d_recs2, c->d_recaux2);
+        std::swap(c->d_recaux, c->d_recaux2);
+        std::swap(c->d_recaux_cap, c->d_recaux2_cap);
+    }
+    HIPCHECK(hipGetLastError());
+    std::swap(c->d_recs, c->d_recs2);
+    std::swap(c->d_recs_cap, c->d_recs2_cap);
+    c->dev_ordered = true;
+    c->dev_ordered_ended = n_ended;
+    return FLUERE_OK;
+}
+
 static int ensure_recs(fluere_ctx* c, uint64_t need) {
     if (need <= c->d_recs_cap) return FLUERE_OK;
     hipFree(c->d_recs);
@@ -5072,6 +5484,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     // costs a gap on the stream); the run's total is host wall time
     c->pass_in_run = true;
     c->has_aux = false;
+    c->dev_ordered = false;
     c->aux.clear();
     const auto t_run0 = std::chrono::steady_clock::now();
     const TableSet T = tables_of(c);
@@ -5133,6 +5546,16 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         if ((rc = enqueue_pass(c, P))) return rc;
     }
     c->prev_nf = ~0ull;  // the pass cleared the flows: unknown until the fetch below
+    // the exact engine's arena for the capture, allocated on the host while
+    // the GPU runs the pass, when its flows are expected to need it (TCP in
+    // Mode A, or Mode B: the census or the last run)
+    if ((c->last_n_complex || c->last_mode_b) && P.spec) {
+        std::vector<Batch> hb(nb);
+        for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
+        ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, c->last_mode_b, timeout_us, c->d_complex, c->d_glob,
+                   &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+        if ((rc = exact_reserve(J, s))) return rc;
+    }
     Glob g;
     uint32_t nf_err[2];
     const auto t_enq = std::chrono::steady_clock::now();
@@ -5201,13 +5624,14 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             HIPCHECK(hipEventRecord(c->ev2, s));
             if ((rc = read_glob(c, g))) return rc;
         }
-        // records stay on the device; fluere_get_records copies and orders them
+        // records stay on the device, the ended prefix ordered there
         n_rec = g.n_rec;
         n_ended = g.n_ended;
         updates = g.n_updates;
         c->dev_n_rec = n_rec;
         c->host_recs = false;
         out.complex_flows = g.n_complex;
+        if ((rc = order_records(c, n_rec, n_ended, false, g.tmin, g.tmax))) return rc;
     } else {
         // exact global state machine (the speculative Mode A results are discarded):
         // in parallel (exact.hip) when the timestamps are non-decreasing, else
@@ -5234,6 +5658,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             c->dev_n_rec = n_rec;
             c->host_recs = false;
             out.sequential_mode = 1;
+            if (c->has_aux && (rc = order_records(c, n_rec, n_ended, true, g.tmin, g.tmax))) return rc;
         } else {
         uint64_t N = c->n_total;
         SeqMeta* meta = nullptr;
@@ -5273,6 +5698,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         for (auto& r : c->recs) updates += r.d_pkts;
         c->host_recs = true;
         c->dev_n_rec = n_rec;
+        c->dev_ordered = false;
         out.sequential_mode = 2;
         }
     }
@@ -5280,6 +5706,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     if (g.n_complex) HIPCHECK(hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s));
     c->last_n_complex = g.n_complex;
     c->last_mode_b = modeB ? 1 : 0;
+    c->runs++;
     c->n_ended = n_ended;
     c->have_results = true;
     float ms_parse = 0;
@@ -5544,13 +5971,6 @@ extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_
     const size_t need = 2 * (n + 1) * 8 + (size_t)(n_owners + 1) * 8 + ((tb + 255) & ~(size_t)255);
     if (need > c->d_wire_tmp_bytes) {
         hipFree(c->d_wire_tmp);
-    hipFree(c->d_v6map);
-    hipFree(c->ar_d);
-    hipFree(c->ar_offs);
-    for (int i = 0; i < 8; i++) {
-        if (c->ar_pin[i]) hipHostFree(c->ar_pin[i]);
-        if (c->ar_ev[i]) hipEventDestroy(c->ar_ev[i]);
-    }
         c->d_wire_tmp = nullptr;
         c->d_wire_tmp_bytes = 0;
         if (hipMalloc(&c->d_wire_tmp, need) != hipSuccess) return FLUERE_E_NOMEM;
@@ -5691,6 +6111,7 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
     const uint32_t nf = std::min(nf_err[0], c->fmax);
     c->dev_n_rec = g.n_rec;
     c->host_recs = false;
+    c->dev_ordered = false;
     c->have_results = true;
     c->local_n_rec = c->local_updates = c->local_ended = 0;
     fluere_stats out{};
@@ -6204,6 +6625,7 @@ extern "C" int fluere_sweep_finish(fluere_ctx* c, const void* d_seeds, fluere_st
     HIPCHECK(hipStreamSynchronize(s));
     c->dev_n_rec = g.n_rec;
     c->host_recs = false;
+    c->dev_ordered = false;
     c->has_aux = true;
     c->have_results = true;
     if (st) {

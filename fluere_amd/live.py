@@ -124,21 +124,23 @@ def _batch_offsets(cur):
 
 
 def replay_batches(data: bytes, interval_ms: int, batch_packets: int = 0) -> Iterator[Tuple[bytes, bool, np.ndarray]]:
-    """A capture file as the batches a ring would deliver: a batch ends where
-    the packets' own clock crosses the next interval boundary (its export flag
-    set), or every batch_packets packets without an export in between.
+    """A capture file as the batches a ring would deliver: a batch ends with
+    the packet whose own clock crosses the next interval boundary (its export
+    flag set), or every batch_packets packets without an export in between.
     Yields (classic pcap image, export, record header offsets)."""
     hdr = data[:24]
     cur, start, n = [], None, 0
     for off, ln, t in pcap_records(data):
         if start is None:
             start = t
-        if interval_ms and t - start >= interval_ms * 1000 and cur:
-            yield hdr + b"".join(cur), True, _batch_offsets(cur)
-            cur, start, n = [], t, 0
         cur.append(data[off:off + ln])
         n += 1
-        if batch_packets and n >= batch_packets:
+        # the interval check follows the packet (live_fluereflow.rs:303-306):
+        # the crossing packet belongs to the interval it closes
+        if interval_ms and t - start >= interval_ms * 1000:
+            yield hdr + b"".join(cur), True, _batch_offsets(cur)
+            cur, start, n = [], t, 0
+        elif batch_packets and n >= batch_packets:
             yield hdr + b"".join(cur), False, _batch_offsets(cur)
             cur, n = [], 0
     if cur:

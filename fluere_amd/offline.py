@@ -99,6 +99,13 @@ class FlowContext:
         """Name of the last pass's hot kernel (k_parse_agg or k_parse_spill)."""
         return self._L.fluere_last_hot_kernel(self._h).decode()
 
+    def last_census(self) -> dict:
+        """The census of the capture attached last (fluere_last_census)."""
+        v = np.zeros(10, dtype=np.uint64)
+        runs = self._L.fluere_last_census(self._h, v.ctypes.data, 10)
+        keys = ("sampled", "keyed", "slow", "tcp", "distinct", "once", "twice", "tmin", "tmax", "flows_est")
+        return {"runs": int(runs), **{k: int(x) for k, x in zip(keys, v)}}
+
     def last_pass_ms(self) -> float:
         """HIP-event time of the whole last parse+key+aggregate pass."""
         return float(self._L.fluere_last_pass_ms(self._h))

@@ -180,8 +180,15 @@ double fluere_last_kernel_ms(fluere_ctx* ctx);
 double fluere_last_pass_ms(fluere_ctx* ctx);
 /* The hot kernel of the last pass: "k_parse_agg" (LDS flow table) or
  * "k_parse_spill" (many flows per window: per-owner LDS bins), chosen from
- * the previous run's flow count.  Static string. */
+ * the flow count: the census of a newly attached capture (its first pass), or
+ * the previous run's exact count (reruns).  Static string. */
 const char* fluere_last_hot_kernel(fluere_ctx* ctx);
+/* The census of the capture attached last (k_census, one sampled pass run
+ * before the first pass after an attach): out[0..9] = packets sampled, hot-
+ * parser keyed, slow class, TCP, distinct keys in the sample, keys seen once,
+ * twice, min / max time (us), estimated flows of the capture.  Returns how
+ * many censuses the context has run (0: none yet). */
+int fluere_last_census(fluere_ctx* ctx, uint64_t* out, int n);
 
 /* Records of the last fluere_run, host memory, ended prefix first (in the
  * reference's emission order), then active flows.  Caller frees with

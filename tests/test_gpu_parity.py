@@ -238,6 +238,47 @@ def test_spill_kernel_chosen_on_rerun(gpu):
             assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"run {run}")
 
 
+CENSUS = {
+    # name: (kind, packets, flows, seed, use_mac, timeout_ms, hot kernel of the first run)
+    "c3_full": (_lib.SYNTH_IMIX, 10_000_000, 100_000, 0xF10E0003, False, 600000, "k_parse_spill"),
+    "c2_small": (_lib.SYNTH_UDP64, 300_000, 1000, 0xF10E0002, False, 600000, "k_parse_agg"),
+    "tcp_2m": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007, False, 600000, "k_parse_spill"),
+    "tcp_2m_t1": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007, False, 1000, "k_parse_spill"),
+    "slow_2m": (_lib.SYNTH_SLOW, 2_000_000, 10_000, 0xF10E0008, False, 600000, None),
+    "c5u_mac": (_lib.SYNTH_MAC64, 1_000_000, 50_000, 0xF10E0005, True, 600000, "k_parse_agg"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CENSUS))
+def test_census_predicts_first_run(gpu, name):
+    """The one-shot seam (`fluere offline`: a fresh context, one run) takes the
+    path a rerun would: the census of the attached capture (k_census, a
+    sampled pass) estimates its flow count, so the first run already picks the
+    hot kernel, the merge owners, k_slow and the filter words.  The estimate
+    is within 25 % of the dictionary's keys, and the records equal the oracle."""
+    kind, n, f, seed, use_mac, t, hot = CENSUS[name]
+    cfg = fluere_amd.synth_cfg(kind, n, f, seed)
+    max_flows = max(1 << 16, 2 * f) if kind != _lib.SYNTH_TCP else n // 2
+    with fluere_amd.FlowContext(timeout_ms=t, use_mac=use_mac, max_flows=max_flows) as ctx:
+        for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, 0, n):
+            ctx.add_device_batch(b, nbytes, o, nb)
+        torch.cuda.synchronize()
+        st = ctx.run()
+        cen = ctx.last_census()
+        kernel = ctx.last_hot_kernel()
+        recs, ne = ctx.records()
+    assert cen["runs"] == 1 and cen["sampled"] == min(n, 1 << 20), cen
+    keyed = st["flows"]
+    if kind != _lib.SYNTH_SLOW:  # (the census keys the hot parser's classes only)
+        assert abs(cen["flows_est"] - keyed) <= 0.25 * keyed, (cen, keyed)
+    else:
+        assert cen["slow"] > 0
+    if hot:
+        assert kernel == hot, (kernel, cen)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg), t, use_mac=use_mac)
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"census {name}")
+
+
 @pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small"])
 def test_second_run_takes_slow_kernel(gpu, name):
     """The first run of a context leaves the slow list to the merge kernel's
