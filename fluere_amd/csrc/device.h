@@ -334,11 +334,11 @@ __device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& 
     uint32_t s;
     int ft;
     unsigned long long v = EMPTY;
-    if (!v6 && !macs) {
+    if (!v6 && !macs && v4_fast(T, k.w[9] & 0xFF)) {
         s = tab_slot(T, 0, ((uint64_t)k.w[0] << 32) | k.w[4], insert);
         if (s == FAIL) return FAIL;
         chain[0] = s;
-        s = tab_slot(T, 1, ((uint64_t)s << 40) | ((uint64_t)k.w[8] << 8) | (k.w[9] & 0xFF), insert, &v);
+        s = tab_slot(T, 1, v4_t1_word(T, s, k.w[8], k.w[9] & 0xFF), insert, &v);
         if (s == FAIL) return FAIL;
         chain[1] = s;
         ft = 1;
@@ -405,6 +405,16 @@ __device__ __forceinline__ uint32_t ckey_bucket_v4(uint32_t lo, uint32_t hi, uin
 // ckey_bucket, or PH_PARSE (the hot parser did not key it: the exact engine
 // parses the packet itself).
 constexpr uint32_t PH_PARSE = 0xFFFFFFFFu;
+// The same words after the merge (flow ids per packet, k_parse_spill runs with
+// AggArgs::pid): a packet the merge resolved carries its dense id (PH_ID | d),
+// or its merge entry (PH_EREF | batch << 21 | owner << 10 | entry), whose
+// dense id the merge's id phase writes to emap[batch << 21 | owner << 10 |
+// entry].  Buckets stay below 2^22, dense ids below 2^26 (MAX_FLOWS).
+constexpr uint32_t PH_ID = 0x80000000u, PH_EREF = 0x40000000u;
+__device__ __forceinline__ uint32_t ph_flow(uint32_t w, const uint32_t* emap) {  // dense id, or FAIL
+    if (w == PH_PARSE || !(w & (PH_ID | PH_EREF))) return FAIL;
+    return (w & PH_ID) ? (w & 0x03FFFFFFu) : emap[w & 0x00FFFFFFu];
+}
 
 // Append one record (Mode A paths): position, updates and ended counters.
 __device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {

@@ -113,6 +113,9 @@ struct ExactJob {
     // B.first - phash_base of each batch first, or null
     const uint32_t* phash = nullptr;
     uint64_t phash_base = 0;
+    // or null: the words also carry the merge's flows (PH_ID / PH_EREF,
+    // device.h), emap its entries' dense ids (Mode A and Mode B)
+    const uint32_t* emap = nullptr;
 };
 
 struct ExactResult {

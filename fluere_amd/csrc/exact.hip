@@ -52,7 +52,10 @@
 namespace fl {
 namespace {
 
-constexpr uint64_t M40 = (1ull << 40) - 1;
+// Per-key positions packed below the dense id: (d << PBITS) | p, p < 2^38
+// packets, d < 2^26 flows (MAX_FLOWS); MP (all ones): none.
+constexpr int PBITS = 38;
+constexpr uint64_t MP = (1ull << PBITS) - 1;
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr int MAX_PASSES = 32;
 enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2, K_LEAD = 3 };
@@ -100,24 +103,33 @@ constexpr uint32_t EXM_PKTS = 1024;
 constexpr int EXM_R = EXM_PKTS / 256;
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
                                                  const uint8_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
-                                                 uint64_t blk0, const uint32_t* phash) {
+                                                 uint64_t blk0, const uint32_t* phash, const uint32_t* emap) {
     __shared__ uint32_t s_c[EXM_PKTS];
     __shared__ uint32_t s_w[2][4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t base = (uint64_t)blockIdx.x * EXM_PKTS;
-    const bool filt = phash && !all && cbits;
-    // phase 1 (the filter words' loads, then their buckets' bytes, all in flight)
+    // the words: filter buckets (Mode A, cbits), or the merge's flows (emap)
+    const bool words = phash && ((!all && cbits) || emap);
+    // phase 1 (the words' loads, then their buckets' bytes / flows' complex
+    // flags, all in flight)
     bool cand[EXM_R];
     uint32_t hw[EXM_R];
 #pragma unroll
     for (int r = 0; r < EXM_R; r++) {
         const uint64_t li = base + r * 256 + tid;
         cand[r] = li < B.n;
-        hw[r] = (filt && cand[r]) ? phash[li] : PH_PARSE;
+        hw[r] = (words && cand[r]) ? phash[li] : PH_PARSE;
     }
 #pragma unroll
-    for (int r = 0; r < EXM_R; r++)
-        if (hw[r] != PH_PARSE) cand[r] = cbits[hw[r] & ((1u << CBITS_LOG2) - 1)] != 0;
+    for (int r = 0; r < EXM_R; r++) {
+        if (hw[r] == PH_PARSE) continue;
+        if (emap && (hw[r] & (PH_ID | PH_EREF))) {
+            const uint32_t d = ph_flow(hw[r], emap);
+            cand[r] = d < T.fmax && (all || cplx[d]);
+        } else if (!all && cbits) {
+            cand[r] = cbits[hw[r] & ((1u << CBITS_LOG2) - 1)] != 0;
+        }
+    }
     uint32_t nc = 0;
 #pragma unroll
     for (int r = 0; r < EXM_R; r++) {
@@ -142,18 +154,26 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
         memset(&m, 0, sizeof m);
         if (i < nc) {
             const uint64_t li = base + s_c[i];
+            const uint32_t wd = words ? phash[li] : PH_PARSE;
+            const bool known = emap && wd != PH_PARSE && (wd & (PH_ID | PH_EREF));
             Parsed P;
             parse_record(B, li, macs != 0, 0, P);
             if (P.cls == 0) {
                 uint8_t dir;
-                CKey k;
-                canon_key(P, macs != 0, k, dir);
-                bool maybe = true;
-                if (!all && cbits) {  // no complex flow has this key's bucket: no dictionary walk
-                    const uint32_t b = ckey_bucket(k.w);
-                    maybe = cbits[b] != 0;
+                uint32_t d;
+                if (known) {  // the merge resolved this packet's flow
+                    dir = canon_dir(P, macs != 0);
+                    d = ph_flow(wd, emap);
+                } else {
+                    CKey k;
+                    canon_key(P, macs != 0, k, dir);
+                    bool maybe = true;
+                    if (!all && cbits) {  // no complex flow has this key's bucket: no dictionary walk
+                        const uint32_t b = ckey_bucket(k.w);
+                        maybe = cbits[b] != 0;
+                    }
+                    d = maybe ? dense_of_key(T, k, false, nullptr, nullptr) : FAIL;
                 }
-                const uint32_t d = maybe ? dense_of_key(T, k, false, nullptr, nullptr) : FAIL;
                 if (d != FAIL && d < T.fmax && (all || cplx[d])) {
                     take = 1;
                     m.t = P.t;
@@ -213,9 +233,9 @@ __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* s
     const unsigned long long d = skey[p];
     hf[p] = (p == 0 || skey[p - 1] != skey[p]) ? 1u : 0u;
     // reversed, so an inclusive min-scan gives the first eligible / FIN-RST
-    // position at or after p within the key (low 40 bits M40: none)
-    re[n - 1 - p] = (d << 40) | ((m.bits & 1) ? p : M40);
-    rf[n - 1 - p] = (d << 40) | ((m.bits & 2) ? p : M40);
+    // position at or after p within the key (low PBITS bits MP: none)
+    re[n - 1 - p] = (d << PBITS) | ((m.bits & 1) ? p : MP);
+    rf[n - 1 - p] = (d << PBITS) | ((m.bits & 2) ? p : MP);
 }
 
 __global__ void __launch_bounds__(256) k_ex_heads(uint64_t n, const uint32_t* hf, const uint32_t* hpos, uint32_t* heads) {
@@ -252,7 +272,7 @@ __global__ void __launch_bounds__(256) k_ex_tindex(uint64_t n, const ExMeta* cm,
 // reversed "k if processed" for the next-processed min-scan
 __global__ void __launch_bounds__(256) k_ex_proc_in(uint64_t n, const uint8_t* pr, unsigned long long* npr) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) npr[n - 1 - k] = pr[k] ? k : M40;
+    if (k < n) npr[n - 1 - k] = pr[k] ? k : MP;
 }
 
 }  // namespace
@@ -355,7 +375,7 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     const uint64_t k = max((uint64_t)k0, lo);
     if (k >= a.n) return NONE64;
     const unsigned long long kp = a.np_rev[a.n - 1 - k];
-    return kp == M40 ? NONE64 : a.cm[kp].gidx;
+    return kp == MP ? NONE64 : a.cm[kp].gidx;
 }
 
 __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
@@ -384,19 +404,19 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
     // shard mode: from "no flow", the lead piece [p0, min(e0, f0 + 1)) and the
     // roles of the instances (the first one, if created at or before f0, is
     // the head; the one still open at the end, after f0, the tail)
-    const unsigned long long f0 = a.nf_rev[a.n - 1 - p0] & M40;
+    const unsigned long long f0 = a.nf_rev[a.n - 1 - p0] & MP;
     int n_inst = 0;
     if (a.shard_mode) {
-        const unsigned long long e0 = a.ne_rev[a.n - 1 - p0] & M40;
-        const uint32_t lead_end = (uint32_t)min(e0 == M40 ? (unsigned long long)pend : e0,
-                                                f0 == M40 ? (unsigned long long)pend : f0 + 1);  // exclusive
+        const unsigned long long e0 = a.ne_rev[a.n - 1 - p0] & MP;
+        const uint32_t lead_end = (uint32_t)min(e0 == MP ? (unsigned long long)pend : e0,
+                                                f0 == MP ? (unsigned long long)pend : f0 + 1);  // exclusive
         const uint32_t d = a.sm[p0].d;
         fluere_flow_annex& ax = a.annex[q];
         const uint32_t* kw = reinterpret_cast<const uint32_t*>(a.flow_key + (size_t)d * 56);
         for (int k = 0; k < 14; k++) ax.key[k] = kw[k];
-        ax.flags = (f0 != M40 ? 1u : 0u) | (lead_end > p0 ? 2u : 0u);
+        ax.flags = (f0 != MP ? 1u : 0u) | (lead_end > p0 ? 2u : 0u);
         ax.mid_last = 0;
-        ax.f0 = f0 != M40 ? a.sm[f0].gidx : NONE64;
+        ax.f0 = f0 != MP ? a.sm[f0].gidx : NONE64;
         a.annex_of[d] = q;
         if (lead_end > p0) {
             a.sflag[p0] = 1;
@@ -407,8 +427,8 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         }
     }
     while (pos < pend) {
-        const unsigned long long ce = a.ne_rev[a.n - 1 - pos] & M40;
-        if (ce == M40) break;
+        const unsigned long long ce = a.ne_rev[a.n - 1 - pos] & MP;
+        if (ce == MP) break;
         const uint32_t c = (uint32_t)ce;
         const ExMeta mc = a.sm[c];
         const uint32_t o = mc.dir;
@@ -433,11 +453,11 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
             front = qh[o];
             jf = a.ej[front];
         }
-        const unsigned long long fe = a.nf_rev[a.n - 1 - c] & M40;
+        const unsigned long long fe = a.nf_rev[a.n - 1 - c] & MP;
         uint32_t end;
         uint8_t kind;
         unsigned long long cj = NONE64, cie = 0, cex = 0;
-        if (fe != M40 && (jf == NONE64 || a.sm[fe].gidx <= jf)) {  // FIN/RST first (the sweep runs after it)
+        if (fe != MP && (jf == NONE64 || a.sm[fe].gidx <= jf)) {  // FIN/RST first (the sweep runs after it)
             end = (uint32_t)fe;
             kind = K_FIN;
             cj = a.sm[fe].gidx;
@@ -464,7 +484,7 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         a.iie[c] = cie;
         a.iex[c] = cex;
         if (a.shard_mode) {
-            const bool head = n_inst == 0 && (f0 == M40 || c <= f0);
+            const bool head = n_inst == 0 && (f0 == MP || c <= f0);
             const bool tail = kind == K_ACTIVE;
             a.irole[c] = head ? (tail ? R_HEAD_TAIL : R_HEAD) : (tail ? R_TAIL : R_RECORD);
             a.ikey[c] = q;
@@ -1019,8 +1039,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            const uint32_t* ph = J.phash && !J.mode_b ? J.phash + (B.first - J.phash_base) : nullptr;
-            k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk, ph);
+            const uint32_t* ph = J.phash && (!J.mode_b || J.emap) ? J.phash + (B.first - J.phash_base) : nullptr;
+            k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk, ph,
+                                                           J.emap);
             blk += gridn(B.n, EXM_PKTS);
         }
     }
@@ -1320,7 +1341,8 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
-            k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk, nullptr);
+            k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk, nullptr,
+                                                           nullptr);
             blk += gridn(B.n, EXM_PKTS);
         }
         unsigned long long last[2] = {0, 0};

@@ -10,6 +10,9 @@
 //
 //   IPv4, no MAC:  T0[(lo_ip << 32) | hi_ip]                      -> s0
 //                  T1[(s0 << 40) | (lo_port << 24) | (hi_port << 8) | proto] -> s1 -> dense id
+//                  (tables of more than 2^24 slots, "wide": T1[(s0 << 33) |
+//                  (ports << 1) | udp] for TCP and UDP, every other protocol
+//                  through the generic chain -- v4_t1_word)
 //   otherwise:     the canonical key serialised to 32-bit units; level 0 takes
 //                  units 0 and 1, level k >= 1 takes (s_{k-1} << 32) | unit k+1.
 //
@@ -40,9 +43,12 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+constexpr uint32_t MAX_TABLE_SLOTS = 1u << 27;  // per table (T1 words keep s0 in 31 bits when wide)
+constexpr uint32_t MAX_FLOWS = 1u << 26;        // dense ids (the exact engine packs id << 38 | position)
+
 struct TableSet {
     unsigned long long* tab[N_TABLES];  // (C + 1) entries of {key, val}; entry C holds the word EMPTY
-    uint32_t C;                          // power of two, <= 1 << 23
+    uint32_t C;                          // power of two, <= MAX_TABLE_SLOTS
     uint32_t fmax;                       // dense id capacity
     uint32_t* n_flows;
     uint32_t* err;
@@ -74,6 +80,19 @@ __device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t 
     }
     atomicOr(T.err, ERR_TABLE_FULL);
     return FAIL;
+}
+
+// The IPv4 fast chain's second-level word.  Tables of up to 2^24 slots keep
+// s0 in 24 bits beside the ports and the protocol; wider tables ("wide", more
+// than 8M flows) keep s0 in 31 bits, the ports and one protocol bit: TCP and
+// UDP only (v4_fast), every other protocol takes the generic chain.  A key
+// always takes the same chain, so either is exact.
+__device__ __forceinline__ bool v4_fast(const TableSet& T, uint32_t proto) {
+    return T.C <= (1u << 24) || proto == 6u || proto == 17u;
+}
+__device__ __forceinline__ uint64_t v4_t1_word(const TableSet& T, uint32_t s0, uint32_t ports, uint32_t proto) {
+    return T.C <= (1u << 24) ? ((uint64_t)s0 << 40) | ((uint64_t)ports << 8) | proto
+                             : ((uint64_t)s0 << 33) | ((uint64_t)ports << 1) | (proto == 17u ? 1u : 0u);
 }
 
 // Canonical key: 14 little-endian u32 words (also fluere_flow_summary.key):

@@ -194,6 +194,15 @@ struct AggArgs {
     unsigned long long* dbg;   // diagnostics (FLUERE_DEBUG): per workgroup {start, flush start, flush end, end} wall clock
     uint32_t* phash;           // or null: per packet of the batch, its ckey_bucket or PH_PARSE (device.h), for
                                // the exact engine's filter (k_ex_meta reads it instead of parsing every packet)
+    // or null: the merge writes each resolved packet's flow (PH_ID / PH_EREF,
+    // device.h) over its word in pid[global index - pid_base], and its
+    // entries' dense ids to emap (k_ex_meta then walks no dictionary)
+    uint32_t* pid;
+    uint32_t* emap;
+    uint64_t pid_base;
+    uint32_t pid_batch;
+    int slow_all;              // k_slow takes every packet of the batch (no hot kernel: captures of the general
+                               // parser's classes, where the hot pass would only list them)
 };
 
 // Front end of the hot kernel: Ethernet / IPv4 (ihl 5) / TCP or UDP parsed
@@ -1493,6 +1502,9 @@ __device__ __forceinline__ uint32_t staged_id(const TableSet& T, const V6Map& M,
 constexpr int MB = 1024;   // merge kernel block
 constexpr int MT = 1024;   // merge table entries (120 B each)
 constexpr int MCH = 1024;  // sets per scan chunk
+#ifndef FLUERE_MERGE_ABL
+#define FLUERE_MERGE_ABL 0  // diagnostics only (wrong results): 1 records loaded, no table; 2 probe, no updates
+#endif
 #ifndef FLUERE_MERGE_GUARD
 #define FLUERE_MERGE_GUARD 1  // read-before-atomic for min / max / positions (0: unconditional)
 #endif
@@ -1867,6 +1879,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     const uint4 v0 = src[0], v1 = src[1];
                     const unsigned long long gi = a.B.first + m_wb[lo_i] + v1.z;
                     const uint32_t k0 = v0.x, k1 = v0.y, k2 = v0.z, tag = v0.w;
+                    if (FLUERE_MERGE_ABL == 1) {  // diagnostics: the loads alone
+                        if ((k0 ^ k1 ^ k2 ^ v1.x ^ v1.y) == 0x12345678u) atomicAdd(&m_pk[0][0], 1u);
+                        continue;
+                    }
                     const uint32_t h = lt_hash(k0, k1, k2, tag);
                     uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
                     int state = 0, probes = 0;
@@ -1890,6 +1906,11 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     }
                     const uint32_t dir = (v1.w >> 8) & 1u, tf = v1.w & 0xFFu;
                     const uint32_t pkt = v1.y & 0xFFFFu, ttl = (v1.y >> 16) & 0xFFu;
+                    if (FLUERE_MERGE_ABL == 2) {  // diagnostics: the probe, no updates
+                        if (state == 1 && pkt == 0x1234u) atomicAdd(&m_pk[0][e], 1u);
+                        continue;
+                    }
+                    if (a.pid && state == 1) a.pid[gi - a.pid_base] = PH_EREF | (a.pid_batch << 21) | (me << 10) | e;
                     if (state == 1) {  // update_flow of one packet (flows.rs:11-42), order-free part
                         atomicAdd(&m_pk[dir][e], 1u);
                         atomicAdd(&m_by[dir][e], (unsigned long long)v1.x);
@@ -1909,6 +1930,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                         spill_to_part(v1.x, v1.y, v1.z, v1.w, a.B.first + m_wb[lo_i], f);
                         const uint32_t d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
                         if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
+                        if (a.pid && d != FAIL && d < a.T.fmax) a.pid[gi - a.pid_base] = PH_ID | d;
                     }
                 }
                 __syncthreads();
@@ -1985,10 +2007,12 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 CKey ck;
                 mac_ckey(kk.x, kk.y, kk.z, tag, xx.x, xx.y, xx.z, ck);
                 d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+            } else if (!v4_fast(a.T, tag >> 24)) {  // wide tables: protocols other than TCP / UDP
+                d = staged_id(a.T, a.v6, kk.x, kk.y, kk.z, tag, a.A.slots);
             } else {       // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
                 unsigned long long v = EMPTY;
                 s0 = tab_slot(a.T, 0, ((uint64_t)kk.x << 32) | kk.y, true);
-                if (s0 != FAIL) s1 = tab_slot(a.T, 1, ((uint64_t)s0 << 40) | ((uint64_t)kk.z << 8) | (tag >> 24), true, &v);
+                if (s0 != FAIL) s1 = tab_slot(a.T, 1, v4_t1_word(a.T, s0, kk.z, tag >> 24), true, &v);
                 if (s1 != FAIL) {
                     val = &a.T.tab[1][2 * s1 + 1];
                     if (v >= PENDING) v = atomicCAS(val, EMPTY, PENDING);
@@ -2035,6 +2059,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         }
         if (wait) atomicOr(a.T.err, ERR_SPIN);
         if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 4] = wall_clock64();
+        if (a.emap) a.emap[((size_t)a.pid_batch << 21) | ((size_t)me << 10) | (uint32_t)e] = (have && d < a.T.fmax) ? d : FAIL;
         if (have && d != FAIL && d < a.T.fmax) {
             FlowPart f;
     #pragma unroll
@@ -2131,7 +2156,8 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 x0 = v1.x; x1 = v1.y; x2 = v1.z;
             }
             FlowPart f;
-            spill_to_part(pay.x, pay.y, pay.z, pay.w, S.base[pay.w >> 9], f);
+            const unsigned long long wbase = S.base[pay.w >> 9];
+            spill_to_part(pay.x, pay.y, pay.z, pay.w, wbase, f);
             uint32_t d;
             if (macs && v0.w != 0xFF000000u) {
                 CKey ck;
@@ -2141,6 +2167,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 d = staged_id(a.T, a.v6, v0.x, v0.y, v0.z, v0.w, a.A.slots);
             }
             if (d != FAIL && d < a.T.fmax) put(d, f);
+            if (a.pid && d != FAIL && d < a.T.fmax) a.pid[wbase + pay.z - a.pid_base] = PH_ID | d;
         }
         if (tail_slow) {
             // the hot workgroups' regions, flattened: exclusive scan of their counts
@@ -2178,6 +2205,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 FlowPart f;
                 pkt_to_part(P.pi, dir, a.B.first + li, f);
                 put(d, f);
+                if (a.pid) a.pid[a.B.first + li - a.pid_base] = PH_ID | d;
             }
             // run counters: one set of atomics per wave
 #pragma unroll
@@ -2245,7 +2273,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
     // the hot workgroups' regions, flattened (wave 0: an exclusive scan, an
     // even run of regions per lane)
     const uint32_t nwg = S.n_wg;  // <= MB
-    if (tid < 64) {
+    if (tid < 64 && !a.slow_all) {
         const uint32_t per = (nwg + 63) / 64;
         uint32_t sum = 0;
         for (uint32_t q = 0; q < per; q++) {
@@ -2269,7 +2297,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         if (tid == 63) s_start[MB] = incl;
     }
     __syncthreads();
-    const unsigned long long n = s_start[MB];
+    const unsigned long long n = a.slow_all ? a.B.n : s_start[MB];
     const unsigned long long i0 = (unsigned long long)blockIdx.x * SLOW_SET;
     const unsigned long long i1 = min(n, i0 + SLOW_SET);
     unsigned long long c_valid = 0, c_drop = 0, c_seg = 0, tmin = NONE64, tmax = 0;
@@ -2280,13 +2308,16 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         Parsed P;
         uint4 wk = make_uint4(0, 0, 0, 0), wx = make_uint4(0, 0, 0, 0), wp = make_uint4(0, 0, 0, 0);
         if (i < i1) {
-            uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
-            while (lo_w < hi_w) {
-                const uint32_t mid = (lo_w + hi_w + 1) >> 1;
-                if (s_start[mid] <= i) lo_w = mid;
-                else hi_w = mid - 1;
+            uint32_t li = (uint32_t)i;
+            if (!a.slow_all) {
+                uint32_t lo_w = 0, hi_w = nwg - 1;  // last region with start <= i
+                while (lo_w < hi_w) {
+                    const uint32_t mid = (lo_w + hi_w + 1) >> 1;
+                    if (s_start[mid] <= i) lo_w = mid;
+                    else hi_w = mid - 1;
+                }
+                li = a.slow[(size_t)lo_w * a.slow_region + (i - s_start[lo_w])];
             }
-            const uint32_t li = a.slow[(size_t)lo_w * a.slow_region + (i - s_start[lo_w])];
             const uint32_t off = a.B.offs[li];
             Win32 W;
             load_win32(a.B, off, W);
@@ -3590,19 +3621,23 @@ struct CensusArgs {
     int macs;
 };
 __global__ void __launch_bounds__(256) k_census(CensusArgs a) {
-    __shared__ unsigned long long s_c[7], s_tmin, s_tmax;
-    const uint32_t tid = threadIdx.x;
-    if (tid < 7) s_c[tid] = 0;
-    if (tid == 0) { s_tmin = NONE64; s_tmax = 0; }
+    __shared__ unsigned long long s_c[9];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid < 9) s_c[tid] = tid == 7 ? NONE64 : 0ull;
     __syncthreads();
     const uint64_t j = (uint64_t)blockIdx.x * 256 + tid;
     const Batch& B = a.B;
-    if (j < a.s_n) {
+    uint32_t cls = HOT_DROP, dd = 0, d1 = 0, d2 = 0;  // d1 / d2: +1, or -1 as 2
+    bool tcp = false, live = j < a.s_n;
+    unsigned long long t = 0;
+    if (live) {
         const uint64_t lo = j * B.n / a.s_n, hi = (j + 1) * B.n / a.s_n;
         uint32_t r = (uint32_t)(j * 0x9E3779B97F4A7C15ull >> 32);
         r ^= r >> 15; r *= 0x2C1B3C6Du; r ^= r >> 12;
         const uint64_t li = lo + (hi > lo ? r % (uint32_t)(hi - lo) : 0u);
-        const uint32_t off = B.offs[li];
+        // (clamped: the census may read a batch before the caller has
+        // finished writing it -- only its predictions would be off)
+        const uint32_t off = (uint32_t)min<uint64_t>(B.offs[li], B.nbytes);
         Win W;
         const uint8_t* p = B.bytes + off;
 #pragma unroll
@@ -3613,14 +3648,10 @@ __global__ void __launch_bounds__(256) k_census(CensusArgs a) {
         }
         W.w[16] = W.w[17] = W.w[18] = W.w[19] = 0u;
         Hot h;
-        const uint32_t cls = hot_parse(B, off, W, h);
-        atomicAdd(&s_c[0], 1ull);
-        if (cls == HOT_SLOW) atomicAdd(&s_c[2], 1ull);
+        cls = hot_parse(B, off, W, h);
         if (cls == HOT_OK) {
-            atomicAdd(&s_c[1], 1ull);
-            if (h.proto == 6u) atomicAdd(&s_c[3], 1ull);
-            atomicMin(&s_tmin, (unsigned long long)h.t);
-            atomicMax(&s_tmax, (unsigned long long)h.t);
+            tcp = h.proto == 6u;
+            t = h.t;
             const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
             bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
             uint64_t mx = 0;
@@ -3645,19 +3676,37 @@ __global__ void __launch_bounds__(256) k_census(CensusArgs a) {
                 const unsigned long long v = atomicCAS(&a.fp[e], 0ull, (unsigned long long)f);
                 if (v == 0ull || v == f) {
                     const uint32_t old = atomicAdd(&a.cnt[e], 1u);
-                    if (old == 0) { atomicAdd(&s_c[4], 1ull); atomicAdd(&s_c[5], 1ull); }
-                    else if (old == 1) { atomicAdd(&s_c[5], ~0ull); atomicAdd(&s_c[6], 1ull); }
-                    else if (old == 2) atomicAdd(&s_c[6], ~0ull);
+                    dd = old == 0;
+                    d1 = old == 0 ? 1u : old == 1 ? 2u : 0u;
+                    d2 = old == 1 ? 1u : old == 2 ? 2u : 0u;
                     break;
                 }
                 e = (e + 1) & mask;
             }
         }
     }
+    // wave totals (ballots), then one LDS add per wave and counter
+    const unsigned long long v[7] = {
+        (unsigned long long)__popcll(__ballot(live)), (unsigned long long)__popcll(__ballot(cls == HOT_OK && live)),
+        (unsigned long long)__popcll(__ballot(cls == HOT_SLOW && live)), (unsigned long long)__popcll(__ballot(tcp)),
+        (unsigned long long)__popcll(__ballot(dd != 0)),
+        (unsigned long long)__popcll(__ballot(d1 == 1)) - (unsigned long long)__popcll(__ballot(d1 == 2)),
+        (unsigned long long)__popcll(__ballot(d2 == 1)) - (unsigned long long)__popcll(__ballot(d2 == 2))};
+    unsigned long long tmn = (cls == HOT_OK && live) ? t : NONE64, tmx = (cls == HOT_OK && live) ? t : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+        tmn = min(tmn, (unsigned long long)__shfl_xor(tmn, o, 64));
+        tmx = max(tmx, (unsigned long long)__shfl_xor(tmx, o, 64));
+    }
+    if (lane == 0) {
+        for (int k = 0; k < 7; k++)
+            if (v[k]) atomicAdd(&s_c[k], v[k]);
+        atomicMin(&s_c[7], tmn);
+        atomicMax(&s_c[8], tmx);
+    }
     __syncthreads();
     if (tid < 7 && s_c[tid]) atomicAdd(&a.out->seen + tid, s_c[tid]);
-    if (tid == 7 && s_tmin != NONE64) atomicMin(&a.out->tmin, s_tmin);
-    if (tid == 8 && s_tmax) atomicMax(&a.out->tmax, s_tmax);
+    if (tid == 7 && s_c[7] != NONE64) atomicMin(&a.out->tmin, s_c[7]);
+    if (tid == 8 && s_c[8]) atomicMax(&a.out->tmax, s_c[8]);
 }
 
 // ===========================================================================
@@ -3749,14 +3798,16 @@ struct fluere_ctx {
     uint64_t last_n_slow = 0;                   // slow-list packets of the last run (k_slow prediction)
     uint64_t last_n_complex = 0;                // complex flows of the last run, and whether it was Mode B:
     int last_mode_b = 0;                        //   the phash prediction (the exact engine's Mode A filter)
-    uint32_t* d_phash = nullptr;                // per packet: ckey_bucket or PH_PARSE (AggArgs::phash)
-    uint64_t phash_cap = 0;
+    uint32_t* d_phash = nullptr;                // per packet: ckey_bucket or PH_PARSE (AggArgs::phash), then the
+    uint64_t phash_cap = 0;                     //   merge's flow words (AggArgs::pid)
+    uint32_t* d_emap = nullptr;                 // merge entry -> dense id (AggArgs::emap), PLAN_BATCHES << 21 words
     bool async_nf = false;                      // fluere_export_async left the shard's flow count in h_ctl->pad[0]
     bool pass_in_run = false;
     bool precleaned = false;                    // the flow state is clear (k_cleanup already enqueued)
     uint32_t run_seq = 0;                       // number of the last run that publishes its counters (Ctl::seq)
     int plan_nb = 0;                            // batches of the last pass
     int plan_spill = 0;                         // the last pass's hot kernel was k_parse_spill
+    int plan_slow_all = 0;                      // ... or k_slow over every packet (no hot kernel)
     double last_run_ms = 0;                     // host wall time of the last fluere_run
     // census of a newly attached capture (k_census): due when batches were
     // attached since the last pass; its sample counts and flow estimate
@@ -3787,6 +3838,8 @@ struct fluere_ctx {
     void* d_ord = nullptr;           // order_records scratch
     size_t d_ord_bytes = 0;
 };
+
+static int prepare_capture(fluere_ctx* c);
 
 static void reset_record_counters(fluere_ctx* c) {
     char* g = (char*)c->d_glob;
@@ -3873,37 +3926,18 @@ static TableSet tables_of(fluere_ctx* c) {
 
 extern "C" int fluere_abi_version(void) { return FLUERE_ABI_VERSION; }
 
-extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
-    if (!out) return FLUERE_E_ARG;
-    *out = nullptr;
-    fluere_ctx* c = new (std::nothrow) fluere_ctx();
-    if (!c) return FLUERE_E_NOMEM;
-    fluere_opts def{};
-    def.timeout_ms = 600000;
-    if (!o) o = &def;
-    c->device = o->device;
-    c->timeout_ms = o->timeout_ms;
-    c->use_mac = o->use_mac ? 1 : 0;
-    uint64_t mf = o->max_flows ? o->max_flows : (1ull << 21);
+// The dictionary and the per-flow state for up to mf flows, empty: every
+// table EMPTY, the accumulators at their identities (what k_cleanup leaves).
+static int alloc_flow_state(fluere_ctx* c, uint64_t mf) {
     uint32_t C = 1u << 16;
-    while (C < 2 * mf && C < (1u << 23)) C <<= 1;
+    while (C < 2 * mf && C < MAX_TABLE_SLOTS) C <<= 1;
     c->C = C;
-    c->fmax = (uint32_t)std::min<uint64_t>(mf, C);
-    int rc = FLUERE_OK;
-    auto fail = [&](int r) { rc = r; fluere_close(c); return r; };
-    if (hipSetDevice(c->device) != hipSuccess) return fail(FLUERE_E_HIP);
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = std::min(prop.multiProcessorCount, MB);  // (slow-list regions: one per hot workgroup, <= MB)
-    if (o->stream) c->stream = (hipStream_t)o->stream;
-    else {
-        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLUERE_E_HIP);
-        c->own_stream = true;
-    }
-    size_t tab_words = (size_t)N_TABLES * 2 * (C + 1);
-    if (hipMalloc(&c->d_tab, tab_words * 8) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    size_t F = c->fmax;
-    size_t acc_bytes = F * (4 * 2 + 8 * 2 + 4 * 4 + 4 * 8 + 8 * 4 + 4 * N_TABLES);
-    if (hipMalloc(&c->d_acc, acc_bytes) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    c->fmax = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(mf, C), MAX_FLOWS);
+    const size_t tab_words = (size_t)N_TABLES * 2 * (C + 1);
+    if (hipMalloc(&c->d_tab, tab_words * 8) != hipSuccess) return FLUERE_E_NOMEM;
+    const size_t F = c->fmax;
+    const size_t acc_bytes = F * (4 * 2 + 8 * 2 + 4 * 4 + 4 * 8 + 8 * 4 + 4 * N_TABLES);
+    if (hipMalloc(&c->d_acc, acc_bytes) != hipSuccess) return FLUERE_E_NOMEM;
     char* p = (char*)c->d_acc;
     auto take = [&](size_t bytes) { char* r = p; p += bytes; return r; };
     for (int q = 0; q < 2; q++) c->acc.by[q] = (unsigned long long*)take(F * 8);
@@ -3916,22 +3950,9 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     for (int q = 0; q < 2; q++) c->acc.mx[q] = (uint32_t*)take(F * 4);
     for (int q = 0; q < 8; q++) c->acc.fl[q] = (uint32_t*)take(F * 4);
     c->acc.slots = (uint32_t*)take(F * 4 * N_TABLES);
-    if (hipMalloc(&c->d_glob, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    c->d_nflows = &reinterpret_cast<Ctl*>(c->d_glob)->n_flows;
-    if (hipHostMalloc(&c->h_ctl, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    memset(c->h_ctl, 0, sizeof(Ctl));
-    if (hipHostMalloc(&c->h_mail, sizeof(HostMail)) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    memset(c->h_mail, 0, sizeof(HostMail));
-    if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    if (hipMalloc(&c->d_complex, F) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    if (hipMalloc(&c->d_fdefer, F * 4) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    if (hipMalloc(&c->d_cbits, 1u << CBITS_LOG2) != hipSuccess) return fail(FLUERE_E_NOMEM);
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
-        hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess ||
-        hipEventCreate(&c->ev_ctl) != hipSuccess)
-        return fail(FLUERE_E_HIP);
-    // initial state: every table EMPTY, accumulators at their identities
+    if (hipMalloc(&c->d_flow_key, F * 56) != hipSuccess) return FLUERE_E_NOMEM;
+    if (hipMalloc(&c->d_complex, F) != hipSuccess) return FLUERE_E_NOMEM;
+    if (hipMalloc(&c->d_fdefer, F * 4) != hipSuccess) return FLUERE_E_NOMEM;
     hipStream_t s = c->stream;
     k_fill_u64<<<grid_for(tab_words, 256), 256, 0, s>>>(c->d_tab, tab_words, EMPTY);
     k_fill_u64<<<grid_for(4 * F, 256), 256, 0, s>>>(c->acc.fa, 4 * F, NONE64);
@@ -3942,7 +3963,65 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     k_fill_u32<<<grid_for(2 * F, 256), 256, 0, s>>>(c->acc.mx[0], 2 * F, 0);
     k_fill_u32<<<grid_for(8 * F, 256), 256, 0, s>>>(c->acc.fl[0], 8 * F, 0);
     k_fill_u32<<<grid_for(F * N_TABLES, 256), 256, 0, s>>>(c->acc.slots, F * N_TABLES, NONE32);
-    if (hipMemsetAsync(c->d_complex, 0, F, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    HIPCHECK(hipMemsetAsync(c->d_complex, 0, F, s));
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+static void free_flow_state(fluere_ctx* c) {
+    hipFree(c->d_tab);
+    hipFree(c->d_acc);
+    hipFree(c->d_flow_key);
+    hipFree(c->d_complex);
+    hipFree(c->d_fdefer);
+    c->d_tab = nullptr;
+    c->d_acc = nullptr;
+    c->d_flow_key = nullptr;
+    c->d_complex = nullptr;
+    c->d_fdefer = nullptr;
+    // the lazily sized per-flow arrays follow the new capacity
+    for (void** q : {(void**)&c->d_active, (void**)&c->d_pay, (void**)&c->d_annex_of, (void**)&c->d_sumpos}) {
+        hipFree(*q);
+        *q = nullptr;
+    }
+}
+
+extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
+    if (!out) return FLUERE_E_ARG;
+    *out = nullptr;
+    fluere_ctx* c = new (std::nothrow) fluere_ctx();
+    if (!c) return FLUERE_E_NOMEM;
+    fluere_opts def{};
+    def.timeout_ms = 600000;
+    if (!o) o = &def;
+    c->device = o->device;
+    c->timeout_ms = o->timeout_ms;
+    c->use_mac = o->use_mac ? 1 : 0;
+    const uint64_t mf = o->max_flows ? o->max_flows : (1ull << 21);
+    int rc = FLUERE_OK;
+    auto fail = [&](int r) { rc = r; fluere_close(c); return r; };
+    if (hipSetDevice(c->device) != hipSuccess) return fail(FLUERE_E_HIP);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = std::min(prop.multiProcessorCount, MB);  // (slow-list regions: one per hot workgroup, <= MB)
+    if (o->stream) c->stream = (hipStream_t)o->stream;
+    else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLUERE_E_HIP);
+        c->own_stream = true;
+    }
+    if ((rc = alloc_flow_state(c, mf))) return fail(rc);
+    if (hipMalloc(&c->d_glob, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    c->d_nflows = &reinterpret_cast<Ctl*>(c->d_glob)->n_flows;
+    if (hipHostMalloc(&c->h_ctl, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    memset(c->h_ctl, 0, sizeof(Ctl));
+    if (hipHostMalloc(&c->h_mail, sizeof(HostMail)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    memset(c->h_mail, 0, sizeof(HostMail));
+    if (hipMalloc(&c->d_cbits, 1u << CBITS_LOG2) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evk0) != hipSuccess ||
+        hipEventCreate(&c->evk1) != hipSuccess || hipEventCreate(&c->evk_first) != hipSuccess ||
+        hipEventCreate(&c->ev_ctl) != hipSuccess)
+        return fail(FLUERE_E_HIP);
+    hipStream_t s = c->stream;
     if (hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s) != hipSuccess) return fail(FLUERE_E_HIP);
     {
         Ctl z{};
@@ -3955,6 +4034,24 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     c->prev_nf = 0;
     (void)rc;
     *out = c;
+    return FLUERE_OK;
+}
+
+// More flows than the context holds (the census's estimate): the reference's
+// HashMap has no bound (offline_fluereflows.rs:61), so the dictionary and the
+// per-flow state are reallocated, empty, for the estimate with headroom, up
+// to MAX_FLOWS (2^26 flows; tables of 2^27 slots, ~40 GB of HBM).  Called
+// between passes only (the flow state holds no results).
+static int grow_flow_state(fluere_ctx* c, uint64_t want) {
+    const uint64_t mf = std::min<uint64_t>(std::max<uint64_t>(want, (uint64_t)c->fmax * 2), MAX_FLOWS);
+    if (mf <= c->fmax) return FLUERE_OK;
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    free_flow_state(c);
+    int rc = alloc_flow_state(c, mf);
+    if (rc) return rc;
+    c->precleaned = true;  // (alloc_flow_state's fills are what a cleanup leaves)
+    c->prev_nf = 0;
+    c->last_nf = std::min<uint64_t>(c->last_nf, c->fmax);
     return FLUERE_OK;
 }
 
@@ -3974,26 +4071,19 @@ extern "C" int fluere_close(fluere_ctx* c) {
     if (!c) return FLUERE_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
     free_batches(c);
-    hipFree(c->d_tab);
-    hipFree(c->d_acc);
+    free_flow_state(c);
     if (c->h_ctl) hipHostFree(c->h_ctl);
     if (c->h_mail) hipHostFree(c->h_mail);
     hipFree(c->d_glob);
-    hipFree(c->d_flow_key);
-    hipFree(c->d_complex);
-    hipFree(c->d_fdefer);
     hipFree(c->d_cbits);
     hipFree(c->d_phash);
-    hipFree(c->d_active);
+    hipFree(c->d_emap);
     hipFree(c->d_batches);
     hipFree(c->d_recs);
-    hipFree(c->d_pay);
     hipFree(c->d_slow);
     hipFree(c->d_stage);
     hipFree(c->d_exact);
     hipFree(c->d_annex);
-    hipFree(c->d_annex_of);
-    hipFree(c->d_sumpos);
     hipFree(c->d_wire_tmp);
     hipFree(c->d_v6map);
     hipFree(c->ar_d);
@@ -4123,6 +4213,7 @@ extern "C" int fluere_add_device_batch(fluere_ctx* c, const uint8_t* d_bytes, ui
                                        const uint32_t* d_offsets, uint64_t n, uint32_t snaplen, int swapped,
                                        int nsec_ts) {
     if (!c || (!d_bytes && n) || (!d_offsets && n) || nbytes >= (1ull << 32)) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
     HostBatch hb;
     hb.b.bytes = d_bytes;
     hb.b.offs = d_offsets;
@@ -4136,7 +4227,7 @@ extern "C" int fluere_add_device_batch(fluere_ctx* c, const uint8_t* d_bytes, ui
     c->census_due = true;
     c->n_total += n;
     c->have_results = false;
-    return FLUERE_OK;
+    return prepare_capture(c);
 }
 
 // libpcap offline walk: stop at the first truncated or
@@ -4545,7 +4636,8 @@ extern "C" int fluere_add_host_pcap(fluere_ctx* c, const uint8_t* file, uint64_t
         memcpy(dst, file + cs, len);
         return true;
     });
-    return rc ? rc : in.finish();
+    if (!rc) rc = in.finish();
+    return rc ? rc : prepare_capture(c);
 }
 
 // File ingress for fluere_offline_file: read() straight into the pinned
@@ -4586,7 +4678,8 @@ extern "C" int fluere_add_pcap_file(fluere_ctx* c, const char* path) {
             return true;
         });
     close(fd);
-    return rc ? rc : in.finish();
+    if (!rc) rc = in.finish();
+    return rc ? rc : prepare_capture(c);
 }
 
 static int upload_batches(fluere_ctx* c) {
@@ -4676,6 +4769,11 @@ static int census(fluere_ctx* c) {
     for (int k = 0; k < 9; k++) c->census_v[k] = v[k];
     c->census_v[9] = F;
     c->census_ran++;
+    // more flows than the context holds: grow it before the pass (live
+    // sessions keep their capacity: their state is sized by it)
+    if (!c->reuse_ingest && F + F / 4 > c->fmax && c->fmax < MAX_FLOWS && !getenv("FLUERE_NO_GROW")) {
+        if ((rc = grow_flow_state(c, F + F / 2))) return rc;
+    }
     // the predictions (the same fields a finished run sets)
     c->last_nf = std::min<uint64_t>(F, c->fmax);
     c->last_n_slow = v[2] ? std::max<uint64_t>(1, v[2] * N / std::max<uint64_t>(1, s_seen)) : 0;
@@ -4723,6 +4821,7 @@ struct PassPlan {
     int macs, abl;
     int spill;     // 1: the hot pass is k_parse_spill (many flows per window), not k_parse_agg
     int phash;     // 1: the hot pass writes the per-packet filter words (AggArgs::phash)
+    int pid;       // 1: the merge writes each packet's flow over them (AggArgs::pid; k_parse_spill runs)
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
     int spec;      // 1: k_finalize publishes the counters to the host itself, a speculative k_cleanup follows
     CleanArgs spec_ca;
@@ -4795,7 +4894,7 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     return std::min<uint32_t>(r, (uint32_t)MAX_OWNERS);
 }
 
-static int plan_batches(fluere_ctx* c, PassPlan& P) {
+static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     AggArgs a;
     memset(&a, 0, sizeof a);
     a.T = tables_of(c);
@@ -4834,6 +4933,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     // merge tail's slower path, or an empty launch)
     const int slow_env = getenv("FLUERE_SLOW_KERNEL") ? atoi(getenv("FLUERE_SLOW_KERNEL")) : -1;  // tests: force it
     a.slow_kernel = slow_env >= 0 ? slow_env : (c->last_n_slow > 0 ? 1 : 0);
+    // k_slow over every packet, no hot kernel, when (nearly) every packet is of
+    // the general parser's classes: the hot pass would only read each window
+    // to list it for k_slow's second read (the slow config: 0.35 of 1.47 ms)
+    static const int sa_env = getenv("FLUERE_SLOW_ALL") ? atoi(getenv("FLUERE_SLOW_ALL")) : -1;  // tests / A/B
+    const bool slow_all =
+        sa_env >= 0 ? sa_env != 0 : (c->n_total > 0 && (uint64_t)c->last_n_slow * 4 >= (uint64_t)c->n_total * 3);
+    if (slow_all) a.slow_kernel = 1;
+    a.slow_all = slow_all ? 1 : 0;
     // k_slow's IPv6 address ids (non-MAC runs): 4 slots per flow of capacity, at most 2^20
     if (a.slow_kernel && !c->use_mac) {
         uint32_t C = 1u << 12;
@@ -4857,6 +4964,22 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     // every packet; 4 bytes per packet written by the hot pass)
     static const int phash_env = getenv("FLUERE_PHASH") ? atoi(getenv("FLUERE_PHASH")) : -1;  // tests / A/B
     P.phash = !c->use_mac && (phash_env >= 0 ? phash_env : (c->last_n_complex > 0 && !c->last_mode_b)) ? 1 : 0;
+    // k_parse_spill runs (every valid packet a record the merge resolves) that
+    // will replay packets (complex flows in Mode A, or Mode B): the merge
+    // writes each packet's flow over its filter word, so k_ex_meta walks no
+    // dictionary (a prediction, like the filter words)
+    {
+        int nbat = 0;
+        for (auto& hb : c->batches) nbat += hb.b.n ? 1 : 0;
+        static const int pid_env = getenv("FLUERE_PID") ? atoi(getenv("FLUERE_PID")) : -1;  // tests / A/B
+        const bool want = pid_env >= 0 ? pid_env != 0 : (c->last_n_complex > 0 || c->last_mode_b);
+        P.pid = (allow_pid && P.spill && !c->use_mac && nbat <= PLAN_BATCHES && want) ? 1 : 0;
+        if (P.pid) P.phash = 1;
+        if (slow_all) P.pid = P.phash = 0;  // (no hot pass writes the words)
+        if (P.pid && !c->d_emap &&
+            hipMalloc(&c->d_emap, ((size_t)PLAN_BATCHES << 21) * sizeof(uint32_t)) != hipSuccess)
+            return FLUERE_E_NOMEM;
+    }
     if (P.phash && c->n_total > c->phash_cap) {
         hipFree(c->d_phash);
         c->d_phash = nullptr;
@@ -4873,8 +4996,8 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
     for (auto& hb : c->batches) {
         if (!hb.b.n) continue;
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
-        unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
-        const uint64_t per = (hb.b.n + grid - 1) / grid;
+        unsigned grid = slow_all ? 0u : (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
+        const uint64_t per = (hb.b.n + std::max(grid, 1u) - 1) / std::max(grid, 1u);
         const uint64_t steps = (per + BLOCK - 1) / BLOCK;
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
@@ -4893,9 +5016,9 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         if (!hb.b.n) continue;
         a.B = hb.b;
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
-        unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
+        unsigned grid = slow_all ? 0u : (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
         // staging: one set per (workgroup, window) -- k_parse_agg's loop bounds
-        const uint64_t per = (hb.b.n + grid - 1) / grid;
+        const uint64_t per = (hb.b.n + std::max(grid, 1u) - 1) / std::max(grid, 1u);
         const uint64_t steps = (per + BLOCK - 1) / BLOCK;
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
@@ -4907,6 +5030,10 @@ static int plan_batches(fluere_ctx* c, PassPlan& P) {
         AggArgs ab = a;
         ab.slow_kernel = n_slow_sets ? a.slow_kernel : 0;
         ab.phash = P.phash ? c->d_phash + (hb.b.first - c->index_base) : nullptr;
+        ab.pid = P.pid ? c->d_phash : nullptr;
+        ab.emap = P.pid ? c->d_emap : nullptr;
+        ab.pid_base = c->index_base;
+        ab.pid_batch = (uint32_t)P.nb;
         const size_t all = sets + n_slow_sets;
         Stage& S = ab.S;
         // layout (16-byte aligned pieces): parts | owner segments (hot, k_slow) | spill_raw | spill | base | off | soff
@@ -4971,11 +5098,11 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     P.clean_grid = done_grid(c, c->prev_nf == ~0ull ? c->fmax : c->prev_nf);
     P.tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
     P.clean = c->precleaned ? 0 : 1;
+    P.spill = spill_mode(c);
     if ((rc = plan_batches(c, P))) return rc;
     static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
     P.macs = c->use_mac;
     P.abl = abl;
-    P.spill = spill_mode(c);
     P.finalize = finalize ? 1 : 0;
     P.h_ctl = c->h_ctl;
     P.d_glob = c->d_glob;
@@ -5025,13 +5152,20 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         void* args[] = {const_cast<AggArgs*>(&a)};
         static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
-        HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, (i == 0 && P.nb > 1) ? c->evk_first : c->evk0,
-                                    c->evk1, 0));
+        hipEvent_t e0 = (i == 0 && P.nb > 1) ? c->evk_first : c->evk0;
+        if (grid)
+            HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, e0, c->evk1, 0));
         const auto t1 = std::chrono::steady_clock::now();
         // the slow list into k_slow's owner segments, before the merge reads them
+        // (every packet without a hot kernel: k_slow carries the timing events)
         if (a.slow_kernel) {
             if (a.v6.C) HIPCHECK(hipMemsetAsync(a.v6.tab[0], 0xFF, (size_t)(a.v6.C + 1) * 3 * 8, s));  // every key EMPTY
-            k_slow<<<P.slow_grid[i], SB, 0, s>>>(a);
+            if (grid) {
+                k_slow<<<P.slow_grid[i], SB, 0, s>>>(a);
+            } else {
+                HIPCHECK(hipExtLaunchKernel((const void*)k_slow, dim3(P.slow_grid[i]), dim3(SB), args, 0, s, e0, c->evk1,
+                                            0));
+            }
         }
         // at most one merge workgroup per CU, each taking owners in turn
         k_merge_partials<<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow took it)
@@ -5118,8 +5252,8 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
                                 : P.abl == 4 ? (const void*)k_parse_agg<4, false>
                                 : P.abl == 5 ? (const void*)k_parse_agg<5, false>
                                              : (const void*)k_parse_agg<0, false>;
-        kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
-        event(c->evk1);
+        if (P.agg_grid[i]) kernel(fn, P.agg_grid[i], BLOCK, a_agg[i]);
+        if (P.agg_grid[i]) event(c->evk1);
         if (P.agg[i].slow_kernel && P.agg[i].v6.C && ok) {
             hipMemsetParams mp{};
             mp.dst = P.agg[i].v6.tab[0];
@@ -5132,6 +5266,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
             prev = n;
         }
         if (P.agg[i].slow_kernel) kernel((const void*)k_slow, P.slow_grid[i], SB, a_agg[i]);
+        if (!P.agg_grid[i]) event(c->evk1);
         kernel((const void*)k_merge_partials, std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, a_agg[i]);
     }
     void* a_fin[] = {&P.fa};
@@ -5243,14 +5378,15 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     memset(&P, 0, sizeof P);
     if ((rc = upload_batches(c))) return rc;
     if ((rc = census(c))) return rc;
-    if ((rc = plan_batches(c, P))) return rc;
+    P.spill = spill_mode(c);
+    if ((rc = plan_batches(c, P, false))) return rc;
     if (P.nb > PLAN_BATCHES) return FLUERE_E_ARG;
     static const int abl = getenv("FLUERE_ABLATE") ? atoi(getenv("FLUERE_ABLATE")) : 0;
     P.macs = c->use_mac;
     P.abl = abl;
-    P.spill = spill_mode(c);
     c->plan_nb = P.nb;
     c->plan_spill = P.spill;
+    c->plan_slow_all = P.nb > 0 && P.agg[0].slow_all;
     c->precleaned = false;
     c->runs++;
     rc = enqueue_batches(c, P);
@@ -5259,6 +5395,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
 }
 
 extern "C" const char* fluere_last_hot_kernel(fluere_ctx* c) {
+    if (c && c->plan_slow_all) return "k_slow";
     return c && c->plan_spill ? "k_parse_spill" : "k_parse_agg";
 }
 
@@ -5308,73 +5445,99 @@ __global__ void __launch_bounds__(256) k_ord_popc(const uint32_t* bits, uint64_t
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w < nw) pc[w] = __popc(bits[w]);
 }
-__device__ __forceinline__ void copy_record(fluere_record* dst, const fluere_record* src) {
-    const uint2* a = reinterpret_cast<const uint2*>(src);
-    uint2* b = reinterpret_cast<uint2*>(dst);
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(fluere_record) / 8); k++) b[k] = a[k];
+// the active records after the ended prefix, in any order (wave-aggregated append)
+__device__ __forceinline__ uint64_t active_slot(bool act, uint64_t n_ended, unsigned long long* ctr) {
+    const uint64_t m = __ballot(act);
+    if (!m) return 0;
+    const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+    unsigned long long b0 = 0;
+    if (lane == lead) b0 = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    b0 = __shfl(b0, lead, 64);
+    return n_ended + b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__global__ void __launch_bounds__(256) k_ord_place(const fluere_record* r, uint64_t n, uint64_t base, const uint32_t* bits,
-                                                   const uint32_t* pre, uint64_t n_ended, fluere_record* out,
+// Mode A: an ended record's place is the number of ended keys below its own
+__global__ void __launch_bounds__(256) k_ord_pos_a(const fluere_record* r, uint64_t n, uint64_t base, const uint32_t* bits,
+                                                   const uint32_t* pre, uint64_t n_ended, uint32_t* pos,
                                                    unsigned long long* act) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const bool live = i < n;
     const uint64_t k = live ? r[i].order_key : NONE64;
     const bool ended = k != NONE64;
-    uint64_t pos = 0;
+    uint64_t p = active_slot(live && !ended, n_ended, act);
     if (ended) {
         const uint64_t q = k - base;
-        pos = pre[q >> 5] + __popc(bits[q >> 5] & ((1u << (q & 31)) - 1u));
+        p = pre[q >> 5] + __popc(bits[q >> 5] & ((1u << (q & 31)) - 1u));
     }
-    // the active records after the ended prefix (wave-aggregated append)
-    const uint64_t m = __ballot(live && !ended);
-    if (m) {
-        const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
-        unsigned long long b0 = 0;
-        if (lane == lead) b0 = atomicAdd(act, (unsigned long long)__popcll(m));
-        b0 = __shfl(b0, lead, 64);
-        if (live && !ended)
-            pos = n_ended + b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    }
-    if (live) copy_record(out + pos, r + i);
+    if (live) pos[i] = (uint32_t)p;
 }
-// Mode B: key1 = (exp + 1 - t0) << b1 | creation index (FIN/RST closes: 0),
-// then key2 = order_key - base (active records: all ones, last)
-__global__ void __launch_bounds__(256) k_ordb_key1(const fluere_record* r, const unsigned long long* aux, uint64_t n,
-                                                   unsigned long long t0, uint64_t base, int b1,
-                                                   unsigned long long* key, uint32_t* idx) {
+// Record i to slot pos[i] (and its two order words): a wave moves its 64
+// consecutive records together, 8-byte words in index order, so every load
+// instruction reads 512 contiguous bytes and every store writes whole runs of
+// 152 bytes (a lane copying its own record strided 152 bytes per lane).
+constexpr uint32_t REC_WORDS = sizeof(fluere_record) / 8;  // 19
+__global__ void __launch_bounds__(256) k_ord_move(const fluere_record* r, const unsigned long long* aux, uint64_t n,
+                                                  const uint32_t* pos, fluere_record* out, unsigned long long* aux_out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u));  // the wave's first record
+    if (w0 >= n) return;
+    const uint32_t nr = (uint32_t)min<uint64_t>(64, n - w0);
+    const uint32_t my = lane < nr ? pos[w0 + lane] : 0u;
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(r + w0);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
+    for (uint32_t e = lane; e < nr * REC_WORDS; e += 64) {
+        const uint32_t j = e / REC_WORDS, k = e - j * REC_WORDS;
+        const uint32_t pj = __shfl(my, j, 64);
+        dst[(size_t)pj * REC_WORDS + k] = src[e];
+    }
+    if (aux && lane < nr) {
+        aux_out[2 * (size_t)my] = aux[2 * (w0 + lane)];
+        aux_out[2 * (size_t)my + 1] = aux[2 * (w0 + lane) + 1];
+    }
+}
+// Mode B: ended records per closing packet (cnt), their group's members
+// listed (mem), each one's rank among them by its order words (exp + 1 after
+// a FIN/RST close's 0, then the firing entry's creation: the BTreeMap's pop
+// order, offline_fluereflows.rs:161-175)
+__global__ void __launch_bounds__(256) k_ob_count(const fluere_record* r, uint64_t n, uint64_t base, uint32_t* cnt,
+                                                  uint32_t* gmax) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    unsigned long long k = 0;
-    if (r[i].order_key != NONE64) {
-        const unsigned long long a0 = aux[2 * i], a1 = aux[2 * i + 1];
-        k = a0 ? (((a0 - t0) << b1) | (a1 - base)) : 0ull;
+    const uint64_t k = r[i].order_key;
+    if (k == NONE64) return;
+    const uint32_t g = atomicAdd(&cnt[k - base], 1u) + 1u;
+    if (g > 1) atomicMax(gmax, g);
+}
+__global__ void __launch_bounds__(256) k_ob_fill(const fluere_record* r, uint64_t n, uint64_t base, uint32_t* cnt,
+                                                 const uint32_t* start, uint32_t* mem) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = r[i].order_key;
+    if (k == NONE64) return;
+    const uint32_t slot = atomicSub(&cnt[k - base], 1u) - 1u;
+    mem[start[k - base] + slot] = (uint32_t)i;
+}
+__global__ void __launch_bounds__(256) k_ob_rank(const fluere_record* r, const unsigned long long* aux, uint64_t n,
+                                                 uint64_t base, const uint32_t* start, const uint32_t* mem,
+                                                 uint64_t n_ended, uint32_t* pos, unsigned long long* act) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = i < n;
+    const uint64_t k = live ? r[i].order_key : NONE64;
+    const bool ended = k != NONE64;
+    uint64_t p = active_slot(live && !ended, n_ended, act);
+    if (ended) {
+        const uint32_t s0 = start[k - base], s1 = start[k - base + 1];
+        uint32_t rank = 0;
+        if (s1 - s0 > 1) {
+            const unsigned long long a0 = aux[2 * i], a1 = aux[2 * i + 1];
+            for (uint32_t q = s0; q < s1; q++) {
+                const uint32_t m = mem[q];
+                const unsigned long long b0 = aux[2 * (size_t)m], b1 = aux[2 * (size_t)m + 1];
+                rank += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && m < i)))) ? 1u : 0u;
+            }
+        }
+        p = s0 + rank;
     }
-    key[i] = k;
-    idx[i] = (uint32_t)i;
-}
-__global__ void __launch_bounds__(256) k_ordb_key2(const fluere_record* r, const uint32_t* idx, uint64_t n, uint64_t base,
-                                                   unsigned long long none, unsigned long long* key) {
-    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    const uint64_t k = r[idx[j]].order_key;
-    key[j] = k == NONE64 ? none : k - base;
-}
-__global__ void __launch_bounds__(256) k_ordb_gather(const fluere_record* r, const unsigned long long* aux,
-                                                     const uint32_t* idx, uint64_t n, fluere_record* out,
-                                                     unsigned long long* aux_out) {
-    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t i = idx[j];
-    copy_record(out + j, r + i);
-    aux_out[2 * j] = aux[2 * i];
-    aux_out[2 * j + 1] = aux[2 * i + 1];
-}
-
-static int bits_of(uint64_t v) {  // bits to hold the values 0..v
-    int b = 1;
-    while (b < 64 && (v >> b)) b++;
-    return b;
+    if (live) pos[i] = (uint32_t)p;
 }
 
 static int ord_scratch(fluere_ctx* c, size_t need) {
@@ -5387,72 +5550,77 @@ static int ord_scratch(fluere_ctx* c, size_t need) {
     return FLUERE_OK;
 }
 
+static int grow_pair(void** a, void** b, uint64_t* cap_b, uint64_t cap_a, size_t unit) {
+    if (*cap_b >= cap_a) return FLUERE_OK;
+    hipFree(*b);
+    *b = nullptr;
+    *cap_b = 0;
+    if (hipMalloc(b, cap_a * unit) != hipSuccess) return FLUERE_E_NOMEM;
+    *cap_b = cap_a;
+    (void)a;
+    return FLUERE_OK;
+}
+
 // Orders the run's n records in d_recs (n_ended of them ended) as
-// [ended][active]; Mode B with the order words in d_recaux.  Stream-ordered,
-// no host wait.  tmin / tmax: the capture's valid times (Mode B key width).
-static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint64_t tmin, uint64_t tmax) {
+// [ended][active]; Mode B with the order words in d_recaux.  Stream-ordered;
+// Mode B reads its largest group (records ending at one packet) once.
+static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b) {
     c->dev_ordered = false;
-    if (!n || !n_ended) return FLUERE_OK;
+    if (!n || !n_ended || n >= (1ull << 32)) return FLUERE_OK;
     hipStream_t s = c->stream;
     const uint64_t base = c->index_base, N = std::max<uint64_t>(c->n_total, 1);
-    if (c->d_recs2_cap < c->d_recs_cap) {
-        hipFree(c->d_recs2);
-        c->d_recs2 = nullptr;
-        c->d_recs2_cap = 0;
-        if (hipMalloc(&c->d_recs2, c->d_recs_cap * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
-        c->d_recs2_cap = c->d_recs_cap;
-    }
+    int rc = grow_pair((void**)&c->d_recs, (void**)&c->d_recs2, &c->d_recs2_cap, c->d_recs_cap, sizeof(fluere_record));
+    if (rc) return rc;
+    if (mode_b && !c->d_recaux) return FLUERE_OK;
+    if (mode_b && (rc = grow_pair((void**)&c->d_recaux, (void**)&c->d_recaux2, &c->d_recaux2_cap, c->d_recaux_cap, 16)))
+        return rc;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const unsigned gn = grid_for(n, 256);
     if (!mode_b) {
         const uint64_t nw = N / 32 + 1;
         size_t tb = 0;
         (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nw, s);
-        int rc = ord_scratch(c, 3 * al(nw * 4) + al(8) + al(tb));
-        if (rc) return rc;
+        if ((rc = ord_scratch(c, 3 * al(nw * 4) + al(8) + al(n * 4) + al(tb)))) return rc;
         char* p = (char*)c->d_ord;
         uint32_t* bits = (uint32_t*)p;
         uint32_t* pc = (uint32_t*)(p + al(nw * 4));
         uint32_t* pre = (uint32_t*)(p + 2 * al(nw * 4));
         unsigned long long* act = (unsigned long long*)(p + 3 * al(nw * 4));
-        void* tmp = p + 3 * al(nw * 4) + al(8);
+        uint32_t* pos = (uint32_t*)(p + 3 * al(nw * 4) + al(8));
+        void* tmp = p + 3 * al(nw * 4) + al(8) + al(n * 4);
         HIPCHECK(hipMemsetAsync(bits, 0, nw * 4, s));
         HIPCHECK(hipMemsetAsync(act, 0, 8, s));
-        k_ord_mark<<<(unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->n_cu * 8), 256, 0, s>>>(c->d_recs, n, base, bits);
+        k_ord_mark<<<(unsigned)std::min<uint64_t>(gn, (uint64_t)c->n_cu * 8), 256, 0, s>>>(c->d_recs, n, base, bits);
         k_ord_popc<<<grid_for(nw, 256), 256, 0, s>>>(bits, nw, pc);
         HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, pc, pre, (int)nw, s));
-        k_ord_place<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, n, base, bits, pre, n_ended, c->d_recs2, act);
+        k_ord_pos_a<<<gn, 256, 0, s>>>(c->d_recs, n, base, bits, pre, n_ended, pos, act);
+        k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, nullptr, n, pos, c->d_recs2, nullptr);
     } else {
-        if (!c->d_recaux) return FLUERE_OK;
-        const unsigned long long t0 = tmin + c->timeout_ms * 1000ull;  // exp + 1 > t0 for every sweep close
-        const int b1 = bits_of(N), b0 = bits_of(tmax >= tmin ? tmax - tmin + 2 : 2);
-        const int bk = bits_of(N);  // order_key - base < N; actives: all ones
-        if (b0 + b1 > 64) return FLUERE_OK;  // (a span past 2^40 us at 2^24 packets: the host orders them)
-        if (c->d_recaux2_cap < c->d_recaux_cap) {
-            hipFree(c->d_recaux2);
-            c->d_recaux2 = nullptr;
-            c->d_recaux2_cap = 0;
-            if (hipMalloc(&c->d_recaux2, c->d_recaux_cap * 16) != hipSuccess) return FLUERE_E_NOMEM;
-            c->d_recaux2_cap = c->d_recaux_cap;
-        }
         size_t tb = 0;
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                                 (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64, s);
-        int rc = ord_scratch(c, 2 * al(n * 8) + 3 * al(n * 4) + al(tb));
-        if (rc) return rc;
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(N + 1), s);
+        if ((rc = ord_scratch(c, 2 * al((N + 1) * 4) + 2 * al(n * 4) + al(16) + al(tb)))) return rc;
         char* p = (char*)c->d_ord;
-        unsigned long long* ka = (unsigned long long*)p;
-        unsigned long long* kb = (unsigned long long*)(p + al(n * 8));
-        uint32_t* ia = (uint32_t*)(p + 2 * al(n * 8));
-        uint32_t* ib = (uint32_t*)(p + 2 * al(n * 8) + al(n * 4));
-        uint32_t* ic = (uint32_t*)(p + 2 * al(n * 8) + 2 * al(n * 4));
-        void* tmp = p + 2 * al(n * 8) + 3 * al(n * 4);
-        k_ordb_key1<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, c->d_recaux, n, t0, base, b1, ka, ia);
-        size_t t = tb;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp, t, ka, kb, ia, ib, (int)n, 0, b0 + b1, s));
-        k_ordb_key2<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, ib, n, base, (1ull << bk) - 1, ka);
-        t = tb;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp, t, ka, kb, ib, ic, (int)n, 0, bk, s));
-        k_ordb_gather<<<grid_for(n, 256), 256, 0, s>>>(c->d_recs, c->d_recaux, ic, n, c->d_recs2, c->d_recaux2);
+        uint32_t* cnt = (uint32_t*)p;
+        uint32_t* start = (uint32_t*)(p + al((N + 1) * 4));
+        uint32_t* mem = (uint32_t*)(p + 2 * al((N + 1) * 4));
+        uint32_t* pos = (uint32_t*)(p + 2 * al((N + 1) * 4) + al(n * 4));
+        unsigned long long* act = (unsigned long long*)(p + 2 * al((N + 1) * 4) + 2 * al(n * 4));
+        uint32_t* gmax = (uint32_t*)(act + 1);
+        void* tmp = p + 2 * al((N + 1) * 4) + 2 * al(n * 4) + al(16);
+        HIPCHECK(hipMemsetAsync(cnt, 0, (N + 1) * 4, s));
+        HIPCHECK(hipMemsetAsync(act, 0, 16, s));
+        k_ob_count<<<gn, 256, 0, s>>>(c->d_recs, n, base, cnt, gmax);
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, start, (int)(N + 1), s));
+        // the largest group: a sweep that ends thousands of flows at one packet
+        // (an idle gap) would make the rank's member scans quadratic
+        unsigned long long g = 0;
+        const void* src[1] = {gmax};
+        const int by[1] = {4};
+        if ((rc = mail_fetch(c->h_mail, s, 1, src, by, &g))) return rc;
+        if (g > 1024) return FLUERE_OK;  // (fetch_records orders them on the host)
+        k_ob_fill<<<gn, 256, 0, s>>>(c->d_recs, n, base, cnt, start, mem);
+        k_ob_rank<<<gn, 256, 0, s>>>(c->d_recs, c->d_recaux, n, base, start, mem, n_ended, pos, act);
+        k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, c->d_recaux, n, pos, c->d_recs2, c->d_recaux2);
         std::swap(c->d_recaux, c->d_recaux2);
         std::swap(c->d_recaux_cap, c->d_recaux2_cap);
     }
@@ -5461,6 +5629,58 @@ static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_
     std::swap(c->d_recs_cap, c->d_recs2_cap);
     c->dev_ordered = true;
     c->dev_ordered_ended = n_ended;
+    return FLUERE_OK;
+}
+
+// The attached capture made ready for its first pass, at attach time (not in
+// live sessions, whose batches are their runs): the chunk descriptors, the
+// census (k_census), and every buffer the first pass would otherwise allocate
+// while the GPU waits, sized from the census -- the staging of the owner count
+// and hot kernel it implies, the slow list, the filter words, the record
+// buffers for its flow estimate, the exact engine's arena when TCP is present,
+// the ordering scratch.  A failed reservation is retried by the run itself.
+static int prepare_capture(fluere_ctx* c) {
+    if (c->reuse_ingest || !c->n_total) return FLUERE_OK;
+    int rc = upload_batches(c);
+    if (!rc) rc = census(c);
+    if (rc) return rc;
+    PassPlan P;
+    memset(&P, 0, sizeof P);
+    P.spill = spill_mode(c);
+    if (plan_batches(c, P) != FLUERE_OK) return FLUERE_OK;  // (stage, slow list, filter words, IPv6 ids)
+    const uint64_t N = c->n_total;
+    const bool tcp = c->last_n_complex != 0;
+    const uint64_t want = std::min<uint64_t>(c->fmax, c->last_nf + c->last_nf / 4 + (tcp ? N / 2 : 0) + 1024);
+    if (ensure_recs(c, want) != FLUERE_OK) return FLUERE_OK;
+    if (grow_pair((void**)&c->d_recs, (void**)&c->d_recs2, &c->d_recs2_cap, c->d_recs_cap, sizeof(fluere_record)))
+        return FLUERE_OK;
+    if (c->last_mode_b) {
+        if (c->d_recaux_cap < c->d_recs_cap) {
+            hipFree(c->d_recaux);
+            c->d_recaux = nullptr;
+            c->d_recaux_cap = 0;
+            if (hipMalloc(&c->d_recaux, c->d_recs_cap * 16) != hipSuccess) return FLUERE_OK;
+            c->d_recaux_cap = c->d_recs_cap;
+        }
+        if (grow_pair((void**)&c->d_recaux, (void**)&c->d_recaux2, &c->d_recaux2_cap, c->d_recaux_cap, 16))
+            return FLUERE_OK;
+    }
+    if (tcp || c->last_mode_b) {
+        const int nb = (int)c->batches.size();
+        std::vector<Batch> hb(nb);
+        for (int i = 0; i < nb; i++) hb[i] = c->batches[i].b;
+        ExactJob J{c->d_batches, hb.data(), nb, tables_of(c), c->use_mac, c->last_mode_b, c->timeout_ms * 1000ull,
+                   c->d_complex, c->d_glob, &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
+        if (exact_reserve(J, c->stream) != FLUERE_OK) return FLUERE_OK;
+    }
+    {   // order_records' scratch (Mode B's bound covers Mode A's)
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        const uint64_t n = c->d_recs_cap;
+        size_t tb = 0;
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(N + 1),
+                                               c->stream);
+        (void)ord_scratch(c, 2 * al((N + 1) * 4) + 2 * al(n * 4) + al(16) + al(tb));
+    }
     return FLUERE_OK;
 }
 
@@ -5498,6 +5718,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     if ((rc = plan_pass(c, P, true))) return rc;
     c->plan_nb = P.nb;
     c->plan_spill = P.spill;
+    c->plan_slow_all = P.nb > 0 && P.agg[0].slow_all;
     const auto t_plan = std::chrono::steady_clock::now();
     // hipGraph replay is opt-in (FLUERE_GRAPH=1): measured on MI355X / ROCm 7.2
     // it is slower than these few direct launches (C2 step 0.264 vs 0.257 ms)
@@ -5514,7 +5735,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             Q.macs = P.macs;
             Q.abl = P.abl;
             Q.spill = P.spill;
-            rc = plan_batches(c, Q);
+            rc = plan_batches(c, Q, false);
             if (!rc) rc = enqueue_batches(c, Q);
             if (rc) break;
         }
@@ -5617,6 +5838,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             if (P.phash) {
                 J.phash = c->d_phash;
                 J.phash_base = c->index_base;
+                J.emap = P.pid ? c->d_emap : nullptr;
             }
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
@@ -5631,7 +5853,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         c->dev_n_rec = n_rec;
         c->host_recs = false;
         out.complex_flows = g.n_complex;
-        if ((rc = order_records(c, n_rec, n_ended, false, g.tmin, g.tmax))) return rc;
+        if ((rc = order_records(c, n_rec, n_ended, false))) return rc;
     } else {
         // exact global state machine (the speculative Mode A results are discarded):
         // in parallel (exact.hip) when the timestamps are non-decreasing, else
@@ -5642,6 +5864,11 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 1, timeout_us, c->d_complex, c->d_glob,
                    &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
         J.mail = c->h_mail;
+        if (P.pid) {  // every valid packet's flow from the merge (AggArgs::pid)
+            J.phash = c->d_phash;
+            J.phash_base = c->index_base;
+            J.emap = c->d_emap;
+        }
         J.recaux = &c->d_recaux;  // the records' order words (fetch_records orders by them)
         J.recaux_cap = &c->d_recaux_cap;
         ExactResult er{};
@@ -5658,7 +5885,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             c->dev_n_rec = n_rec;
             c->host_recs = false;
             out.sequential_mode = 1;
-            if (c->has_aux && (rc = order_records(c, n_rec, n_ended, true, g.tmin, g.tmax))) return rc;
+            if (c->has_aux && (rc = order_records(c, n_rec, n_ended, true))) return rc;
         } else {
         uint64_t N = c->n_total;
         SeqMeta* meta = nullptr;

@@ -145,7 +145,8 @@ extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, i
     o.use_mac = use_mac;
     // flow capacity from the file size (a record is at least 16 bytes; flows
     // rarely exceed one per 64 bytes of capture).  The reference's HashMap has
-    // no limit: a capture with more flows reopens with twice the capacity.
+    // no limit: the first pass grows the context to its census's estimate, and
+    // a capture with still more flows reopens with twice the capacity.
     o.max_flows = std::max<uint64_t>(1 << 16, std::min<uint64_t>((uint64_t)sb.st_size / 64, 1 << 22));
     fluere_ctx* c = nullptr;
     fluere_stats st{};
@@ -155,7 +156,7 @@ extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, i
         if (rc) return rc;
         rc = fluere_add_pcap_file(c, pcap_path);
         if (!rc) rc = fluere_run(c, &st);
-        if (rc != FLUERE_E_TABLE_FULL || o.max_flows >= (1ull << 23)) break;
+        if (rc != FLUERE_E_TABLE_FULL || o.max_flows >= (1ull << 26)) break;  // (MAX_FLOWS)
         fluere_close(c);
         c = nullptr;
         o.max_flows *= 2;

@@ -211,6 +211,29 @@ def test_phash_filter_realistic_tcp(gpu, spill, t, mutate, monkeypatch):
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp phash spill={spill} t={t} mutate={mutate}")
 
 
+@pytest.mark.parametrize("pid", ["0", "1"])
+@pytest.mark.parametrize("t", [600000, 1000])
+@pytest.mark.parametrize("cap", [None, "3"])
+def test_merge_flow_words_realistic_tcp(gpu, pid, t, cap, monkeypatch):
+    """The merge's per-packet flows (FLUERE_PID=1, k_parse_spill): every
+    resolved packet's filter word becomes its dense id or merge entry (the
+    lean spill path, the global path, the overflow list and the general
+    parser's list in the merge tail -- with 3-record owner segments most
+    records take the overflow list), so k_ex_meta replays Mode A's complex
+    flows and Mode B's every packet without a dictionary walk.  A capture
+    with mutated headers inside TCP flows (drops, slow classes) equals the
+    oracle either way."""
+    monkeypatch.setenv("FLUERE_PID", pid)
+    monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
+    if cap:
+        monkeypatch.setenv("FLUERE_OWNER_CAP", cap)
+    data = _mutated_pcap(fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 1_000_000, 10_000, 0xF10E0057)),
+                         13, 1)
+    want = pyoracle.offline(data, t)
+    csv, ne, st = _gpu_csv(data, t, max_flows=1 << 20)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp pid={pid} t={t} cap={cap}")
+
+
 def test_phash_chosen_on_rerun(gpu):
     """A context whose last run replayed complex flows in Mode A writes the
     filter words on the next runs (the prediction); every run equals the oracle."""
@@ -244,7 +267,7 @@ CENSUS = {
     "c2_small": (_lib.SYNTH_UDP64, 300_000, 1000, 0xF10E0002, False, 600000, "k_parse_agg"),
     "tcp_2m": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007, False, 600000, "k_parse_spill"),
     "tcp_2m_t1": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007, False, 1000, "k_parse_spill"),
-    "slow_2m": (_lib.SYNTH_SLOW, 2_000_000, 10_000, 0xF10E0008, False, 600000, None),
+    "slow_2m": (_lib.SYNTH_SLOW, 2_000_000, 10_000, 0xF10E0008, False, 600000, "k_slow"),
     "c5u_mac": (_lib.SYNTH_MAC64, 1_000_000, 50_000, 0xF10E0005, True, 600000, "k_parse_agg"),
 }
 
@@ -277,6 +300,30 @@ def test_census_predicts_first_run(gpu, name):
         assert kernel == hot, (kernel, cen)
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg), t, use_mac=use_mac)
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"census {name}")
+
+
+@pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small", "c5u_mac_small",
+                                  "many_flows"])
+@pytest.mark.parametrize("cap", [None, "3"])
+def test_slow_kernel_takes_every_packet(gpu, name, cap, monkeypatch):
+    """k_slow over every packet without a hot kernel (FLUERE_SLOW_ALL=1; chosen
+    when nearly every packet is of the general parser's classes): the register
+    parsers, parse_mid and the general parser's list cover the fast classes
+    too, so any capture equals the oracle; with 3-record segments most records
+    take the overflow list."""
+    monkeypatch.setenv("FLUERE_SLOW_ALL", "1")
+    if cap:
+        monkeypatch.setenv("FLUERE_OWNER_CAP", cap)
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=use_mac)
+    with fluere_amd.FlowContext(use_mac=use_mac, max_flows=max(1 << 16, 2 * f)) as ctx:
+        ctx.add_host_pcap(data)
+        st = ctx.run()
+        assert ctx.last_hot_kernel() == "k_slow"
+        recs, ne = ctx.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"slow-all {name}")
+    assert st["packets"] == n
 
 
 @pytest.mark.parametrize("name", ["slow_small", "slow_many_flows", "slow_mac", "c3_imix_small"])
@@ -714,6 +761,27 @@ def test_offline_file_grows_flow_table(gpu, tmp_path):
     got = (tmp_path / "o" / "many_converted.csv").read_text()
     assert st["records"] == n
     assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "offline_file many flows")
+
+
+def test_offline_file_ten_million_flows(gpu, tmp_path):
+    """More flows than the narrow dictionary holds (2^24 slots per table, ~8M
+    flows): a 14M-packet capture with ~10.7M distinct 5-tuples through the
+    drop-in seam.  fluere_offline_file opens with 4M flows (file size); the
+    census of the attached capture grows the context to its estimate (tables
+    of 2^25 slots: the wide IPv4 chain, flow_table.h v4_t1_word) before the
+    first pass, and the CSV equals the oracle's (the reference's HashMap has
+    no bound, offline_fluereflows.rs:61)."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_UDP64, 14_000_000, 25_000_000, 0xF10E00A1)
+    data = fluere_amd.synth_pcap(cfg)
+    path = tmp_path / "big.pcap"
+    path.write_bytes(data)
+    st = fluere_amd.fluereflow_fileparse(fluere_amd.Args(fluere_amd.Files(file=str(path))), out_dir=str(tmp_path / "o"))
+    assert st["records"] > 10_000_000, st
+    got = (tmp_path / "o" / "big_converted.csv").read_text()
+    want = pyoracle.offline(data)
+    del data
+    assert want["n"] == st["records"]
+    assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "offline_file 10M flows")
 
 
 # ---- realistic TCP (FLUERE_SYNTH_TCP): the exact state machine at scale

@@ -45,6 +45,10 @@ for st in "$@"; do
       c=${st#trace:}
       bash tools/trace.sh $TAG $c
       cp gpurun_out/trace_${TAG}_$c/timeline.txt "$O/timeline_$c.txt" ;;
+    vtrace:*)  # vtrace:<variant>:<config>: the kernel timeline of a variant build (tools/variants.sh)
+      v=${st#vtrace:}; c=${v#*:}; v=${v%%:*}
+      FLUERE_LIB=$R/fluere_amd/variants/libfluere_gpu_$v.so bash tools/trace.sh ${v} $c
+      cp gpurun_out/trace_${v}_$c/timeline.txt "$O/timeline_${v}_$c.txt" ;;
     debug:*)
       c=${st#debug:}
       FLUERE_DEBUG=1 timeout -k 10 240 python -u bench.py --config $c --no-cpu-baseline --no-imix --steps 2 --warmup 1 > "$O/debug_$c.log" 2>&1
