@@ -131,7 +131,7 @@ def measure(name, args, world, rank, local, stream, torch, dist, fluere_amd, fdi
     # the one-shot seam (`fluere offline` converts a capture once): a fresh
     # context on the same resident batches, its first run timed on the host
     # (the census, every allocation and choice the first run makes included)
-    cold = cold_run(fluere_amd, batches, C, max_flows, local) if world == 1 else {}
+    cold = cold_run(fluere_amd, batches, C, max_flows, local) if world == 1 and not args.no_cold else {}
 
     # records of the whole job: every rank holds its own flows' records
     recs, ne = ctx.records()
@@ -177,6 +177,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-imix", action="store_true", help="default line without its IMIX (c3) object")
+    ap.add_argument("--no-cold", action="store_true", help="skip the one-shot (fresh context) run")
     args = ap.parse_args()
 
     import torch

@@ -335,11 +335,10 @@ __device__ __forceinline__ uint32_t dense_of_key(const TableSet& T, const CKey& 
     int ft;
     unsigned long long v = EMPTY;
     if (!v6 && !macs && v4_fast(T, k.w[9] & 0xFF)) {
-        s = tab_slot(T, 0, ((uint64_t)k.w[0] << 32) | k.w[4], insert);
-        if (s == FAIL) return FAIL;
-        chain[0] = s;
-        s = tab_slot(T, 1, v4_t1_word(T, s, k.w[8], k.w[9] & 0xFF), insert, &v);
-        if (s == FAIL) return FAIL;
+        uint32_t s0;
+        v4_slots(T, k.w[0], k.w[4], k.w[8], k.w[9] & 0xFF, insert, s0, s, &v);
+        if (s0 == FAIL || s == FAIL) return FAIL;
+        chain[0] = s0;
         chain[1] = s;
         ft = 1;
     } else {

@@ -156,8 +156,16 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
             const uint64_t li = base + s_c[i];
             const uint32_t wd = words ? phash[li] : PH_PARSE;
             const bool known = emap && wd != PH_PARSE && (wd & (PH_ID | PH_EREF));
+            // the register parser first (an 80-byte window), the general one
+            // only for the classes it declines
             Parsed P;
-            parse_record(B, li, macs != 0, 0, P);
+            {
+                const uint32_t off = B.offs[li];
+                Win W;
+                load_win(B, off, W);
+                parse_loaded_fast(B, off, W, macs != 0, P);
+            }
+            if (P.cls == 2) parse_record(B, li, macs != 0, 0, P);
             if (P.cls == 0) {
                 uint8_t dir;
                 uint32_t d;

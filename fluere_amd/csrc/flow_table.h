@@ -10,6 +10,8 @@
 //
 //   IPv4, no MAC:  T0[(lo_ip << 32) | hi_ip]                      -> s0
 //                  T1[(s0 << 40) | (lo_port << 24) | (hi_port << 8) | proto] -> s1 -> dense id
+//                  (T1's probe starts at a hash of the whole key, so both
+//                  tables' first probes travel together: v4_slots)
 //                  (tables of more than 2^24 slots, "wide": T1[(s0 << 33) |
 //                  (ports << 1) | udp] for TCP and UDP, every other protocol
 //                  through the generic chain -- v4_t1_word)
@@ -59,12 +61,13 @@ struct TableSet {
 // Each probe loads the whole 16-byte entry {key, val}; *val_out receives the
 // value word seen with the matching key (possibly stale: EMPTY/PENDING), so a
 // final-level lookup of a published flow costs one round trip.
-__device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t w, bool insert,
-                                            unsigned long long* val_out = nullptr) {
+// h0: the probe's first slot (tab_slot: the word's own hash).
+__device__ __forceinline__ uint32_t tab_slot_at(const TableSet& T, int t, uint64_t w, uint32_t h0, bool insert,
+                                               unsigned long long* val_out = nullptr) {
     unsigned long long* tab = T.tab[t];
     if (val_out) *val_out = EMPTY;
     if (w == EMPTY) return T.C;  // the sentinel word has a dedicated slot
-    uint32_t h = (uint32_t)mix64(w) & (T.C - 1);
+    uint32_t h = h0 & (T.C - 1);
     for (int p = 0; p < MAX_PROBE; p++) {
         const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&tab[2 * h]);
         if (e.x == w) {
@@ -81,6 +84,10 @@ __device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t 
     atomicOr(T.err, ERR_TABLE_FULL);
     return FAIL;
 }
+__device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t w, bool insert,
+                                            unsigned long long* val_out = nullptr) {
+    return tab_slot_at(T, t, w, (uint32_t)mix64(w), insert, val_out);
+}
 
 // The IPv4 fast chain's second-level word.  Tables of up to 2^24 slots keep
 // s0 in 24 bits beside the ports and the protocol; wider tables ("wide", more
@@ -93,6 +100,32 @@ __device__ __forceinline__ bool v4_fast(const TableSet& T, uint32_t proto) {
 __device__ __forceinline__ uint64_t v4_t1_word(const TableSet& T, uint32_t s0, uint32_t ports, uint32_t proto) {
     return T.C <= (1u << 24) ? ((uint64_t)s0 << 40) | ((uint64_t)ports << 8) | proto
                              : ((uint64_t)s0 << 33) | ((uint64_t)ports << 1) | (proto == 17u ? 1u : 0u);
+}
+
+// The IPv4 fast chain in one round trip: T1's probe starts at a hash of the
+// whole key (lo_ip, hi_ip, ports, proto), not of its word, which holds T0's
+// slot s0 -- so the first probes of both tables are in flight together, and
+// T1's word is compared once s0 is known.  (The word still decides: a slot
+// holds exactly one word, and a key always starts its probe at one place.)
+__device__ __forceinline__ uint32_t v4_t1_start(uint32_t lo, uint32_t hi, uint32_t ports, uint32_t proto) {
+    return (uint32_t)mix64((((uint64_t)lo << 32) | hi) ^ mix64(((uint64_t)ports << 8) | proto | (1ull << 48)));
+}
+__device__ __forceinline__ void v4_slots(const TableSet& T, uint32_t lo, uint32_t hi, uint32_t ports, uint32_t proto,
+                                         bool insert, uint32_t& s0, uint32_t& s1, unsigned long long* v) {
+    const uint64_t w0 = ((uint64_t)lo << 32) | hi;
+    const uint32_t h1 = v4_t1_start(lo, hi, ports, proto) & (T.C - 1);
+    const ulonglong2 e1 = *reinterpret_cast<const ulonglong2*>(&T.tab[1][2 * h1]);  // (in flight with T0's probe)
+    s1 = FAIL;
+    *v = EMPTY;
+    s0 = tab_slot(T, 0, w0, insert);
+    if (s0 == FAIL) return;
+    const uint64_t w1 = v4_t1_word(T, s0, ports, proto);
+    if (w1 != EMPTY && e1.x == w1) {  // the first probe hit
+        s1 = h1;
+        *v = e1.y;
+        return;
+    }
+    s1 = tab_slot_at(T, 1, w1, h1, insert, v);
 }
 
 // Canonical key: 14 little-endian u32 words (also fluere_flow_summary.key):

@@ -117,6 +117,8 @@ struct Stage {
                                   // stores; k_merge_partials sums them: no contended atomics at the end)
     uint32_t W;                   // sets per workgroup
     uint32_t O;                   // merge owners (k_merge_partials workgroups)
+    uint32_t no_parts;            // the hot pass staged no partials (k_parse_spill, or k_slow alone): the merge
+                                  // reads the owner segments only
     uint32_t n_sets;              // sets: the hot kernel's n_hot, then k_slow's (when it runs)
     uint32_t n_wg;                // hot-kernel workgroups
     uint32_t n_hot;               // the hot kernel's sets (n_wg * W)
@@ -1502,6 +1504,12 @@ __device__ __forceinline__ uint32_t staged_id(const TableSet& T, const V6Map& M,
 constexpr int MB = 1024;   // merge kernel block
 constexpr int MT = 1024;   // merge table entries (120 B each)
 constexpr int MCH = 1024;  // sets per scan chunk
+#ifndef FLUERE_MERGE_NOPART
+#define FLUERE_MERGE_NOPART 0  // diagnostics only (wrong results with partials): the spill path's code alone
+#endif
+#ifndef FLUERE_MERGE_TAIL
+#define FLUERE_MERGE_TAIL 1  // diagnostics only (0: no tail, wrong results): the register cost of the tail
+#endif
 #ifndef FLUERE_MERGE_ABL
 #define FLUERE_MERGE_ABL 0  // diagnostics only (wrong results): 1 records loaded, no table; 2 probe, no updates
 #endif
@@ -1659,9 +1667,12 @@ __device__ __forceinline__ void finalize_emit(EmitLds& S, const FinArgs& a, cons
     }
 }
 
+// (MACS: a run with MAC keys -- the entries' MAC sidecars; a kernel of its own
+// so the 5-tuple runs keep 16 KiB of LDS and none of the MAC paths' code)
+template <bool MACS>
 __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint4 m_key[MT];
-    __shared__ uint4 m_kx[MT];  // MAC runs: the MAC sidecar of each entry (w = 1 once written)
+    __shared__ uint4 m_kx[MACS ? MT : 1];  // MAC runs: the MAC sidecar of each entry (w = 1 once written)
     __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
     __shared__ unsigned long long m_by[2][MT], m_fa[MT], m_fc[MT], m_fr[MT], m_la[MT];
     __shared__ uint32_t m_nclaim, m_base;
@@ -1670,6 +1681,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // and the window's first packet (relative to the batch): a record's
     // loads then depend on LDS reads only
     __shared__ uint32_t m_lo[MCH], m_start[MCH], m_wb[MCH], m_scan[MB / 64 + 1];
+    // per group of 64 flattened indices: the set holding its first index (the
+    // spill records' wave-uniform search, one LDS read instead of a binary search)
+    constexpr uint32_t MGRP = 2048;
+    __shared__ uint16_t m_grp[MGRP];
     const int tid = threadIdx.x;
     const unsigned long long c0 = clock64();
     if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 0] = wall_clock64();
@@ -1678,7 +1693,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_dspill_all = __hip_atomic_load(&a.g->n_dspill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool macs = a.macs != 0;
+    constexpr bool macs = MACS;
     const Stage& S = a.S;
     auto reduce_stats = [&]() {
         // the hot kernel's per-workgroup statistics -> the run counters (one wave)
@@ -1715,20 +1730,23 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     __shared__ uint32_t s_me;
     if (tid == 0) s_me = blockIdx.x;
     __syncthreads();
+    const int pass0 = S.no_parts ? 1 : 0;  // (no partials: the segments' pass alone)
     for (uint32_t me = s_me; me < S.O; me = s_me) {
+        // the first chunk's bounds, loaded before the LDS initialisation
+        // (partials: their offsets; no partials: the segments' counts)
         uint32_t pre_lo[MCH / MB], pre_hi[MCH / MB];
         unsigned long long pre_wb[MCH / MB];
     #pragma unroll
         for (int q = 0; q < MCH / MB; q++) {
             const uint32_t set = tid * (MCH / MB) + q;
             const bool in = set < a.S.n_sets;
-            pre_lo[q] = in ? a.S.off[(size_t)me * a.S.n_sets + set] : 0;
-            pre_hi[q] = in ? a.S.off[(size_t)(me + 1) * a.S.n_sets + set] : 0;
+            pre_lo[q] = in && !pass0 ? a.S.off[(size_t)me * a.S.n_sets + set] : 0;
+            pre_hi[q] = !in ? 0 : pass0 ? a.S.soff[(size_t)me * a.S.n_sets + set] : a.S.off[(size_t)(me + 1) * a.S.n_sets + set];
             pre_wb[q] = in ? a.S.base[set] : 0;
         }
         for (int e = tid; e < MT; e += MB) {
             m_key[e] = make_uint4(0, 0, 0, 0);
-            m_kx[e] = make_uint4(0, 0, 0, 0);
+            if (MACS) m_kx[e] = make_uint4(0, 0, 0, 0);
             m_pk[0][e] = m_pk[1][e] = 0;
             m_by[0][e] = m_by[1][e] = 0;
             m_mn[0][e] = m_mn[1][e] = NONE32;
@@ -1748,7 +1766,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
         // owner's segments (each a one-packet partial), through the same
         // machinery; the overflow list is the tail's.
         const int passes = n_dspill_all ? 2 : 1;  // no spills: one pass
-        for (int pass = 0; pass < passes; pass++)
+        for (int pass = FLUERE_MERGE_NOPART ? 1 : pass0; pass < passes; pass++)
         for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
             const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
             const uint32_t* offs = pass ? S.soff : S.off;
@@ -1758,7 +1776,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 const uint32_t set = c0s + tid * (MCH / MB) + q;
                 uint32_t lo = 0, hi = 0;
                 unsigned long long wb = 0, rb = 0;
-                if (pass == 0 && c0s == 0) {  // prefetched
+                if (pass == pass0 && c0s == 0) {  // prefetched
                     lo = pre_lo[q];
                     hi = pre_hi[q];
                     wb = pre_wb[q];
@@ -1776,13 +1794,17 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 tot += len[q];
             }
             uint32_t run = block_exclusive_scan(tot, m_scan) ;
+            const uint32_t total = m_scan[MB / 64];  // (block_exclusive_scan ends with a barrier)
+            const bool grp = pass == 1 && total <= 64u * MGRP;
     #pragma unroll
             for (int q = 0; q < MCH / MB; q++) {
                 m_start[tid * (MCH / MB) + q] = run;
+                if (grp && len[q])
+                    for (uint32_t g = (run + 63) >> 6; g <= (run + len[q] - 1) >> 6; g++)
+                        m_grp[g] = (uint16_t)(tid * (MCH / MB) + q);
                 run += len[q];
             }
             __syncthreads();
-            const uint32_t total = m_scan[MB / 64];
             if (a.dbg && tid == 0 && c0s == 0 && pass == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 2] = wall_clock64();
             // one record (a staged partial or a spilled packet): find or claim
             // its merge entry, then the update (or the global path)
@@ -1796,7 +1818,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                             const uint4 kk = m_key[e];
                             bool xm = true;
                             if (macs) {  // MAC words
-                                const uint4 xx = m_kx[e];
+                                const uint4 xx = m_kx[MACS ? e : 0];
                                 xm = xx.w == 1u && xx.x == x0 && xx.y == x1 && xx.z == x2;
                             }
                             if (kk.w & LT_READY) {
@@ -1807,7 +1829,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                                 m_key[e].x = k0;
                                 m_key[e].y = k1;
                                 m_key[e].z = k2;
-                                if (macs) m_kx[e] = make_uint4(x0, x1, x2, 1u);
+                                if (MACS) m_kx[e] = make_uint4(x0, x1, x2, 1u);
                                 __threadfence_block();
                                 atomicExch(&m_key[e].w, tag | LT_READY);
                                 state = 1;
@@ -1868,10 +1890,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 for (uint32_t idx = tid; idx < total; idx += MB) {
                     const uint32_t iw = __builtin_amdgcn_readfirstlane(idx);  // the wave's smallest index
                     uint32_t lo_i = 0, hi_i = nset - 1;
-                    while (lo_i < hi_i) {
-                        const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-                        if (m_start[mid] <= iw) lo_i = mid;
-                        else hi_i = mid - 1;
+                    if (grp) {
+                        lo_i = m_grp[iw >> 6];  // (iw is a multiple of 64: lane 0's index)
+                    } else {
+                        while (lo_i < hi_i) {
+                            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                            if (m_start[mid] <= iw) lo_i = mid;
+                            else hi_i = mid - 1;
+                        }
                     }
                     while (lo_i + 1 < nset && m_start[lo_i + 1] <= idx) lo_i++;
                     const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
@@ -1936,6 +1962,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 __syncthreads();
                 continue;
             }
+            if (FLUERE_MERGE_NOPART) continue;
             for (uint32_t idx = tid; idx < total; idx += MB) {
                 uint32_t lo_i = 0, hi_i = nset - 1;  // last set with start <= idx
                 while (lo_i < hi_i) {
@@ -2003,7 +2030,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             } else if (tag == 0xFF000000u) {
                 d = kk.x;  // MAC kernels' partials carry dense ids
             } else if (macs) {  // a spilled MAC-kernel key: one dictionary walk per flow and owner
-                const uint4 xx = m_kx[e];
+                const uint4 xx = m_kx[MACS ? e : 0];
                 CKey ck;
                 mac_ckey(kk.x, kk.y, kk.z, tag, xx.x, xx.y, xx.z, ck);
                 d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
@@ -2011,8 +2038,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 d = staged_id(a.T, a.v6, kk.x, kk.y, kk.z, tag, a.A.slots);
             } else {       // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
                 unsigned long long v = EMPTY;
-                s0 = tab_slot(a.T, 0, ((uint64_t)kk.x << 32) | kk.y, true);
-                if (s0 != FAIL) s1 = tab_slot(a.T, 1, v4_t1_word(a.T, s0, kk.z, tag >> 24), true, &v);
+                v4_slots(a.T, kk.x, kk.y, kk.z, tag >> 24, true, s0, s1, &v);
                 if (s1 != FAIL) {
                     val = &a.T.tab[1][2 * s1 + 1];
                     if (v >= PENDING) v = atomicCAS(val, EMPTY, PENDING);
@@ -2093,7 +2119,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     const unsigned long long n_gen_all =
         a.slow_kernel ? __hip_atomic_load(&a.g->n_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     const bool tail_slow = a.slow_kernel ? n_gen_all != 0 : n_slow_all != 0;
-    if (tail_slow || n_spill_all) {
+    if (FLUERE_MERGE_TAIL && (tail_slow || n_spill_all)) {
         // The tail: the overflow list (spills past their owner segment's
         // capacity: full keys, no parse) and the packets for the general
         // parser: the whole slow list (packets the hot kernel left over: IPv6,
@@ -4936,7 +4962,8 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     // k_slow over every packet, no hot kernel, when (nearly) every packet is of
     // the general parser's classes: the hot pass would only read each window
     // to list it for k_slow's second read (the slow config: 0.35 of 1.47 ms)
-    static const int sa_env = getenv("FLUERE_SLOW_ALL") ? atoi(getenv("FLUERE_SLOW_ALL")) : -1;  // tests / A/B
+    // (tests set these between runs: read per plan, not cached)
+    const int sa_env = getenv("FLUERE_SLOW_ALL") ? atoi(getenv("FLUERE_SLOW_ALL")) : -1;  // tests / A/B
     const bool slow_all =
         sa_env >= 0 ? sa_env != 0 : (c->n_total > 0 && (uint64_t)c->last_n_slow * 4 >= (uint64_t)c->n_total * 3);
     if (slow_all) a.slow_kernel = 1;
@@ -4962,7 +4989,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     // per-packet filter words for the exact engine when the last run replayed
     // complex flows in Mode A (a prediction: without them k_ex_meta parses
     // every packet; 4 bytes per packet written by the hot pass)
-    static const int phash_env = getenv("FLUERE_PHASH") ? atoi(getenv("FLUERE_PHASH")) : -1;  // tests / A/B
+    const int phash_env = getenv("FLUERE_PHASH") ? atoi(getenv("FLUERE_PHASH")) : -1;  // tests / A/B
     P.phash = !c->use_mac && (phash_env >= 0 ? phash_env : (c->last_n_complex > 0 && !c->last_mode_b)) ? 1 : 0;
     // k_parse_spill runs (every valid packet a record the merge resolves) that
     // will replay packets (complex flows in Mode A, or Mode B): the merge
@@ -4971,7 +4998,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     {
         int nbat = 0;
         for (auto& hb : c->batches) nbat += hb.b.n ? 1 : 0;
-        static const int pid_env = getenv("FLUERE_PID") ? atoi(getenv("FLUERE_PID")) : -1;  // tests / A/B
+        const int pid_env = getenv("FLUERE_PID") ? atoi(getenv("FLUERE_PID")) : -1;  // tests / A/B
         const bool want = pid_env >= 0 ? pid_env != 0 : (c->last_n_complex > 0 || c->last_mode_b);
         P.pid = (allow_pid && P.spill && !c->use_mac && nbat <= PLAN_BATCHES && want) ? 1 : 0;
         if (P.pid) P.phash = 1;
@@ -5055,6 +5082,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         S.O = O;
         S.n_hot = (uint32_t)sets;
         S.n_sets = (uint32_t)all;
+        S.no_parts = (P.spill || slow_all) && !c->use_mac ? 1u : 0u;
         if (P.nb < PLAN_BATCHES) {
             P.agg[P.nb] = ab;
             P.agg_grid[P.nb] = grid;
@@ -5168,7 +5196,8 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
             }
         }
         // at most one merge workgroup per CU, each taking owners in turn
-        k_merge_partials<<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow took it)
+        if (P.macs) k_merge_partials<true><<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);
+        else k_merge_partials<false><<<std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, 0, s>>>(a);  // + the slow list (unless k_slow took it)
         if (hostprof) {
             const auto t2 = std::chrono::steady_clock::now();
             auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
@@ -5267,7 +5296,8 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
         }
         if (P.agg[i].slow_kernel) kernel((const void*)k_slow, P.slow_grid[i], SB, a_agg[i]);
         if (!P.agg_grid[i]) event(c->evk1);
-        kernel((const void*)k_merge_partials, std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, a_agg[i]);
+        kernel(P.macs ? (const void*)k_merge_partials<true> : (const void*)k_merge_partials<false>,
+               std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu), MB, a_agg[i]);
     }
     void* a_fin[] = {&P.fa};
     if (P.finalize) {
@@ -5435,96 +5465,84 @@ extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
 //    stable radix sorts by the packed order words, then by order_key, and a
 //    gather of the records and their words.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ord_mark(const fluere_record* r, uint64_t n, uint64_t base, uint32_t* bits) {
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t k = r[i].order_key;
-        if (k != NONE64) atomicOr(&bits[(k - base) >> 5], 1u << ((k - base) & 31));
+// pass 1: every record's order_key into a compact array (one strided read
+// of the 152-byte records), the ended ones marked (Mode A: one bit per
+// packet; Mode B: a count per closing packet and the largest group), and the
+// active records counted per block of 256 (their places follow the ended
+// prefix in record order: a scan of the block counts, no shared counter)
+__global__ void __launch_bounds__(256) k_ord_keys(const fluere_record* r, uint64_t n, uint64_t base, int mode_b,
+                                                  unsigned long long* okey, uint32_t* bits, uint32_t* cnt,
+                                                  uint32_t* gmax, uint32_t* blk_act) {
+    __shared__ uint32_t s_act;
+    if (threadIdx.x == 0) s_act = 0;
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = i < n;
+    const uint64_t k = live ? r[i].order_key : NONE64;
+    if (live) okey[i] = k;
+    const bool ended = k != NONE64;
+    if (ended) {
+        if (!mode_b) {
+            atomicOr(&bits[(k - base) >> 5], 1u << ((k - base) & 31));
+        } else {
+            const uint32_t g = atomicAdd(&cnt[k - base], 1u) + 1u;
+            if (g > 1) atomicMax(gmax, g);
+        }
     }
+    const uint64_t am = __ballot(live && !ended);
+    if ((threadIdx.x & 63) == 0 && am) atomicAdd(&s_act, (uint32_t)__popcll(am));
+    __syncthreads();
+    if (threadIdx.x == 0) blk_act[blockIdx.x] = s_act;
 }
 __global__ void __launch_bounds__(256) k_ord_popc(const uint32_t* bits, uint64_t nw, uint32_t* pc) {
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w < nw) pc[w] = __popc(bits[w]);
 }
-// the active records after the ended prefix, in any order (wave-aggregated append)
-__device__ __forceinline__ uint64_t active_slot(bool act, uint64_t n_ended, unsigned long long* ctr) {
-    const uint64_t m = __ballot(act);
-    if (!m) return 0;
-    const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
-    unsigned long long b0 = 0;
-    if (lane == lead) b0 = atomicAdd(ctr, (unsigned long long)__popcll(m));
-    b0 = __shfl(b0, lead, 64);
-    return n_ended + b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-// Mode A: an ended record's place is the number of ended keys below its own
-__global__ void __launch_bounds__(256) k_ord_pos_a(const fluere_record* r, uint64_t n, uint64_t base, const uint32_t* bits,
-                                                   const uint32_t* pre, uint64_t n_ended, uint32_t* pos,
-                                                   unsigned long long* act) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool live = i < n;
-    const uint64_t k = live ? r[i].order_key : NONE64;
-    const bool ended = k != NONE64;
-    uint64_t p = active_slot(live && !ended, n_ended, act);
-    if (ended) {
-        const uint64_t q = k - base;
-        p = pre[q >> 5] + __popc(bits[q >> 5] & ((1u << (q & 31)) - 1u));
-    }
-    if (live) pos[i] = (uint32_t)p;
-}
-// Record i to slot pos[i] (and its two order words): a wave moves its 64
-// consecutive records together, 8-byte words in index order, so every load
-// instruction reads 512 contiguous bytes and every store writes whole runs of
-// 152 bytes (a lane copying its own record strided 152 bytes per lane).
-constexpr uint32_t REC_WORDS = sizeof(fluere_record) / 8;  // 19
-__global__ void __launch_bounds__(256) k_ord_move(const fluere_record* r, const unsigned long long* aux, uint64_t n,
-                                                  const uint32_t* pos, fluere_record* out, unsigned long long* aux_out) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u));  // the wave's first record
-    if (w0 >= n) return;
-    const uint32_t nr = (uint32_t)min<uint64_t>(64, n - w0);
-    const uint32_t my = lane < nr ? pos[w0 + lane] : 0u;
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(r + w0);
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
-    for (uint32_t e = lane; e < nr * REC_WORDS; e += 64) {
-        const uint32_t j = e / REC_WORDS, k = e - j * REC_WORDS;
-        const uint32_t pj = __shfl(my, j, 64);
-        dst[(size_t)pj * REC_WORDS + k] = src[e];
-    }
-    if (aux && lane < nr) {
-        aux_out[2 * (size_t)my] = aux[2 * (w0 + lane)];
-        aux_out[2 * (size_t)my + 1] = aux[2 * (w0 + lane) + 1];
-    }
-}
-// Mode B: ended records per closing packet (cnt), their group's members
-// listed (mem), each one's rank among them by its order words (exp + 1 after
-// a FIN/RST close's 0, then the firing entry's creation: the BTreeMap's pop
-// order, offline_fluereflows.rs:161-175)
-__global__ void __launch_bounds__(256) k_ob_count(const fluere_record* r, uint64_t n, uint64_t base, uint32_t* cnt,
-                                                  uint32_t* gmax) {
+// Mode B: each closing packet's group members listed (mem[start[k] ..])
+__global__ void __launch_bounds__(256) k_ob_fill(const unsigned long long* okey, uint64_t n, uint64_t base,
+                                                 uint32_t* cnt, const uint32_t* start, uint32_t* mem) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const uint64_t k = r[i].order_key;
-    if (k == NONE64) return;
-    const uint32_t g = atomicAdd(&cnt[k - base], 1u) + 1u;
-    if (g > 1) atomicMax(gmax, g);
-}
-__global__ void __launch_bounds__(256) k_ob_fill(const fluere_record* r, uint64_t n, uint64_t base, uint32_t* cnt,
-                                                 const uint32_t* start, uint32_t* mem) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t k = r[i].order_key;
+    const uint64_t k = okey[i];
     if (k == NONE64) return;
     const uint32_t slot = atomicSub(&cnt[k - base], 1u) - 1u;
     mem[start[k - base] + slot] = (uint32_t)i;
 }
-__global__ void __launch_bounds__(256) k_ob_rank(const fluere_record* r, const unsigned long long* aux, uint64_t n,
-                                                 uint64_t base, const uint32_t* start, const uint32_t* mem,
-                                                 uint64_t n_ended, uint32_t* pos, unsigned long long* act) {
+// pass 2: each record's place, then the records (and Mode B's order words)
+// moved there.  An ended record: Mode A, the ended keys below its own (bit
+// rank); Mode B, its group's start plus its rank among the group by order
+// words (exp + 1 after a FIN/RST close's 0, then the firing entry's creation:
+// the BTreeMap's pop order, offline_fluereflows.rs:161-175).  An active
+// record: after the ended prefix, in record order.  A wave moves its 64
+// consecutive records together, 8-byte words in index order: every load
+// instruction reads 512 contiguous bytes, every store writes whole 152-byte
+// runs (a lane copying its own record, strided 152 bytes per lane, does not).
+constexpr uint32_t REC_WORDS = sizeof(fluere_record) / 8;  // 19
+__global__ void __launch_bounds__(256) k_ord_move(const fluere_record* r, const unsigned long long* aux, uint64_t n,
+                                                  uint64_t base, const unsigned long long* okey, const uint32_t* bits,
+                                                  const uint32_t* pre, const uint32_t* start, const uint32_t* mem,
+                                                  const uint32_t* blk_pre, uint64_t n_ended, fluere_record* out,
+                                                  unsigned long long* aux_out) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const bool live = i < n;
-    const uint64_t k = live ? r[i].order_key : NONE64;
+    const uint64_t k = live ? okey[i] : NONE64;
     const bool ended = k != NONE64;
-    uint64_t p = active_slot(live && !ended, n_ended, act);
-    if (ended) {
+    // the active records' rank in the block (waves before this one, lanes before this lane)
+    const uint64_t am = __ballot(live && !ended);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(am);
+    __syncthreads();
+    uint32_t p = 0;
+    if (live && !ended) {
+        uint32_t before = 0;
+        for (uint32_t q = 0; q < w; q++) before += s_w[q];
+        p = (uint32_t)n_ended + blk_pre[blockIdx.x] + before +
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+    } else if (ended && !start) {
+        const uint64_t q = k - base;
+        p = pre[q >> 5] + __popc(bits[q >> 5] & ((1u << (q & 31)) - 1u));
+    } else if (ended) {
         const uint32_t s0 = start[k - base], s1 = start[k - base + 1];
         uint32_t rank = 0;
         if (s1 - s0 > 1) {
@@ -5537,7 +5555,22 @@ __global__ void __launch_bounds__(256) k_ob_rank(const fluere_record* r, const u
         }
         p = s0 + rank;
     }
-    if (live) pos[i] = (uint32_t)p;
+    if (aux && live) {
+        aux_out[2 * (size_t)p] = aux[2 * i];
+        aux_out[2 * (size_t)p + 1] = aux[2 * i + 1];
+    }
+    const uint64_t w0 = i - lane;  // the wave's first record (whole waves: blockDim is a multiple of 64)
+    if (w0 >= n) return;
+    const uint32_t nr = (uint32_t)min<uint64_t>(64, n - w0);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(r + w0);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
+    const uint32_t total = nr * REC_WORDS;
+    for (uint32_t b = 0; b < total; b += 64) {  // (wave-uniform: every lane takes part in the shuffle)
+        const uint32_t e = b + lane, ec = min(e, total - 1);
+        const uint32_t j = ec / REC_WORDS, kk = ec - j * REC_WORDS;
+        const uint32_t pj = __shfl(p, j, 64);
+        if (e < total) dst[(size_t)pj * REC_WORDS + kk] = src[e];
+    }
 }
 
 static int ord_scratch(fluere_ctx* c, size_t need) {
@@ -5576,51 +5609,50 @@ static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_
         return rc;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const unsigned gn = grid_for(n, 256);
+    const uint64_t nw = N / 32 + 1;                 // Mode A: bit words
+    const uint64_t nk = mode_b ? N + 1 : nw;        // the scanned array: Mode A bit counts, Mode B group counts
+    size_t tb = 0, tb2 = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nk, s);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)gn, s);
+    tb = std::max(tb, tb2);
+    // scratch: okey[n] | cnt-or-bits[nk] | pc[nw] | pre-or-start[nk] | mem[n] | blk[gn] | blk_pre[gn] | gmax | tmp
+    if ((rc = ord_scratch(c, al(n * 8) + 2 * al(nk * 4) + al(nw * 4) + al(n * 4) + 2 * al(gn * 4) + al(16) + al(tb))))
+        return rc;
+    char* p = (char*)c->d_ord;
+    auto take = [&](size_t bytes) { char* q = p; p += al(bytes); return q; };
+    unsigned long long* okey = (unsigned long long*)take(n * 8);
+    uint32_t* cb = (uint32_t*)take(nk * 4);   // Mode A bits, Mode B counts
+    uint32_t* pc = (uint32_t*)take(nw * 4);
+    uint32_t* ps = (uint32_t*)take(nk * 4);   // Mode A bit-count prefix, Mode B group starts
+    uint32_t* mem = (uint32_t*)take(n * 4);
+    uint32_t* blk = (uint32_t*)take(gn * 4);
+    uint32_t* blk_pre = (uint32_t*)take(gn * 4);
+    uint32_t* gmax = (uint32_t*)take(16);
+    void* tmp = p;
+    HIPCHECK(hipMemsetAsync(cb, 0, nk * 4, s));
+    HIPCHECK(hipMemsetAsync(gmax, 0, 4, s));
+    k_ord_keys<<<gn, 256, 0, s>>>(c->d_recs, n, base, mode_b ? 1 : 0, okey, cb, cb, gmax, blk);
+    size_t t = tb;
+    HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, blk, blk_pre, (int)gn, s));
     if (!mode_b) {
-        const uint64_t nw = N / 32 + 1;
-        size_t tb = 0;
-        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nw, s);
-        if ((rc = ord_scratch(c, 3 * al(nw * 4) + al(8) + al(n * 4) + al(tb)))) return rc;
-        char* p = (char*)c->d_ord;
-        uint32_t* bits = (uint32_t*)p;
-        uint32_t* pc = (uint32_t*)(p + al(nw * 4));
-        uint32_t* pre = (uint32_t*)(p + 2 * al(nw * 4));
-        unsigned long long* act = (unsigned long long*)(p + 3 * al(nw * 4));
-        uint32_t* pos = (uint32_t*)(p + 3 * al(nw * 4) + al(8));
-        void* tmp = p + 3 * al(nw * 4) + al(8) + al(n * 4);
-        HIPCHECK(hipMemsetAsync(bits, 0, nw * 4, s));
-        HIPCHECK(hipMemsetAsync(act, 0, 8, s));
-        k_ord_mark<<<(unsigned)std::min<uint64_t>(gn, (uint64_t)c->n_cu * 8), 256, 0, s>>>(c->d_recs, n, base, bits);
-        k_ord_popc<<<grid_for(nw, 256), 256, 0, s>>>(bits, nw, pc);
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, pc, pre, (int)nw, s));
-        k_ord_pos_a<<<gn, 256, 0, s>>>(c->d_recs, n, base, bits, pre, n_ended, pos, act);
-        k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, nullptr, n, pos, c->d_recs2, nullptr);
+        k_ord_popc<<<grid_for(nw, 256), 256, 0, s>>>(cb, nw, pc);
+        t = tb;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, pc, ps, (int)nw, s));
+        k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, nullptr, n, base, okey, cb, ps, nullptr, nullptr, blk_pre, n_ended,
+                                      c->d_recs2, nullptr);
     } else {
-        size_t tb = 0;
-        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(N + 1), s);
-        if ((rc = ord_scratch(c, 2 * al((N + 1) * 4) + 2 * al(n * 4) + al(16) + al(tb)))) return rc;
-        char* p = (char*)c->d_ord;
-        uint32_t* cnt = (uint32_t*)p;
-        uint32_t* start = (uint32_t*)(p + al((N + 1) * 4));
-        uint32_t* mem = (uint32_t*)(p + 2 * al((N + 1) * 4));
-        uint32_t* pos = (uint32_t*)(p + 2 * al((N + 1) * 4) + al(n * 4));
-        unsigned long long* act = (unsigned long long*)(p + 2 * al((N + 1) * 4) + 2 * al(n * 4));
-        uint32_t* gmax = (uint32_t*)(act + 1);
-        void* tmp = p + 2 * al((N + 1) * 4) + 2 * al(n * 4) + al(16);
-        HIPCHECK(hipMemsetAsync(cnt, 0, (N + 1) * 4, s));
-        HIPCHECK(hipMemsetAsync(act, 0, 16, s));
-        k_ob_count<<<gn, 256, 0, s>>>(c->d_recs, n, base, cnt, gmax);
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, start, (int)(N + 1), s));
+        t = tb;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, cb, ps, (int)(N + 1), s));
         // the largest group: a sweep that ends thousands of flows at one packet
-        // (an idle gap) would make the rank's member scans quadratic
+        // (an idle gap) would make the members' rank scans quadratic
         unsigned long long g = 0;
         const void* src[1] = {gmax};
         const int by[1] = {4};
         if ((rc = mail_fetch(c->h_mail, s, 1, src, by, &g))) return rc;
         if (g > 1024) return FLUERE_OK;  // (fetch_records orders them on the host)
-        k_ob_fill<<<gn, 256, 0, s>>>(c->d_recs, n, base, cnt, start, mem);
-        k_ob_rank<<<gn, 256, 0, s>>>(c->d_recs, c->d_recaux, n, base, start, mem, n_ended, pos, act);
-        k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, c->d_recaux, n, pos, c->d_recs2, c->d_recaux2);
+        k_ob_fill<<<gn, 256, 0, s>>>(okey, n, base, cb, ps, mem);
+        k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, c->d_recaux, n, base, okey, nullptr, nullptr, ps, mem, blk_pre, n_ended,
+                                      c->d_recs2, c->d_recaux2);
         std::swap(c->d_recaux, c->d_recaux2);
         std::swap(c->d_recaux_cap, c->d_recaux2_cap);
     }
@@ -5675,11 +5707,12 @@ static int prepare_capture(fluere_ctx* c) {
     }
     {   // order_records' scratch (Mode B's bound covers Mode A's)
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-        const uint64_t n = c->d_recs_cap;
+        const uint64_t n = c->d_recs_cap, gn = (n + 255) / 256, nw = N / 32 + 1;
         size_t tb = 0;
         (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(N + 1),
                                                c->stream);
-        (void)ord_scratch(c, 2 * al((N + 1) * 4) + 2 * al(n * 4) + al(16) + al(tb));
+        (void)ord_scratch(c, al(n * 8) + 2 * al((N + 1) * 4) + al(nw * 4) + al(n * 4) + 2 * al(gn * 4) + al(16) +
+                                 al(tb));
     }
     return FLUERE_OK;
 }
@@ -5796,7 +5829,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     // the run needs no more device work (the same test, on the same counters)
     const bool spec_cleared = P.spec && run_complete(g, nf_err[1], P.spec_ca.timeout_us, P.spec_ca.recs_cap);
     if (!(nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = nf_err[0];
-    c->last_n_slow = g.n_slow;
+    // (a pass of k_slow over every packet lists none: the prediction stays)
+    c->last_n_slow = c->plan_slow_all ? std::max<uint64_t>(g.n_slow, c->n_total) : g.n_slow;
     debug_counters(c, &g);
     FinArgs fa = P.fa;
     fa.host_ctl = nullptr;  // re-launches below read the counters back with copies

@@ -4,6 +4,7 @@
 #   tools/gpu_run.sh <tag> <steps...>
 # steps: tests[:<pytest -k expr>]  smoke  bench  cfg:<config>  cold:<config>  prof:<config>
 #        trace:<config> (kernel timeline of the last step)  debug:<config> (FLUERE_DEBUG counters)
+#        vtrace:<variant>:<config>  hostinc:<config> (host-inclusive rate)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TAG=$1
@@ -49,6 +50,10 @@ for st in "$@"; do
       v=${st#vtrace:}; c=${v#*:}; v=${v%%:*}
       FLUERE_LIB=$R/fluere_amd/variants/libfluere_gpu_$v.so bash tools/trace.sh ${v} $c
       cp gpurun_out/trace_${v}_$c/timeline.txt "$O/timeline_${v}_$c.txt" ;;
+    hostinc:*)  # hostinc:<config>: fluere offline on a file in the page cache (host-inclusive rate), with host timings
+      c=${st#hostinc:}
+      FLUERE_HOSTPROF=1 timeout -k 10 300 python -u tools/host_inclusive.py --config $c > "$O/hostinc_$c.log" 2>&1
+      tail -3 "$O/hostinc_$c.log" ;;
     debug:*)
       c=${st#debug:}
       FLUERE_DEBUG=1 timeout -k 10 240 python -u bench.py --config $c --no-cpu-baseline --no-imix --steps 2 --warmup 1 > "$O/debug_$c.log" 2>&1
