@@ -1129,7 +1129,11 @@ __device__ __forceinline__ uint32_t own_add_n(uint32_t* arr, uint32_t o, uint32_
     return (atomicAdd(&arr[o >> 1], n << ((o & 1) * 16)) >> ((o & 1) * 16)) & 0xFFFFu;
 }
 
+// MACS (-M): the canonical MAC pair joins the key; a record is four 16-byte
+// words -- key, MAC words + hash, payload, zero (k_parse_agg<MACS>'s spills)
+template <bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
+    constexpr uint32_t RU = MACS ? 4u : 2u;  // 16-byte words per record
     __shared__ uint4 s_bin[SPB_WORDS];
     __shared__ uint32_t s_cl[MAX_OWNERS], s_wr[MAX_OWNERS];  // per bin: slots claimed / records written
     __shared__ uint32_t s_scnt[OWN_WORDS];                   // per owner: records in its segment (packed)
@@ -1139,8 +1143,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
     const Stage& S = a.S;
     const Batch& B = a.B;
     const uint32_t O = S.O;
-    const uint32_t BIN = (uint32_t)(SPB_WORDS / 2) / O;  // records per bin: 16 (256 owners) .. 2 (2048)
-    const uint32_t PPB = 2 * BIN;                         // 16-byte pieces per bin
+    const uint32_t BIN = (uint32_t)(SPB_WORDS / RU) / O;  // records per bin: 16 (256 owners) .. 2 (2048); MACS: 8 .. 1
+    const uint32_t PPB = RU * BIN;                         // 16-byte pieces per bin
     for (uint32_t o = tid; o < MAX_OWNERS; o += BLOCK) s_cl[o] = s_wr[o] = 0;
     for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
     if (tid < 3) s_cnt[tid] = 0;
@@ -1158,13 +1162,13 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
     // a lane's overflow record (its owner segment is full): the workgroup's
     // raw buffer, listed at the window flush (k_parse_agg's overflow list)
     auto overflow = [&](uint32_t q, uint32_t h, uint4 v) {
-        uint4* dst = reinterpret_cast<uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2 + (size_t)h * SPILL_WG + q;
+        uint4* dst = reinterpret_cast<uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * RU + (size_t)h * SPILL_WG + q;
         *dst = v;
     };
     for (uint64_t ws = 0; ws < nsteps; ws += WIN_ITERS) {
         const uint32_t set = blockIdx.x * S.W + win;
         const uint32_t nch = (uint32_t)min<uint64_t>(WIN_ITERS, nsteps - ws) * WAVES;
-        uint4* seg0 = reinterpret_cast<uint4*>(S.dspill) + (size_t)set * O * S.cap_o * 2;
+        uint4* seg0 = reinterpret_cast<uint4*>(S.dspill) + (size_t)set * O * S.cap_o * RU;
         auto li_of = [&](uint32_t c) -> uint64_t {
             return beg + (ws + c / WAVES) * stride + (uint64_t)(c % WAVES) * 64 + lane;
         };
@@ -1204,16 +1208,31 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
             c_drop += (live & (cls == HOT_DROP)) ? 1 : 0;
             const bool valid = live & (cls == HOT_OK);
             const bool slow = live & (cls == HOT_SLOW);
-            // canonical key (lower endpoint first, flow_table.h)
+            // canonical key (lower endpoint first, flow_table.h; MACS: the MAC breaks a tie)
             const uint32_t sp = h.ports >> 16, dp = h.ports & 0xFFFFu;
-            const bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
+            bool gt = (h.sip > h.dip) | ((h.sip == h.dip) & (sp > dp));
+            uint32_t m0 = 0, m1 = 0, m2 = 0;
+            if (MACS) {
+                const uint64_t dmac = ((uint64_t)__builtin_amdgcn_perm(W.w[5], W.w[4], 0x00010203u) << 16) |
+                                      __builtin_amdgcn_perm(W.w[5], W.w[4], 0x0C0C0405u);  // frame bytes 0..5
+                const uint64_t smac = ((uint64_t)__builtin_amdgcn_perm(W.w[6], W.w[5], 0x02030405u) << 16) |
+                                      __builtin_amdgcn_perm(W.w[6], W.w[5], 0x0C0C0607u);  // frame bytes 6..11
+                if ((h.sip == h.dip) & (sp == dp)) gt = smac > dmac;
+                const uint64_t lom = gt ? dmac : smac, him = gt ? smac : dmac;
+                m0 = (uint32_t)(lom >> 16);
+                m1 = ((uint32_t)(lom & 0xFFFF) << 16) | (uint32_t)(him & 0xFFFF);
+                m2 = (uint32_t)(him >> 16);
+            }
             const uint4 w_key = make_uint4(gt ? h.dip : h.sip, gt ? h.sip : h.dip,
                                            gt ? __builtin_amdgcn_alignbit(h.ports, h.ports, 16) : h.ports, h.proto << 24);
             const bool elig = (h.proto != 6u) | ((h.tf & 2u) != 0);
             const uint4 w_pay = make_uint4(h.doct, h.pkt | (h.ttl << 16) | ((elig ? 1u : 0u) << 24), (uint32_t)(li - wbase),
                                            h.tf | ((gt ? 1u : 0u) << 8));
-            const uint32_t o = owner_of(lt_hash(w_key.x, w_key.y, w_key.z, w_key.w), O);
-            if (a.phash && live) a.phash[li] = valid ? ckey_bucket_v4(w_key.x, w_key.y, w_key.z, h.proto) : PH_PARSE;
+            uint32_t hk = lt_hash(w_key.x, w_key.y, w_key.z, w_key.w);
+            if (MACS) hk = mac_hash(hk, m0, m1, m2);
+            const uint4 w_mac = make_uint4(m0, m1, m2, hk);
+            const uint32_t o = owner_of(hk, O);
+            if (!MACS && a.phash && live) a.phash[li] = valid ? ckey_bucket_v4(w_key.x, w_key.y, w_key.z, h.proto) : PH_PARSE;
             if (valid) {
                 c_valid++;
                 tmin = min(tmin, (unsigned long long)h.t);
@@ -1228,9 +1247,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                 if (pend) {
                     const uint32_t slot = atomicAdd(&s_cl[o], 1u);
                     if (slot < BIN) {
-                        uint4* b = &s_bin[(o * BIN + slot) * 2];
+                        uint4* b = &s_bin[(o * BIN + slot) * RU];
                         b[0] = w_key;
-                        b[1] = w_pay;
+                        if (MACS) {
+                            b[1] = w_mac;
+                            b[2] = w_pay;
+                            b[3] = make_uint4(0, 0, 0, 0);
+                        } else {
+                            b[1] = w_pay;
+                        }
                         __threadfence_block();
                         if (atomicAdd(&s_wr[o], 1u) + 1 == BIN) done = o;
                         pend = false;
@@ -1248,17 +1273,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                     const bool act = m != 0 && j < 64 / PPB;  // (64 % PPB != 0: the spare lanes idle)
                     const uint32_t src = act ? (uint32_t)__builtin_ctzll(m) : 0u;
                     const uint32_t bo = __shfl(done, src, 64), bp = __shfl(pos, src, 64);
+                    const uint32_t r = pc / RU, hh = pc % RU;
+                    const bool ovf = act && bp + r >= S.cap_o;
+                    uint32_t q = 0;  // (the overflow slot: from the record's first lane, every lane shuffling)
+                    if (ovf && hh == 0) q = atomicAdd(&s_nspill, 1u);
+                    q = __shfl(q, lane & ~(RU - 1), 64);
                     if (act) {
-                        const uint32_t r = pc >> 1, hh = pc & 1;
-                        const uint4 v = s_bin[(bo * BIN + r) * 2 + hh];
-                        if (bp + r < S.cap_o) {
-                            seg0[((size_t)bo * S.cap_o + bp + r) * 2 + hh] = v;
-                        } else {  // past the segment's capacity: the overflow list
-                            uint32_t q = 0;
-                            if (hh == 0) q = atomicAdd(&s_nspill, 1u);
-                            q = __shfl(q, lane & ~1u, 64);
-                            overflow(q, hh, v);
-                        }
+                        const uint4 v = s_bin[(bo * BIN + r) * RU + hh];
+                        if (!ovf) seg0[((size_t)bo * S.cap_o + bp + r) * RU + hh] = v;
+                        else overflow(q, hh, v);  // past the segment's capacity: the overflow list
                     }
                     // drop the group's bins (the first 64 / PPB set bits)
                     for (uint32_t k = 0; k < 64 / PPB && fm; k++) fm &= fm - 1;
@@ -1291,15 +1314,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
             if (!k) continue;
             const uint32_t p0 = own_add_n(s_scnt, o, k);
             for (uint32_t r = 0; r < k; r++) {
-                const uint4 v0 = s_bin[(o * BIN + r) * 2], v1 = s_bin[(o * BIN + r) * 2 + 1];
+                const uint4* v = &s_bin[(o * BIN + r) * RU];
                 if (p0 + r < S.cap_o) {
-                    uint4* d = seg0 + ((size_t)o * S.cap_o + p0 + r) * 2;
-                    d[0] = v0;
-                    d[1] = v1;
+                    uint4* d = seg0 + ((size_t)o * S.cap_o + p0 + r) * RU;
+#pragma unroll
+                    for (uint32_t u = 0; u < RU; u++) d[u] = v[u];
                 } else {
                     const uint32_t q = atomicAdd(&s_nspill, 1u);
-                    overflow(q, 0, v0);
-                    overflow(q, 1, v1);
+#pragma unroll
+                    for (uint32_t u = 0; u < RU; u++) overflow(q, u, v[u]);
                 }
             }
             s_cl[o] = s_wr[o] = 0;
@@ -1314,16 +1337,18 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
         }
         __syncthreads();
         if (nsp) {  // overflow records -> the overflow list (the set in fl's high bits)
-            const uint4* raw = reinterpret_cast<const uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * 2;
+            const uint4* raw = reinterpret_cast<const uint4*>(S.spill_raw) + (size_t)blockIdx.x * SPILL_WG * RU;
             const unsigned long long sb = s_sbase;
+            constexpr uint32_t PAY = RU == 4 ? 2u : 1u;  // the payload word (its fl field carries the set)
             for (uint32_t i = tid; i < nsp; i += BLOCK) {
                 // (written by other waves of this workgroup: nontemporal loads bypass the CU's L1)
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 k0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(raw + i));
-                const u32x4 k1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(raw + SPILL_WG + i));
-                uint4* dst = reinterpret_cast<uint4*>(S.spill) + (sb + i) * 2;
-                dst[0] = make_uint4(k0.x, k0.y, k0.z, k0.w);
-                dst[1] = make_uint4(k1.x, k1.y, k1.z, k1.w | (set << 9));
+                uint4* dst = reinterpret_cast<uint4*>(S.spill) + (sb + i) * RU;
+#pragma unroll
+                for (uint32_t u = 0; u < RU; u++) {
+                    const u32x4 kk = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(raw + u * SPILL_WG + i));
+                    dst[u] = make_uint4(kk.x, kk.y, kk.z, kk.w | (u == PAY ? (set << 9) : 0u));
+                }
             }
         }
         for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
@@ -4300,14 +4325,19 @@ extern "C" int64_t fluere_pcap_index(const uint8_t* file, uint64_t nbytes, uint6
 }
 
 // ---------------------------------------------------------------------------
-// Host ingress.  The capture streams to the device in order through two
-// pinned staging chunks (the copy of one chunk overlaps filling the next),
-// and the record index is built on the host from the staged bytes while they
-// are still in cache: one pass over the headers, libpcap offline semantics
-// (stop at the first bad or truncated record).  The whole capture lands in
-// one device allocation; batches (< 4 GiB each, u32 offsets) are sub-ranges.
+// Host ingress.  The capture streams to the device in order through pinned
+// staging chunks (the copy of one chunk overlaps filling the next), and the
+// record index is built on the host from the staged bytes: libpcap offline
+// semantics (stop at the first bad or truncated record).  The record chain is
+// a pointer chase (each header gives the next one's offset), latency-bound
+// once the bytes have left the cache, so each reader thread walks its own
+// chunk as it fills it (in L2-sized pieces), from a record start it
+// recognises (a run of plausible headers); the calling thread then only
+// checks that the true chain meets the reader's: a chunk whose guessed start
+// was wrong is walked from the true position until the chains meet (or to
+// its end).  The whole capture lands in one device allocation; batches
+// (< 4 GiB each, u32 offsets) are sub-ranges.
 // ---------------------------------------------------------------------------
-constexpr uint64_t kIngestChunk = 32ull << 20;
 constexpr uint32_t kSnapMax = 262144;
 constexpr uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
 
@@ -4315,6 +4345,11 @@ constexpr uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
 // (pread from the file, or a copy of the host buffer) while the calling
 // thread indexes the chunks in order and enqueues their H2D copies.
 constexpr int kIngestSlots = 8;  // at most; FLUERE_INGEST_SLOTS / _READERS (diagnostics) pick fewer
+static uint64_t ingest_chunk() {  // staging chunk bytes (FLUERE_INGEST_CHUNK_MB: diagnostics)
+    static const uint64_t v =
+        (uint64_t)(getenv("FLUERE_INGEST_CHUNK_MB") ? std::max(1, std::min(64, atoi(getenv("FLUERE_INGEST_CHUNK_MB")))) : 32) << 20;
+    return v;
+}
 static int ingest_slots() {
     static const int v = getenv("FLUERE_INGEST_SLOTS") ? std::max(2, std::min(kIngestSlots, atoi(getenv("FLUERE_INGEST_SLOTS")))) : 4;
     return v;
@@ -4323,6 +4358,17 @@ static int ingest_readers() {
     static const int v = getenv("FLUERE_INGEST_READERS") ? std::max(1, std::min(16, atoi(getenv("FLUERE_INGEST_READERS")))) : 3;
     return v;
 }
+constexpr uint64_t kFillPiece = 512ull << 10;  // a reader fills and walks this much at a time (in L2)
+constexpr int kSyncRun = 8;                    // plausible headers in a row that make a record start
+
+// One chunk's record chain as its reader walked it (offsets chunk-relative).
+struct ChunkChain {
+    std::vector<uint32_t> so;  // record starts
+    int64_t start = -1;        // the first record start taken; -1 none yet, -2 none found
+    uint64_t next = 0;         // where the chain continues (may lie past the chunk)
+    uint64_t scan = 0;         // the record-start search position
+    bool stopped = false;      // the chain met a record libpcap's walk stops at
+};
 
 struct Ingest {
     fluere_ctx* c;
@@ -4337,7 +4383,17 @@ struct Ingest {
     uint64_t pos = 24;
     bool stopped = false;
     uint8_t tail[16];
-    std::vector<uint64_t> offs;      // absolute record offsets
+    // the record index: pieces of the chains the readers walked, and of the
+    // calling thread's own walk (absolute offsets, seq64), in capture order
+    struct Piece {
+        int64_t chunk;  // -1: seq64[i0, i0 + n)
+        size_t i0, n;
+    };
+    std::vector<Piece> pieces;
+    std::vector<uint64_t> seq64;
+    std::vector<ChunkChain> chains;  // per chunk, when the readers walk
+    uint64_t nrec = 0;
+    uint32_t snap_file = kSnapMax;   // the global header's snaplen (record-start plausibility)
     std::vector<size_t> cut;         // first record of each batch
     std::vector<uint64_t> cut_base;  // byte offset of each batch
     // the capture side's record offsets (fluere_live_batch_indexed): the
@@ -4362,7 +4418,7 @@ struct Ingest {
         if (nbytes < 24) return FLUERE_E_PCAP;
         size = nbytes;
         nslots = ingest_slots();
-        const int ns_ = (int)std::min<uint64_t>(nslots, (nbytes + kIngestChunk - 1) / kIngestChunk);
+        const int ns_ = (int)std::min<uint64_t>(nslots, (nbytes + ingest_chunk() - 1) / ingest_chunk());
         const auto ta = std::chrono::steady_clock::now();
         if (c->reuse_ingest) {
             static_assert(kIngestSlots == 8, "arena slots");
@@ -4376,7 +4432,7 @@ struct Ingest {
             }
             d = c->ar_d;
             for (int i = 0; i < ns_; i++) {
-                if (!c->ar_pin[i] && hipHostMalloc(&c->ar_pin[i], kIngestChunk, hipHostMallocDefault) != hipSuccess)
+                if (!c->ar_pin[i] && hipHostMalloc(&c->ar_pin[i], ingest_chunk(), hipHostMallocDefault) != hipSuccess)
                     return FLUERE_E_NOMEM;
                 if (!c->ar_ev[i] && hipEventCreateWithFlags(&c->ar_ev[i], hipEventDisableTiming) != hipSuccess)
                     return FLUERE_E_HIP;
@@ -4386,13 +4442,15 @@ struct Ingest {
             return FLUERE_OK;
         }
         if (hipMalloc(&d, nbytes + 256) != hipSuccess) return FLUERE_E_NOMEM;
+        const auto tb = std::chrono::steady_clock::now();
         for (int i = 0; i < ns_; i++) {
-            if (hipHostMalloc(&pin[i], kIngestChunk, hipHostMallocDefault) != hipSuccess) return FLUERE_E_NOMEM;
+            if (hipHostMalloc(&pin[i], ingest_chunk(), hipHostMallocDefault) != hipSuccess) return FLUERE_E_NOMEM;
             if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return FLUERE_E_HIP;
         }
         if (getenv("FLUERE_HOSTPROF"))
-            fprintf(stderr, "[fluere] ingest setup (device buffer, %d pinned slots): %.1f ms\n", ns_,
-                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - ta).count());
+            fprintf(stderr, "[fluere] ingest setup: device buffer %.1f ms, %d pinned slots of %llu MiB %.1f ms\n",
+                    1e3 * std::chrono::duration<double>(tb - ta).count(), ns_, (unsigned long long)(ingest_chunk() >> 20),
+                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count());
         return FLUERE_OK;
     }
     // staging slot for chunk k, free once its previous copy has completed
@@ -4408,10 +4466,10 @@ struct Ingest {
     // staging slot (reader threads), feed() indexes and copies them in order.
     template <class Fill>
     int run(uint64_t nbytes, Fill fill) {
-        const uint64_t nch = (nbytes + kIngestChunk - 1) / kIngestChunk;
+        const uint64_t nch = (nbytes + ingest_chunk() - 1) / ingest_chunk();
         if (nch <= 1) {  // one chunk: no threads
             for (uint64_t k = 0; k < nch; k++) {
-                const uint64_t cs = k * kIngestChunk, len = std::min(kIngestChunk, nbytes - cs);
+                const uint64_t cs = k * ingest_chunk(), len = std::min(ingest_chunk(), nbytes - cs);
                 if (!fill(slot(k), cs, len)) return FLUERE_E_IO;
                 const int rc = feed(k, cs, len);
                 if (rc) return rc;
@@ -4419,6 +4477,12 @@ struct Ingest {
             return FLUERE_OK;
         }
         const int NS = nslots, NR = ingest_readers();
+        // the global header first: the readers' walks need its byte order
+        if (!given) {
+            if (!fill(pin[0], 0, 24)) return FLUERE_E_IO;
+            if (int rc = global_header(pin[0])) return rc;
+            chains.resize(nch);
+        }
         std::atomic<int64_t> filled[kIngestSlots];
         for (auto& f : filled) f.store(-1);
         std::atomic<int64_t> fed{-1};
@@ -4430,8 +4494,19 @@ struct Ingest {
                 while ((int64_t)k - NS > fed.load() && !stop.load()) std::this_thread::yield();
                 if (stop.load()) return;
                 if (k >= (uint64_t)NS && hipEventSynchronize(ev[i]) != hipSuccess) { fail = true; stop = true; return; }
-                const uint64_t cs = k * kIngestChunk, len = std::min(kIngestChunk, nbytes - cs);
-                if (!fill(pin[i], cs, len)) { fail = true; stop = true; return; }
+                const uint64_t cs = k * ingest_chunk(), len = std::min(ingest_chunk(), nbytes - cs);
+                if (given) {
+                    if (!fill(pin[i], cs, len)) { fail = true; stop = true; return; }
+                } else {
+                    ChunkChain& ch = chains[k];
+                    ch.so.reserve(len / 128 + 64);
+                    if (k == 0) ch.start = ch.next = 24;
+                    for (uint64_t f = 0; f < len; f += kFillPiece) {
+                        const uint64_t pl = std::min(kFillPiece, len - f);
+                        if (!fill(pin[i] + f, cs + f, pl)) { fail = true; stop = true; return; }
+                        chain_walk(pin[i], cs, f + pl, len, ch);
+                    }
+                }
                 filled[i].store((int64_t)k);
             }
         };
@@ -4447,7 +4522,7 @@ struct Ingest {
             while (filled[i].load() != (int64_t)k && !fail.load()) std::this_thread::yield();
             const auto w1 = std::chrono::steady_clock::now();
             if (fail.load()) { rc = FLUERE_E_IO; break; }
-            const uint64_t cs = k * kIngestChunk, len = std::min(kIngestChunk, nbytes - cs);
+            const uint64_t cs = k * ingest_chunk(), len = std::min(ingest_chunk(), nbytes - cs);
             rc = feed(k, cs, len);
             fed.store((int64_t)k);
             wait_s += std::chrono::duration<double>(w1 - w0).count();
@@ -4467,25 +4542,110 @@ struct Ingest {
         memcpy(&v, p, 4);
         return sw ? __builtin_bswap32(v) : v;
     }
+    int global_header(const uint8_t* b) {  // pcap global header (libpcap offline)
+        uint32_t magic;
+        memcpy(&magic, b, 4);
+        if (magic == 0xa1b2c3d4u) {
+        } else if (magic == 0xd4c3b2a1u) sw = 1;
+        else if (magic == 0xa1b23c4du) ns = 1;
+        else if (magic == 0x4d3cb2a1u) { sw = 1; ns = 1; }
+        else return FLUERE_E_PCAP;
+        snap = rd32(b + 16);
+        if (snap == 0 || snap > kSnapMax) snap = kSnapMax;
+        snap_file = snap;
+        return FLUERE_OK;
+    }
+    // Is q (chunk-relative, bytes [0, avail) present) the start of kSyncRun
+    // plausible record headers in a row?  1 yes, 0 no, -1 not enough bytes
+    // yet.  Plausible: caplen within the snaplen and the wire length, a
+    // nonzero wire length, a sub-second fraction in range.  Only a speed
+    // question: a wrong guess costs the calling thread a walk, never a result.
+    int plausible_run(const uint8_t* b, uint64_t q, uint64_t avail, uint64_t len) const {
+        const uint32_t frac_max = ns ? 1000000000u : 1000000u;
+        for (int d = 0; d < kSyncRun; d++) {
+            if (q >= len) return d > 0 ? 1 : 0;  // the run leaves the chunk
+            if (q + 16 > avail) return avail == len ? (d > 0 ? 1 : 0) : -1;
+            const uint32_t frac = rd32(b + q + 4), incl = rd32(b + q + 8), orig = rd32(b + q + 12);
+            if (frac >= frac_max || incl > snap_file || incl > orig || orig == 0 || orig > (1u << 20)) return 0;
+            q += 16 + (uint64_t)incl;
+        }
+        return 1;
+    }
+    // reader side: extend chunk [cs, cs + len)'s chain over its bytes [0, avail)
+    void chain_walk(const uint8_t* b, uint64_t cs, uint64_t avail, uint64_t len, ChunkChain& ch) const {
+        if (ch.start == -2) return;
+        if (ch.start < 0) {
+            // a record starts within the first kSnapMax + 16 bytes of any chunk
+            const uint64_t lim = std::min<uint64_t>(len, kSnapMax + 32);
+            while (ch.scan < lim) {
+                const int r = plausible_run(b, ch.scan, avail, len);
+                if (r < 0) return;  // wait for the next piece
+                if (r > 0) break;
+                ch.scan++;
+            }
+            if (ch.scan >= lim) { ch.start = -2; return; }
+            ch.start = (int64_t)ch.scan;
+            ch.next = ch.scan;
+        }
+        uint64_t p = ch.next;
+        while (!ch.stopped && p + 16 <= avail) {
+            const uint32_t incl = rd32(b + p + 8);
+            if (incl > kSnapMax || cs + p + 16 + (uint64_t)incl > size) {
+                ch.stopped = true;
+                break;
+            }
+            ch.so.push_back((uint32_t)p);
+            p += 16 + (uint64_t)incl;
+        }
+        ch.next = p;
+    }
+    void push_rec(uint64_t off) {
+        if (pieces.empty() || pieces.back().chunk >= 0) pieces.push_back({-1, seq64.size(), 0});
+        seq64.push_back(off);
+        pieces.back().n++;
+        nrec++;
+    }
+    // calling thread: the true chain met chunk k's at its record j (or its end)
+    void take_chain(uint64_t k, uint64_t cs, size_t j) {
+        const ChunkChain& ch = chains[k];
+        const size_t n = ch.so.size() - j;
+        const uint64_t end = cs + ch.next;
+        if (n) {
+            if (end - cut_base.back() > kMaxBatch)  // a 4-GiB batch boundary inside: place it record by record
+                for (size_t i = j; i < ch.so.size(); i++) {
+                    const uint64_t e = cs + (i + 1 < ch.so.size() ? ch.so[i + 1] : ch.next);
+                    if (e - cut_base.back() > kMaxBatch) {
+                        cut.push_back(nrec + (i - j));
+                        cut_base.push_back(cs + ch.so[i]);
+                    }
+                }
+            pieces.push_back({(int64_t)k, j, n});
+            nrec += n;
+        }
+        pos = end;
+        if (ch.stopped) stopped = true;
+    }
     // chunk k = bytes [cs, cs + len) of the capture, already in slot(k)
     int feed(uint64_t k, uint64_t cs, uint64_t len) {
         const uint8_t* b = pin[k % nslots];
-        if (cs == 0) {  // pcap global header (libpcap offline)
-            uint32_t magic;
-            memcpy(&magic, b, 4);
-            if (magic == 0xa1b2c3d4u) {
-            } else if (magic == 0xd4c3b2a1u) sw = 1;
-            else if (magic == 0xa1b23c4du) ns = 1;
-            else if (magic == 0x4d3cb2a1u) { sw = 1; ns = 1; }
-            else return FLUERE_E_PCAP;
-            snap = rd32(b + 16);
-            if (snap == 0 || snap > kSnapMax) snap = kSnapMax;
+        if (cs == 0) {
+            if (int rc = global_header(b)) return rc;
             cut.push_back(0);
             cut_base.push_back(24);
         }
         const uint64_t ce = cs + len;
         uint8_t h[16];
+        const ChunkChain* ch = k < chains.size() && chains[k].start >= 0 ? &chains[k] : nullptr;
+        size_t j = 0;
         while (!given && !stopped && pos + 16 <= ce) {
+            if (ch && pos >= cs) {  // has the true chain met the reader's?
+                const uint64_t r = pos - cs;
+                while (j < ch->so.size() && ch->so[j] < r) j++;
+                if (j < ch->so.size() ? ch->so[j] == r : r == ch->next) {
+                    take_chain(k, cs, j);
+                    break;
+                }
+            }
             const uint8_t* hp;
             if (pos >= cs) {
                 hp = b + (pos - cs);
@@ -4499,10 +4659,10 @@ struct Ingest {
                 break;
             }
             if (pos + 16 + incl - cut_base.back() > kMaxBatch) {
-                cut.push_back(offs.size());
+                cut.push_back(nrec);
                 cut_base.push_back(pos);
             }
-            offs.push_back(pos);
+            push_rec(pos);
             pos += 16 + (uint64_t)incl;
         }
         if (pos + 16 > size) stopped = true;
@@ -4559,18 +4719,44 @@ struct Ingest {
         for (uint64_t i = 0; i < m; i++) {
             const uint64_t end = i + 1 < m ? given[i + 1] : given[i] + 16 + incl_of(i);
             if (end - cut_base.back() > kMaxBatch) {
-                cut.push_back(offs.size());
+                cut.push_back(nrec);
                 cut_base.push_back(given[i]);
             }
-            offs.push_back(given[i]);
+            push_rec(given[i]);
             pos = end;
+        }
+    }
+    // records [g0, g1) of the index, batch-relative
+    void fill_rel(uint32_t* out, size_t g0, size_t g1, const std::vector<size_t>& pstart) const {
+        if (g0 >= g1) return;
+        size_t pi = (size_t)(std::upper_bound(pstart.begin(), pstart.end(), g0) - pstart.begin()) - 1;
+        size_t q = (size_t)(std::upper_bound(cut.begin(), cut.end(), g0) - cut.begin()) - 1;
+        size_t g = g0;
+        while (g < g1) {
+            const Piece& P = pieces[pi];
+            const size_t e = std::min(g1, pstart[pi + 1]);
+            while (g < e) {
+                while (q + 1 < cut.size() && cut[q + 1] <= g) q++;
+                const size_t lim = q + 1 < cut.size() ? std::min(e, cut[q + 1]) : e;
+                const uint64_t sub = cut_base[q];
+                size_t i = P.i0 + (g - pstart[pi]);
+                if (P.chunk < 0) {
+                    for (; g < lim; g++, i++) out[g - g0] = (uint32_t)(seq64[i] - sub);
+                } else {
+                    const uint32_t* so = chains[P.chunk].so.data();
+                    const uint64_t base = (uint64_t)P.chunk * ingest_chunk() - sub;  // mod 2^64
+                    for (; g < lim; g++, i++) out[g - g0] = (uint32_t)(base + so[i]);
+                }
+            }
+            pi++;
         }
     }
     // the index as batches of the context (device bytes handed over)
     int finish() {
+        const auto tf = std::chrono::steady_clock::now();
         if (given && !cut.empty()) walk_given();
         HIPCHECK(hipMemsetAsync(d + size, 0, 256, c->stream));
-        const size_t n = offs.size();
+        const size_t n = nrec;
         uint32_t* d_offs = nullptr;
         if (c->reuse_ingest) {
             if (std::max<size_t>(n, 1) > c->ar_offs_cap) {
@@ -4585,13 +4771,48 @@ struct Ingest {
         } else if (hipMalloc(&d_offs, std::max<size_t>(n, 1) * 4) != hipSuccess) {
             return FLUERE_E_NOMEM;
         }
-        std::vector<uint32_t> rel(std::max<size_t>(n, 1));
-        for (size_t q = 0; q < cut.size(); q++) {
-            const size_t i0 = cut[q], i1 = q + 1 < cut.size() ? cut[q + 1] : n;
-            for (size_t k = i0; k < i1; k++) rel[k] = (uint32_t)(offs[k] - cut_base[q]);
+        // batch-relative u32 offsets, written into the staging slots (pinned)
+        // a slot's worth at a time, by threads when there are many
+        std::vector<size_t> pstart(pieces.size() + 1, 0);
+        for (size_t q = 0; q < pieces.size(); q++) pstart[q + 1] = pstart[q] + pieces[q].n;
+        const size_t per = ingest_chunk() / 4;
+        for (size_t g0 = 0, part = 0; g0 < n; g0 += per, part++) {
+            const size_t g1 = std::min(n, g0 + per);
+            const int i = (int)(part % nslots);
+            if (!pin[i]) {
+                if (c->reuse_ingest) {
+                    if (!c->ar_pin[i] && hipHostMalloc(&c->ar_pin[i], ingest_chunk(), hipHostMallocDefault) != hipSuccess)
+                        return FLUERE_E_NOMEM;
+                    if (!c->ar_ev[i] && hipEventCreateWithFlags(&c->ar_ev[i], hipEventDisableTiming) != hipSuccess)
+                        return FLUERE_E_HIP;
+                    pin[i] = c->ar_pin[i];
+                    ev[i] = c->ar_ev[i];
+                } else {
+                    if (hipHostMalloc(&pin[i], ingest_chunk(), hipHostMallocDefault) != hipSuccess) return FLUERE_E_NOMEM;
+                    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return FLUERE_E_HIP;
+                }
+            }
+            if (busy[i]) HIPCHECK(hipEventSynchronize(ev[i]));
+            uint32_t* out = reinterpret_cast<uint32_t*>(pin[i]);
+            const int T = g1 - g0 >= (1u << 20) ? 8 : 1;
+            if (T == 1) {
+                fill_rel(out, g0, g1, pstart);
+            } else {
+                std::vector<std::thread> th;
+                for (int t = 0; t < T; t++) {
+                    const size_t a = g0 + (g1 - g0) * t / T, e = g0 + (g1 - g0) * (t + 1) / T;
+                    th.emplace_back([this, out, a, e, g0, &pstart] { fill_rel(out + (a - g0), a, e, pstart); });
+                }
+                for (auto& x : th) x.join();
+            }
+            HIPCHECK(hipMemcpyAsync(d_offs + g0, out, (g1 - g0) * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHECK(hipEventRecord(ev[i], c->stream));
+            busy[i] = true;
         }
-        if (n) HIPCHECK(hipMemcpyAsync(d_offs, rel.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHECK(hipStreamSynchronize(c->stream));  // rel is pageable; staging slots free
+        HIPCHECK(hipStreamSynchronize(c->stream));  // staging slots free
+        if (getenv("FLUERE_HOSTPROF"))
+            fprintf(stderr, "[fluere] ingest finish (%llu records, %zu pieces): %.1f ms\n", (unsigned long long)n,
+                    pieces.size(), 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - tf).count());
         for (int i = 0; i < kIngestSlots; i++) busy[i] = false;
         bool first = true;
         for (size_t q = 0; q < cut.size(); q++) {
@@ -5101,15 +5322,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
 // past the table).  A prediction from the last run: either kernel is exact.
 static int spill_mode(const fluere_ctx* c) {
     const int env = getenv("FLUERE_SPILL_MODE") ? atoi(getenv("FLUERE_SPILL_MODE")) : -1;  // tests: force either kernel
-    if (c->use_mac) return 0;
-    if (merge_owners(c) < 128) return 0;  // bins of more than 32 records: more than a wave per bin
+    if (merge_owners(c) < 128) return 0;  // bins of more than 32 (MACS: 16) records: more than a wave per bin
     if (env >= 0) return env;
     const double F = (double)c->last_nf;
     if (F <= 0) return 0;
     uint64_t nmax = 0;
     for (auto& hb : c->batches) nmax = std::max<uint64_t>(nmax, hb.b.n);
     const double w = std::min<double>((double)WIN_ITERS * BLOCK, (double)nmax / std::max(1, c->n_cu));
-    return F * (1.0 - std::exp(-w / F)) > 2.0 * NS ? 1 : 0;
+    return F * (1.0 - std::exp(-w / F)) > 2.0 * (c->use_mac ? NS_MAC : NS) ? 1 : 0;
 }
 
 static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
@@ -5166,7 +5386,7 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         const AggArgs& a = P.agg[i];
         if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 40, s));  // n_slow, n_spill, n_dspill, n_gen, n_owner (k_cleanup zeroed them for batch 0)
         const unsigned grid = P.agg_grid[i];
-        const void* fn = P.spill ? (const void*)k_parse_spill
+        const void* fn = P.spill ? (P.macs ? (const void*)k_parse_spill<true> : (const void*)k_parse_spill<false>)
                        : P.macs ? (const void*)k_parse_agg<0, true>
                          : P.abl == 1 ? (const void*)k_parse_agg<1, false>
                          : P.abl == 2 ? (const void*)k_parse_agg<2, false>
@@ -5273,7 +5493,7 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
         if (i == 0 && P.nb > 1) event(c->evk_first);
         event(c->evk0);
         a_agg[i][0] = &P.agg[i];
-        const void* fn = P.spill ? (const void*)k_parse_spill
+        const void* fn = P.spill ? (P.macs ? (const void*)k_parse_spill<true> : (const void*)k_parse_spill<false>)
                        : P.macs ? (const void*)k_parse_agg<0, true>
                                 : P.abl == 1 ? (const void*)k_parse_agg<1, false>
                                 : P.abl == 2 ? (const void*)k_parse_agg<2, false>
@@ -5673,9 +5893,14 @@ static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_
 // the ordering scratch.  A failed reservation is retried by the run itself.
 static int prepare_capture(fluere_ctx* c) {
     if (c->reuse_ingest || !c->n_total) return FLUERE_OK;
+    static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = upload_batches(c);
     if (!rc) rc = census(c);
     if (rc) return rc;
+    if (hostprof)
+        fprintf(stderr, "[fluere] attach: upload + census %.1f ms\n",
+                1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     PassPlan P;
     memset(&P, 0, sizeof P);
     P.spill = spill_mode(c);

@@ -11,6 +11,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -151,11 +152,22 @@ extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, i
     fluere_ctx* c = nullptr;
     fluere_stats st{};
     int rc;
+    const bool prof = getenv("FLUERE_HOSTPROF") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {  // FLUERE_HOSTPROF: the call's phases
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[fluere] offline_file %s: %.1f ms\n", what, 1e3 * std::chrono::duration<double>(t - t_last).count());
+        t_last = t;
+    };
     for (;;) {
         rc = fluere_open(&o, &c);
         if (rc) return rc;
+        lap("open");
         rc = fluere_add_pcap_file(c, pcap_path);
+        lap("attach");
         if (!rc) rc = fluere_run(c, &st);
+        lap("run");
         if (rc != FLUERE_E_TABLE_FULL || o.max_flows >= (1ull << 26)) break;  // (MAX_FLOWS)
         fluere_close(c);
         c = nullptr;
@@ -167,8 +179,11 @@ extern "C" int fluere_offline_file(const char* pcap_path, uint64_t timeout_ms, i
     fluere_record* recs = nullptr;
     uint64_t nr = 0, ne = 0;
     rc = fluere_get_records(c, &recs, &nr, &ne);
+    lap("records");
     if (!rc) rc = fluere_write_csv(recs, nr, out.c_str());
+    lap("csv");
     fluere_records_free(recs);
     fluere_close(c);
+    lap("close");
     return rc ? rc : run_rc;
 }

@@ -165,13 +165,14 @@ def test_spill_overflow_list(gpu, name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["c1_udp64_1flow", "c2_udp64_small", "c3_imix_small", "many_flows", "slow_small",
-                                  "slow_many_flows", "c3_imix_2m"])
+                                  "slow_many_flows", "c3_imix_2m", "c5u_mac_small", "c5_vlan_small", "slow_mac"])
 @pytest.mark.parametrize("cap", [None, "3"])
 def test_spill_kernel_matches_oracle(gpu, name, cap, monkeypatch):
     """k_parse_spill (the hot pass for many flows per window: every valid
     packet through the per-owner LDS bins into its owner's segment, full bins
-    written out by the wave) forced on every capture kind, also with owner
-    segments of 3 records (nearly every record through the overflow list)."""
+    written out by the wave) forced on every capture kind -- MAC keys (-M)
+    with 64-byte records -- also with owner segments of 3 records (nearly
+    every record through the overflow list)."""
     monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
     if cap:
         monkeypatch.setenv("FLUERE_OWNER_CAP", cap)
@@ -608,6 +609,63 @@ def test_file_ingest_across_chunks(gpu, tmp_path):
     st = fluere_amd.fluereflow_fileparse(fluere_amd.Args(fluere_amd.Files(file=str(path))), out_dir=str(tmp_path / "out"))
     got = (tmp_path / "out" / "cap_converted.csv").read_text()
     assert_csv_equal(got, st["ended"], want["csv"], want["n_ended"], "fluere_offline_file")
+
+
+def _ingest_case(case):
+    """Captures of 2-3 staging chunks that test the reader threads' record
+    chains (fluere_gpu.hip, Ingest): payloads full of plausible record headers,
+    a bad record mid-capture, a byte-swapped nanosecond capture, and records
+    of ~200 KB (within and over the global header's snaplen)."""
+    import struct
+
+    import pktbuild as pb
+    if case == "bad_mid":
+        data = bytearray(fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 260_000, 4000, 0xF13E)))
+        off = 24
+        while off < 45 << 20:
+            off += 16 + struct.unpack_from("<I", data, off + 8)[0]
+        struct.pack_into("<I", data, off + 8, 1 << 20)  # caplen over 256 KiB: libpcap stops here
+        return bytes(data)
+    pk = []
+    if case == "embedded":
+        fake = b"".join(struct.pack("<IIII", 1_700_000_000, 1000 + i, 20, 20) + bytes(20) for i in range(24))
+        for i in range(90_000):
+            f = pb.eth() + pb.ipv4("10.2.0.1", f"10.2.{i % 200}.9", 17, pb.udp(4000 + i % 17, 53, fake[: 600 + 36 * (i % 9)]))
+            pk.append((1_700_000_000 + i // 1000, i % 1000 * 1000, f))
+        return pb.pcap(pk, snaplen=65535)
+    if case == "swapped_ns":
+        for i in range(60_000):
+            f = pb.eth() + pb.ipv4("10.3.0.1", f"10.3.{i % 250}.7", 17, pb.udp(7000 + i % 13, 9000, bytes(1100 + i % 97)))
+            pk.append((1_700_000_000 + i // 5000, (i * 77_777) % 1_000_000_000, f))
+        return pb.pcap(pk, nsec=True, swapped=True)
+    big = case == "jumbo_over_snaplen"
+    for i in range(420):
+        f = pb.eth() + pb.ipv4("10.4.0.1", f"10.4.0.{i % 50}", 17, pb.udp(1000 + i % 7, 2000, bytes(972)), tl=1000)
+        f = f + bytes((200_000 if i % 2 == 0 else 120_000 + 13 * i) - len(f))
+        pk.append((1_700_000_000 + i, 0, f))
+    return pb.pcap(pk, snaplen=65535 if big else 262144)
+
+
+@pytest.mark.parametrize("case", ["embedded", "bad_mid", "swapped_ns", "jumbo", "jumbo_over_snaplen"])
+def test_file_ingest_reader_chains(gpu, tmp_path, case):
+    """The file and host-buffer ingests index each chunk on its reader thread
+    from a guessed record start; the calling thread keeps libpcap's walk
+    exact (record count and flows equal the oracle's on the same bytes)."""
+    data = _ingest_case(case)
+    assert len(data) > 60 << 20  # two staging chunks and more
+    want = pyoracle.offline(data)
+    path = tmp_path / "cap.pcap"
+    path.write_bytes(data)
+    for attach in ("file", "host"):
+        with fluere_amd.FlowContext(max_flows=1 << 16) as ctx:
+            if attach == "file":
+                ctx.add_pcap_file(str(path))
+            else:
+                ctx.add_host_pcap(data)
+            assert ctx.n_packets == want["packets"], (attach, ctx.n_packets, want["packets"])
+            ctx.run()
+            recs, ne = ctx.records()
+        assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"{case} {attach}")
 
 
 def test_truncated_tail_record(gpu, tmp_path):

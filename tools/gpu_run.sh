@@ -4,7 +4,7 @@
 #   tools/gpu_run.sh <tag> <steps...>
 # steps: tests[:<pytest -k expr>]  smoke  bench  cfg:<config>  cold:<config>  prof:<config>
 #        trace:<config> (kernel timeline of the last step)  debug:<config> (FLUERE_DEBUG counters)
-#        vtrace:<variant>:<config>  hostinc:<config> (host-inclusive rate)
+#        vtrace:<variant>:<config>  hostinc:<config> (host-inclusive rate)  h2d (copy rates)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TAG=$1
@@ -54,6 +54,9 @@ for st in "$@"; do
       c=${st#hostinc:}
       FLUERE_HOSTPROF=1 timeout -k 10 300 python -u tools/host_inclusive.py --config $c > "$O/hostinc_$c.log" 2>&1
       tail -3 "$O/hostinc_$c.log" ;;
+    h2d)  # host -> HBM copy rate by staging allocation kind
+      timeout -k 10 120 ./tools/h2d_probe 4096 32 > "$O/h2d.log" 2>&1
+      cat "$O/h2d.log" ;;
     debug:*)
       c=${st#debug:}
       FLUERE_DEBUG=1 timeout -k 10 240 python -u bench.py --config $c --no-cpu-baseline --no-imix --steps 2 --warmup 1 > "$O/debug_$c.log" 2>&1
