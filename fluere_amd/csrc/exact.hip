@@ -277,6 +277,33 @@ __global__ void __launch_bounds__(256) k_ex_tindex(uint64_t n, const ExMeta* cm,
     tbl[b] = (uint32_t)lo;
 }
 
+// Mode B, one pass over the capture-order times: monotonicity (*bad), and
+// the time-bucket index of k_ex_tindex as range starts (starts[b] = the first
+// packet of bucket b's range, written by that packet; zero elsewhere) for an
+// inclusive max-scan.  The buckets are k_ex_tindex's: t0 = t_0, nb given,
+// bw = (t_last - t0) / nb + 1 (the host computes the same from the same
+// times); with times that go backwards the index is not used.
+__global__ void __launch_bounds__(256) k_ex_tscan(uint64_t n, const ExMeta* cm, uint64_t nb, uint32_t* starts,
+                                                  uint32_t* bad) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long t0 = cm[0].t, tl = cm[n - 1].t;
+    const uint64_t bw = max((uint64_t)1, (tl > t0 ? tl - t0 : 0) / nb + 1);
+    auto bucket = [&](unsigned long long v) -> uint64_t { return v <= t0 ? 0 : min(nb, (uint64_t)((v - t0) / bw)); };
+    bool back = false;
+    if (k < n) {
+        const unsigned long long t = cm[k].t;
+        const uint64_t bk = bucket(t);
+        if (k > 0) {
+            const unsigned long long tp = cm[k - 1].t;
+            back = t < tp;
+            const uint64_t bp = bucket(tp);
+            if (bk > bp) starts[bp + 1] = (uint32_t)k;  // buckets (bp, bk] start at k
+        }
+        if (k == n - 1 && bk + 1 <= nb) starts[bk + 1] = (uint32_t)n;  // the buckets past the last time
+    }
+    if (__ballot(back) && (threadIdx.x & 63) == 0) *bad = 1u;
+}
+
 // reversed "k if processed" for the next-processed min-scan
 __global__ void __launch_bounds__(256) k_ex_proc_in(uint64_t n, const uint8_t* pr, unsigned long long* npr) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -355,10 +382,55 @@ __device__ __forceinline__ unsigned long long exp_of(uint64_t t, uint64_t timeou
     return t + timeout_us < t ? NONE64 : t + timeout_us;  // (saturating)
 }
 
+// The first position in [lo, hi) whose value is >= x (values non-decreasing
+// over the range), hi if none.  Eight probes a round, their loads in flight
+// together: the chase is a chain of dependent loads per key, and an elephant
+// key's searches were its longest links (log2 of its packets, one load each).
+template <class Get>
+__device__ __forceinline__ uint64_t lower_bound8(uint64_t lo, uint64_t hi, unsigned long long x, Get get) {
+    while (hi - lo > 8) {
+        const uint64_t step = (hi - lo) / 9 + 1;
+        unsigned long long v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint64_t q = lo + (uint64_t)(i + 1) * step;
+            v[i] = q < hi ? get(q) : NONE64;
+        }
+        int cnt = 0;  // probes below x: a prefix
+#pragma unroll
+        for (int i = 0; i < 8; i++) cnt += (lo + (uint64_t)(i + 1) * step < hi && v[i] < x) ? 1 : 0;
+        const uint64_t nlo = cnt ? lo + (uint64_t)cnt * step + 1 : lo;
+        const uint64_t nq = lo + (uint64_t)(cnt + 1) * step;
+        hi = cnt < 8 && nq < hi ? nq : hi;
+        lo = nlo;
+    }
+    unsigned long long v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = lo + i < hi ? get(lo + i) : NONE64;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) cnt += (lo + i < hi && v[i] < x) ? 1 : 0;
+    return lo + cnt;
+}
+
 // sweep point of the entry pushed at sorted position c: the first processed
 // packet k >= c (capture order) with t_k >= exp -> its packet index
-__device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, uint32_t c, unsigned long long exp) {
-    const uint32_t k0 = a.sval[c];
+// (k0 = sval[c] and the time bucket's range [lo, hi) are loaded by the caller,
+// before the stores of the queue insert, so that they are in flight early)
+__device__ __forceinline__ void sweep_bucket(const ChaseArgs& a, unsigned long long exp, uint64_t& lo, uint64_t& hi) {
+    lo = 0;
+    hi = a.n;
+    if (a.fext || a.tree || exp == NONE64) return;
+    if (exp <= a.t0) {
+        hi = 0;
+    } else {
+        const uint64_t b = (exp - a.t0) / a.bw;
+        if (b >= a.nb) lo = a.n;
+        else { lo = a.tbl[b]; hi = a.tbl[b + 1]; }
+    }
+}
+__device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, uint32_t k0, unsigned long long exp,
+                                                          uint64_t lo, uint64_t hi) {
     if (a.fext) return a.fext[k0];
     if (exp == NONE64) return NONE64;
     if (a.tree) {
@@ -367,19 +439,7 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     }
     // non-decreasing times: lower_bound (within the exp's time bucket), then
     // the next processed packet
-    uint64_t lo = 0, hi = a.n;
-    if (exp <= a.t0) {
-        hi = 0;
-    } else {
-        const uint64_t b = (exp - a.t0) / a.bw;
-        if (b >= a.nb) lo = a.n;
-        else { lo = a.tbl[b]; hi = a.tbl[b + 1]; }
-    }
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (a.cm[mid].t < exp) lo = mid + 1;
-        else hi = mid;
-    }
+    lo = lower_bound8(lo, hi, exp, [&](uint64_t q) { return (unsigned long long)a.cm[q].t; });
     const uint64_t k = max((uint64_t)k0, lo);
     if (k >= a.n) return NONE64;
     const unsigned long long kp = a.np_rev[a.n - 1 - k];
@@ -440,11 +500,18 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         const uint32_t c = (uint32_t)ce;
         const ExMeta mc = a.sm[c];
         const uint32_t o = mc.dir;
+        // the loads that depend on c alone, issued before the queue's stores
+        const unsigned long long fe = a.nf_rev[a.n - 1 - c] & MP;
+        const unsigned long long fg = fe != MP ? a.sm[fe].gidx : 0;
         unsigned long long jf = NONE64;
         uint32_t front = NOPOS;
         if (a.mode_b) {
+            const uint32_t k0 = a.sval[c];
+            const unsigned long long ex = exp_of(mc.t, a.timeout_us);
+            uint64_t blo, bhi;
+            sweep_bucket(a, ex, blo, bhi);
             drop_upto(mc.gidx, false);  // entries that fired while the key had no flow
-            a.ej[c] = sweep_point(a, c, exp_of(mc.t, a.timeout_us));
+            a.ej[c] = sweep_point(a, k0, ex, blo, bhi);
             // sorted insert, from the tail (non-decreasing times: at the tail)
             uint32_t p = qt[o];
             while (p != NOPOS && before(c, p)) p = a.plink[p];
@@ -461,22 +528,16 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
             front = qh[o];
             jf = a.ej[front];
         }
-        const unsigned long long fe = a.nf_rev[a.n - 1 - c] & MP;
         uint32_t end;
         uint8_t kind;
         unsigned long long cj = NONE64, cie = 0, cex = 0;
-        if (fe != MP && (jf == NONE64 || a.sm[fe].gidx <= jf)) {  // FIN/RST first (the sweep runs after it)
+        if (fe != MP && (jf == NONE64 || fg <= jf)) {  // FIN/RST first (the sweep runs after it)
             end = (uint32_t)fe;
             kind = K_FIN;
-            cj = a.sm[fe].gidx;
+            cj = fg;
         } else if (jf != NONE64) {  // swept: the key's last packet at or before the sweeping packet
-            uint32_t lo = c, hi = pend - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (a.sm[mid].gidx <= jf) lo = mid;
-                else hi = mid - 1;
-            }
-            end = lo;
+            // (sm[c].gidx <= jf: the entry fires at or after its creation)
+            end = (uint32_t)max((uint64_t)c, lower_bound8(c, pend, jf + 1, [&](uint64_t q) { return (unsigned long long)a.sm[q].gidx; }) - 1);
             kind = K_SWEEP;
             cj = jf;
             cie = a.sm[front].gidx;
@@ -983,6 +1044,9 @@ static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* 
         (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                           hipcub::Min(), n, s);
         tmp = std::max(tmp, t);
+        (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, hipcub::Max(),
+                                                n / 16 + 2, s);
+        tmp = std::max(tmp, t);
     }
     if (tmp_out) *tmp_out = tmp;
     return bytes_for(N, N, tmp);
@@ -1127,10 +1191,20 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, hf, hpos, in, s));
     k_ex_heads<<<gridn(n, 256), 256, 0, s>>>(n, hf, hpos, heads);
     HIPCHECK(hipMemsetAsync(ctr, 0, 16, s));
-    if (J.mode_b) {
+    // Mode B: monotonicity and the time-bucket index in one pass (a max-scan
+    // of range starts, no binary searches); small runs: the two kernels
+    const uint64_t nb_dev = n / 16 + 1;
+    const bool tscan = J.mode_b && n >= 64;
+    if (tscan) {
+        uint32_t* starts = S->idx;  // (free until the seed requests; n >= nb + 1)
+        HIPCHECK(hipMemsetAsync(starts, 0, (nb_dev + 1) * 4, s));
+        k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, nb_dev, starts, ctr + 1);
+        tb = tmp;
+        HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, starts, S->tbl, hipcub::Max(), (int)(nb_dev + 1), s));
+    } else if (J.mode_b) {
         k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1);
-        HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed
     }
+    if (J.mode_b) HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed
     // one host read: key count, monotonicity, the first and last times.  Mode
     // A (not shard mode) needs none of them on the host: the key count stays
     // on the device and the chase's grid covers the replayed packets (every
@@ -1166,9 +1240,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     if (J.mode_b && S->mono) {
         const unsigned long long tt[2] = {hv[3], hv[4]};
         t0 = tt[0];
-        nb = n / 16 + 1;
-        bw = std::max<uint64_t>(1, (tt[1] - tt[0]) / nb + 1);  // nb * bw > the span
-        k_ex_tindex<<<gridn(nb + 1, 256), 256, 0, s>>>(n, cm, t0, bw, nb, S->tbl);
+        nb = nb_dev;
+        bw = std::max<uint64_t>(1, (tt[1] - tt[0]) / nb + 1);  // nb * bw > the span (k_ex_tscan's buckets)
+        if (!tscan) k_ex_tindex<<<gridn(nb + 1, 256), 256, 0, s>>>(n, cm, t0, bw, nb, S->tbl);
         HIPCHECK(hipGetLastError());
     }
     S->ca = ChaseArgs{n, S->n_keys, heads, sm, sval, ne_rev, nf_rev, J.mode_b, J.timeout_us, cm, S->np_rev,

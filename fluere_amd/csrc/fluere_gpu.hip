@@ -3891,6 +3891,7 @@ struct fluere_ctx {
 };
 
 static int prepare_capture(fluere_ctx* c);
+static int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m);
 
 static void reset_record_counters(fluere_ctx* c) {
     char* g = (char*)c->d_glob;
@@ -3909,15 +3910,36 @@ static void reset_record_counters(fluere_ctx* c) {
 // order is the reference's; this one is deterministic.
 static int fetch_records(fluere_ctx* c) {
     if (c->host_recs) return FLUERE_OK;
+    static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     hipStream_t s = c->stream;
     const uint64_t n = c->dev_n_rec;
     c->recs.resize(n);
     c->aux.assign(c->has_aux ? 2 * n : 0, 0ull);
+    // many active flows after a device ordering: sorted by first packet on the
+    // device (stable radix sort, the host sort's order), into d_recs2
+    const uint64_t ne0 = c->dev_ordered ? std::min<uint64_t>(c->dev_ordered_ended, n) : 0;
+    const bool dev_act = c->dev_ordered && !c->has_aux && n - ne0 >= 4096 && sort_actives(c, ne0, n - ne0) == FLUERE_OK;
+    if (dev_act) {
+        if (ne0) HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, ne0 * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipMemcpyAsync(c->recs.data() + ne0, c->d_recs2, (n - ne0) * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (hostprof)
+            fprintf(stderr, "[fluere] records: %llu to the host (%llu actives sorted on the device) %.1f ms\n",
+                    (unsigned long long)n, (unsigned long long)(n - ne0),
+                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        c->n_ended = ne0;
+        c->host_recs = true;
+        return FLUERE_OK;
+    }
     if (n)
         HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
     if (n && c->has_aux)
         HIPCHECK(hipMemcpyAsync(c->aux.data(), c->d_recaux, 2 * n * 8, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
+    if (hostprof)
+        fprintf(stderr, "[fluere] records: %llu to the host %.1f ms\n", (unsigned long long)n,
+                1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     if (c->dev_ordered) {
         const uint64_t ne = std::min<uint64_t>(c->dev_ordered_ended, n);
         auto& R = c->recs;
@@ -4347,15 +4369,15 @@ constexpr uint64_t kMaxBatch = (1ull << 32) - (1ull << 20);
 constexpr int kIngestSlots = 8;  // at most; FLUERE_INGEST_SLOTS / _READERS (diagnostics) pick fewer
 static uint64_t ingest_chunk() {  // staging chunk bytes (FLUERE_INGEST_CHUNK_MB: diagnostics)
     static const uint64_t v =
-        (uint64_t)(getenv("FLUERE_INGEST_CHUNK_MB") ? std::max(1, std::min(64, atoi(getenv("FLUERE_INGEST_CHUNK_MB")))) : 32) << 20;
+        (uint64_t)(getenv("FLUERE_INGEST_CHUNK_MB") ? std::max(1, std::min(64, atoi(getenv("FLUERE_INGEST_CHUNK_MB")))) : 4) << 20;
     return v;
 }
 static int ingest_slots() {
-    static const int v = getenv("FLUERE_INGEST_SLOTS") ? std::max(2, std::min(kIngestSlots, atoi(getenv("FLUERE_INGEST_SLOTS")))) : 4;
+    static const int v = getenv("FLUERE_INGEST_SLOTS") ? std::max(2, std::min(kIngestSlots, atoi(getenv("FLUERE_INGEST_SLOTS")))) : 8;
     return v;
 }
 static int ingest_readers() {
-    static const int v = getenv("FLUERE_INGEST_READERS") ? std::max(1, std::min(16, atoi(getenv("FLUERE_INGEST_READERS")))) : 3;
+    static const int v = getenv("FLUERE_INGEST_READERS") ? std::max(1, std::min(16, atoi(getenv("FLUERE_INGEST_READERS")))) : 8;
     return v;
 }
 constexpr uint64_t kFillPiece = 512ull << 10;  // a reader fills and walks this much at a time (in L2)
@@ -5811,6 +5833,46 @@ static int grow_pair(void** a, void** b, uint64_t* cap_b, uint64_t cap_a, size_t
     if (hipMalloc(b, cap_a * unit) != hipSuccess) return FLUERE_E_NOMEM;
     *cap_b = cap_a;
     (void)a;
+    return FLUERE_OK;
+}
+
+// The active tail [ne, ne + m) of d_recs sorted by first packet (stable: the
+// run's order among equal ones) into d_recs2 [0, m).
+__global__ void k_act_keys(const fluere_record* r, uint64_t m, unsigned long long* keys, uint32_t* vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    keys[i] = r[i].first;
+    vals[i] = (uint32_t)i;
+}
+__global__ void k_act_gather(const fluere_record* src, const uint32_t* perm, uint64_t m, fluere_record* dst) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one word of one record
+    if (e >= m * REC_WORDS) return;
+    const uint64_t j = e / REC_WORDS, k = e - j * REC_WORDS;
+    reinterpret_cast<uint64_t*>(dst)[e] = reinterpret_cast<const uint64_t*>(src)[(uint64_t)perm[j] * REC_WORDS + k];
+}
+
+static int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m) {
+    if (m >= (1ull << 31) || !m) return FLUERE_E_ARG;
+    hipStream_t s = c->stream;
+    int rc = grow_pair((void**)&c->d_recs, (void**)&c->d_recs2, &c->d_recs2_cap, c->d_recs_cap, sizeof(fluere_record));
+    if (rc || c->d_recs2_cap < m) return rc ? rc : FLUERE_E_NOMEM;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, 64, s);
+    if ((rc = ord_scratch(c, 2 * al(m * 8) + 2 * al(m * 4) + al(tb)))) return rc;
+    char* p = (char*)c->d_ord;
+    auto take = [&](size_t bytes) { char* q = p; p += al(bytes); return q; };
+    unsigned long long* k0 = (unsigned long long*)take(m * 8);
+    unsigned long long* k1 = (unsigned long long*)take(m * 8);
+    uint32_t* v0 = (uint32_t*)take(m * 4);
+    uint32_t* v1 = (uint32_t*)take(m * 4);
+    const fluere_record* act = c->d_recs + ne;
+    k_act_keys<<<grid_for(m, 256), 256, 0, s>>>(act, m, k0, v0);
+    size_t t = tb;
+    HIPCHECK(hipcub::DeviceRadixSort::SortPairs(p, t, k0, k1, v0, v1, (int)m, 0, 64, s));
+    k_act_gather<<<grid_for(m * REC_WORDS, 256), 256, 0, s>>>(act, v1, m, c->d_recs2);
+    HIPCHECK(hipGetLastError());
     return FLUERE_OK;
 }
 

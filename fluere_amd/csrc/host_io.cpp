@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fluere_gpu.h"
@@ -81,34 +82,57 @@ const char* kHeader =
 
 }  // namespace
 
+// one row (FlowRecord's csv order, fluereflow.rs / exporter)
+static void put_row(Out& o, const fluere_record& r) {
+    o.ip(r.src_v6, r.source);
+    o.put(",", 1);
+    o.ip(r.dst_v6, r.destination);
+    const uint64_t v[] = {r.src_port, r.dst_port, r.prot, r.d_pkts, r.d_octets, r.in_pkts, r.out_pkts,
+                          r.in_bytes, r.out_bytes, r.first, r.last, r.min_pkt, r.max_pkt, r.min_ttl,
+                          r.max_ttl, r.cnt[0], r.cnt[1], r.cnt[2], r.cnt[3], r.cnt[4], r.cnt[5],
+                          r.cnt[6], r.cnt[7], r.cnt[8], r.tos};
+    for (uint64_t x : v) { o.put(",", 1); o.u(x); }
+    o.put("\n", 1);
+}
+
+// a row is at most two IPv6 texts (39) and 25 numbers of 20 digits, with separators
+constexpr uint64_t kRowMax = 2 * 39 + 25 * 20 + 27;
+
 extern "C" uint64_t fluere_format_csv(const fluere_record* recs, uint64_t n, char* buf, uint64_t cap) {
     Out o{buf, cap, 0};
     o.put(kHeader);
-    for (uint64_t i = 0; i < n; i++) {
-        const fluere_record& r = recs[i];
-        o.ip(r.src_v6, r.source);
-        o.put(",", 1);
-        o.ip(r.dst_v6, r.destination);
-        const uint64_t v[] = {r.src_port, r.dst_port, r.prot, r.d_pkts, r.d_octets, r.in_pkts, r.out_pkts,
-                              r.in_bytes, r.out_bytes, r.first, r.last, r.min_pkt, r.max_pkt, r.min_ttl,
-                              r.max_ttl, r.cnt[0], r.cnt[1], r.cnt[2], r.cnt[3], r.cnt[4], r.cnt[5],
-                              r.cnt[6], r.cnt[7], r.cnt[8], r.tos};
-        for (uint64_t x : v) { o.put(",", 1); o.u(x); }
-        o.put("\n", 1);
-    }
+    for (uint64_t i = 0; i < n; i++) put_row(o, recs[i]);
     return o.n;
 }
 
+// Rows are formatted once, in blocks by threads when there are many, and
+// written in order.
 extern "C" int fluere_write_csv(const fluere_record* recs, uint64_t n, const char* path) {
     if (!path || (!recs && n)) return FLUERE_E_ARG;
-    uint64_t need = fluere_format_csv(recs, n, nullptr, 0);
-    std::vector<char> b(need);
-    fluere_format_csv(recs, n, b.data(), need);
+    const int T = n >= (1u << 16) ? 8 : 1;
+    std::vector<std::string> part(T);
+    auto work = [&](int t) {
+        const uint64_t i0 = n * t / T, i1 = n * (t + 1) / T, blk = 4096;
+        std::vector<char> tmp(blk * kRowMax);
+        for (uint64_t b = i0; b < i1; b += blk) {
+            Out o{tmp.data(), tmp.size(), 0};
+            for (uint64_t i = b; i < std::min(i1, b + blk); i++) put_row(o, recs[i]);
+            part[t].append(tmp.data(), o.n);
+        }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++) th.emplace_back(work, t);
+        for (auto& x : th) x.join();
+    }
     FILE* f = fopen(path, "wb");
     if (!f) return FLUERE_E_IO;
-    size_t w = fwrite(b.data(), 1, need, f);
-    int rc = fclose(f);
-    return (w == need && rc == 0) ? FLUERE_OK : FLUERE_E_IO;
+    bool ok = fwrite(kHeader, 1, strlen(kHeader), f) == strlen(kHeader);
+    for (const auto& p : part) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+    const int rc = fclose(f);
+    return (ok && rc == 0) ? FLUERE_OK : FLUERE_E_IO;
 }
 
 static std::string file_stem(const std::string& p) {

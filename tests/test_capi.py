@@ -55,6 +55,22 @@ def test_csv_writer_matches_golden(name):
         assert fluere_amd.format_csv(recs) == want
 
 
+def test_csv_file_writer_blocks(tmp_path):
+    """fluere_write_csv formats blocks of rows on threads: the file equals the
+    one-pass formatter's text (rows past 2^16, v4 and v6 mixed)."""
+    rng = np.random.default_rng(0xC5F)
+    n = 70_001
+    recs = np.zeros(n, dtype=_lib.RECORD_DTYPE)
+    raw = recs.view(np.uint8).reshape(n, -1)
+    raw[:] = rng.integers(0, 256, raw.shape, dtype=np.uint8)
+    recs["src_v6"] = rng.integers(0, 2, n)
+    recs["dst_v6"] = rng.integers(0, 2, n)
+    path = tmp_path / "w.csv"
+    buf = np.ascontiguousarray(recs)
+    assert _lib.lib().fluere_write_csv(buf.ctypes.data, n, str(path).encode()) == 0
+    assert path.read_text() == fluere_amd.format_csv(buf)
+
+
 def test_csv_writer_ipv6_display():
     recs = np.zeros(4, dtype=RECORD_DTYPE)
     cases = ["::", "::ffff:1.2.3.4", "1:0:0:1:0:0:0:1", "2001:db8:0:1:1:1:1:1"]

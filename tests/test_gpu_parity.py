@@ -269,7 +269,8 @@ CENSUS = {
     "tcp_2m": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007, False, 600000, "k_parse_spill"),
     "tcp_2m_t1": (_lib.SYNTH_TCP, 2_000_000, 20_000, 0xF10E0007, False, 1000, "k_parse_spill"),
     "slow_2m": (_lib.SYNTH_SLOW, 2_000_000, 10_000, 0xF10E0008, False, 600000, "k_slow"),
-    "c5u_mac": (_lib.SYNTH_MAC64, 1_000_000, 50_000, 0xF10E0005, True, 600000, "k_parse_agg"),
+    "c5u_mac": (_lib.SYNTH_MAC64, 1_000_000, 50_000, 0xF10E0005, True, 600000, "k_parse_spill"),
+    "mac_few": (_lib.SYNTH_MAC64, 1_000_000, 300, 0xF10E0015, True, 600000, "k_parse_agg"),
 }
 
 
