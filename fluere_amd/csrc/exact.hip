@@ -376,41 +376,20 @@ struct ChaseArgs {
     uint32_t* annex_of;
     const uint8_t* flow_key;  // TableSet::flow_key (56-byte canonical keys by dense id)
     const uint32_t* d_nkeys = nullptr;  // Mode A: the key count, written on the device (no host read)
+    // Incremental Mode B passes (non-decreasing times, one GPU; null: off).  A
+    // key's chase depends on the processed set only through its sweep
+    // lookups, so a pass re-chases only the keys one of whose lookups now
+    // answers differently (k_ex_check) and keeps the other keys' instances.
+    uint8_t* stamp = nullptr;         // per position: the pass that made it an instance start
+    uint8_t* kpass = nullptr;         // per key: the pass that last chased it
+    const uint8_t* kdirty = nullptr;  // the keys this pass chases (null: every key)
+    uint32_t* elook = nullptr;        // per creation: its sweep lookup's start position (NOPOS: none)
+    uint32_t* ekp = nullptr;          //               the answer (capture index; NOPOS: none)
+    uint32_t pass_id = 0;
 };
 
 __device__ __forceinline__ unsigned long long exp_of(uint64_t t, uint64_t timeout_us) {
     return t + timeout_us < t ? NONE64 : t + timeout_us;  // (saturating)
-}
-
-// The first position in [lo, hi) whose value is >= x (values non-decreasing
-// over the range), hi if none.  Eight probes a round, their loads in flight
-// together: the chase is a chain of dependent loads per key, and an elephant
-// key's searches were its longest links (log2 of its packets, one load each).
-template <class Get>
-__device__ __forceinline__ uint64_t lower_bound8(uint64_t lo, uint64_t hi, unsigned long long x, Get get) {
-    while (hi - lo > 8) {
-        const uint64_t step = (hi - lo) / 9 + 1;
-        unsigned long long v[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint64_t q = lo + (uint64_t)(i + 1) * step;
-            v[i] = q < hi ? get(q) : NONE64;
-        }
-        int cnt = 0;  // probes below x: a prefix
-#pragma unroll
-        for (int i = 0; i < 8; i++) cnt += (lo + (uint64_t)(i + 1) * step < hi && v[i] < x) ? 1 : 0;
-        const uint64_t nlo = cnt ? lo + (uint64_t)cnt * step + 1 : lo;
-        const uint64_t nq = lo + (uint64_t)(cnt + 1) * step;
-        hi = cnt < 8 && nq < hi ? nq : hi;
-        lo = nlo;
-    }
-    unsigned long long v[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = lo + i < hi ? get(lo + i) : NONE64;
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) cnt += (lo + i < hi && v[i] < x) ? 1 : 0;
-    return lo + cnt;
 }
 
 // sweep point of the entry pushed at sorted position c: the first processed
@@ -429,8 +408,9 @@ __device__ __forceinline__ void sweep_bucket(const ChaseArgs& a, unsigned long l
         else { lo = a.tbl[b]; hi = a.tbl[b + 1]; }
     }
 }
-__device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, uint32_t k0, unsigned long long exp,
-                                                          uint64_t lo, uint64_t hi) {
+__device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, uint32_t c, uint32_t k0,
+                                                          unsigned long long exp, uint64_t lo, uint64_t hi) {
+    if (a.elook) a.elook[c] = NOPOS;  // (a lookup that no processed set changes)
     if (a.fext) return a.fext[k0];
     if (exp == NONE64) return NONE64;
     if (a.tree) {
@@ -439,10 +419,18 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     }
     // non-decreasing times: lower_bound (within the exp's time bucket), then
     // the next processed packet
-    lo = lower_bound8(lo, hi, exp, [&](uint64_t q) { return (unsigned long long)a.cm[q].t; });
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a.cm[mid].t < exp) lo = mid + 1;
+        else hi = mid;
+    }
     const uint64_t k = max((uint64_t)k0, lo);
     if (k >= a.n) return NONE64;
     const unsigned long long kp = a.np_rev[a.n - 1 - k];
+    if (a.elook) {
+        a.elook[c] = (uint32_t)k;
+        a.ekp[c] = kp == MP ? NOPOS : (uint32_t)kp;
+    }
     return kp == MP ? NONE64 : a.cm[kp].gidx;
 }
 
@@ -450,6 +438,8 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n_keys = a.d_nkeys ? *a.d_nkeys : a.n_keys;
     if (q >= n_keys) return;
+    if (a.kdirty && !a.kdirty[q]) return;  // incremental pass: this key's instances stand
+    if (a.kpass) a.kpass[q] = (uint8_t)a.pass_id;
     const uint32_t p0 = a.heads[q];
     const uint32_t pend = q + 1 < n_keys ? a.heads[q + 1] : (uint32_t)a.n;
     // pending expiry entries per orientation, sorted by (sweep point, exp,
@@ -511,7 +501,7 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
             uint64_t blo, bhi;
             sweep_bucket(a, ex, blo, bhi);
             drop_upto(mc.gidx, false);  // entries that fired while the key had no flow
-            a.ej[c] = sweep_point(a, k0, ex, blo, bhi);
+            a.ej[c] = sweep_point(a, c, k0, ex, blo, bhi);
             // sorted insert, from the tail (non-decreasing times: at the tail)
             uint32_t p = qt[o];
             while (p != NOPOS && before(c, p)) p = a.plink[p];
@@ -536,8 +526,13 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
             kind = K_FIN;
             cj = fg;
         } else if (jf != NONE64) {  // swept: the key's last packet at or before the sweeping packet
-            // (sm[c].gidx <= jf: the entry fires at or after its creation)
-            end = (uint32_t)max((uint64_t)c, lower_bound8(c, pend, jf + 1, [&](uint64_t q) { return (unsigned long long)a.sm[q].gidx; }) - 1);
+            uint32_t lo = c, hi = pend - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (a.sm[mid].gidx <= jf) lo = mid;
+                else hi = mid - 1;
+            }
+            end = lo;
             kind = K_SWEEP;
             cj = jf;
             cie = a.sm[front].gidx;
@@ -546,7 +541,8 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
             end = pend - 1;
             kind = K_ACTIVE;
         }
-        a.sflag[c] = 1;
+        if (a.stamp) a.stamp[c] = (uint8_t)a.pass_id;
+        else a.sflag[c] = 1;
         a.iend[c] = end;
         a.ikind[c] = kind;
         a.ij[c] = cj;
@@ -563,6 +559,26 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         if (a.mode_b && kind != K_ACTIVE) drop_upto(cj, true);
         pos = end + 1;
     }
+}
+
+// incremental pass: key q is dirty when one of the lookups of its last chase
+// (at its instance starts, the previous pass's sflag) answers differently over
+// this pass's processed set
+__global__ void __launch_bounds__(256) k_ex_check(uint64_t n, const uint32_t* sflag, const uint32_t* elook,
+                                                  const uint32_t* ekp, const unsigned long long* np_rev,
+                                                  const uint32_t* hf, const uint32_t* hpos, uint8_t* kdirty) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n || !sflag[p]) return;
+    const uint32_t L = elook[p];
+    if (L == NOPOS) return;
+    const unsigned long long kp = np_rev[n - 1 - L];
+    if ((kp == MP ? NOPOS : (uint32_t)kp) != ekp[p]) kdirty[hpos[p] + hf[p] - 1] = 1;
+}
+// the instance starts of every key's last chase
+__global__ void __launch_bounds__(256) k_ex_flags(uint64_t n, const uint8_t* stamp, const uint8_t* kpass,
+                                                  const uint32_t* hf, const uint32_t* hpos, uint32_t* sflag) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) sflag[p] = stamp[p] == kpass[hpos[p] + hf[p] - 1] ? 1u : 0u;
 }
 
 // ---- 5. members, processed set, reduction keys ------------------------------
@@ -995,6 +1011,9 @@ struct ExactSession {
     uint32_t *val, *sval, *hf, *hpos, *heads, *link, *plink, *sflag, *iend, *incl, *ist, *alist, *ctr, *tbl;
     uint32_t *idx, *ikey;
     uint8_t *pr, *ikind, *irole;
+    uint8_t *stamp, *kpass, *kdirty;
+    uint32_t *elook, *ekp;
+    uint32_t pass_no = 0;
     Agg* aggs;
     fluere_flow_annex* annex = nullptr;
     ChaseArgs ca;
@@ -1024,6 +1043,7 @@ static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* 
         add(n * sizeof(Agg)); add(16);                                // aggs, nruns/counters
         add(n * 4); add(n * 8);                                       // idx, hi2 (seed requests)
         add(n); add(n * 4);                                           // irole, ikey
+        add(n); add(n); add(n); add(n * 4); add(n * 4);               // stamp, kpass, kdirty, elook, ekp
         if (J.mode_b) add(2 * P * 8);                                 // tree
         add((n / 16 + 4) * 4);                                        // tbl
         add(tmp);
@@ -1137,6 +1157,11 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     S->ej = A.take<unsigned long long>(N);
     S->link = A.take<uint32_t>(N);
     S->plink = A.take<uint32_t>(N);
+    S->stamp = A.take<uint8_t>(N);
+    S->kpass = A.take<uint8_t>(N);
+    S->kdirty = A.take<uint8_t>(N);
+    S->elook = A.take<uint32_t>(N);
+    S->ekp = A.take<uint32_t>(N);
     S->sflag = A.take<uint32_t>(N);
     S->iend = A.take<uint32_t>(N);
     S->ikind = A.take<uint8_t>(N);
@@ -1275,8 +1300,34 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
             if (rc) return rc;
         }
     }
-    HIPCHECK(hipMemsetAsync(S->sflag, 0, n * 4, s));
-    k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
+    // incremental passes: non-decreasing times, the sweep points of this GPU
+    static const bool no_inc = getenv("FLUERE_EXACT_NO_INC") != nullptr;  // (A/B)
+    const bool inc = J.mode_b && !fext && S->mono && !J.shard_mode && !no_inc;
+    const uint32_t pid = ++S->pass_no;
+    if (inc && pid < 255) {
+        if (pid == 1) {
+            HIPCHECK(hipMemsetAsync(S->stamp, 0, n, s));
+            S->ca.kdirty = nullptr;
+        } else {
+            HIPCHECK(hipMemsetAsync(S->kdirty, 0, S->n_keys, s));
+            k_ex_check<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->elook, S->ekp, S->np_rev, S->hf, S->hpos, S->kdirty);
+            S->ca.kdirty = S->kdirty;
+        }
+        S->ca.stamp = S->stamp;
+        S->ca.kpass = S->kpass;
+        S->ca.elook = S->elook;
+        S->ca.ekp = S->ekp;
+        S->ca.pass_id = pid;
+        k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
+        k_ex_flags<<<gridn(n, 256), 256, 0, s>>>(n, S->stamp, S->kpass, S->hf, S->hpos, S->sflag);
+    } else {
+        S->ca.stamp = nullptr;
+        S->ca.kpass = nullptr;
+        S->ca.kdirty = nullptr;
+        S->ca.elook = S->ca.ekp = nullptr;
+        HIPCHECK(hipMemsetAsync(S->sflag, 0, n * 4, s));
+        k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
+    }
     tb = S->tmp;
     HIPCHECK(hipcub::DeviceScan::InclusiveSum(S->tp, tb, S->sflag, S->incl, in, s));
     k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->incl, S->ist);
