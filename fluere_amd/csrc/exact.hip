@@ -386,6 +386,7 @@ struct ChaseArgs {
     uint32_t* elook = nullptr;        // per creation: its sweep lookup's start position (NOPOS: none)
     uint32_t* ekp = nullptr;          //               the answer (capture index; NOPOS: none)
     uint32_t pass_id = 0;
+    int np_all = 0;  // every replayed packet processed (the first pass's guess): next processed = itself
 };
 
 __device__ __forceinline__ unsigned long long exp_of(uint64_t t, uint64_t timeout_us) {
@@ -426,7 +427,7 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     }
     const uint64_t k = max((uint64_t)k0, lo);
     if (k >= a.n) return NONE64;
-    const unsigned long long kp = a.np_rev[a.n - 1 - k];
+    const unsigned long long kp = a.np_all ? k : a.np_rev[a.n - 1 - k];
     if (a.elook) {
         a.elook[c] = (uint32_t)k;
         a.ekp[c] = kp == MP ? NOPOS : (uint32_t)kp;
@@ -1290,7 +1291,10 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     size_t tb;
     S->R.iterations++;
     S->ca.fext = fext;
-    if (J.mode_b && !fext) {  // the sweep-point index over this pass's processed packets
+    // the first pass guesses every replayed packet processed (exact_begin's
+    // fill of pr): the next processed packet at or after k is k, no scan
+    S->ca.np_all = J.mode_b && !fext && S->mono && S->pass_no == 0 && !pr_out ? 1 : 0;
+    if (J.mode_b && !fext && !S->ca.np_all) {  // the sweep-point index over this pass's processed packets
         if (S->mono) {
             k_ex_proc_in<<<gridn(n, 256), 256, 0, s>>>(n, S->pr, S->npr);
             tb = S->tmp;
