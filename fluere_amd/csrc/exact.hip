@@ -416,6 +416,10 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     if (exp == NONE64) return NONE64;
     if (a.tree) {
         const uint64_t k = tree_first(a.tree, a.tree_P, k0, exp + 1);
+        if (a.elook) {  // (times that go backwards: the lookup starts at k0 with this exp)
+            a.elook[c] = k0;
+            a.ekp[c] = k >= a.n ? NOPOS : (uint32_t)k;
+        }
         return k >= a.n ? NONE64 : a.cm[k].gidx;
     }
     // non-decreasing times: lower_bound (within the exp's time bucket), then
@@ -567,13 +571,22 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
 // this pass's processed set
 __global__ void __launch_bounds__(256) k_ex_check(uint64_t n, const uint32_t* sflag, const uint32_t* elook,
                                                   const uint32_t* ekp, const unsigned long long* np_rev,
-                                                  const uint32_t* hf, const uint32_t* hpos, uint8_t* kdirty) {
+                                                  const uint32_t* hf, const uint32_t* hpos, uint8_t* kdirty,
+                                                  const unsigned long long* tree, uint64_t tree_P, const ExMeta* sm,
+                                                  uint64_t timeout_us) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n || !sflag[p]) return;
     const uint32_t L = elook[p];
     if (L == NOPOS) return;
-    const unsigned long long kp = np_rev[n - 1 - L];
-    if ((kp == MP ? NOPOS : (uint32_t)kp) != ekp[p]) kdirty[hpos[p] + hf[p] - 1] = 1;
+    uint32_t r;
+    if (tree) {  // backward times: the first processed packet at or after L with t > exp
+        const uint64_t k = tree_first(tree, tree_P, L, exp_of(sm[p].t, timeout_us) + 1);
+        r = k >= n ? NOPOS : (uint32_t)k;
+    } else {
+        const unsigned long long kp = np_rev[n - 1 - L];
+        r = kp == MP ? NOPOS : (uint32_t)kp;
+    }
+    if (r != ekp[p]) kdirty[hpos[p] + hf[p] - 1] = 1;
 }
 // the instance starts of every key's last chase
 __global__ void __launch_bounds__(256) k_ex_flags(uint64_t n, const uint8_t* stamp, const uint8_t* kpass,
@@ -1306,7 +1319,7 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     }
     // incremental passes: non-decreasing times, the sweep points of this GPU
     static const bool no_inc = getenv("FLUERE_EXACT_NO_INC") != nullptr;  // (A/B)
-    const bool inc = J.mode_b && !fext && S->mono && !J.shard_mode && !no_inc;
+    const bool inc = J.mode_b && !fext && !J.shard_mode && !no_inc;
     const uint32_t pid = ++S->pass_no;
     if (inc && pid < 255) {
         if (pid == 1) {
@@ -1314,7 +1327,8 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
             S->ca.kdirty = nullptr;
         } else {
             HIPCHECK(hipMemsetAsync(S->kdirty, 0, S->n_keys, s));
-            k_ex_check<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->elook, S->ekp, S->np_rev, S->hf, S->hpos, S->kdirty);
+            k_ex_check<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->elook, S->ekp, S->np_rev, S->hf, S->hpos, S->kdirty,
+                                                     S->mono ? nullptr : S->tree, S->tree_P, S->sm, J.timeout_us);
             S->ca.kdirty = S->kdirty;
         }
         S->ca.stamp = S->stamp;
