@@ -40,6 +40,7 @@ for st in "$@"; do
       c=${st#prof:}
       bash tools/prof.sh ${TAG}_$c $c
       cp gpurun_out/prof_${TAG}_$c/summary.txt "$O/pmc_$c.txt"
+      cp gpurun_out/prof_${TAG}_$c/summary.json "$O/pmc_$c.json"
       f=$(find gpurun_out/prof_${TAG}_$c/trace -name "*kernel_stats.csv" | head -1)
       cp "$f" "$O/kernel_stats_$c.csv" ;;
     trace:*)

@@ -55,7 +55,7 @@ def main():
     d = sys.argv[1]
     out = {"kernels": kernel_stats(d), "passes": {}}
     # default: the hot kernel of the run (k_parse_spill for many-flow captures)
-    hot = {k: sum(v["total_us"] for n, v in out["kernels"].items() if _match(n, k)) for k in ("k_parse_agg", "k_parse_spill")}
+    hot = {k: sum(v["total_us"] for n, v in out["kernels"].items() if _match(n, k)) for k in ("k_parse_agg", "k_parse_spill", "k_slow")}
     kern = sys.argv[2] if len(sys.argv) > 2 else max(hot, key=hot.get)
     for sub in sorted(os.listdir(d)):
         if os.path.isdir(os.path.join(d, sub)) and sub != "trace":
