@@ -52,6 +52,19 @@
 #include "pcapng.h"
 #include "synth.h"
 
+// FLUERE_ALLOC_LOG (diagnostics): every device allocation of the library, with
+// its source line and time -- the allocations a run makes while the GPU waits
+static hipError_t fl_dmalloc(void** p, size_t bytes, int line) {
+    static const bool log = getenv("FLUERE_ALLOC_LOG") != nullptr;
+    if (!log) return (hipMalloc)(p, bytes);
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = (hipMalloc)(p, bytes);
+    fprintf(stderr, "[fluere] hipMalloc line %d: %zu bytes, %.1f us\n", line, bytes,
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    return e;
+}
+#define hipMalloc(p, bytes) fl_dmalloc(reinterpret_cast<void**>(p), (bytes), __LINE__)
+
 using namespace fl;
 
 static_assert(sizeof(fluere_record) == 152, "fluere_record ABI");
@@ -3891,6 +3904,15 @@ struct fluere_ctx {
 };
 
 static int prepare_capture(fluere_ctx* c);
+
+// 512 B of private memory a lane, 1024-thread workgroups: more than any
+// kernel of a run uses (k_merge_partials 304 B, k_compose 440 B); stores
+// nothing (n is never 1)
+__global__ void __launch_bounds__(1024) k_scratch_warm(uint8_t* out, uint32_t n) {
+    volatile uint32_t buf[128];
+    for (uint32_t i = 0; i < 128; i++) buf[(i * 7u + threadIdx.x) & 127u] = i;
+    if (n == 1u) out[threadIdx.x] = (uint8_t)buf[threadIdx.x & 127u];
+}
 static int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m);
 
 static void reset_record_counters(fluere_ctx* c) {
@@ -4096,6 +4118,11 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
         return fail(FLUERE_E_HIP);
     hipStream_t s = c->stream;
     if (hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s) != hipSuccess) return fail(FLUERE_E_HIP);
+    // the stream's scratch (private memory) backing, sized now: the first
+    // kernel that needs more than the queue has (the merge, 304 B a lane)
+    // otherwise waits ~130 us in the first run for the runtime to grow it
+    k_scratch_warm<<<1, 1024, 0, s>>>(c->d_cbits, 0u);
+    if (hipGetLastError() != hipSuccess) return fail(FLUERE_E_HIP);
     {
         Ctl z{};
         z.g.tmin = NONE64;

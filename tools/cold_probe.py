@@ -22,7 +22,16 @@ cfg = fluere_amd.synth_cfg(C["kind"], n, C["flows"], C["seed"])
 batches = fluere_amd.synth_device_batches(cfg, 0, n)
 torch.cuda.synchronize()
 max_flows = max(1 << 16, 2 * C["flows"]) if C["kind"] not in (4, 6) else n // 2
+keep = None
+if len(sys.argv) > 3 and sys.argv[3] == "keep":  # a steady context stays open (as in bench.py's cold run)
+    keep = fluere_amd.FlowContext(timeout_ms=C.get("timeout_ms", 600000), use_mac=C["use_mac"], max_flows=max_flows)
+    for b, o, nbytes, nb in batches:
+        keep.add_device_batch(b, nbytes, o, nb)
+    for _ in range(3):
+        keep.run()
+    torch.cuda.synchronize()
 for r in range(reps):
+    print(f"--- rep {r}", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     ctx = fluere_amd.FlowContext(timeout_ms=C.get("timeout_ms", 600000), use_mac=C["use_mac"], max_flows=max_flows)
     t1 = time.perf_counter()
@@ -30,8 +39,10 @@ for r in range(reps):
         ctx.add_device_batch(b, nbytes, o, nb)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
+    print("--- first run", file=sys.stderr, flush=True)
     st = ctx.run()
     t3 = time.perf_counter()
+    print("--- rerun", file=sys.stderr, flush=True)
     st2 = ctx.run()
     t4 = time.perf_counter()
     print(f"{cfg_name} rep {r}: open {1e3 * (t1 - t0):.2f} ms attach {1e3 * (t2 - t1):.2f} ms "

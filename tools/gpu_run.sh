@@ -34,7 +34,7 @@ for st in "$@"; do
       tail -1 "$O/bench_$c.log" | cut -c1-300 ;;
     cold:*)
       c=${st#cold:}
-      timeout -k 10 120 python -u tools/cold_probe.py $c 3 > "$O/cold_$c.log" 2>&1
+      FLUERE_HOSTPROF=1 timeout -k 10 120 python -u tools/cold_probe.py $c 3 > "$O/cold_$c.log" 2>&1
       grep rep "$O/cold_$c.log" ;;
     prof:*)
       c=${st#prof:}
