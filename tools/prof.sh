@@ -13,7 +13,7 @@ CFG=${2:-c2}
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/prof_$TAG
 mkdir -p "$O"
-B=(python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --config "$CFG")
+B=(python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-imix --no-cold --config "$CFG")
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- "${B[@]}" > "$O/trace.log" 2>&1
 timeout -k 10 240 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/fetch" -o run -- "${B[@]}" > "$O/fetch.log" 2>&1
 timeout -k 10 240 rocprofv3 --output-format csv --pmc WRITE_SIZE TCC_EA0_RDREQ_sum -d "$O/write" -o run -- "${B[@]}" > "$O/write.log" 2>&1
