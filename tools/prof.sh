@@ -25,7 +25,7 @@ if [ "${PROF_SQ:-0}" = "1" ]; then
       SQ_WAIT_INST_LDS -d "$O/lds$A" -o run -- "${B[@]}" > "$O/lds$A.log" 2>&1
   done
 fi
-python3 "$R/tools/pmc_summary.py" "$O" > "$O/summary.txt" 2>&1
+python3 "$R/tools/pmc_summary.py" "$O" ${PROF_KERNEL:-} > "$O/summary.txt" 2>&1
 # keep the summaries and the kernel-stats tables; drop the bulky per-dispatch CSVs
 find "$O" -type f \( -name "*counter_collection.csv" -o -name "*kernel_trace.csv" -o -name "*agent_info.csv" \) -size +1M -delete
 du -sh "$O" > "$O/DONE"
