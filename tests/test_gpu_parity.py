@@ -453,6 +453,23 @@ def test_sharded_realistic_tcp(gpu, G, wire):
         c.close()
 
 
+@pytest.mark.parametrize("wire", [False, True])
+def test_sharded_steps_repeat_with_slow_packets(gpu, wire):
+    """Two steps of the sharded exchange on the same contexts over a capture of
+    general-parser packets (IPv6: the k_slow address ids), with small blocks
+    so the capacity retry grows the wide / wire scratch between passes: the
+    second step equals the oracle like the first (no state freed under it)."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_SLOW, 200_000, 3_000, 0xF10E0027)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    ls, ctxs = _logical_shards(cfg, 2, cap=32, cap_annex=8, wire=wire)
+    for step in range(2):
+        ls.run()
+        recs, ne = ls.records()
+        assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"sharded slow step {step}")
+    for c in ctxs:
+        c.close()
+
+
 def test_sharded_cut_short_block_is_an_error(gpu):
     """A block with more flows than its capacity: the merge refuses it."""
     cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 40_000, 2000, 0xF10E0004)
