@@ -57,7 +57,10 @@ namespace {
 constexpr int PBITS = 38;
 constexpr uint64_t MP = (1ull << PBITS) - 1;
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
-constexpr int MAX_PASSES = 32;
+// (a chain of sweep dependencies settles one link per pass; incremental passes
+// re-chase only the keys that changed, so a long chain stays far cheaper than
+// the sequential kernel: test_mode_b_sweep_chain_passes)
+constexpr int MAX_PASSES = 250;
 enum : uint8_t { K_FIN = 0, K_SWEEP = 1, K_ACTIVE = 2, K_LEAD = 3 };
 // shard mode: role of a run in the flow's annex
 enum : uint8_t { R_RECORD = 0, R_HEAD = 1, R_TAIL = 2, R_HEAD_TAIL = 3, R_LEAD = 4 };

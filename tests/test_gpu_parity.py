@@ -886,6 +886,41 @@ def test_tcp_realistic_matches_oracle(gpu, name):
             assert st["sequential_mode"] == 1  # the parallel sweep, not the fallback
 
 
+def _sweep_chain(L, T_us=10_000):
+    """A capture whose Mode B fixed point needs about L passes: key K_i opens
+    with a SYN early; its entry fires at the first processed packet at or
+    after exp_i, which is K_(i-1)'s ACK R_(i-1) (K_0's: a UDP packet), and
+    R_(i-1) is processed only when K_(i-1)'s own entry did not fire before
+    it -- processed(R_i) = not processed(R_(i-1)), a chain the parallel
+    chase settles one link per pass (offline_fluereflows.rs:161-175)."""
+    import pktbuild as pb
+    S, F, A = pb.SYN, pb.FIN, pb.ACK
+    pk = []
+    for i in range(L):  # SYNs at t = i us
+        f = pb.eth() + pb.ipv4(f"10.9.{i // 200}.{i % 200 + 1}", "10.8.0.2", 6, pb.tcp(1000 + i, 80, S))
+        pk.append((0, i, f))
+    base = T_us
+    pk.append((0, base, pb.eth() + pb.ipv4("10.7.0.1", "10.7.0.2", 17, pb.udp(53, 53))))  # Q_0, always processed
+    for i in range(L):  # R_i at exp_(i+1) = T + i + 1
+        f = pb.eth() + pb.ipv4(f"10.9.{i // 200}.{i % 200 + 1}", "10.8.0.2", 6, pb.tcp(1000 + i, 80, A))
+        pk.append((0, base + i + 1, f))
+    return pb.pcap(pk)
+
+
+@pytest.mark.parametrize("L", [3, 20, 120, 400])
+def test_mode_b_sweep_chain_passes(gpu, L):
+    """The pass count of an adversarial capture: a chain of L
+    sweep dependencies takes about L incremental passes; past MAX_PASSES the
+    run falls back to the sequential kernel -- exact either way."""
+    data = _sweep_chain(L)
+    want = pyoracle.offline(data, 10)
+    csv, ne, st = _gpu_csv(data, 10)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"sweep chain L={L}")
+    if st["sequential_mode"] == 1:  # the parallel sweep settled it
+        assert st["passes"] >= min(L, 3), st
+    print(f"L={L}: passes {st['passes']} sequential_mode {st['sequential_mode']}")
+
+
 def test_mode_b_backward_time_fixture(gpu):
     """Timestamps that go backwards (edge_keys): the sweep points come from
     the max segment tree and the pending entries are kept in pop order, so the
