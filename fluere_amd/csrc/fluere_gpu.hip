@@ -1925,11 +1925,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 // searched once, each lane steps forward over the few sets
                 // its index is past) and update_flow of one packet written
                 // out directly instead of through a FlowPart.
-                for (uint32_t idx = tid; idx < total; idx += MB) {
-                    const uint32_t iw = __builtin_amdgcn_readfirstlane(idx);  // the wave's smallest index
+                // the set of flattened index id (the wave's smallest index
+                // searched once, each lane stepping forward past the few sets
+                // its index is beyond)
+                auto set_of = [&](uint32_t id) -> uint32_t {
+                    const uint32_t iw = __builtin_amdgcn_readfirstlane(id);
                     uint32_t lo_i = 0, hi_i = nset - 1;
                     if (grp) {
-                        lo_i = m_grp[iw >> 6];  // (iw is a multiple of 64: lane 0's index)
+                        lo_i = m_grp[iw >> 6];  // (the set of the group's first index: a lower bound)
                     } else {
                         while (lo_i < hi_i) {
                             const uint32_t mid = (lo_i + hi_i + 1) >> 1;
@@ -1937,10 +1940,30 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                             else hi_i = mid - 1;
                         }
                     }
-                    while (lo_i + 1 < nset && m_start[lo_i + 1] <= idx) lo_i++;
-                    const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                    const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * 2;
-                    const uint4 v0 = src[0], v1 = src[1];
+                    while (lo_i + 1 < nset && m_start[lo_i + 1] <= id) lo_i++;
+                    return lo_i;
+                };
+                // one record ahead: the next iteration's record is loaded
+                // while this one is probed and aggregated in LDS
+                uint32_t lo_n = 0;
+                uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+                if ((uint32_t)tid < total) {
+                    lo_n = set_of(tid);
+                    const uint4* src = reinterpret_cast<const uint4*>(S.dspill) +
+                                       ((size_t)m_lo[lo_n] + ((uint32_t)tid - m_start[lo_n])) * 2;
+                    n0 = src[0];
+                    n1 = src[1];
+                }
+                for (uint32_t idx = tid; idx < total; idx += MB) {
+                    const uint32_t lo_i = lo_n;
+                    const uint4 v0 = n0, v1 = n1;
+                    if (idx + MB < total) {
+                        lo_n = set_of(idx + MB);
+                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) +
+                                           ((size_t)m_lo[lo_n] + (idx + MB - m_start[lo_n])) * 2;
+                        n0 = src[0];
+                        n1 = src[1];
+                    }
                     const unsigned long long gi = a.B.first + m_wb[lo_i] + v1.z;
                     const uint32_t k0 = v0.x, k1 = v0.y, k2 = v0.z, tag = v0.w;
                     if (FLUERE_MERGE_ABL == 1) {  // diagnostics: the loads alone
