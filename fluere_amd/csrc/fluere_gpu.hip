@@ -1917,8 +1917,9 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                         if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
                     }
             };
-            if (pass == 1 && !macs) {
-                // Spilled packets (no MACs), the lean path: the merge is
+            if (pass == 1) {
+                // Spilled packets, the lean path (MAC runs: 64-byte records,
+                // the MAC words and the hash beside the key): the merge is
                 // instruction-bound (PMC on C3: 28 % of wave time issuing at
                 // 4 waves per SIMD, 14k VALU + 7k SALU instructions per wave),
                 // so no binary search per record (the wave's first index is
@@ -1945,24 +1946,27 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 };
                 // one record ahead: the next iteration's record is loaded
                 // while this one is probed and aggregated in LDS
+                constexpr uint32_t RW = MACS ? 4u : 2u;  // 16-byte words per record
                 uint32_t lo_n = 0;
-                uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+                uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, nx = n0;
                 if ((uint32_t)tid < total) {
                     lo_n = set_of(tid);
                     const uint4* src = reinterpret_cast<const uint4*>(S.dspill) +
-                                       ((size_t)m_lo[lo_n] + ((uint32_t)tid - m_start[lo_n])) * 2;
+                                       ((size_t)m_lo[lo_n] + ((uint32_t)tid - m_start[lo_n])) * RW;
                     n0 = src[0];
-                    n1 = src[1];
+                    n1 = src[MACS ? 2 : 1];
+                    if (MACS) nx = src[1];
                 }
                 for (uint32_t idx = tid; idx < total; idx += MB) {
                     const uint32_t lo_i = lo_n;
-                    const uint4 v0 = n0, v1 = n1;
+                    const uint4 v0 = n0, v1 = n1, vx = nx;  // key, payload, (MACS) MAC words + hash
                     if (idx + MB < total) {
                         lo_n = set_of(idx + MB);
                         const uint4* src = reinterpret_cast<const uint4*>(S.dspill) +
-                                           ((size_t)m_lo[lo_n] + (idx + MB - m_start[lo_n])) * 2;
+                                           ((size_t)m_lo[lo_n] + (idx + MB - m_start[lo_n])) * RW;
                         n0 = src[0];
-                        n1 = src[1];
+                        n1 = src[MACS ? 2 : 1];
+                        if (MACS) nx = src[1];
                     }
                     const unsigned long long gi = a.B.first + m_wb[lo_i] + v1.z;
                     const uint32_t k0 = v0.x, k1 = v0.y, k2 = v0.z, tag = v0.w;
@@ -1970,20 +1974,26 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                         if ((k0 ^ k1 ^ k2 ^ v1.x ^ v1.y) == 0x12345678u) atomicAdd(&m_pk[0][0], 1u);
                         continue;
                     }
-                    const uint32_t h = lt_hash(k0, k1, k2, tag);
+                    const uint32_t h = MACS ? vx.w : lt_hash(k0, k1, k2, tag);
                     uint32_t e = (h * 0x85EBCA77u) >> 22;  // 10 bits: MT == 1024
                     int state = 0, probes = 0;
                     for (int it = 0; it < 128; it++) {  // find or claim (the hot kernel's protocol)
                         if (state == 0) {
                             const uint4 kk = m_key[e];
+                            bool xm = true;
+                            if (MACS) {  // the MAC words (the sidecar is written before the entry is published)
+                                const uint4 xx = m_kx[MACS ? e : 0];
+                                xm = xx.w == 1u && xx.x == vx.x && xx.y == vx.y && xx.z == vx.z;
+                            }
                             if (kk.w & LT_READY) {
-                                if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2) state = 1;
+                                if (kk.w == (tag | LT_READY) && kk.x == k0 && kk.y == k1 && kk.z == k2 && xm) state = 1;
                                 else if (++probes == 64) state = 2;
                                 else e = (e + 1) & (MT - 1);
                             } else if (kk.w == 0 && atomicCAS(&m_key[e].w, 0u, LT_CLAIM) == 0u) {
                                 m_key[e].x = k0;
                                 m_key[e].y = k1;
                                 m_key[e].z = k2;
+                                if (MACS) m_kx[MACS ? e : 0] = make_uint4(vx.x, vx.y, vx.z, 1u);
                                 __threadfence_block();
                                 atomicExch(&m_key[e].w, tag | LT_READY);
                                 state = 1;
@@ -2015,7 +2025,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     } else {  // no entry within 64 probes: the global path
                         FlowPart f;
                         spill_to_part(v1.x, v1.y, v1.z, v1.w, a.B.first + m_wb[lo_i], f);
-                        const uint32_t d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
+                        uint32_t d;
+                        if (MACS && tag != 0xFF000000u) {
+                            CKey ck;
+                            mac_ckey(k0, k1, k2, tag, vx.x, vx.y, vx.z, ck);
+                            d = dense_of_key(a.T, ck, true, a.A.slots, nullptr);
+                        } else {
+                            d = staged_id(a.T, a.v6, k0, k1, k2, tag, a.A.slots);
+                        }
                         if (d != FAIL && d < a.T.fmax) part_to_global(a.A, d, f);
                         if (a.pid && d != FAIL && d < a.T.fmax) a.pid[gi - a.pid_base] = PH_ID | d;
                     }
@@ -5375,7 +5392,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         S.O = O;
         S.n_hot = (uint32_t)sets;
         S.n_sets = (uint32_t)all;
-        S.no_parts = (P.spill || slow_all) && !c->use_mac ? 1u : 0u;
+        S.no_parts = (P.spill || slow_all) ? 1u : 0u;
         if (P.nb < PLAN_BATCHES) {
             P.agg[P.nb] = ab;
             P.agg_grid[P.nb] = grid;
