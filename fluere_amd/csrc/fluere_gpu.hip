@@ -5768,7 +5768,8 @@ extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
 //  * Mode A: an ended record's order_key (its closing packet's index) is
 //    unique -- a packet closes at most one instance of its key -- so its
 //    place is the count of ended keys below it: one bit per packet, a
-//    popcount scan, one scatter;
+//    popcount scan, one scatter (of every record, or -- at most a quarter
+//    ended -- of the ended ones and the actives they displace: k_ord_out);
 //  * Mode B: a sweep ends several flows at one packet, in the BTreeMap's pop
 //    order (exp, then push order) after a FIN/RST close (order words aux):
 //    stable radix sorts by the packed order words, then by order_key, and a
@@ -5882,6 +5883,79 @@ __global__ void __launch_bounds__(256) k_ord_move(const fluere_record* r, const 
     }
 }
 
+// Mode A with few ended records (at most a quarter): only they and the active
+// records in the first n_ended places move.  k_ord_out copies the ended ones
+// to their places in `out` and lists the holes they leave past n_ended;
+// k_ord_fill moves the head's active records into those holes (the actives
+// keep no order of their own: fetch_records sorts them); the ordered prefix
+// is copied back.  About 4 x 152 B per ended record instead of 2 x 152 B per
+// record.
+// A wave copies the records of its lanes with `want` set, 8-byte words in
+// order (as k_ord_move).  Called by every thread of the block.
+__device__ __forceinline__ void wave_copy_recs(uint32_t* s_l, const fluere_record* r, uint64_t w0, bool want,
+                                               uint32_t p, fluere_record* out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(want);
+    if (want) s_l[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = lane;
+    __syncthreads();
+    const uint32_t total = (uint32_t)__popcll(m) * REC_WORDS;
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(r);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
+    for (uint32_t b = 0; b < total; b += 64) {  // (wave-uniform)
+        const uint32_t e = b + lane, ec = min(e, total - 1);
+        const uint32_t j = ec / REC_WORDS, kk = ec - j * REC_WORDS;
+        const uint32_t L = s_l[j];
+        const uint32_t pj = __shfl(p, L, 64);
+        if (e < total) dst[(size_t)pj * REC_WORDS + kk] = src[(w0 + L) * REC_WORDS + kk];
+    }
+}
+// the active records before record i (in the block's wave order)
+__device__ __forceinline__ uint32_t act_before(uint32_t* s_w, uint64_t am, const uint32_t* blk_pre) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(am);
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t q = 0; q < w; q++) before += s_w[q];
+    return blk_pre[blockIdx.x] + before +
+           __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+}
+__global__ void __launch_bounds__(256) k_ord_out(const fluere_record* r, uint64_t n, uint64_t base,
+                                                 const unsigned long long* okey, const uint32_t* bits,
+                                                 const uint32_t* pre, const uint32_t* blk_pre, uint64_t n_ended,
+                                                 fluere_record* out, uint32_t* holes, uint32_t* head_act) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_l[4][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = i < n;
+    const uint64_t k = live ? okey[i] : NONE64;
+    const bool ended = k != NONE64;
+    const uint32_t ab = act_before(s_w, __ballot(live && !ended), blk_pre);
+    if (i == n_ended) *head_act = ab;  // the head's active records (n_ended < n)
+    uint32_t p = 0;
+    if (ended) {
+        const uint64_t q = k - base;
+        p = pre[q >> 5] + __popc(bits[q >> 5] & ((1u << (q & 31)) - 1u));
+        if (i >= n_ended) holes[i - ab] = (uint32_t)i;  // ended records before i: i - ab
+    }
+    wave_copy_recs(s_l[w], r, i - lane, ended, p, out);
+}
+// the head's active records (i < n_ended; the i-th of them is its
+// act_before) into the holes past n_ended, which start at ended rank
+// n_ended - head_act
+__global__ void __launch_bounds__(256) k_ord_fill(fluere_record* r, const unsigned long long* okey,
+                                                  const uint32_t* blk_pre, uint64_t n_ended, const uint32_t* holes,
+                                                  const uint32_t* head_act) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_l[4][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool act = i < n_ended && okey[i] == NONE64;
+    const uint32_t ab = act_before(s_w, __ballot(act), blk_pre);
+    const uint32_t p = act ? holes[ab + (uint32_t)n_ended - *head_act] : 0u;
+    wave_copy_recs(s_l[w], r, i - lane, act, p, r);
+}
+
 static int ord_scratch(fluere_ctx* c, size_t need) {
     if (need <= c->d_ord_bytes) return FLUERE_OK;
     hipFree(c->d_ord);
@@ -5987,6 +6061,16 @@ static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_
         k_ord_popc<<<grid_for(nw, 256), 256, 0, s>>>(cb, nw, pc);
         t = tb;
         HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, pc, ps, (int)nw, s));
+        static const bool all_move = getenv("FLUERE_ORD_MOVE_ALL") != nullptr;
+        if (!all_move && n_ended * 4 <= n) {  // few ended: only they and the head's actives move (k_ord_out)
+            k_ord_out<<<gn, 256, 0, s>>>(c->d_recs, n, base, okey, cb, ps, blk_pre, n_ended, c->d_recs2, mem, gmax);
+            k_ord_fill<<<grid_for(n_ended, 256), 256, 0, s>>>(c->d_recs, okey, blk_pre, n_ended, mem, gmax);
+            HIPCHECK(hipMemcpyAsync(c->d_recs, c->d_recs2, n_ended * sizeof(fluere_record), hipMemcpyDeviceToDevice, s));
+            HIPCHECK(hipGetLastError());
+            c->dev_ordered = true;
+            c->dev_ordered_ended = n_ended;
+            return FLUERE_OK;
+        }
         k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, nullptr, n, base, okey, cb, ps, nullptr, nullptr, blk_pre, n_ended,
                                       c->d_recs2, nullptr);
     } else {
