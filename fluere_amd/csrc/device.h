@@ -76,6 +76,7 @@ struct Glob {
     unsigned long long clean_done;                        // k_cleanup: workgroups finished
     unsigned long long fin_done;                          // k_finalize: workgroups finished
     unsigned long long n_fdefer;                          // k_finalize: certified flows left to k_finalize_gen
+    unsigned long long n_okey;                            // emitters: order keys written beside the records
 };
 static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16 &&
                   offsetof(Glob, n_gen) == offsetof(Glob, n_slow) + 24 && offsetof(Glob, n_owner) == offsetof(Glob, n_slow) + 32,
@@ -88,6 +89,26 @@ struct Ctl {
     uint32_t seq;  // host copy only: k_finalize's last workgroup writes the run's number here last
     uint32_t pad[13];
 };
+
+// The records' order keys, one word per record slot in an array beside the
+// record buffer (order_records reads them instead of one word of every
+// 152-byte record).  Its pointer sits where the Ctl allocation ends, outside
+// what k_cleanup clears; {nullptr, 0} until the host sizes it.  Glob::n_okey
+// counts the words written since the run counters were reset: the array
+// holds the run's keys when it equals n_rec.
+struct OkeyRef {
+    unsigned long long* p;
+    unsigned long long cap;
+};
+__device__ __forceinline__ OkeyRef okey_ref(const Glob* g) {
+    return *reinterpret_cast<const OkeyRef*>(reinterpret_cast<const char*>(g) + sizeof(Ctl));
+}
+// records [base, base + n) emitted: how many of them have an order-key slot
+__device__ __forceinline__ unsigned long long okey_count(const OkeyRef& o, uint64_t cap, unsigned long long base,
+                                                         unsigned long long n) {
+    const unsigned long long lim = min((unsigned long long)cap, o.cap);
+    return base >= lim ? 0ull : min(n, lim - base);
+}
 
 #define HIPCHECK(x)                                                                                  \
     do {                                                                                             \
@@ -419,6 +440,11 @@ __device__ __forceinline__ uint32_t ph_flow(uint32_t w, const uint32_t* emap) { 
 __device__ __forceinline__ void emit_record(Glob* g, fluere_record* out, uint64_t cap, const fluere_record& r) {
     const unsigned long long pos = atomicAdd(&g->n_rec, 1ull);
     if (pos < cap) out[pos] = r;
+    const OkeyRef o = okey_ref(g);
+    if (okey_count(o, cap, pos, 1)) {
+        o.p[pos] = r.order_key;
+        atomicAdd(&g->n_okey, 1ull);
+    }
     atomicAdd(&g->n_updates, (unsigned long long)r.d_pkts);
     if (r.order_key != NONE64) atomicAdd(&g->n_ended, 1ull);
 }
@@ -491,9 +517,13 @@ __device__ __forceinline__ void emit_record_wave(Glob* g, fluere_record* out, ui
         if (em) atomicAdd(&g->n_ended, (unsigned long long)__popcll(em));
     }
     base = __shfl(base, lead, 64);
+    const OkeyRef o = okey_ref(g);
+    const unsigned long long nok = okey_count(o, cap, base, (unsigned long long)__popcll(m));
+    if ((uint32_t)(threadIdx.x & 63) == lead && nok) atomicAdd(&g->n_okey, nok);
     if (want) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         if (base + rank < cap) out[base + rank] = r;
+        if (rank < nok) o.p[base + rank] = r.order_key;
     }
 }
 
@@ -538,11 +568,15 @@ __device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_re
         S.n = t[0];
         if (t[1]) atomicAdd(&g->n_updates, t[1]);
         if (t[2]) atomicAdd(&g->n_ended, t[2]);
+        const unsigned long long nok = okey_count(okey_ref(g), cap, S.base, t[0]);
+        if (nok) atomicAdd(&g->n_okey, nok);
     }
     __syncthreads();
     if (want) {
         const uint32_t i = S.w[w][0] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         S.rec[i] = r;
+        const OkeyRef o = okey_ref(g);
+        if (okey_count(o, cap, S.base + i, 1)) o.p[S.base + i] = r.order_key;
         if (aux && S.base + i < cap)
             *reinterpret_cast<ulonglong2*>(aux + 2 * (S.base + i)) = make_ulonglong2(a0, a1);
     }
@@ -586,6 +620,8 @@ __device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_r
         }
         S.base = t[0] ? atomicAdd(&g->n_rec, t[0]) : 0ull;
         S.n = t[0];
+        const unsigned long long nok = okey_count(okey_ref(g), cap, S.base, t[0]);
+        if (nok) atomicAdd(&g->n_okey, nok);
         if (tot) {
             tot[0] += t[1];
             tot[1] += t[2];
@@ -598,6 +634,8 @@ __device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_r
     if (want) {
         const uint32_t i = S.w[w][0] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         S.slot[i] = (uint16_t)threadIdx.x;
+        const OkeyRef o = okey_ref(g);
+        if (okey_count(o, cap, S.base + i, 1)) o.p[S.base + i] = S.rec[threadIdx.x].order_key;
         if (aux && S.base + i < cap)
             *reinterpret_cast<ulonglong2*>(aux + 2 * (S.base + i)) = make_ulonglong2(a0, a1);
     }

@@ -3941,6 +3941,9 @@ struct fluere_ctx {
     uint64_t d_recaux2_cap = 0;
     void* d_ord = nullptr;           // order_records scratch
     size_t d_ord_bytes = 0;
+    unsigned long long* d_okey = nullptr;  // the records' order keys, written by the emitters (OkeyRef)
+    uint64_t d_okey_cap = 0;
+    OkeyRef okref{};                       // its device copy follows the Ctl in d_glob
 };
 
 static int prepare_capture(fluere_ctx* c);
@@ -3959,7 +3962,7 @@ static void reset_record_counters(fluere_ctx* c) {
     char* g = (char*)c->d_glob;
     for (size_t off : {offsetof(Glob, n_rec), offsetof(Glob, n_complex), offsetof(Glob, n_complex_pkts),
                        offsetof(Glob, n_heads), offsetof(Glob, n_updates), offsetof(Glob, n_ended),
-                       offsetof(Glob, n_fdefer)})
+                       offsetof(Glob, n_fdefer), offsetof(Glob, n_okey)})
         hipMemsetAsync(g + off, 0, 8, c->stream);
 }
 
@@ -4144,7 +4147,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
         c->own_stream = true;
     }
     if ((rc = alloc_flow_state(c, mf))) return fail(rc);
-    if (hipMalloc(&c->d_glob, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_glob, sizeof(Ctl) + sizeof(OkeyRef)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     c->d_nflows = &reinterpret_cast<Ctl*>(c->d_glob)->n_flows;
     if (hipHostMalloc(&c->h_ctl, sizeof(Ctl)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     memset(c->h_ctl, 0, sizeof(Ctl));
@@ -4167,6 +4170,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
         Ctl z{};
         z.g.tmin = NONE64;
         if (hipMemcpyAsync(c->d_glob, &z, sizeof z, hipMemcpyHostToDevice, s) != hipSuccess) return fail(FLUERE_E_HIP);
+        if (hipMemsetAsync((char*)c->d_glob + sizeof(Ctl), 0, sizeof(OkeyRef), s) != hipSuccess) return fail(FLUERE_E_HIP);
     }
     if (hipStreamSynchronize(s) != hipSuccess) return fail(FLUERE_E_HIP);
     // the state above is what k_cleanup leaves: the first pass needs none
@@ -4238,6 +4242,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_recaux2);
     hipFree(c->d_ord);
     hipFree(c->d_recaux);
+    hipFree(c->d_okey);
     sweep_free(c);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -5776,20 +5781,21 @@ extern "C" double fluere_last_pass_ms(fluere_ctx* c) {
 //    gather of the records and their words.
 // ---------------------------------------------------------------------------
 // pass 1: every record's order_key into a compact array (one strided read
-// of the 152-byte records), the ended ones marked (Mode A: one bit per
+// of the 152-byte records; none when the emitters wrote the array: ok_in),
+// the ended ones marked (Mode A: one bit per
 // packet; Mode B: a count per closing packet and the largest group), and the
 // active records counted per block of 256 (their places follow the ended
 // prefix in record order: a scan of the block counts, no shared counter)
 __global__ void __launch_bounds__(256) k_ord_keys(const fluere_record* r, uint64_t n, uint64_t base, int mode_b,
-                                                  unsigned long long* okey, uint32_t* bits, uint32_t* cnt,
-                                                  uint32_t* gmax, uint32_t* blk_act) {
+                                                  const unsigned long long* ok_in, unsigned long long* okey,
+                                                  uint32_t* bits, uint32_t* cnt, uint32_t* gmax, uint32_t* blk_act) {
     __shared__ uint32_t s_act;
     if (threadIdx.x == 0) s_act = 0;
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const bool live = i < n;
-    const uint64_t k = live ? r[i].order_key : NONE64;
-    if (live) okey[i] = k;
+    const uint64_t k = live ? (ok_in ? ok_in[i] : r[i].order_key) : NONE64;
+    if (live && !ok_in) okey[i] = k;
     const bool ended = k != NONE64;
     if (ended) {
         if (!mode_b) {
@@ -6020,7 +6026,9 @@ static int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m) {
 // Orders the run's n records in d_recs (n_ended of them ended) as
 // [ended][active]; Mode B with the order words in d_recaux.  Stream-ordered;
 // Mode B reads its largest group (records ending at one packet) once.
-static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b) {
+// n_okey: the run's Glob::n_okey (the order-key array holds every record's
+// key when it equals n).
+static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint64_t n_okey) {
     c->dev_ordered = false;
     if (!n || !n_ended || n >= (1ull << 32)) return FLUERE_OK;
     hipStream_t s = c->stream;
@@ -6044,6 +6052,9 @@ static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_
     char* p = (char*)c->d_ord;
     auto take = [&](size_t bytes) { char* q = p; p += al(bytes); return q; };
     unsigned long long* okey = (unsigned long long*)take(n * 8);
+    static const bool no_okey = getenv("FLUERE_NO_OKEY") != nullptr;
+    const bool have_okey = !no_okey && c->d_okey && n_okey == n && n <= c->d_okey_cap;
+    if (have_okey) okey = c->d_okey;
     uint32_t* cb = (uint32_t*)take(nk * 4);   // Mode A bits, Mode B counts
     uint32_t* pc = (uint32_t*)take(nw * 4);
     uint32_t* ps = (uint32_t*)take(nk * 4);   // Mode A bit-count prefix, Mode B group starts
@@ -6054,7 +6065,8 @@ static int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_
     void* tmp = p;
     HIPCHECK(hipMemsetAsync(cb, 0, nk * 4, s));
     HIPCHECK(hipMemsetAsync(gmax, 0, 4, s));
-    k_ord_keys<<<gn, 256, 0, s>>>(c->d_recs, n, base, mode_b ? 1 : 0, okey, cb, cb, gmax, blk);
+    k_ord_keys<<<gn, 256, 0, s>>>(c->d_recs, n, base, mode_b ? 1 : 0, have_okey ? c->d_okey : nullptr, okey, cb, cb,
+                                  gmax, blk);
     size_t t = tb;
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, blk, blk_pre, (int)gn, s));
     if (!mode_b) {
@@ -6155,14 +6167,34 @@ static int prepare_capture(fluere_ctx* c) {
     return FLUERE_OK;
 }
 
+// The order-key array at the record buffer's capacity (without it
+// order_records reads the keys from the records).  Only before the run's
+// records are emitted: a new array holds no keys.
+static int okey_fit(fluere_ctx* c) {
+    const uint64_t cap = c->d_recs_cap;
+    if (c->d_okey_cap < cap) {
+        hipFree(c->d_okey);
+        c->d_okey = nullptr;
+        c->d_okey_cap = 0;
+        if (hipMalloc(&c->d_okey, cap * 8) == hipSuccess) c->d_okey_cap = cap;
+        else (void)hipGetLastError();
+        c->okref = OkeyRef{c->d_okey, c->d_okey_cap};
+        HIPCHECK(hipMemcpyAsync((char*)c->d_glob + sizeof(Ctl), &c->okref, sizeof(OkeyRef), hipMemcpyHostToDevice,
+                                c->stream));
+        // keys counted into the old array are not in this one
+        HIPCHECK(hipMemsetAsync((char*)c->d_glob + offsetof(Glob, n_okey), 0, 8, c->stream));
+    }
+    return FLUERE_OK;
+}
+
 static int ensure_recs(fluere_ctx* c, uint64_t need) {
-    if (need <= c->d_recs_cap) return FLUERE_OK;
+    if (need <= c->d_recs_cap) return okey_fit(c);
     hipFree(c->d_recs);
     c->d_recs = nullptr;
     uint64_t cap = std::max<uint64_t>(need, 1024);
     if (hipMalloc(&c->d_recs, cap * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
     c->d_recs_cap = cap;
-    return FLUERE_OK;
+    return okey_fit(c);
 }
 
 extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
@@ -6325,7 +6357,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         c->dev_n_rec = n_rec;
         c->host_recs = false;
         out.complex_flows = g.n_complex;
-        if ((rc = order_records(c, n_rec, n_ended, false))) return rc;
+        if ((rc = order_records(c, n_rec, n_ended, false, g.n_okey))) return rc;
     } else {
         // exact global state machine (the speculative Mode A results are discarded):
         // in parallel (exact.hip) when the timestamps are non-decreasing, else
@@ -6357,7 +6389,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             c->dev_n_rec = n_rec;
             c->host_recs = false;
             out.sequential_mode = 1;
-            if (c->has_aux && (rc = order_records(c, n_rec, n_ended, true))) return rc;
+            if (c->has_aux && (rc = order_records(c, n_rec, n_ended, true, g.n_okey))) return rc;
         } else {
         uint64_t N = c->n_total;
         SeqMeta* meta = nullptr;
