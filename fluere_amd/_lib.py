@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import struct
 
 import numpy as np
 
@@ -55,7 +56,14 @@ class Stats(ctypes.Structure):
                 ("total_ms", ctypes.c_double)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        # one unpack of the 96 bytes (per-field getattr costs ~3 us, about 1 %
+        # of a C2 step)
+        return dict(zip(_STATS_NAMES, _STATS_LAYOUT.unpack_from(self)))
+
+
+_STATS_NAMES = tuple(k for k, _ in Stats._fields_)
+_STATS_LAYOUT = struct.Struct("<9Q2I2d")
+assert _STATS_LAYOUT.size == ctypes.sizeof(Stats)
 
 
 class SynthCfg(ctypes.Structure):
