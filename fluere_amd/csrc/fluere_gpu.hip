@@ -5814,13 +5814,15 @@ __global__ void __launch_bounds__(256) k_ord_popc(const uint32_t* bits, uint64_t
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w < nw) pc[w] = __popc(bits[w]);
 }
-// Mode B: each closing packet's group members listed (mem[start[k] ..])
+// Mode B: each closing packet's group members listed (mem[start[k] ..]), groups
+// of two or more
 __global__ void __launch_bounds__(256) k_ob_fill(const unsigned long long* okey, uint64_t n, uint64_t base,
                                                  uint32_t* cnt, const uint32_t* start, uint32_t* mem) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint64_t k = okey[i];
     if (k == NONE64) return;
+    if (start[k - base + 1] - start[k - base] == 1) return;  // a group of one: k_ord_move reads no members
     const uint32_t slot = atomicSub(&cnt[k - base], 1u) - 1u;
     mem[start[k - base] + slot] = (uint32_t)i;
 }
