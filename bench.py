@@ -97,7 +97,8 @@ def measure(name, args, world, rank, local, stream, torch, dist, fluere_amd, fdi
             # per-shard aggregation, then the flow-table merge: per-owner
             # blocks, one RCCL all_to_all, each owner merges its own flows
             st = exchange.step()
-        # HIP events around the hot kernel on the context stream (fluere_stats.parse_ms)
+        # HIP events carried by the hot-kernel dispatches on the context stream,
+        # summed over the step's launches (fluere_stats.parse_ms)
         kernel_ms.append(st["parse_ms"] if world == 1 else ctx.last_kernel_ms())
         pass_ms.append(st["total_ms"] if world == 1 else ctx.last_pass_ms())
         return st
@@ -163,9 +164,11 @@ def roofline(m):
             "frac": round(m["achieved"] / HBM_PEAK_GBS, 4), "traffic": m["traffic"],
             # also against the measured copy rate (MI355X_MICROARCH.md)
             "frac_vs_copy_6290": round(m["achieved"] / HBM_COPY_GBS, 4),
+            # kernel_ms: the step's hot-kernel launches, their device times summed
+            # (HIP events carried by each dispatch); per launch: divided by their count
             "kernel": m["kernel"], "kernel_ms": round(m["kernel_avg"], 4),
-            # > 1: kernel_ms spans the first launch's start to the last one's end
             "launches_per_step": m["launches"],
+            "kernel_ms_per_launch": round(m["kernel_avg"] / max(1, m["launches"]), 4),
             "algorithmic_bytes_per_launch": BYTES_PER_PKT * m["n"] // max(1, m["launches"])}
 
 
@@ -257,6 +260,8 @@ def main():
                             "frac": round(imix["achieved"] / HBM_PEAK_GBS, 4), "traffic": imix["traffic"],
                             "records": int(imix["n_recs"]), "records_ended": int(imix["n_ended"]),
                             "roofline": roofline(imix), **imix["cold"]}
+            if world == 1 and not args.no_cpu_baseline:
+                line["imix"]["cpu_baseline"] = cpu_baseline(imix["cfg"], imix["C"])
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(m["cfg"], C)
         print(json.dumps(line))

@@ -12,7 +12,7 @@
 //                  T1[(s0 << 40) | (lo_port << 24) | (hi_port << 8) | proto] -> s1 -> dense id
 //                  (T1's probe starts at a hash of the whole key, so both
 //                  tables' first probes travel together: v4_slots)
-//                  (tables of more than 2^24 slots, "wide": T1[(s0 << 33) |
+//                  (tables of 2^24 slots and more, "wide": T1[(s0 << 33) |
 //                  (ports << 1) | udp] for TCP and UDP, every other protocol
 //                  through the generic chain -- v4_t1_word)
 //   otherwise:     the canonical key serialised to 32-bit units; level 0 takes
@@ -51,6 +51,7 @@ constexpr uint32_t MAX_FLOWS = 1u << 26;        // dense ids (the exact engine p
 struct TableSet {
     unsigned long long* tab[N_TABLES];  // (C + 1) entries of {key, val}; entry C holds the word EMPTY
     uint32_t C;                          // power of two, <= MAX_TABLE_SLOTS
+    uint32_t wide;                       // the IPv4 chain's wide level-1 words (C >= 2^24, v4_t1_word)
     uint32_t fmax;                       // dense id capacity
     uint32_t* n_flows;
     uint32_t* err;
@@ -89,17 +90,19 @@ __device__ __forceinline__ uint32_t tab_slot(const TableSet& T, int t, uint64_t 
     return tab_slot_at(T, t, w, (uint32_t)mix64(w), insert, val_out);
 }
 
-// The IPv4 fast chain's second-level word.  Tables of up to 2^24 slots keep
-// s0 in 24 bits beside the ports and the protocol; wider tables ("wide", more
-// than 8M flows) keep s0 in 31 bits, the ports and one protocol bit: TCP and
-// UDP only (v4_fast), every other protocol takes the generic chain.  A key
-// always takes the same chain, so either is exact.
+// The IPv4 fast chain's second-level word.  Tables of fewer than 2^24 slots
+// keep s0 (which can be the sentinel slot C) in 24 bits beside the ports and
+// the protocol; larger tables ("wide", 8M flows and more) keep s0 in 31 bits,
+// the ports and one protocol bit: TCP and UDP only (v4_fast), every other
+// protocol takes the generic chain.  A key always takes the same chain, so
+// either is exact.  (TableSet::wide also forces the wide layout on small
+// tables: FLUERE_WIDE_TABLES, a test seam for these paths.)
 __device__ __forceinline__ bool v4_fast(const TableSet& T, uint32_t proto) {
-    return T.C <= (1u << 24) || proto == 6u || proto == 17u;
+    return !T.wide || proto == 6u || proto == 17u;
 }
 __device__ __forceinline__ uint64_t v4_t1_word(const TableSet& T, uint32_t s0, uint32_t ports, uint32_t proto) {
-    return T.C <= (1u << 24) ? ((uint64_t)s0 << 40) | ((uint64_t)ports << 8) | proto
-                             : ((uint64_t)s0 << 33) | ((uint64_t)ports << 1) | (proto == 17u ? 1u : 0u);
+    return !T.wide ? ((uint64_t)s0 << 40) | ((uint64_t)ports << 8) | proto
+                   : ((uint64_t)s0 << 33) | ((uint64_t)ports << 1) | (proto == 17u ? 1u : 0u);
 }
 
 // The IPv4 fast chain in one round trip: T1's probe starts at a hash of the

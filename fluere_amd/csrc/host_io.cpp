@@ -17,6 +17,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <functional>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -106,27 +108,51 @@ extern "C" uint64_t fluere_format_csv(const fluere_record* recs, uint64_t n, cha
 }
 
 // Rows are formatted once, in blocks by threads when there are many, and
-// written in order.
+// written in order.  A block's buffer is appended whenever it has less than a
+// row's bound left; a row that would not fit its bound (cannot happen: the
+// bound is exact) is formatted again into a buffer of its own size.
+static void format_rows(const fluere_record* recs, uint64_t i0, uint64_t i1, std::string& out) {
+    std::vector<char> tmp(256 * kRowMax);
+    Out o{tmp.data(), tmp.size(), 0};
+    for (uint64_t i = i0; i < i1; i++) {
+        if (tmp.size() - o.n < kRowMax) {
+            out.append(tmp.data(), o.n);
+            o.n = 0;
+        }
+        const uint64_t at = o.n;
+        put_row(o, recs[i]);
+        if (o.n > o.cap) {  // (the row did not fit: its bytes past the buffer were not written)
+            Out z{nullptr, 0, 0};
+            put_row(z, recs[i]);
+            std::vector<char> big(z.n);
+            Out b{big.data(), big.size(), 0};
+            put_row(b, recs[i]);
+            out.append(tmp.data(), at);
+            out.append(big.data(), b.n);
+            o.n = 0;
+        }
+    }
+    out.append(tmp.data(), o.n);
+}
+
 extern "C" int fluere_write_csv(const fluere_record* recs, uint64_t n, const char* path) {
     if (!path || (!recs && n)) return FLUERE_E_ARG;
-    const int T = n >= (1u << 16) ? 8 : 1;
+    int T = n >= (1u << 16) ? 8 : 1;
     std::vector<std::string> part(T);
-    auto work = [&](int t) {
-        const uint64_t i0 = n * t / T, i1 = n * (t + 1) / T, blk = 4096;
-        std::vector<char> tmp(blk * kRowMax);
-        for (uint64_t b = i0; b < i1; b += blk) {
-            Out o{tmp.data(), tmp.size(), 0};
-            for (uint64_t i = b; i < std::min(i1, b + blk); i++) put_row(o, recs[i]);
-            part[t].append(tmp.data(), o.n);
-        }
-    };
-    if (T == 1) {
-        work(0);
-    } else {
+    if (T > 1) {
+        // threads; if the runtime cannot start them, the calling thread formats every row
         std::vector<std::thread> th;
-        for (int t = 0; t < T; t++) th.emplace_back(work, t);
+        try {
+            for (int t = 0; t < T; t++) th.emplace_back(format_rows, recs, n * t / T, n * (t + 1) / T, std::ref(part[t]));
+        } catch (const std::exception&) {
+            for (auto& x : th) x.join();
+            th.clear();
+            T = 1;
+            part.assign(1, std::string());
+        }
         for (auto& x : th) x.join();
     }
+    if (T == 1) format_rows(recs, 0, n, part[0]);
     FILE* f = fopen(path, "wb");
     if (!f) return FLUERE_E_IO;
     bool ok = fwrite(kHeader, 1, strlen(kHeader), f) == strlen(kHeader);

@@ -886,6 +886,47 @@ def test_tcp_realistic_matches_oracle(gpu, name):
             assert st["sequential_mode"] == 1  # the parallel sweep, not the fallback
 
 
+def _splice_icmp(data, every=7, pairs=300):
+    """The records of a classic pcap with an ICMP echo frame after every
+    `every`-th one (its neighbour's timestamp, so times keep their order);
+    `pairs` address pairs, so ICMP flows have several packets."""
+    import struct
+    import pktbuild as pb
+    out = [data[:24]]
+    p, k = 24, 0
+    while p + 16 <= len(data):
+        sec, frac, incl, _ = struct.unpack_from("<IIII", data, p)
+        out.append(data[p:p + 16 + incl])
+        p += 16 + incl
+        k += 1
+        if k % every == 0:
+            j = (k // every) % pairs
+            f = pb.eth() + pb.ipv4(f"172.16.{j // 250}.{j % 250 + 1}", "172.17.0.9", 1, b"\x08\x00" + bytes(30), ttl=40 + j % 9)
+            out.append(struct.pack("<IIII", sec, frac, len(f), len(f)) + f)
+    return b"".join(out)
+
+
+def test_wide_tables_mixed_protocols(gpu, monkeypatch):
+    """The wide IPv4 dictionary layout (flow_table.h v4_t1_word: tables of
+    2^24 slots and more) forced on small tables (FLUERE_WIDE_TABLES): TCP
+    through the exact engine and the Mode B sweep, UDP, and ICMP flows, which
+    the wide layout sends through the generic chain (v4_fast) -- including the
+    merge's staged_id branch -- all equal the oracle."""
+    monkeypatch.setenv("FLUERE_WIDE_TABLES", "1")
+    data = _splice_icmp(fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 200_000, 2_000, 0xF10E0057)))
+    for t in (600000, 5):
+        want = pyoracle.offline(data, t)
+        csv, ne, st = _gpu_csv(data, t, max_flows=1 << 17)
+        assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"wide tables t={t}")
+        if t == 5:
+            assert st["sequential_mode"] == 1, st
+    for spill in ("0", "1"):  # both hot kernels (the spill kernel's records go through the merge's wide branch)
+        monkeypatch.setenv("FLUERE_SPILL_MODE", spill)
+        want = pyoracle.offline(data, 600000)
+        csv, ne, st = _gpu_csv(data, 600000, max_flows=1 << 17)
+        assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"wide tables spill={spill}")
+
+
 def _sweep_chain(L, T_us=10_000):
     """A capture whose Mode B fixed point needs about L passes: key K_i opens
     with a SYN early; its entry fires at the first processed packet at or
