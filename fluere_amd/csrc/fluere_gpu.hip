@@ -892,6 +892,7 @@ struct PassPlan {
     uint32_t slow_grid[PLAN_BATCHES];  // k_slow workgroups (its sets); 0: the merge tail takes the slow list
     int macs, abl;
     int spill;     // 1: the hot pass is k_parse_spill (many flows per window), not k_parse_agg
+    int lean_merge;  // 1: runs without partials merge their owners in k_merge_spill (0: k_merge_partials, A/B)
     int phash;     // 1: the hot pass writes the per-packet filter words (AggArgs::phash)
     int pid;       // 1: the merge writes each packet's flow over them (AggArgs::pid; k_parse_spill runs)
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
@@ -1157,6 +1158,14 @@ static int spill_mode(const fluere_ctx* c) {
     return F * (1.0 - std::exp(-w / F)) > 2.0 * (c->use_mac ? NS_MAC : NS) ? 1 : 0;
 }
 
+// k_merge_spill for the runs without partials (not MAC runs: their 64-byte
+// records stay with k_merge_partials); FLUERE_LEAN_MERGE=0: k_merge_partials
+// for every run (A/B)
+static int lean_merge(const fluere_ctx* c) {
+    const int env = getenv("FLUERE_LEAN_MERGE") ? atoi(getenv("FLUERE_LEAN_MERGE")) : -1;
+    return !c->use_mac && env != 0 ? 1 : 0;
+}
+
 static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     memset(&P, 0, sizeof P);  // byte-comparable (padding included)
     int rc;
@@ -1172,6 +1181,7 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
     P.tab_words = (size_t)N_TABLES * 2 * (c->C + 1);
     P.clean = c->precleaned ? 0 : 1;
     P.spill = spill_mode(c);
+    P.lean_merge = lean_merge(c);
     if ((rc = plan_batches(c, P))) return rc;
     static const int abl = diag_knob("FLUERE_ABLATE");
     P.macs = c->use_mac;
@@ -1234,9 +1244,20 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
             }
         }
         // at most one merge workgroup per CU, each taking owners in turn
-        // + the slow list (unless k_slow took it)
-        HIPCHECK(hipLaunchKernel(merge_kernel(P.macs), dim3(std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu)), dim3(MB),
-                                 args, 0, s));
+        // + the slow list (unless k_slow took it).  Runs without partials
+        // (k_parse_spill, k_slow): the lean owner merge, then the tail alone
+        // (overflow list, general-parser packets, run statistics)
+        const dim3 mgrid(std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu));
+        if (P.lean_merge && a.S.no_parts) {
+            HIPCHECK(hipLaunchKernel((const void*)k_merge_spill, mgrid, dim3(MB), args, 0, s));
+            AggArgs at = a;
+            at.tail_only = 1;
+            at.dbg = nullptr;  // (FLUERE_DEBUG: the phase clocks are k_merge_spill's)
+            void* targs[] = {&at};
+            HIPCHECK(hipLaunchKernel(merge_kernel(P.macs), dim3((uint32_t)c->n_cu), dim3(MB), targs, 0, s));
+        } else {
+            HIPCHECK(hipLaunchKernel(merge_kernel(P.macs), mgrid, dim3(MB), args, 0, s));
+        }
         if (hostprof) {
             const auto t2 = std::chrono::steady_clock::now();
             auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
@@ -1452,6 +1473,7 @@ extern "C" int fluere_parse_aggregate(fluere_ctx* c) {
     if ((rc = upload_batches(c))) return rc;
     if ((rc = census(c))) return rc;
     P.spill = spill_mode(c);
+    P.lean_merge = lean_merge(c);
     if ((rc = plan_batches(c, P, false))) return rc;
     if (P.nb > PLAN_BATCHES) return FLUERE_E_ARG;
     static const int abl = diag_knob("FLUERE_ABLATE");
@@ -1627,6 +1649,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             Q.macs = P.macs;
             Q.abl = P.abl;
             Q.spill = P.spill;
+            Q.lean_merge = P.lean_merge;
             rc = plan_batches(c, Q, false);
             if (!rc) rc = enqueue_batches(c, Q);
             if (rc) break;

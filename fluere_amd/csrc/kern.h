@@ -62,9 +62,11 @@ static_assert(sizeof(Part) == 80, "Part layout");
 // merged by its owner like a one-packet partial.
 struct alignas(16) Spill {
     uint32_t k0, k1, k2, tag;     // LDS key words (tag = proto << 24)
-    uint32_t doct, pt, loc, fl;   // pt = pkt | ttl << 16 | elig << 24; fl = tf | dir << 8 (| set << 9: overflow list)
+    uint32_t doct, pt, loc, fl;   // pt = pkt | ttl << 16 | elig << 24; fl = tf | dir << 8 (| set << 9: overflow list;
+                                  // set SPILL_BATCH_REL: loc is relative to the batch's first packet)
 };
 static_assert(sizeof(Spill) == 32, "Spill layout");
+constexpr uint32_t SPILL_BATCH_REL = 0x7FFFFFu;
 // MAC kernels: a spilled packet takes two records: {k0, k1, k2, tag},
 // {m0, m1, m2, key hash}, {doct, pt, loc, fl}, padding.
 __host__ __device__ constexpr int spill_units(bool macs) { return macs ? 2 : 1; }
@@ -177,6 +179,8 @@ struct AggArgs {
     uint32_t* emap;
     uint64_t pid_base;
     uint32_t pid_batch;
+    int tail_only;             // k_merge_partials: no owners (k_merge_spill merged them), only the run
+                               // statistics and the tail (overflow list, general-parser packets)
     int slow_all;              // k_slow takes every packet of the batch (no hot kernel: captures of the general
                                // parser's classes, where the hot pass would only list them)
 };
@@ -755,6 +759,7 @@ __global__ void __launch_bounds__(64) k_seq_run(SeqArgs a);
 __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words);
 __global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v);
 __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v);
+__global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a);
 // templated kernels: their host stubs, by configuration
 const void* hot_kernel(int spill, int macs, int abl);  // hot.hip: k_parse_agg / k_parse_spill
 const void* merge_kernel(int macs);                     // merge.hip: k_merge_partials

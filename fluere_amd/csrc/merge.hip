@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     // early takes the next one (owners' record phases spread, e.g. C3 99-199
     // us).  No counter when every workgroup has one owner.
     __shared__ uint32_t s_me;
-    if (tid == 0) s_me = blockIdx.x;
+    if (tid == 0) s_me = a.tail_only ? S.O : blockIdx.x;  // (tail_only: k_merge_spill took the owners)
     __syncthreads();
     const int pass0 = S.no_parts ? 1 : 0;  // (no partials: the segments' pass alone)
     for (uint32_t me = s_me; me < S.O; me = s_me) {
@@ -660,7 +660,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 x0 = v1.x; x1 = v1.y; x2 = v1.z;
             }
             FlowPart f;
-            const unsigned long long wbase = S.base[pay.w >> 9];
+            const unsigned long long wbase = (pay.w >> 9) == SPILL_BATCH_REL ? a.B.first : S.base[pay.w >> 9];
             spill_to_part(pay.x, pay.y, pay.z, pay.w, wbase, f);
             uint32_t d;
             if (macs && v0.w != 0xFF000000u) {
@@ -1164,6 +1164,441 @@ __global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v
 __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
+}
+
+// ---------------------------------------------------------------------------
+// k_merge_spill: the owner merge of runs whose hot pass staged no partials
+// (k_parse_spill, k_slow): every record is one packet (Spill, 32 B) in its
+// owner's segment of a set.  Lean per record, and loads kept in flight:
+//  * an owner's segments of a chunk of sets are flattened (exclusive scan of
+//    their counts); a wave takes strips of 256 consecutive flattened records,
+//    four per lane, all eight 16-byte loads issued before the first is used;
+//  * a record's set comes from a 64-record group map (every lane of a
+//    64-aligned group starts from the same set) and a forward step;
+//  * one LDS read per record gives the segment's record base and the window's
+//    first packet (relative to the batch): positions are u32 batch-relative in
+//    LDS, the update is update_flow's order-free part (flows.rs:11-42) as
+//    unguarded LDS atomics.
+// The overflow list and the general-parser packets are not read here:
+// k_merge_partials (tail_only) takes them, and the run statistics, after it.
+// ---------------------------------------------------------------------------
+// The merge's rare paths, out of line: inlined, the dictionary's generic
+// chain (dense_of_key, up to 12 levels) puts tens of KiB of code between the
+// instructions of the record loop.
+#ifndef FLUERE_MS_STRIP
+#define FLUERE_MS_STRIP 2
+#endif
+#ifndef FLUERE_MS_BATCH
+#define FLUERE_MS_BATCH 1  // the strip's first probes issued together (0: each record's probe loop alone; A/B)
+#endif
+#ifndef FLUERE_MS_ABL
+#define FLUERE_MS_ABL 0  // diagnostics only (wrong results): 1 the record loads alone, 2 + the probe, no updates
+#endif
+#ifndef FLUERE_MS_COLD
+#define FLUERE_MS_COLD 1  // the global path out of line (0: inlined; A/B)
+#endif
+#if FLUERE_MS_COLD
+#define MS_COLD __noinline__
+#else
+#define MS_COLD __forceinline__
+#endif
+__device__ MS_COLD uint32_t staged_id_cold(const AggArgs* ap, uint4 kk, uint32_t tag) {
+    const AggArgs& a = *ap;
+    if (kk.w & V6_TAG) {
+        CKey ck;
+        v6_ckey(a.v6, kk.x, kk.y, kk.z, tag, ck);
+        return dense_of_key(a.T, ck, true, a.A.slots, &a.g->generic_used);
+    }
+    return staged_id(a.T, a.v6, kk.x, kk.y, kk.z, tag, a.A.slots);
+}
+
+// The IPv4 chain for a key its merge owner resolves (k_merge_spill): each
+// level's word by a CAS first -- a new word costs one atomic round trip (a
+// read, then a CAS, cost two), a present one returns itself.  fresh: this
+// call inserted the T1 word (the flow has no dense id yet).
+__device__ __forceinline__ uint32_t tab_claim(const TableSet& T, int t, uint64_t w, uint32_t h0, bool& fresh) {
+    unsigned long long* tab = T.tab[t];
+    fresh = false;
+    if (w == EMPTY) return T.C;
+    uint32_t h = h0 & (T.C - 1);
+    for (int p = 0; p < MAX_PROBE; p++) {
+        const unsigned long long old = atomicCAS(&tab[2 * h], EMPTY, (unsigned long long)w);
+        if (old == EMPTY) { fresh = true; return h; }
+        if (old == w) return h;
+        h = (h + 1) & (T.C - 1);
+    }
+    atomicOr(T.err, ERR_TABLE_FULL);
+    return FAIL;
+}
+__device__ __forceinline__ void v4_claim(const TableSet& T, uint32_t lo, uint32_t hi, uint32_t ports, uint32_t proto,
+                                         uint32_t& s0, uint32_t& s1, bool& fresh1) {
+    bool f0;
+    s1 = FAIL;
+    fresh1 = false;
+    const uint64_t w0 = ((uint64_t)lo << 32) | hi;
+    s0 = tab_claim(T, 0, w0, (uint32_t)mix64(w0), f0);
+    if (s0 == FAIL) return;
+    s1 = tab_claim(T, 1, v4_t1_word(T, s0, ports, proto), v4_t1_start(lo, hi, ports, proto), fresh1);
+}
+
+constexpr int MS_STRIP = FLUERE_MS_STRIP;
+// k_merge_spill's key table: MK entries probed in pairs (two-choice: the
+// key's home pair e1 and a second pair e2), each holding its aggregate slot
+// (< MT) in bits 8..21 of its last word (the tag's protocol, bits 24..31, and
+// flags, bits 0..7, stay readable)
+constexpr int MK = 2048;
+constexpr uint32_t MS_SLOT_MASK = 0x3FFFu << 8, MS_NOSLOT = 0x3FFFu;
+static_assert(MT <= 0x3FFF, "slots fit the entry's slot field");
+static_assert((LT_READY | LT_CLAIM) & MS_SLOT_MASK ? false : true, "the slot field clears the state bits");
+__device__ __forceinline__ void ms_pairs(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag, uint32_t& e1, uint32_t& e2) {
+    uint32_t x = k0 ^ __builtin_amdgcn_alignbit(k1, k1, 11) ^ __builtin_amdgcn_alignbit(k2, k2, 22) ^ (tag >> 24) ^ (tag << 7);
+    x ^= x >> 16;
+    x = __umul24(x, 0x9E3779u) ^ (x >> 24);
+    x = __umul24(x ^ (x >> 13), 0x5BD1E9u) ^ (x >> 9);
+    e1 = (x & (MK - 1)) & ~1u;
+    e2 = ((x >> 11) & (MK - 1)) & ~1u;
+    if (e2 == e1) e2 ^= 2u;
+}
+// merge-table home slot of a staged key (10 bits: MT == 1024): the key words
+// folded, then mixed with full-rate 24-bit multiplies (lt_hash's 32-bit
+// multiplies are quarter rate: a fifth of the record loop's VALU time)
+__device__ __forceinline__ uint32_t ms_slot(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t tag) {
+    uint32_t x = k0 ^ __builtin_amdgcn_alignbit(k1, k1, 11) ^ __builtin_amdgcn_alignbit(k2, k2, 22) ^ (tag >> 24) ^ (tag << 7);
+    x ^= x >> 16;
+    x = __umul24(x, 0x9E3779u) ^ (x >> 24);
+    x = __umul24(x ^ (x >> 13), 0x5BD1E9u);
+    return (x >> 6) & (MT - 1);
+}  // records per lane per strip (a strip: 64 * MS_STRIP records of one wave)
+constexpr uint32_t MS_GRP = 1024;  // 64-record groups mapped in LDS (owners of more records: a binary search)
+__global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
+    // the arguments in the kernarg segment, for the out-of-line paths (a
+    // reference to `a` would copy the whole struct to every lane's stack)
+    const AggArgs* kargs = (const AggArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    // key table: MK entries {k0, k1, k2, tag | READY / CLAIM | slot << 8}, probed as
+    // two-choice pairs; the aggregates below are per slot (MT), in claim order
+    __shared__ uint4 m_key[MK];
+    __shared__ uint16_t m_sk[MT];  // key entry of each slot
+    __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
+    __shared__ unsigned long long m_by[2][MT];
+    __shared__ uint32_t m_pos[4][MT];  // first, first create-eligible, first FIN/RST (min), last + 1 (max): batch-relative
+    // per non-empty segment of the chunk (k: its rank): {record index - flattened start (mod 2^32),
+    // window base}, flattened start; per group of 64 flattened records {segment of its first
+    // record, 0, 64-bit mask of the records that start a segment}
+    __shared__ uint2 m_sd[MCH];
+    __shared__ uint32_t m_st[MCH];
+    __shared__ uint4 m_ginfo[MS_GRP];
+    __shared__ uint32_t m_scan[MB / 64 + 1], m_nclaim, m_base, s_me, m_nslot;
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    const Stage& S = a.S;
+    const uint64_t bfirst = a.B.first;
+    const uint4* recs = reinterpret_cast<const uint4*>(S.dspill);
+    if (tid == 0) s_me = blockIdx.x;
+    __syncthreads();
+    unsigned long long* dbg = a.dbg ? a.dbg + 4096 * 8 - 2048 + blockIdx.x * 8 : nullptr;  // (FLUERE_DEBUG: phase clocks)
+    for (uint32_t me = s_me; me < S.O; me = s_me) {
+        if (dbg && tid == 0) dbg[0] = wall_clock64();
+        for (int e = tid; e < MK; e += MB) m_key[e] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) m_nslot = 0;
+        for (int e = tid; e < MT; e += MB) {
+            m_pk[0][e] = m_pk[1][e] = 0;
+            m_by[0][e] = m_by[1][e] = 0;
+            m_mn[0][e] = m_mn[1][e] = NONE32;
+            m_mx[0][e] = m_mx[1][e] = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) m_fl[q][e] = 0;
+            m_pos[0][e] = m_pos[1][e] = m_pos[2][e] = NONE32;
+            m_pos[3][e] = 0;
+        }
+        for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
+            const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
+            // this owner's segment of each set of the chunk: count, record base, window base
+            static_assert(MCH == MB, "one set per thread");
+            const uint32_t s = c0s + tid;
+            uint32_t cnt = 0, rb = 0, wb = 0;
+            if ((uint32_t)tid < nset) {
+                cnt = S.soff[(size_t)me * S.n_sets + s];
+                rb = s < S.n_hot ? (uint32_t)(((unsigned long long)s * S.O + me) * S.cap_o)
+                                 : (uint32_t)(S.slow_rec0 + ((unsigned long long)(s - S.n_hot) * S.O + me) * S.cap_s);
+                wb = (uint32_t)(S.base[s] - bfirst);
+            }
+            // the non-empty segments, compacted (k: rank among them), with their
+            // flattened starts (exclusive scan of the counts)
+            if (dbg && tid == 0 && c0s == 0) dbg[1] = wall_clock64();
+            const uint32_t st0 = block_exclusive_scan(cnt, m_scan);  // (ends with a barrier)
+            const uint32_t total = m_scan[MB / 64];
+            const uint32_t k = block_exclusive_scan(cnt ? 1u : 0u, m_scan);
+            const uint32_t nk = m_scan[MB / 64];
+            const uint32_t ngrp = (total + 63) / 64;
+            const bool grp = ngrp <= MS_GRP;
+            if (grp)
+                for (uint32_t g = tid; g < ngrp; g += MB) m_ginfo[g] = make_uint4(0, 0, 0, 0);
+            if (cnt) {
+                m_sd[k] = make_uint2(rb - st0, wb);
+                m_st[k] = st0;
+            }
+            __syncthreads();
+            // per group of 64 flattened records: the segment holding its first
+            // record, and a bit per later record that starts a segment
+            if (grp && cnt) {
+                if (st0 & 63) atomicOr(&m_ginfo[st0 >> 6].z + ((st0 & 63) >> 5), 1u << (st0 & 31));
+                for (uint32_t g = (st0 + 63) >> 6; g <= (st0 + cnt - 1) >> 6; g++) m_ginfo[g].x = k;
+            }
+            __syncthreads();
+            // record f's segment (rank k) -> {record index - flattened start, window base}
+            auto seg_of = [&](uint32_t f) -> uint2 {
+                uint32_t kk;
+                if (grp) {
+                    const uint4 gi = m_ginfo[f >> 6];  // (the same for every lane of a 64-aligned group)
+                    const uint32_t p = f & 63;
+                    const unsigned long long msk = ((unsigned long long)gi.w << 32) | gi.z;
+                    kk = gi.x + (uint32_t)__popcll(msk & ((2ull << p) - 2ull));
+                } else {
+                    uint32_t lo = 0, hi = nk - 1;  // last segment starting at or before f
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi + 1) >> 1;
+                        if (m_st[mid] <= f) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    kk = lo;
+                }
+                return m_sd[kk];
+            };
+            // strips of 64 * MS_STRIP records; record u * 64 + lane of a strip is
+            // this lane's u-th.  Two strips in flight per wave: the next one's
+            // loads are issued before this one is probed and aggregated.
+            const uint32_t nstrip = (total + 64 * MS_STRIP - 1) / (64 * MS_STRIP);
+            auto fetch = [&](uint32_t sp, uint4 (&v0)[MS_STRIP], uint4 (&v1)[MS_STRIP], uint32_t (&wbr)[MS_STRIP]) {
+                uint2 sd[MS_STRIP];
+                uint32_t fc[MS_STRIP];
+#pragma unroll
+                for (int u = 0; u < MS_STRIP; u++) {
+                    fc[u] = min(sp * (64 * MS_STRIP) + u * 64 + lane, total - 1);  // (past the end: the last record, unused)
+                    sd[u] = seg_of(fc[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < MS_STRIP; u++) {
+                    const uint32_t idx = sd[u].x + fc[u];
+                    v0[u] = recs[(size_t)idx * 2];
+                    v1[u] = recs[(size_t)idx * 2 + 1];
+                    wbr[u] = sd[u].y;
+                }
+            };
+            auto process = [&](uint32_t sp, const uint4 (&v0)[MS_STRIP], const uint4 (&v1)[MS_STRIP],
+                               const uint32_t (&wbr)[MS_STRIP]) {
+                if (FLUERE_MS_ABL == 1) {  // diagnostics (wrong results): the records' loads alone
+#pragma unroll
+                    for (int u = 0; u < MS_STRIP; u++)
+                        if ((v0[u].x ^ v0[u].y ^ v0[u].z ^ v1[u].x ^ v1[u].y ^ wbr[u]) == 0x12345678u) atomicAdd(&m_pk[0][0], 1u);
+                    return;
+                }
+                // first probes of the strip's records together: both candidate
+                // pairs of each key (four 16-byte reads, one LDS round trip); the
+                // claim loop runs only for new keys and keys placed further on
+                uint32_t e1[MS_STRIP], e2[MS_STRIP];
+                uint4 kp[MS_STRIP][4];
+#pragma unroll
+                for (int u = 0; u < MS_STRIP; u++) {
+                    ms_pairs(v0[u].x, v0[u].y, v0[u].z, v0[u].w, e1[u], e2[u]);
+                    kp[u][0] = m_key[e1[u]];
+                    kp[u][1] = m_key[e1[u] + 1];
+                    kp[u][2] = m_key[e2[u]];
+                    kp[u][3] = m_key[e2[u] + 1];
+                }
+#pragma unroll
+                for (int u = 0; u < MS_STRIP; u++) {
+                    const uint32_t f = sp * (64 * MS_STRIP) + u * 64 + lane;
+                    const bool live = f < total;
+                    const uint32_t k0 = v0[u].x, k1 = v0[u].y, k2 = v0[u].z, tag = v0[u].w;
+                    const uint32_t rel = wbr[u] + v1[u].z;  // batch-relative packet index
+                    const uint32_t want = tag | LT_READY;
+                    uint32_t e = MS_NOSLOT;
+#pragma unroll
+                    for (int j = 3; j >= 0; j--)
+                        if ((((kp[u][j].w & ~MS_SLOT_MASK) ^ want) | (kp[u][j].x ^ k0) | (kp[u][j].y ^ k1) | (kp[u][j].z ^ k2)) == 0u)
+                            e = (kp[u][j].w >> 8) & 0x3FFFu;
+                    int state = !live ? 3 : e != MS_NOSLOT ? 1 : 0;
+                    if (__ballot(state == 0)) {
+                        // the key's probe sequence: pair e1, pair e2, then pairs from e2 + 2
+                        uint32_t pe = e1[u];
+                        int steps = 0;
+                        for (int it = 0; it < 4 * MK; it++) {  // (bounded: every pass reads or claims)
+                            if (state == 0) {
+                                const uint4 ka = m_key[pe], kb = m_key[pe + 1];
+                                const bool ma = (((ka.w & ~MS_SLOT_MASK) ^ want) | (ka.x ^ k0) | (ka.y ^ k1) | (ka.z ^ k2)) == 0u;
+                                const bool mb = (((kb.w & ~MS_SLOT_MASK) ^ want) | (kb.x ^ k0) | (kb.y ^ k1) | (kb.z ^ k2)) == 0u;
+                                if (ma | mb) {
+                                    e = ((ma ? ka.w : kb.w) >> 8) & 0x3FFFu;
+                                    state = e < MT ? 1 : 2;
+                                } else if ((ka.w & LT_READY) && (kb.w & LT_READY)) {
+                                    if (++steps == MK / 2) state = 2;
+                                    else pe = steps == 1 ? e2[u] : (pe + 2) & (MK - 1);
+                                } else {
+                                    // the pair's first free entry (an entry being written is read again next pass)
+                                    const uint32_t fe = ka.w == 0 ? pe : ((ka.w & LT_READY) && kb.w == 0 ? pe + 1 : MK);
+                                    if (fe < MK && atomicCAS(&m_key[fe].w, 0u, LT_CLAIM) == 0u) {
+                                        uint32_t sl = atomicAdd(&m_nslot, 1u);
+                                        if (sl >= MT) sl = MS_NOSLOT;  // no aggregate slot left: the key's records take the global path
+                                        else m_sk[sl] = (uint16_t)fe;
+                                        m_key[fe].x = k0;
+                                        m_key[fe].y = k1;
+                                        m_key[fe].z = k2;
+                                        __threadfence_block();
+                                        atomicExch(&m_key[fe].w, want | (sl << 8));
+                                        e = sl;
+                                        state = sl < MT ? 1 : 2;
+                                    }
+                                }
+                            }
+                            if (__ballot(state == 0) == 0) break;
+                        }
+                    }
+                    const uint32_t dir = (v1[u].w >> 8) & 1u, tf = v1[u].w & 0xFFu;
+                    const uint32_t pkt = v1[u].y & 0xFFFFu, ttl = (v1[u].y >> 16) & 0xFFu;
+                    if (FLUERE_MS_ABL == 2) {  // diagnostics (wrong results): the probe, no updates
+                        if (state == 1 && pkt == 0x1234u) atomicAdd(&m_pk[0][e & (MT - 1)], 1u);
+                        continue;
+                    }
+                    if (state == 1) {  // update_flow of one packet (flows.rs:11-42), order-free part
+                        if (a.pid) a.pid[bfirst + rel - a.pid_base] = PH_EREF | (a.pid_batch << 21) | (me << 10) | e;
+                        atomicAdd(&m_pk[dir][e], 1u);
+                        atomicAdd(&m_by[dir][e], (unsigned long long)v1[u].x);
+                        atomicMin(&m_mn[0][e], pkt);
+                        atomicMin(&m_mn[1][e], ttl);
+                        atomicMax(&m_mx[0][e], pkt);
+                        atomicMax(&m_mx[1][e], ttl);
+                        atomicMin(&m_pos[0][e], rel);
+                        atomicMin(&m_pos[1][e], ((v1[u].y >> 24) & 1u) ? rel : NONE32);
+                        atomicMax(&m_pos[3][e], rel + 1);
+                        if (tf) {
+                            for (uint32_t t = tf; t; t &= t - 1) atomicAdd(&m_fl[__builtin_ctz(t)][e], 1u);
+                            if (tf & 5u) atomicMin(&m_pos[2][e], rel);
+                        }
+                    } else if (state == 2) {  // no aggregate slot: the overflow list (the tail takes it)
+                        const unsigned long long q = atomicAdd(&a.g->n_spill, 1ull);
+                        uint4* dst = reinterpret_cast<uint4*>(S.spill) + q * 2;
+                        dst[0] = v0[u];
+                        dst[1] = make_uint4(v1[u].x, v1[u].y, rel, (v1[u].w & 0x1FFu) | (SPILL_BATCH_REL << 9));
+                    }
+                }
+            };
+            if (dbg && tid == 0 && c0s == 0) dbg[2] = wall_clock64();
+            if (total) {
+                uint4 a0[MS_STRIP], a1[MS_STRIP], b0[MS_STRIP], b1[MS_STRIP];
+                uint32_t aw[MS_STRIP], bw[MS_STRIP];
+                uint32_t sp = wv;
+                fetch(sp, a0, a1, aw);
+                while (sp < nstrip) {  // (uniform)
+                    const uint32_t sq = sp + MB / 64;
+                    fetch(sq < nstrip ? sq : sp, b0, b1, bw);  // (always issued: no branch merges loading registers)
+                    process(sp, a0, a1, aw);
+                    if (sq >= nstrip) break;
+                    const uint32_t sr = sq + MB / 64;
+                    fetch(sr < nstrip ? sr : sq, a0, a1, aw);
+                    process(sq, b0, b1, bw);
+                    sp = sr;
+                }
+            }
+            __syncthreads();
+        }
+        // Dense ids: thread per entry (MT == MB), as k_merge_partials: the owner
+        // is the only inserter of its keys; one atomicAdd on the flow counter
+        // gives the workgroup's new ids.
+        static_assert(MT == MB, "one merge entry per thread");
+        if (dbg && tid == 0) dbg[3] = wall_clock64();
+        if (tid == 0) m_nclaim = 0;
+        __syncthreads();
+        const int e = tid;  // aggregate slot
+        const bool have = (uint32_t)e < min(m_nslot, (uint32_t)MT);
+        uint4 kk = have ? m_key[m_sk[e]] : make_uint4(0, 0, 0, 0);
+        kk.w &= ~MS_SLOT_MASK;
+        const uint32_t tag = kk.w & 0xFF000000u;
+        uint32_t d = FAIL, s0 = FAIL, s1 = FAIL, rank = 0;
+        bool claimed = false, wait = false;
+        unsigned long long* val = nullptr;
+        if (have) {
+            if (!(kk.w & V6_TAG) && tag == 0xFF000000u) {
+                d = kk.x;  // k_slow's keys of the dictionary's other chains carry dense ids
+            } else if ((kk.w & V6_TAG) || !v4_fast(a.T, tag >> 24)) {
+                // an IPv6 5-tuple from k_slow (address ids, any protocol), or (wide tables) a
+                // protocol other than TCP / UDP
+                d = staged_id_cold(kargs, kk, tag);
+            } else {  // IPv4 5-tuple: flow_table.h chain T0 (ip pair) -> T1 (slot, ports, proto)
+                unsigned long long v = EMPTY;
+                bool fresh = false;
+                v4_claim(a.T, kk.x, kk.y, kk.z, tag >> 24, s0, s1, fresh);
+                if (s1 != FAIL) {
+                    val = &a.T.tab[1][2 * s1 + 1];
+                    // a key this owner inserted has no id yet and no other claimer
+                    // (its owner is the only one that resolves it in this kernel)
+                    v = fresh ? EMPTY : atomicCAS(val, EMPTY, PENDING);
+                    if (v == EMPTY) {
+                        claimed = true;
+                        rank = atomicAdd(&m_nclaim, 1u);
+                    } else if (v == PENDING) {
+                        wait = true;
+                    } else {
+                        d = (uint32_t)v;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (dbg && tid == 0) dbg[7] = wall_clock64();
+        if (tid == 0) m_base = m_nclaim ? atomicAdd(a.T.n_flows, m_nclaim) : 0;
+        __syncthreads();
+        if (dbg && tid == 0) dbg[6] = wall_clock64();
+        if (claimed) {
+            d = m_base + rank;
+            if (d >= a.T.fmax) {
+                atomicOr(a.T.err, ERR_FLOWS_FULL);
+                d = FAIL;
+            } else {
+                uint32_t* dst = (uint32_t*)(a.T.flow_key + (size_t)d * 56);
+#pragma unroll
+                for (int k = 0; k < 14; k++) dst[k] = k == 0 ? kk.x : k == 4 ? kk.y : k == 8 ? kk.z : k == 9 ? tag >> 24 : 0;
+#pragma unroll
+                for (int j = 0; j < N_TABLES; j++) a.A.slots[(size_t)d * N_TABLES + j] = j == 0 ? s0 : j == 1 ? s1 : NONE32;
+            }
+            atomicExch(val, (unsigned long long)d);
+        }
+        for (int sp = 0; sp < (1 << 20); sp++) {  // a claim held elsewhere: poll (wave-uniform)
+            if (__ballot(wait) == 0) break;
+            if (wait) {
+                const unsigned long long v = __hip_atomic_load(val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v != PENDING && v != EMPTY) {
+                    d = (uint32_t)v;
+                    wait = false;
+                }
+            }
+            if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(16);
+        }
+        if (wait) atomicOr(a.T.err, ERR_SPIN);
+        if (dbg && tid == 0) dbg[4] = wall_clock64();
+        if (a.emap) a.emap[((size_t)a.pid_batch << 21) | ((size_t)me << 10) | (uint32_t)e] = (have && d < a.T.fmax) ? d : FAIL;
+        if (have && d != FAIL && d < a.T.fmax) {
+            FlowPart f;
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                f.pk[q] = m_pk[q][e];
+                f.by[q] = m_by[q][e];
+                f.mn[q] = m_mn[q][e];
+                f.mx[q] = m_mx[q][e];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) f.fl[q] = m_fl[q][e];
+            const uint32_t p0 = m_pos[0][e], p1 = m_pos[1][e], p2 = m_pos[2][e], p3 = m_pos[3][e];
+            f.fa = p0 == NONE32 ? NONE64 : bfirst + p0;
+            f.fc = p1 == NONE32 ? NONE64 : bfirst + p1;
+            f.fr = p2 == NONE32 ? NONE64 : bfirst + p2;
+            f.la = p3 ? bfirst + p3 : 0;
+            part_to_global(a.A, d, f);
+        }
+        if (dbg && tid == 0) dbg[5] = wall_clock64();
+        __syncthreads();  // (the next owner re-initialises the table)
+        if (tid == 0) s_me = S.O > gridDim.x ? gridDim.x + (uint32_t)atomicAdd(&a.g->n_owner, 1ull) : S.O;
+        __syncthreads();
+    }
 }
 
 const void* merge_kernel(int macs) {

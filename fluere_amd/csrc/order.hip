@@ -262,6 +262,76 @@ int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m) {
     return FLUERE_OK;
 }
 
+// Mode B with a large sweep group (an idle gap that ends thousands of flows
+// at one packet): every record in the reference's order by stable LSD radix
+// sorts -- by the firing entry's creation (aux[1]), then by exp + 1 (aux[0],
+// 0 for a FIN/RST close), then by the ending packet (order_key; active
+// records, NONE64, last) -- and one gather of the records and their words.
+__global__ void k_ob_keys(const unsigned long long* okey, const unsigned long long* aux, uint64_t n, int word,
+                          unsigned long long* keys, uint32_t* vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = word < 2 ? aux[2 * i + word] : okey[i];
+    vals[i] = (uint32_t)i;
+}
+__global__ void k_ob_rekey(const unsigned long long* okey, const unsigned long long* aux, const uint32_t* perm,
+                           uint64_t n, int word, unsigned long long* keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = perm[i];
+    keys[i] = word < 2 ? aux[2 * (size_t)j + word] : okey[j];
+}
+__global__ void k_ob_gather_aux(const unsigned long long* aux, const uint32_t* perm, uint64_t n, unsigned long long* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = perm[i];
+    out[2 * i] = aux[2 * (size_t)j];
+    out[2 * i + 1] = aux[2 * (size_t)j + 1];
+}
+
+static int order_sorted(fluere_ctx* c, uint64_t n, uint64_t n_ended, const unsigned long long* okey) {
+    hipStream_t s = c->stream;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64, s);
+    // (okey lives in the ordering scratch or the emitters' array: the keys get a buffer of their own)
+    void* buf = nullptr;
+    if (hipMalloc(&buf, 2 * al(n * 8) + 2 * al(n * 4) + al(tb)) != hipSuccess) return FLUERE_E_NOMEM;
+    char* p = (char*)buf;
+    auto take = [&](size_t bytes) { char* q = p; p += al(bytes); return q; };
+    unsigned long long* k0 = (unsigned long long*)take(n * 8);
+    unsigned long long* k1 = (unsigned long long*)take(n * 8);
+    uint32_t* v0 = (uint32_t*)take(n * 4);
+    uint32_t* v1 = (uint32_t*)take(n * 4);
+    void* tmp = p;
+    const unsigned g = grid_for(n, 256);
+    int rc = FLUERE_OK;
+    for (int word = 1; word >= -1 && rc == FLUERE_OK; word--) {  // aux[1], aux[0], order_key (word 2)
+        const int w = word < 0 ? 2 : word;
+        if (word == 1) k_ob_keys<<<g, 256, 0, s>>>(okey, c->d_recaux, n, w, k0, v0);
+        else k_ob_rekey<<<g, 256, 0, s>>>(okey, c->d_recaux, v0, n, w, k0);
+        size_t t = tb;
+        if (hipcub::DeviceRadixSort::SortPairs(tmp, t, k0, k1, v0, v1, (int)n, 0, 64, s) != hipSuccess) rc = FLUERE_E_HIP;
+        std::swap(v0, v1);  // the permutation so far (stable: ties keep the last pass's order)
+    }
+    if (rc == FLUERE_OK) {
+        k_act_gather<<<grid_for(n * REC_WORDS, 256), 256, 0, s>>>(c->d_recs, v0, n, c->d_recs2);
+        k_ob_gather_aux<<<g, 256, 0, s>>>(c->d_recaux, v0, n, c->d_recaux2);
+        if (hipGetLastError() != hipSuccess) rc = FLUERE_E_HIP;
+    }
+    HIPCHECK(hipStreamSynchronize(s));  // (then the scratch is released)
+    hipFree(buf);
+    if (rc) return rc;
+    std::swap(c->d_recaux, c->d_recaux2);
+    std::swap(c->d_recaux_cap, c->d_recaux2_cap);
+    std::swap(c->d_recs, c->d_recs2);
+    std::swap(c->d_recs_cap, c->d_recs2_cap);
+    c->dev_ordered = true;
+    c->dev_ordered_ended = n_ended;
+    return FLUERE_OK;
+}
+
 // Orders the run's n records in d_recs (n_ended of them ended) as
 // [ended][active]; Mode B with the order words in d_recaux.  Stream-ordered;
 // Mode B reads its largest group (records ending at one packet) once.
@@ -333,7 +403,7 @@ int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint
         const void* src[1] = {gmax};
         const int by[1] = {4};
         if ((rc = mail_fetch(c->h_mail, s, 1, src, by, &g))) return rc;
-        if (g > 1024) return FLUERE_OK;  // (fetch_records orders them on the host)
+        if (g > 1024) return order_sorted(c, n, n_ended, okey);  // (rank scans would be quadratic)
         k_ob_fill<<<gn, 256, 0, s>>>(okey, n, base, cb, ps, mem);
         k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, c->d_recaux, n, base, okey, nullptr, nullptr, ps, mem, blk_pre, n_ended,
                                       c->d_recs2, c->d_recaux2);

@@ -962,6 +962,31 @@ def test_mode_b_sweep_chain_passes(gpu, L):
     print(f"L={L}: passes {st['passes']} sequential_mode {st['sequential_mode']}")
 
 
+def test_mode_b_large_sweep_group(gpu):
+    """An idle gap longer than the timeout after 12k flow creations: the first
+    packet after it sweeps every one of them (offline_fluereflows.rs:161-175),
+    one group of 12k ended records, ordered on the device by the BTreeMap's
+    pop order -- exp (six creation times, 2k flows each), then push order --
+    with stable radix sorts (groups over 1024 used to fall back
+    to the host)."""
+    import pktbuild as pb
+    pk = []
+    for i in range(12_000):
+        t = 100 * (i // 2000)  # six creation times: equal exp within each
+        src = f"10.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}"
+        pk.append((0, t, pb.eth() + pb.ipv4(src, "10.200.0.1", 17, pb.udp(1000 + i % 50000, 5353, b"q" * 12))))
+        if i % 3 == 0:  # a second packet for some flows
+            pk.append((0, t + 1, pb.eth() + pb.ipv4("10.200.0.1", src, 17, pb.udp(5353, 1000 + i % 50000, b"r" * 30))))
+    pk.sort(key=lambda x: x[1])
+    pk.append((5, 0, pb.eth() + pb.ipv4("10.250.0.1", "10.250.0.2", 17, pb.udp(7, 7, b"x" * 12))))  # t = 5 s
+    data = pb.pcap(pk)
+    want = pyoracle.offline(data, 1000)
+    assert want["n_ended"] >= 12_000
+    csv, ne, st = _gpu_csv(data, 1000)
+    assert st["sequential_mode"] == 1, st
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], "large sweep group")
+
+
 def test_mode_b_backward_time_fixture(gpu):
     """Timestamps that go backwards (edge_keys): the sweep points come from
     the max segment tree and the pending entries are kept in pop order, so the
