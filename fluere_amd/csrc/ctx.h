@@ -42,6 +42,7 @@ struct fluere_ctx {
     Acc acc{};
     uint32_t* d_nflows = nullptr;  // [0] n_flows, [1] err (inside the d_glob allocation: Ctl)
     Glob* d_glob = nullptr;        // Ctl
+    unsigned long long* d_bctr = nullptr;  // per-batch counters of a pass of several batches (AggArgs::bc), 8 x 8 words
     Ctl* h_ctl = nullptr;          // pinned host copy
     HostMail* h_mail = nullptr;    // pinned mailbox of the exact engine's host reads (exact.h)
     bool batches_dirty = true;

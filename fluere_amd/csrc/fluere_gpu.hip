@@ -506,6 +506,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
     if (hipHostMalloc(&c->h_mail, sizeof(HostMail)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     memset(c->h_mail, 0, sizeof(HostMail));
     if (hipMalloc(&c->d_cbits, 1u << CBITS_LOG2) != hipSuccess) return fail(FLUERE_E_NOMEM);
+    if (hipMalloc(&c->d_bctr, 8 * 8 * sizeof(unsigned long long)) != hipSuccess) return fail(FLUERE_E_NOMEM);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreate(&c->ev_ctl) != hipSuccess)
@@ -600,6 +601,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     if (c->h_mail) hipHostFree(c->h_mail);
     hipFree(c->d_glob);
     hipFree(c->d_cbits);
+    hipFree(c->d_bctr);
     hipFree(c->d_phash);
     hipFree(c->d_emap);
     hipFree(c->d_batches);
@@ -893,6 +895,8 @@ struct PassPlan {
     int macs, abl;
     int spill;     // 1: the hot pass is k_parse_spill (many flows per window), not k_parse_agg
     int lean_merge;  // 1: runs without partials merge their owners in k_merge_spill (0: k_merge_partials, A/B)
+    int one_merge;   // 1: one k_merge_spill over every batch of the pass (after all the hot passes)
+    MergeSrc ms;     // the owner segments of every batch (k_merge_spill)
     int phash;     // 1: the hot pass writes the per-packet filter words (AggArgs::phash)
     int pid;       // 1: the merge writes each packet's flow over them (AggArgs::pid; k_parse_spill runs)
     int clean;     // 1: the pass starts with k_cleanup (0: the last fluere_run already cleared its flows)
@@ -1000,7 +1004,6 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     a.slow = c->d_slow;
     a.slow_cnt = c->d_slow + maxn;
     a.gen = c->d_slow + maxn + MB;
-    a.slow_n = &c->d_glob->n_slow;
     a.slow_abl = diag_knob("FLUERE_SLOW_ABL");
     // k_slow when the last run had slow packets (a wrong guess costs only the
     // merge tail's slower path, or an empty launch)
@@ -1066,7 +1069,14 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         a.dbg = g_hot_dbg;
     }
     // staging for the largest batch (every batch reuses it, in stream order)
-    size_t need_max = 0;
+    // One owner merge per pass (k_merge_spill over every batch's segments) when
+    // no batch stages partials: each batch keeps a staging area of its own.
+    // Otherwise every batch is merged right after its hot pass and reuses one.
+    int nbat = 0;
+    for (auto& hb : c->batches) nbat += hb.b.n ? 1 : 0;
+    P.one_merge = P.lean_merge && (P.spill || slow_all) && nbat > 1 && nbat <= MS_BATCHES ? 1 : 0;
+    size_t need_max = 0, need_sum = 0;
+    std::vector<size_t> stage_off;
     for (auto& hb : c->batches) {
         if (!hb.b.n) continue;
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
@@ -1076,8 +1086,12 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         const uint32_t W = (uint32_t)std::max<uint64_t>(1, (steps + WIN_ITERS - 1) / WIN_ITERS);
         const size_t sets = (size_t)grid * W, cells = sets * NS;
         const uint32_t O = merge_owners(c);
-        need_max = std::max(need_max, stage_bytes(cells, sets, O, grid, hb.b.n, c->use_mac, a.slow_kernel != 0));
+        const size_t sb = (stage_bytes(cells, sets, O, grid, hb.b.n, c->use_mac, a.slow_kernel != 0) + 255) & ~(size_t)255;
+        stage_off.push_back(P.one_merge ? need_sum : 0);
+        need_sum += sb;
+        need_max = std::max(need_max, sb);
     }
+    if (P.one_merge) need_max = need_sum;
     if (need_max > c->d_stage_bytes) {
         hipFree(c->d_stage);
         c->d_stage = nullptr;
@@ -1089,6 +1103,10 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     for (auto& hb : c->batches) {
         if (!hb.b.n) continue;
         a.B = hb.b;
+        char* stage = (char*)c->d_stage + stage_off[P.nb];
+        // the batch's counters: Glob's for a pass of one batch, else its own (zeroed per pass)
+        a.bc = nbat > 1 ? c->d_bctr + 8 * (size_t)P.nb : &c->d_glob->n_slow;
+        a.slow_n = a.bc;
         uint64_t want = (hb.b.n + BLOCK * 8 - 1) / (BLOCK * 8);
         unsigned grid = slow_all ? 0u : (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->n_cu));
         // staging: one set per (workgroup, window) -- k_parse_agg's loop bounds
@@ -1111,7 +1129,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         const size_t all = sets + n_slow_sets;
         Stage& S = ab.S;
         // layout (16-byte aligned pieces): parts | owner segments (hot, k_slow) | spill_raw | spill | base | off | soff
-        S.part = (Part*)c->d_stage;
+        S.part = (Part*)stage;
         S.cap_o = owner_cap(sets, O);
         S.cap_s = cap_s;
         S.slow_rec0 = (unsigned long long)sets * O * S.cap_o;
@@ -1130,6 +1148,22 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         S.n_hot = (uint32_t)sets;
         S.n_sets = (uint32_t)all;
         S.no_parts = (P.spill || slow_all) ? 1u : 0u;
+        if (P.nb < MS_BATCHES) {
+            SegSrc& sg = P.ms.b[P.nb];
+            sg.dspill = S.dspill;
+            sg.soff = S.soff;
+            sg.base = S.base;
+            sg.spill = S.spill;
+            sg.bc = ab.bc;
+            sg.slow_rec0 = S.slow_rec0;
+            sg.first = hb.b.first;
+            sg.cap_o = S.cap_o;
+            sg.cap_s = S.cap_s;
+            sg.n_sets = S.n_sets;
+            sg.n_hot = S.n_hot;
+            sg.slow_kernel = (uint32_t)ab.slow_kernel;
+            P.ms.nb = P.nb + 1;
+        }
         if (P.nb < PLAN_BATCHES) {
             P.agg[P.nb] = ab;
             P.agg_grid[P.nb] = grid;
@@ -1217,9 +1251,10 @@ static int plan_pass(fluere_ctx* c, PassPlan& P, bool finalize) {
 
 static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
     hipStream_t s = c->stream;
+    // the batches' own counters (AggArgs::bc; a pass of one batch uses Glob's, which k_cleanup zeroed)
+    if (P.nb > 1) HIPCHECK(hipMemsetAsync(c->d_bctr, 0, 8 * 8 * (size_t)P.nb, s));
     for (int i = 0; i < P.nb; i++) {
         const AggArgs& a = P.agg[i];
-        if (i > 0) HIPCHECK(hipMemsetAsync(&c->d_glob->n_slow, 0, 40, s));  // n_slow, n_spill, n_dspill, n_gen, n_owner (k_cleanup zeroed them for batch 0)
         const unsigned grid = P.agg_grid[i];
         const void* fn = hot_kernel(P.spill, P.macs, P.abl);
         // HIP events carried by the dispatch itself (start / stop timestamps of
@@ -1248,8 +1283,14 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         // (k_parse_spill, k_slow): the lean owner merge, then the tail alone
         // (overflow list, general-parser packets, run statistics)
         const dim3 mgrid(std::min<uint32_t>(P.owners[i], (uint32_t)c->n_cu));
-        if (P.lean_merge && a.S.no_parts) {
-            HIPCHECK(hipLaunchKernel((const void*)k_merge_spill, mgrid, dim3(MB), args, 0, s));
+        if (P.one_merge) {
+            // (after the last batch's hot pass: below)
+        } else if (P.lean_merge && a.S.no_parts) {
+            MergeSrc one = P.ms;
+            one.b[0] = P.ms.b[i];
+            one.nb = 1;
+            void* margs[] = {const_cast<AggArgs*>(&a), &one};
+            HIPCHECK(hipLaunchKernel((const void*)k_merge_spill, mgrid, dim3(MB), margs, 0, s));
             AggArgs at = a;
             at.tail_only = 1;
             at.dbg = nullptr;  // (FLUERE_DEBUG: the phase clocks are k_merge_spill's)
@@ -1262,6 +1303,21 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
             const auto t2 = std::chrono::steady_clock::now();
             auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
             fprintf(stderr, "[fluere] launch: hot %.1f merge %.1f us\n", us(t0, t1), us(t1, t2));
+        }
+    }
+    if (P.one_merge) {
+        // one owner merge over every batch's segments (each flow resolved and
+        // accumulated once per pass), then each batch's tail: its overflow list,
+        // general-parser packets and run statistics
+        void* margs[] = {const_cast<AggArgs*>(&P.agg[0]), const_cast<MergeSrc*>(&P.ms)};
+        HIPCHECK(hipLaunchKernel((const void*)k_merge_spill, dim3(std::min<uint32_t>(P.owners[0], (uint32_t)c->n_cu)),
+                                 dim3(MB), margs, 0, s));
+        for (int i = 0; i < P.nb; i++) {
+            AggArgs at = P.agg[i];
+            at.tail_only = 1;
+            at.dbg = nullptr;
+            void* targs[] = {&at};
+            HIPCHECK(hipLaunchKernel(merge_kernel(P.macs), dim3((uint32_t)c->n_cu), dim3(MB), targs, 0, s));
         }
     }
     HIPCHECK(hipGetLastError());
@@ -1293,6 +1349,7 @@ static int enqueue_pass(fluere_ctx* c, const PassPlan& P) {
 // timestamps on this runtime, explicit event-record nodes do.  `P` must stay
 // alive and unchanged while the graph exists (kernel nodes point at its args).
 static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
+    if (P.one_merge) return FLUERE_E_ARG;  // (a pass merged once runs direct launches)
     hipGraph_t g = nullptr;
     HIPCHECK(hipGraphCreate(&g, 0));
     hipGraphNode_t prev = nullptr, n = nullptr;
@@ -1319,13 +1376,13 @@ static int build_pass_graph(fluere_ctx* c, PassPlan& P, hipGraphExec_t* out) {
     if (P.clean) kernel((const void*)k_cleanup, P.clean_grid, 256, a_clean);
     void* a_agg[PLAN_BATCHES][1];
     for (int i = 0; i < P.nb && ok; i++) {
-        if (i > 0) {
+        if (i == 0 && P.nb > 1) {  // the batches' own counters (AggArgs::bc)
             hipMemsetParams mp{};
-            mp.dst = &c->d_glob->n_slow;
+            mp.dst = c->d_bctr;
             mp.elementSize = 4;
-            mp.width = 10;  // n_slow, n_spill, n_dspill, n_gen, n_owner
+            mp.width = 16 * (size_t)P.nb;
             mp.height = 1;
-            mp.pitch = 16;
+            mp.pitch = 0;
             mp.value = 0;
             ok = hipGraphAddMemsetNode(&n, g, &prev, 1, &mp) == hipSuccess;
             prev = n;
@@ -1539,6 +1596,7 @@ int prepare_capture(fluere_ctx* c) {
     PassPlan P;
     memset(&P, 0, sizeof P);
     P.spill = spill_mode(c);
+    P.lean_merge = lean_merge(c);
     if (plan_batches(c, P) != FLUERE_OK) return FLUERE_OK;  // (stage, slow list, filter words, IPv6 ids)
     const uint64_t N = c->n_total;
     const bool tcp = c->last_n_complex != 0;

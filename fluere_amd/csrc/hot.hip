@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             if (l == 63) own_set(arr, O, incl);
         }
         const uint32_t nsp = s_nspill;  // overflow records of this window
-        if (tid == 128) s_sbase = nsp ? atomicAdd(&a.g->n_spill, (unsigned long long)nsp) : 0ull;
+        if (tid == 128) s_sbase = nsp ? atomicAdd(&a.bc[1], (unsigned long long)nsp) : 0ull;
         if (tid == 0) ovf_total += nsp;
         lds_barrier();
         for (uint32_t o = tid; o <= O; o += BLOCK) {
@@ -736,7 +736,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         a.slow_cnt[blockIdx.x] = s_slow;
         if (s_slow) atomicAdd(a.slow_n, (unsigned long long)s_slow);
         // spills in owner segments: every LDS-table miss but the overflow
-        if (s_cnt[2] > ovf_total) atomicAdd(&a.g->n_dspill, s_cnt[2] - ovf_total);
+        if (s_cnt[2] > ovf_total) atomicAdd(&a.bc[2], s_cnt[2] - ovf_total);
         if (a.dbg) {
             const unsigned long long rt_end = wall_clock64();
             a.dbg[blockIdx.x * 8 + 0] = rt_start;
@@ -963,7 +963,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
         }
         __syncthreads();  // (every overflow record written before the list copy below)
         const uint32_t nsp = s_nspill;
-        if (tid == 128) s_sbase = nsp ? atomicAdd(&a.g->n_spill, (unsigned long long)nsp) : 0ull;
+        if (tid == 128) s_sbase = nsp ? atomicAdd(&a.bc[1], (unsigned long long)nsp) : 0ull;
         if (tid == 0) { ovf_total += nsp; S.base[set] = B.first + wbase; s_chunk = 0; }
         for (uint32_t o = tid; o <= O; o += BLOCK) {
             S.off[(size_t)o * S.n_sets + set] = 0;  // no partials
@@ -1027,7 +1027,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
         st[5] = st[6] = st[7] = 0;
         a.slow_cnt[blockIdx.x] = s_slow;
         if (s_slow) atomicAdd(a.slow_n, (unsigned long long)s_slow);
-        if (s_cnt[0] > ovf_total) atomicAdd(&a.g->n_dspill, s_cnt[0] - ovf_total);
+        if (s_cnt[0] > ovf_total) atomicAdd(&a.bc[2], s_cnt[0] - ovf_total);
         if (a.dbg) {
             a.dbg[blockIdx.x * 8 + 0] = rt_start;
             a.dbg[blockIdx.x * 8 + 1] = a.dbg[blockIdx.x * 8 + 2] = a.dbg[blockIdx.x * 8 + 3] = wall_clock64();

@@ -159,7 +159,11 @@ struct AggArgs {
     Glob* g;
     uint32_t* slow;            // packets (batch-local indices) the hot parser left to the general parser:
                                // workgroup b's in slow[b * slow_region, + slow_cnt[b])
-    unsigned long long* slow_n;  // their total (the merge's "any slow packet" test)
+    unsigned long long* slow_n;  // their total (the merge's "any slow packet" test): bc[0]
+    // the batch's counters {slow-list packets, overflow-list records, owner-segment
+    // spills, general-parser list, merge owners claimed}: Glob::n_slow.. for a pass of
+    // one batch, else the batch's own area (their merges can run after every batch)
+    unsigned long long* bc;
     V6Map v6;                  // k_slow's IPv6 address ids (C = 0: none)
     uint32_t* gen;             // k_slow: the slow packets parse_fast / parse_mid leave to the general parser
                                // (batch-local indices, Glob::n_gen of them; the merge tail takes them)
@@ -376,6 +380,25 @@ __device__ __forceinline__ void part_to_global(const Acc& A, uint32_t d, const F
     if (f.fc != NONE64) atomicMin(&A.fc[d], f.fc);
     if (f.fr != NONE64) atomicMin(&A.fr[d], f.fr);
     if (f.la) atomicMax(&A.la[d], f.la - 1);
+}
+
+// part_to_global for a flow whose accumulators have no other writer in the
+// run (k_merge_spill, when no tail adds to them): plain stores over the
+// identities k_cleanup left
+__device__ __forceinline__ void part_store_global(const Acc& A, uint32_t d, const FlowPart& f) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        A.pk[q][d] = f.pk[q];
+        A.by[q][d] = f.by[q];
+        A.mn[q][d] = f.mn[q];
+        A.mx[q][d] = f.mx[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) A.fl[q][d] = f.fl[q];
+    A.fa[d] = f.fa;
+    A.fc[d] = f.fc;
+    A.fr[d] = f.fr;
+    A.la[d] = f.la ? f.la - 1 : 0;
 }
 
 __device__ __forceinline__ void part_of_stage(const Part& p, unsigned long long base, FlowPart& f) {
@@ -759,7 +782,24 @@ __global__ void __launch_bounds__(64) k_seq_run(SeqArgs a);
 __global__ void __launch_bounds__(256) k_cleanup(CleanArgs a, size_t tab_words);
 __global__ void k_fill_u64(unsigned long long* p, size_t n, unsigned long long v);
 __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v);
-__global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a);
+// k_merge_spill's input: the owner segments of every batch of a pass (one
+// merge per pass; a batch's staging is its own)
+struct SegSrc {
+    const Spill* dspill;
+    const uint32_t* soff;
+    const unsigned long long* base;
+    Spill* spill;                 // the batch's overflow list (records without an aggregate slot)
+    unsigned long long* bc;       // the batch's counters (AggArgs::bc)
+    unsigned long long slow_rec0, first;
+    uint32_t cap_o, cap_s, n_sets, n_hot;
+    uint32_t slow_kernel;         // the batch's slow list went to k_slow (its tail: the general-parser list)
+};
+constexpr int MS_BATCHES = 8;
+struct MergeSrc {
+    SegSrc b[MS_BATCHES];
+    int nb;
+};
+__global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a, MergeSrc ms);
 // templated kernels: their host stubs, by configuration
 const void* hot_kernel(int spill, int macs, int abl);  // hot.hip: k_parse_agg / k_parse_spill
 const void* merge_kernel(int macs);                     // merge.hip: k_merge_partials

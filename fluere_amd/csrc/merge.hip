@@ -128,8 +128,8 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     if (a.dbg && tid == 0) a.dbg[4096 * 8 - 2048 + blockIdx.x * 8 + 0] = wall_clock64();
     // loads issued before the LDS initialisation (their latency overlaps it):
     // this owner's segment bounds of the first set chunk, and the run counters
-    const unsigned long long n_spill_all = __hip_atomic_load(&a.g->n_spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long n_dspill_all = __hip_atomic_load(&a.g->n_dspill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long n_spill_all = __hip_atomic_load(&a.bc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long n_dspill_all = __hip_atomic_load(&a.bc[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long n_slow_all = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     constexpr bool macs = MACS;
     const Stage& S = a.S;
@@ -149,6 +149,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             }
         if (tid == 0) {
             Glob* g = a.g;
+            if (a.bc != &g->n_slow && a.bc[0]) atomicAdd(&g->n_slow, a.bc[0]);  // (the run's slow-list total)
             if (v[0]) atomicAdd(&g->valid, v[0]);
             if (v[1]) atomicAdd(&g->dropped, v[1]);
             if (v[2]) atomicAdd(&g->n_kc_miss, v[2]);
@@ -587,7 +588,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
             atomicAdd(&a.g->cyc_m_ids, clock64() - c1);
         }
         __syncthreads();  // (the next owner re-initialises the table)
-        if (tid == 0) s_me = S.O > gridDim.x ? gridDim.x + (uint32_t)atomicAdd(&a.g->n_owner, 1ull) : S.O;
+        if (tid == 0) s_me = S.O > gridDim.x ? gridDim.x + (uint32_t)atomicAdd(&a.bc[4], 1ull) : S.O;
         __syncthreads();
     }
     // the hot kernel's per-workgroup statistics -> the run counters (one wave
@@ -595,7 +596,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
     if (blockIdx.x == gridDim.x - 1 && tid < 64) reduce_stats();
     // k_slow ran: its general-parser list (flat); else the whole slow list
     const unsigned long long n_gen_all =
-        a.slow_kernel ? __hip_atomic_load(&a.g->n_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        a.slow_kernel ? __hip_atomic_load(&a.bc[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     const bool tail_slow = a.slow_kernel ? n_gen_all != 0 : n_slow_all != 0;
     if (FLUERE_MERGE_TAIL && (tail_slow || n_spill_all)) {
         // The tail: the overflow list (spills past their owner segment's
@@ -882,7 +883,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         if (gm) {
             const uint32_t lead = __builtin_ctzll(gm);
             unsigned long long b0 = 0;
-            if ((uint32_t)(tid & 63) == lead) b0 = atomicAdd(&a.g->n_gen, (unsigned long long)__popcll(gm));
+            if ((uint32_t)(tid & 63) == lead) b0 = atomicAdd(&a.bc[3], (unsigned long long)__popcll(gm));
             b0 = __shfl(b0, lead, 64);
             if (gen) a.gen[b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] = gli;
         }
@@ -906,7 +907,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         if (om) {
             const uint32_t lead = __builtin_ctzll(om);
             unsigned long long b0 = 0;
-            if ((uint32_t)(tid & 63) == lead) b0 = atomicAdd(&a.g->n_spill, (unsigned long long)__popcll(om));
+            if ((uint32_t)(tid & 63) == lead) b0 = atomicAdd(&a.bc[1], (unsigned long long)__popcll(om));
             b0 = __shfl(b0, lead, 64);
             if (ovf) {
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u));
@@ -940,7 +941,7 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
     if ((tid & 63) == 0) {
         if (c_valid) { atomicAdd(&a.g->valid, c_valid); atomicMin(&a.g->tmin, tmin); atomicMax(&a.g->tmax, tmax); }
         if (c_drop) atomicAdd(&a.g->dropped, c_drop);
-        if (c_seg) atomicAdd(&a.g->n_dspill, c_seg);
+        if (c_seg) atomicAdd(&a.bc[2], c_seg);
     }
 }
 
@@ -1270,7 +1271,7 @@ __device__ __forceinline__ uint32_t ms_slot(uint32_t k0, uint32_t k1, uint32_t k
     return (x >> 6) & (MT - 1);
 }  // records per lane per strip (a strip: 64 * MS_STRIP records of one wave)
 constexpr uint32_t MS_GRP = 1024;  // 64-record groups mapped in LDS (owners of more records: a binary search)
-__global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
+__global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a, MergeSrc ms) {
     // the arguments in the kernarg segment, for the out-of-line paths (a
     // reference to `a` would copy the whole struct to every lane's stack)
     const AggArgs* kargs = (const AggArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1280,23 +1281,42 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
     __shared__ uint16_t m_sk[MT];  // key entry of each slot
     __shared__ uint32_t m_pk[2][MT], m_mn[2][MT], m_mx[2][MT], m_fl[8][MT];
     __shared__ unsigned long long m_by[2][MT];
-    __shared__ uint32_t m_pos[4][MT];  // first, first create-eligible, first FIN/RST (min), last + 1 (max): batch-relative
+    __shared__ uint32_t m_pos[4][MT];  // first, first create-eligible, first FIN/RST (min), last + 1 (max):
+                                       // relative to the pass's first packet (batch 0's)
     // per non-empty segment of the chunk (k: its rank): {record index - flattened start (mod 2^32),
     // window base}, flattened start; per group of 64 flattened records {segment of its first
     // record, 0, 64-bit mask of the records that start a segment}
     __shared__ uint2 m_sd[MCH];
     __shared__ uint32_t m_st[MCH];
     __shared__ uint4 m_ginfo[MS_GRP];
-    __shared__ uint32_t m_scan[MB / 64 + 1], m_nclaim, m_base, s_me, m_nslot;
+    __shared__ uint32_t m_scan[MB / 64 + 1], m_nclaim, m_base, s_me, m_nslot, s_sole;
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wv = tid >> 6;
-    const Stage& S = a.S;
-    const uint64_t bfirst = a.B.first;
-    const uint4* recs = reinterpret_cast<const uint4*>(S.dspill);
-    if (tid == 0) s_me = blockIdx.x;
+    const uint32_t O = a.S.O;
+    const uint64_t bfirst = ms.b[0].first;  // positions in LDS: relative to the pass's first packet
+    if (tid == 0) {
+        s_me = blockIdx.x;
+        // No tail adds to the owners' flows (no overflow list from the hot pass, no
+        // general-parser packets): each owner is the only writer of its flows'
+        // accumulators, and writes them with plain stores.  (Records this merge
+        // sends to the overflow list belong to keys without a slot: other flows.
+        // A count raised by them here only makes the choice conservative.)
+        uint32_t sole = 1;
+        for (int bi = 0; bi < ms.nb; bi++) {
+            const unsigned long long* bc = ms.b[bi].bc;
+            const unsigned long long ovf = __hip_atomic_load(&bc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long gen = __hip_atomic_load(&bc[ms.b[bi].slow_kernel ? 3 : 0], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+            // (k_slow's keys: a flow whose IPv6 addresses found no id in the address
+            // map travels as its dense id, others of it as address ids: two owners)
+            if (ovf || gen || ms.b[bi].slow_kernel) sole = 0;
+        }
+        s_sole = sole;
+    }
     __syncthreads();
+    const bool sole = s_sole != 0;
     unsigned long long* dbg = a.dbg ? a.dbg + 4096 * 8 - 2048 + blockIdx.x * 8 : nullptr;  // (FLUERE_DEBUG: phase clocks)
-    for (uint32_t me = s_me; me < S.O; me = s_me) {
+    for (uint32_t me = s_me; me < O; me = s_me) {
         if (dbg && tid == 0) dbg[0] = wall_clock64();
         for (int e = tid; e < MK; e += MB) m_key[e] = make_uint4(0, 0, 0, 0);
         if (tid == 0) m_nslot = 0;
@@ -1310,7 +1330,11 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
             m_pos[0][e] = m_pos[1][e] = m_pos[2][e] = NONE32;
             m_pos[3][e] = 0;
         }
-        for (uint32_t c0s = 0; c0s < S.n_sets; c0s += MCH) {
+        for (int bi = 0; bi < ms.nb; bi++)
+        for (uint32_t c0s = 0; c0s < ms.b[bi].n_sets; c0s += MCH) {
+            const SegSrc& S = ms.b[bi];
+            const uint4* recs = reinterpret_cast<const uint4*>(S.dspill);
+            const uint32_t bshift = (uint32_t)(S.first - bfirst);  // the batch's first packet in the pass
             const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
             // this owner's segment of each set of the chunk: count, record base, window base
             static_assert(MCH == MB, "one set per thread");
@@ -1318,13 +1342,13 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
             uint32_t cnt = 0, rb = 0, wb = 0;
             if ((uint32_t)tid < nset) {
                 cnt = S.soff[(size_t)me * S.n_sets + s];
-                rb = s < S.n_hot ? (uint32_t)(((unsigned long long)s * S.O + me) * S.cap_o)
-                                 : (uint32_t)(S.slow_rec0 + ((unsigned long long)(s - S.n_hot) * S.O + me) * S.cap_s);
+                rb = s < S.n_hot ? (uint32_t)(((unsigned long long)s * O + me) * S.cap_o)
+                                 : (uint32_t)(S.slow_rec0 + ((unsigned long long)(s - S.n_hot) * O + me) * S.cap_s);
                 wb = (uint32_t)(S.base[s] - bfirst);
             }
             // the non-empty segments, compacted (k: rank among them), with their
             // flattened starts (exclusive scan of the counts)
-            if (dbg && tid == 0 && c0s == 0) dbg[1] = wall_clock64();
+            if (dbg && tid == 0 && c0s == 0 && bi == 0) dbg[1] = wall_clock64();
             const uint32_t st0 = block_exclusive_scan(cnt, m_scan);  // (ends with a barrier)
             const uint32_t total = m_scan[MB / 64];
             const uint32_t k = block_exclusive_scan(cnt ? 1u : 0u, m_scan);
@@ -1410,7 +1434,7 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
                     const uint32_t f = sp * (64 * MS_STRIP) + u * 64 + lane;
                     const bool live = f < total;
                     const uint32_t k0 = v0[u].x, k1 = v0[u].y, k2 = v0[u].z, tag = v0[u].w;
-                    const uint32_t rel = wbr[u] + v1[u].z;  // batch-relative packet index
+                    const uint32_t rel = wbr[u] + v1[u].z;  // the packet's index in the pass
                     const uint32_t want = tag | LT_READY;
                     uint32_t e = MS_NOSLOT;
 #pragma unroll
@@ -1460,7 +1484,7 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
                         continue;
                     }
                     if (state == 1) {  // update_flow of one packet (flows.rs:11-42), order-free part
-                        if (a.pid) a.pid[bfirst + rel - a.pid_base] = PH_EREF | (a.pid_batch << 21) | (me << 10) | e;
+                        if (a.pid) a.pid[bfirst + rel - a.pid_base] = PH_EREF | (me << 10) | e;  // (batch field 0: one merge per pass)
                         atomicAdd(&m_pk[dir][e], 1u);
                         atomicAdd(&m_by[dir][e], (unsigned long long)v1[u].x);
                         atomicMin(&m_mn[0][e], pkt);
@@ -1475,14 +1499,15 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
                             if (tf & 5u) atomicMin(&m_pos[2][e], rel);
                         }
                     } else if (state == 2) {  // no aggregate slot: the overflow list (the tail takes it)
-                        const unsigned long long q = atomicAdd(&a.g->n_spill, 1ull);
+                        // (the batch's list, positions relative to the batch: its tail takes it)
+                        const unsigned long long q = atomicAdd(&S.bc[1], 1ull);
                         uint4* dst = reinterpret_cast<uint4*>(S.spill) + q * 2;
                         dst[0] = v0[u];
-                        dst[1] = make_uint4(v1[u].x, v1[u].y, rel, (v1[u].w & 0x1FFu) | (SPILL_BATCH_REL << 9));
+                        dst[1] = make_uint4(v1[u].x, v1[u].y, rel - bshift, (v1[u].w & 0x1FFu) | (SPILL_BATCH_REL << 9));
                     }
                 }
             };
-            if (dbg && tid == 0 && c0s == 0) dbg[2] = wall_clock64();
+            if (dbg && tid == 0 && c0s == 0 && bi == 0) dbg[2] = wall_clock64();
             if (total) {
                 uint4 a0[MS_STRIP], a1[MS_STRIP], b0[MS_STRIP], b1[MS_STRIP];
                 uint32_t aw[MS_STRIP], bw[MS_STRIP];
@@ -1575,7 +1600,7 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
         }
         if (wait) atomicOr(a.T.err, ERR_SPIN);
         if (dbg && tid == 0) dbg[4] = wall_clock64();
-        if (a.emap) a.emap[((size_t)a.pid_batch << 21) | ((size_t)me << 10) | (uint32_t)e] = (have && d < a.T.fmax) ? d : FAIL;
+        if (a.emap) a.emap[((size_t)me << 10) | (uint32_t)e] = (have && d < a.T.fmax) ? d : FAIL;
         if (have && d != FAIL && d < a.T.fmax) {
             FlowPart f;
 #pragma unroll
@@ -1592,11 +1617,12 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a) {
             f.fc = p1 == NONE32 ? NONE64 : bfirst + p1;
             f.fr = p2 == NONE32 ? NONE64 : bfirst + p2;
             f.la = p3 ? bfirst + p3 : 0;
-            part_to_global(a.A, d, f);
+            if (sole) part_store_global(a.A, d, f);
+            else part_to_global(a.A, d, f);
         }
         if (dbg && tid == 0) dbg[5] = wall_clock64();
         __syncthreads();  // (the next owner re-initialises the table)
-        if (tid == 0) s_me = S.O > gridDim.x ? gridDim.x + (uint32_t)atomicAdd(&a.g->n_owner, 1ull) : S.O;
+        if (tid == 0) s_me = O > gridDim.x ? gridDim.x + (uint32_t)atomicAdd(&ms.b[0].bc[4], 1ull) : O;
         __syncthreads();
     }
 }
