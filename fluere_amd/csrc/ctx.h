@@ -136,6 +136,49 @@ struct fluere_ctx {
     unsigned long long* d_okey = nullptr;  // the records' order keys, written by the emitters (OkeyRef)
     uint64_t d_okey_cap = 0;
     OkeyRef okref{};                       // its device copy follows the Ctl in d_glob
+    // the ordering enqueued behind k_finalize (order.hip: so_plan): two bit
+    // arrays used in turn (each run clears the other's dirty words), scratch
+    uint32_t* d_sob = nullptr;       // [2][sob_cap] key bit words
+    uint64_t sob_cap = 0;
+    uint64_t sob_dirty[2] = {0, 0};  // words a past run may have set, per array
+    uint32_t* d_sorb = nullptr;      // [2][sorb_cap] record bit words
+    uint64_t sorb_cap = 0;
+    uint64_t sorb_dirty[2] = {0, 0};
+    int sob_cur = 0;
+    void* d_sos = nullptr;           // wpre | tpre | ctr | holes
+    size_t sos_bytes = 0;
+    bool so_next = false;            // the last run was complete with ended records: enqueue the ordering
+    uint64_t so_last_n = 0, so_last_ne = 0;
+};
+
+// The Mode A ordering enqueued behind k_finalize, before the host has read
+// the run's counters (order.hip).  Its kernels read the counters on the
+// device and do nothing unless the run is complete (run_complete, the same
+// test as the speculative k_cleanup's) with ended records.
+struct SoArgs {
+    const Glob* g;
+    const uint32_t* err;
+    unsigned long long timeout_us, recs_cap;
+    fluere_record* r;   // d_recs
+    fluere_record* r2;  // d_recs2 (capacity >= recs_cap)
+    uint64_t base;      // the capture's first packet index
+    uint64_t nw;        // key bit words of this run: N / 32 + 1
+    uint32_t kt, rt;    // tiles of 1024 words: key bits, record bits
+    uint32_t* bits;     // [nw] key bits: one per packet, zero on entry
+    uint32_t* zbits;    // the other key array: its first zn words cleared for the next run
+    uint64_t zn;
+    uint16_t* wpre;     // [nw] key bits below each word within its tile
+    uint32_t* rbits;    // record bits: one per record, set by k_finalize when ended (zero on entry)
+    uint32_t* zrbits;   // the other record array: its first zrn words cleared for the next run
+    uint64_t zrn;
+    uint16_t* rwpre;    // their per-word prefixes within a tile
+    uint32_t* tpre;     // [kt + rt] tile totals, then their exclusive prefixes
+    uint32_t* holes;    // [recs_cap] the ended records at or past n_ended, by rank
+};
+struct SoLaunch {
+    SoArgs a;
+    unsigned g_scan, g_out, g_fill;
+    int on;
 };
 
 
@@ -177,6 +220,9 @@ int grow_pair(void** a, void** b, uint64_t* cap_b, uint64_t cap_a, size_t unit);
 int ord_scratch(fluere_ctx* c, size_t need);  // order.hip
 int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint64_t n_okey);  // order.hip
 int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m);  // order.hip
+int so_plan(fluere_ctx* c, SoLaunch& L, unsigned long long timeout_us);  // order.hip
+int so_enqueue(fluere_ctx* c, const SoLaunch& L);                        // order.hip
+void so_free(fluere_ctx* c);                                             // order.hip
 int add_host_pcap_indexed(fluere_ctx* c, const uint8_t* file, uint64_t nbytes, const uint64_t* rec_off, uint64_t n_recs);  // ingest.hip
 
 // order.hip

@@ -599,7 +599,7 @@ __device__ __forceinline__ void emit_record_block(EmitLds& S, Glob* g, fluere_re
 __device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_record* out, uint64_t cap, bool want,
                                                    uint32_t d_pkts, bool ended, unsigned long long* aux = nullptr,
                                                    unsigned long long a0 = 0, unsigned long long a1 = 0,
-                                                   unsigned long long* tot = nullptr) {
+                                                   unsigned long long* tot = nullptr, uint32_t* rbits = nullptr) {
     const uint32_t w = threadIdx.x >> 6;
     const uint64_t m = __ballot(want), em = __ballot(want && ended);
     const unsigned long long upd = wave_sum(want ? (unsigned long long)d_pkts : 0ull);
@@ -636,6 +636,7 @@ __device__ __forceinline__ void emit_inplace_block(EmitLds& S, Glob* g, fluere_r
         S.slot[i] = (uint16_t)threadIdx.x;
         const OkeyRef o = okey_ref(g);
         if (okey_count(o, cap, S.base + i, 1)) o.p[S.base + i] = S.rec[threadIdx.x].order_key;
+        if (rbits && ended && S.base + i < cap) atomicOr(&rbits[(S.base + i) >> 5], 1u << ((S.base + i) & 31));
         if (aux && S.base + i < cap)
             *reinterpret_cast<ulonglong2*>(aux + 2 * (S.base + i)) = make_ulonglong2(a0, a1);
     }

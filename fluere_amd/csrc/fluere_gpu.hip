@@ -623,6 +623,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_recs2);
     hipFree(c->d_recaux2);
     hipFree(c->d_ord);
+    so_free(c);
     hipFree(c->d_recaux);
     hipFree(c->d_okey);
     sweep_free(c);
@@ -906,6 +907,7 @@ struct PassPlan {
     int finalize;  // fluere_run: k_finalize + counters copy
     FinArgs fa;
     unsigned fin_grid;
+    SoLaunch so;   // the Mode A ordering behind k_finalize (spec runs; order.hip)
     Ctl* h_ctl;
     Glob* d_glob;
 };
@@ -1335,6 +1337,7 @@ static int enqueue_pass(fluere_ctx* c, const PassPlan& P) {
         if (P.spec) {
             // k_finalize's last workgroup writes the counters to the pinned
             // host copy and publishes P.fa.seq; the speculative cleanup follows
+            if (P.so.on && (rc = so_enqueue(c, P.so))) return rc;
             k_cleanup<<<P.spec_grid, 256, 0, s>>>(P.spec_ca, P.tab_words);
         } else {
             HIPCHECK(hipMemcpyAsync(P.h_ctl, P.d_glob, sizeof(Ctl), hipMemcpyDeviceToHost, s));
@@ -1738,6 +1741,15 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         P.spec = 1;
         P.fa.host_ctl = c->h_ctl;
         P.fa.seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
+        // the ordering behind k_finalize when the last run was complete with
+        // ended records (the steady state of a repeated workload)
+        static const bool so_off = getenv("FLUERE_SO") && atoi(getenv("FLUERE_SO")) == 0;
+        if (!so_off && c->so_next && (rc = so_plan(c, P.so, timeout_us))) return rc;
+        if (P.so.on) {  // k_finalize sets the key bits
+            P.fa.kbits = P.so.a.bits;
+            P.fa.kbase = P.so.a.base;
+            P.fa.rbits = P.so.a.rbits;
+        }
         if ((rc = enqueue_pass(c, P))) return rc;
     }
     c->prev_nf = ~0ull;  // the pass cleared the flows: unknown until the fetch below
@@ -1769,11 +1781,16 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
     // the speculative cleanup behind the copy clears the flows exactly when
     // the run needs no more device work (the same test, on the same counters)
     const bool spec_cleared = P.spec && run_complete(g, nf_err[1], P.spec_ca.timeout_us, P.spec_ca.recs_cap);
+    c->so_next = spec_cleared && g.n_ended > 0;
+    c->so_last_n = g.n_rec;
+    c->so_last_ne = g.n_ended;
     if (!(nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = nf_err[0];
     // (a pass of k_slow over every packet lists none: the prediction stays)
     c->last_n_slow = c->plan_slow_all ? std::max<uint64_t>(g.n_slow, c->n_total) : g.n_slow;
     debug_counters(c, &g);
     FinArgs fa = P.fa;
+    fa.kbits = nullptr;     // (and set no ordering bits)
+    fa.rbits = nullptr;
     fa.host_ctl = nullptr;  // re-launches below read the counters back with copies
     if (nf_err[1] & (ERR_TABLE_FULL | ERR_SPIN)) return FLUERE_E_TABLE_FULL;
     if (nf_err[1] & ERR_FLOWS_FULL) return FLUERE_E_TABLE_FULL;
@@ -1828,7 +1845,19 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         c->dev_n_rec = n_rec;
         c->host_recs = false;
         out.complex_flows = g.n_complex;
-        if ((rc = order_records(c, n_rec, n_ended, false, g.n_okey))) return rc;
+        if (spec_cleared && P.so.on) {
+            // ordered on the device behind k_finalize (k_so_*)
+            if (n_ended && n_rec < (1ull << 32)) {
+                if (n_ended * 4 > n_rec) {  // every record moved to d_recs2
+                    std::swap(c->d_recs, c->d_recs2);
+                    std::swap(c->d_recs_cap, c->d_recs2_cap);
+                }
+                c->dev_ordered = true;
+                c->dev_ordered_ended = n_ended;
+            }
+        } else if ((rc = order_records(c, n_rec, n_ended, false, g.n_okey))) {
+            return rc;
+        }
     } else {
         // exact global state machine (the speculative Mode A results are discarded):
         // in parallel (exact.hip) when the timestamps are non-decreasing, else

@@ -555,6 +555,9 @@ struct FinArgs {
     uint8_t* cbits = nullptr;       // the exact engine's complex-flow filter (ckey_bucket: a byte per bucket), or null
     uint32_t* defer = nullptr;      // k_finalize: certified flows whose first packet needs the general
                                     // parser (Glob::n_fdefer of them), finalized by k_finalize_gen
+    uint32_t* kbits = nullptr;      // k_finalize: the ordering's key bits (SoArgs::bits), set at each ended
+    unsigned long long kbase = 0;   //   record's closing packet (index - kbase), or null
+    uint32_t* rbits = nullptr;      //   and its record bits (SoArgs::rbits), set at each ended record
 };
 
 // A flow's order-free aggregate (the accumulators of one dense id).

@@ -964,8 +964,13 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
         bool cplx = false;
         unsigned long long cplx_pkts = 0;
         const bool want = d < nf && finalize_one<false>(a, d, r, cplx, cplx_pkts);
-        emit_inplace_block(S, a.g, a.out, a.out_cap, want, want ? r.d_pkts : 0u, want && r.order_key != NONE64, nullptr, 0,
-                           0, tot);
+        const unsigned long long ok = want ? r.order_key : NONE64;
+        emit_inplace_block(S, a.g, a.out, a.out_cap, want, want ? r.d_pkts : 0u, ok != NONE64, nullptr, 0, 0, tot,
+                           a.rbits);
+        if (a.kbits && ok != NONE64) {  // (the ordering behind the pass: k_so_*)
+            const unsigned long long q = ok - a.kbase;
+            atomicOr(&a.kbits[q >> 5], 1u << (q & 31));
+        }
         n_cplx += cplx ? 1 : 0;
         cplx_all += cplx_pkts;
     }

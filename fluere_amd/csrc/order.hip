@@ -417,3 +417,301 @@ int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint
     c->dev_ordered_ended = n_ended;
     return FLUERE_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Mode A ordering enqueued behind k_finalize (SoArgs).  The host used to wait
+// for the run's counters, then launch the ordering (bit marks, two library
+// scans, the moves): its launches, the scans' host-side work and the wake-up
+// left the GPU idle for most of the ~90 us the ordering took.  Here three
+// kernels are queued with the pass; they read n_rec / n_ended on the device
+// and act only when the run is complete (run_complete: the same test the
+// speculative k_cleanup takes, and the host after it), so a run that needs
+// the exact engine or Mode B finds d_recs untouched and orders it itself.
+// Every place comes from prefix counts over two bit arrays -- no shared
+// counters (same-address atomics from every CU serialize), no spinning:
+//  * key bits: one per packet, set by k_finalize at each ended record's
+//    closing packet; an ended record's place is the count of key bits below
+//    its own;
+//  * record bits: one per record, set by k_finalize when it is ended; E(i), the ended
+//    records before record i, pairs the k-th hole (an ended record at or
+//    past n_ended) with the k-th active record of the prefix.
+//  k_so_scan  for both arrays, per word, the bits below it in its tile of
+//             1024 words, and the tile totals; it also clears the other
+//             arrays' dirty words for the next run (no memset);
+//  k_so_out   (the tile totals scanned in LDS first) every ended record to its
+//             place in d_recs2, a hole listed when it sits past the prefix; at
+//             most a quarter ended only they move, else every record does
+//             (the actives after the prefix in record order) and the host
+//             swaps the buffers;
+//  k_so_fill  the prefix's active records into the holes, then the ordered
+//             prefix over d_recs (a workgroup per 64 records).
+// Grids are any size: the record loops stride over the device counts.
+__device__ __forceinline__ bool so_go(const SoArgs& a, uint64_t& n, uint64_t& ne, const unsigned long long*& ok) {
+    const Glob& g = *a.g;
+    n = g.n_rec;
+    ne = g.n_ended;
+    const OkeyRef o = okey_ref(a.g);
+    ok = (o.p && g.n_okey == n && n <= o.cap) ? o.p : nullptr;
+    return run_complete(g, *a.err, a.timeout_us, a.recs_cap) && n && ne && n < (1ull << 32);
+}
+__device__ __forceinline__ uint64_t so_key(const SoArgs& a, const unsigned long long* ok, uint64_t i) {
+    return ok ? ok[i] : a.r[i].order_key;
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// s[0, T) = the exclusive prefix of src[0, T) (256 threads; ends with a barrier)
+__device__ void lds_exclusive_scan(uint32_t* s, const uint32_t* src, uint32_t T) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t t = tid; t < T; t += 256) s[t] = src[t];
+    __syncthreads();
+    const uint32_t c = (T + 255) / 256, lo = min(T, tid * c), hi = min(T, lo + c);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; k++) sum += s[k];
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += y;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (uint32_t q = 0; q < wv; q++) run += s_w[q];
+    for (uint32_t k = lo; k < hi; k++) {
+        const uint32_t v = s[k];
+        s[k] = run;
+        run += v;
+    }
+    __syncthreads();
+}
+// The listed records (lanes with `want` of the 64 at w0) to out[p], 8-byte
+// words in order, by `nw` waves (the w-th takes every nw-th group of 64
+// words): every load first, then every store -- one memory round trip, not
+// one per 64 words.  Called by those waves alike (one list, block-uniform when
+// nw > 1: the list is published with a barrier).
+template <int NW>
+__device__ __forceinline__ void copy_listed(uint32_t* s_l, const fluere_record* r, uint64_t w0, bool want,
+                                            uint32_t p, fluere_record* out, uint32_t wv) {
+    constexpr uint32_t IT = (REC_WORDS + NW - 1) / NW;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(want);
+    if (NW == 1 && !m) return;
+    if (want && wv == 0) s_l[lanes_below(m)] = lane;
+    if (NW > 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint32_t total = (uint32_t)__popcll(m) * REC_WORDS;
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(r);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
+    unsigned long long v[IT];
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+        const uint32_t e = (u * NW + wv) * 64 + lane;
+        if (e < total) {
+            const uint32_t j = e / REC_WORDS, kk = e - j * REC_WORDS;
+            v[u] = src[(w0 + s_l[j]) * REC_WORDS + kk];
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+        const uint32_t b = (u * NW + wv) * 64;
+        if (b < total) {  // (wave-uniform: every lane takes part in the shuffle)
+            const uint32_t e = b + lane, ec = min(e, total - 1);
+            const uint32_t j = ec / REC_WORDS, kk = ec - j * REC_WORDS;
+            const uint32_t pj = __shfl(p, (int)s_l[j], 64);
+            if (e < total) dst[(size_t)pj * REC_WORDS + kk] = v[u];
+        }
+    }
+    if (NW > 1) {
+        __syncthreads();  // (s_l is rewritten by the next call)
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// grid: the key tiles (a.kt) then the record tiles (a.rt), 1024 words each;
+// 1024 threads
+__global__ void __launch_bounds__(MB) k_so_scan(SoArgs a) {
+    __shared__ uint32_t s_scan[MB / 64 + 1];
+    for (uint64_t w = (uint64_t)blockIdx.x * MB + threadIdx.x; w < a.zn; w += (uint64_t)gridDim.x * MB) a.zbits[w] = 0;
+    for (uint64_t w = (uint64_t)blockIdx.x * MB + threadIdx.x; w < a.zrn; w += (uint64_t)gridDim.x * MB) a.zrbits[w] = 0;
+    uint64_t n, ne;
+    const unsigned long long* ok;
+    if (!so_go(a, n, ne, ok)) return;
+    const bool rec = blockIdx.x >= a.kt;
+    const uint64_t w = (uint64_t)(rec ? blockIdx.x - a.kt : blockIdx.x) * MB + threadIdx.x;
+    const uint64_t nw = rec ? (n + 31) / 32 : a.nw;
+    const uint32_t word = w < nw ? (rec ? a.rbits : a.bits)[w] : 0u;
+    const uint32_t pre = block_exclusive_scan((uint32_t)__popc(word), s_scan);  // (at most 1023 x 32: fits 16 bits)
+    if (w < nw) (rec ? a.rwpre : a.wpre)[w] = (uint16_t)pre;
+    if (threadIdx.x == 0) a.tpre[blockIdx.x] = s_scan[MB / 64];
+}
+
+// dynamic LDS: (kt + rt) words, the tile prefixes
+__global__ void __launch_bounds__(256) k_so_out(SoArgs a) {
+    extern __shared__ uint32_t s_tp[];
+    __shared__ uint32_t s_l[4][64];
+    uint64_t n, ne;
+    const unsigned long long* ok;
+    if (!so_go(a, n, ne, ok)) return;
+    lds_exclusive_scan(s_tp, a.tpre, a.kt + a.rt);  // key tiles, then record tiles (offset by the key total)
+    const uint32_t* rtp = s_tp + a.kt;
+    const uint32_t r0 = rtp[0];
+    const bool few = ne * 4 <= n;
+    // ended records before the prefix's end: E(ne)
+    uint32_t e_ne = 0;
+    if (few) e_ne = rtp[(ne >> 5) >> 10] - r0 + a.rwpre[ne >> 5] + (uint32_t)__popc(a.rbits[ne >> 5] & ((1u << (ne & 31)) - 1u));
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wv) * 64; w0 < n; w0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = w0 + lane;
+        const bool live = i < n;
+        const uint64_t k = live ? so_key(a, ok, i) : NONE64;
+        const bool ended = k != NONE64;
+        const uint64_t em = __ballot(ended);
+        const uint32_t e_i = rtp[(w0 >> 5) >> 10] - r0 + a.rwpre[w0 >> 5] + lanes_below(em);  // E(i)
+        uint32_t p = 0;
+        if (ended) {
+            const uint64_t q = k - a.base, w = q >> 5;
+            p = s_tp[w >> 10] + a.wpre[w] + (uint32_t)__popc(a.bits[w] & ((1u << (q & 31)) - 1u));
+        }
+        if (few) {
+            if (ended && i >= ne) a.holes[e_i - e_ne] = (uint32_t)i;
+            copy_listed<1>(s_l[wv], a.r, w0, ended, p, a.r2, 0);
+        } else {
+            if (live && !ended) p = (uint32_t)ne + ((uint32_t)i - e_i);
+            copy_listed<1>(s_l[wv], a.r, w0, live, p, a.r2, 0);
+        }
+    }
+}
+
+// dynamic LDS: rt words, the record tiles' prefixes; a workgroup per 64
+// records of the prefix, its four waves sharing the copies
+__global__ void __launch_bounds__(256) k_so_fill(SoArgs a) {
+    extern __shared__ uint32_t s_tp[];
+    __shared__ uint32_t s_l[64];
+    uint64_t n, ne;
+    const unsigned long long* ok;
+    if (!so_go(a, n, ne, ok) || ne * 4 > n) return;
+    lds_exclusive_scan(s_tp, a.tpre + a.kt, a.rt);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t w0 = (uint64_t)blockIdx.x * 64; w0 < ne; w0 += (uint64_t)gridDim.x * 64) {  // (block-uniform)
+        const uint64_t j = w0 + lane;
+        const bool ended = (a.rbits[j >> 5] >> (j & 31)) & 1u;
+        const bool act = j < ne && !ended;
+        const uint64_t em = __ballot(ended);
+        const uint32_t e_j = s_tp[(w0 >> 5) >> 10] + a.rwpre[w0 >> 5] + lanes_below(em);
+        const uint32_t p = act ? a.holes[(uint32_t)j - e_j] : 0u;  // the k-th active takes the k-th hole
+        copy_listed<4>(s_l, a.r, w0, act, p, a.r, wv);  // (every hole lies past the prefix)
+        const uint32_t nr = (uint32_t)min<uint64_t>(64, ne - w0);
+        copy_listed<4>(s_l, a.r2, w0, lane < nr, (uint32_t)j, a.r, wv);  // then the ordered prefix over it
+    }
+}
+
+void so_free(fluere_ctx* c) {
+    hipFree(c->d_sob);
+    hipFree(c->d_sos);
+    hipFree(c->d_sorb);
+    c->d_sorb = nullptr;
+    c->sorb_cap = 0;
+    c->d_sob = nullptr;
+    c->d_sos = nullptr;
+    c->sob_cap = 0;
+    c->sos_bytes = 0;
+}
+
+// The launches and scratch of one run's ordering; flips the key bit arrays
+// (call right before so_enqueue).  L.on = 0 when it does not apply.
+constexpr uint64_t SO_MAX_TILES = 12288;  // key + record tiles: 48 KiB of tile prefixes in LDS
+
+int so_plan(fluere_ctx* c, SoLaunch& L, unsigned long long timeout_us) {
+    L.on = 0;
+    const uint64_t N = std::max<uint64_t>(c->n_total, 1), nw = N / 32 + 1;
+    const uint64_t kt = (nw + MB - 1) / MB;
+    const uint64_t rw = (c->d_recs_cap + 63) / 64 * 2, rt = (rw + MB - 1) / MB;
+    if (c->d_recs_cap >= (1ull << 32) || kt + rt > SO_MAX_TILES) return FLUERE_OK;  // (the prefixes live in LDS)
+    int rc = grow_pair((void**)&c->d_recs, (void**)&c->d_recs2, &c->d_recs2_cap, c->d_recs_cap, sizeof(fluere_record));
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    if (c->sob_cap < nw) {
+        hipFree(c->d_sob);
+        c->d_sob = nullptr;
+        c->sob_cap = 0;
+        const uint64_t cap = nw + nw / 4;
+        if (hipMalloc(&c->d_sob, 2 * cap * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        HIPCHECK(hipMemsetAsync(c->d_sob, 0, 2 * cap * 4, s));
+        c->sob_cap = cap;
+        c->sob_dirty[0] = c->sob_dirty[1] = 0;
+    }
+    if (c->sorb_cap < rw) {
+        hipFree(c->d_sorb);
+        c->d_sorb = nullptr;
+        c->sorb_cap = 0;
+        const uint64_t cap = rw + rw / 4;
+        if (hipMalloc(&c->d_sorb, 2 * cap * 4) != hipSuccess) return FLUERE_E_NOMEM;
+        HIPCHECK(hipMemsetAsync(c->d_sorb, 0, 2 * cap * 4, s));
+        c->sorb_cap = cap;
+        c->sorb_dirty[0] = c->sorb_dirty[1] = 0;
+    }
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t need = al(nw * 2) + al(rw * 2) + al((kt + rt) * 4) + al(c->d_recs_cap * 4);
+    if (c->sos_bytes < need) {
+        hipFree(c->d_sos);
+        c->d_sos = nullptr;
+        c->sos_bytes = 0;
+        if (hipMalloc(&c->d_sos, need + need / 4) != hipSuccess) return FLUERE_E_NOMEM;
+        c->sos_bytes = need + need / 4;
+    }
+    char* p = (char*)c->d_sos;
+    auto take = [&](size_t bytes) { char* q = p; p += al(bytes); return q; };
+    SoArgs& a = L.a;
+    a.g = c->d_glob;
+    a.err = tables_of(c).err;
+    a.timeout_us = timeout_us;
+    a.recs_cap = c->d_recs_cap;
+    a.r = c->d_recs;
+    a.r2 = c->d_recs2;
+    a.base = c->index_base;
+    a.nw = nw;
+    a.kt = (uint32_t)kt;
+    a.rt = (uint32_t)rt;
+    a.wpre = (uint16_t*)take(nw * 2);
+    a.rwpre = (uint16_t*)take(rw * 2);
+    a.tpre = (uint32_t*)take((kt + rt) * 4);
+    a.holes = (uint32_t*)take(c->d_recs_cap * 4);
+    const int cur = c->sob_cur;
+    a.bits = c->d_sob + (size_t)cur * c->sob_cap;
+    a.zbits = c->d_sob + (size_t)(cur ^ 1) * c->sob_cap;
+    a.zn = c->sob_dirty[cur ^ 1];
+    c->sob_dirty[cur] = std::max(c->sob_dirty[cur], nw);
+    c->sob_dirty[cur ^ 1] = 0;
+    a.rbits = c->d_sorb + (size_t)cur * c->sorb_cap;
+    a.zrbits = c->d_sorb + (size_t)(cur ^ 1) * c->sorb_cap;
+    a.zrn = c->sorb_dirty[cur ^ 1];
+    c->sorb_dirty[cur] = std::max(c->sorb_dirty[cur], rw);
+    c->sorb_dirty[cur ^ 1] = 0;
+    c->sob_cur = cur ^ 1;
+    auto clampg = [](uint64_t n, unsigned per) {
+        return (unsigned)std::min<uint64_t>(std::max<uint64_t>(grid_for(n, per), 8), 4096);
+    };
+    L.g_out = clampg(c->so_last_n, 256);
+    L.g_fill = clampg(c->so_last_ne, 64);
+    L.g_scan = (unsigned)(kt + rt);
+    L.on = 1;
+    return FLUERE_OK;
+}
+
+int so_enqueue(fluere_ctx* c, const SoLaunch& L) {
+    hipStream_t s = c->stream;
+    k_so_scan<<<L.g_scan, MB, 0, s>>>(L.a);
+    k_so_out<<<L.g_out, 256, (L.a.kt + L.a.rt) * 4, s>>>(L.a);
+    k_so_fill<<<L.g_fill, 256, L.a.rt * 4, s>>>(L.a);
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}

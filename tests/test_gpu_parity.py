@@ -1337,3 +1337,57 @@ def test_fluere_live_cli(gpu, tmp_path):
         # the CLI writes the export in order: FIN/RST-closed prefix first
         assert_csv_equal(got, w["n_ordered"], w["csv"], w["n_ordered"], f.name)
         assert len(rows) == w["csv"].count("\n") - 1
+
+
+def _ended_mix(n_flows, ended_frac, seed, pkts_per_flow=4):
+    """n_flows flows over interleaved packets: a share of them TCP flows closed
+    by a FIN as their last packet (ended records, Mode A), the rest UDP flows
+    left active."""
+    import random
+    import pktbuild as pb
+    rng = random.Random(seed)
+    ev = []
+    for i in range(n_flows):
+        src = f"10.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}"
+        t0 = rng.randrange(0, 5_000_000)
+        closed = rng.random() < ended_frac
+        for k in range(pkts_per_flow):
+            t = t0 + k * rng.randrange(1, 2000)
+            if closed:
+                fl = pb.FIN | pb.ACK if k == pkts_per_flow - 1 else (pb.SYN if k == 0 else pb.ACK)
+                f = pb.eth() + pb.ipv4(src, "10.200.0.1", 6, pb.tcp(1000 + i % 50000, 443, fl, b"d" * (k * 7)))
+            else:
+                f = pb.eth() + pb.ipv4(src, "10.200.0.2", 17, pb.udp(2000 + i % 50000, 53, b"u" * (8 + k)))
+            ev.append((t, i, k, f))
+    ev.sort(key=lambda e: (e[0], e[1], e[2]))
+    return pb.pcap([(t // 1_000_000, t % 1_000_000, f) for t, _, _, f in ev])
+
+
+def test_device_ordering_behind_finalize(gpu):
+    """A run after a complete Mode A run with ended records orders them on the
+    device behind k_finalize (k_so_*, no host round trip): few ended (only they
+    and the prefix's actives move) and most ended (every record moves), a
+    capture that then needs the exact engine (the queued ordering stands down:
+    run_complete fails on the device and the host orders after the engine),
+    and captures of other sizes on the same context (the bit arrays used in
+    turn, each cleared by the next run but one).  Every run equals the oracle."""
+    cases = [
+        ("few", _ended_mix(6000, 0.1, 1), 3),
+        ("many", _ended_mix(6000, 0.9, 2), 3),
+        ("tcp_complex", fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 120_000, 1_500, 0xF10E0037)), 2),
+        ("big", _ended_mix(30000, 0.3, 3), 2),
+        ("small_after_big", _ended_mix(2000, 0.2, 4), 3),
+        ("many_again", _ended_mix(6000, 0.9, 5), 2),
+    ]
+    with fluere_amd.FlowContext(max_flows=1 << 17) as ctx:
+        for name, data, runs in cases:
+            want = pyoracle.offline(data, 600000)
+            assert want["n_ended"] > 0, name
+            ctx.reset()
+            ctx.add_host_pcap(data)
+            for k in range(runs):
+                st = ctx.run()
+                recs, ne = ctx.records()
+                assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"{name} run {k}")
+            if name == "tcp_complex":
+                assert st["complex_flows"] > 0, st
