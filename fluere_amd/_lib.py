@@ -26,6 +26,7 @@ CLI_PATH = os.path.join(_HERE, "fluere")
 # enum fluere_status
 OK = 0
 E_ARG, E_IO, E_PCAP, E_HIP, E_NOMEM, E_TABLE_FULL, E_UNSUPPORTED, E_STATE = range(-1, -9, -1)
+RETRY = 2  # fluere_merge_gathered_finish: redo the device-agreed step with the host-driven sequence
 NEED_SWEEP = 1  # fluere_merge_gathered: complete the merge with the sweep composition (fluere_sweep_*)
 _ERR_NAMES = {
     E_ARG: "bad argument", E_IO: "I/O error", E_PCAP: "not a pcap capture", E_HIP: "HIP error / no GPU",
@@ -182,6 +183,9 @@ def lib() -> ctypes.CDLL:
                                      ctypes.POINTER(U64)]),
         "fluere_export_async": (I, [P, P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, P]),
         "fluere_merge_gathered": (I, [P, P, ctypes.c_uint32, U64, U64, ctypes.POINTER(Stats)]),
+        "fluere_merge_gathered_async": (I, [P, P, ctypes.c_uint32, U64, U64, P]),
+        "fluere_merge_gathered_finish": (I, [P, ctypes.POINTER(Stats)]),
+        "fluere_host_waits": (U64, [P]),
         "fluere_wire_bound": (U64, [U64, U64]),
         "fluere_wire_pack": (I, [P, P, U32, U64, U64, P, P]),
         "fluere_wire_unpack": (I, [P, P, U32, P, U64, U64, P]),

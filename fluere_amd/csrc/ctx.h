@@ -15,6 +15,10 @@ struct HostBatch {
     uint2* own_desc = nullptr;  // chunk descriptors (built by upload_batches)
 };
 
+namespace fl {
+struct MergePending;
+}
+
 struct fluere_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -147,6 +151,10 @@ struct fluere_ctx {
     int sob_cur = 0;
     void* d_sos = nullptr;           // wpre | tpre | ctr | holes
     size_t sos_bytes = 0;
+    // the owner merge of the device-agreed sharded step (shard.hip)
+    fl::MergePending* merge_p = nullptr;
+    std::chrono::steady_clock::time_point merge_t0{};
+    uint64_t host_waits = 0;         // blocking host waits on the stream (ctx_sync, wait_published polls)
     bool so_next = false;            // the last run was complete with ended records: enqueue the ordering
     uint64_t so_last_n = 0, so_last_ne = 0;
 };
@@ -200,7 +208,12 @@ TableSet tables_of(fluere_ctx* c);  // fluere_gpu.hip
 void reset_record_counters(fluere_ctx* c);  // fluere_gpu.hip
 unsigned flow_grid(fluere_ctx* c);  // fluere_gpu.hip
 unsigned done_grid(fluere_ctx* c, uint64_t n);  // fluere_gpu.hip
-int clear_flows(fluere_ctx* c);  // fluere_gpu.hip
+int clear_flows(fluere_ctx* c);
+// hipStreamSynchronize of the context stream, counted (fluere_host_waits)
+inline hipError_t ctx_sync(fluere_ctx* c) {
+    c->host_waits++;
+    return hipStreamSynchronize(c->stream);
+}  // fluere_gpu.hip
 int wait_published(fluere_ctx* c, uint32_t seq, Glob& g, uint32_t (&nf_err)[2]);  // fluere_gpu.hip
 int read_glob(fluere_ctx* c, Glob& g);  // fluere_gpu.hip
 int prepare_capture(fluere_ctx* c);  // fluere_gpu.hip
@@ -215,6 +228,7 @@ void free_flow_state(fluere_ctx* c);  // fluere_gpu.hip
 int grow_flow_state(fluere_ctx* c, uint64_t want);  // fluere_gpu.hip
 int bulk_clean(const fluere_ctx* c, uint64_t nf);  // fluere_gpu.hip
 void sweep_free(fluere_ctx* c);  // shard.hip
+void merge_pending_free(fluere_ctx* c);  // shard.hip
 int grow_recs_keep(fluere_ctx* c, uint64_t need, uint64_t keep);  // shard.hip
 int grow_pair(void** a, void** b, uint64_t* cap_b, uint64_t cap_a, size_t unit);  // order.hip
 int ord_scratch(fluere_ctx* c, size_t need);  // order.hip

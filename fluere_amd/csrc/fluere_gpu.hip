@@ -339,7 +339,7 @@ int fetch_records(fluere_ctx* c) {
     if (dev_act) {
         if (ne0) HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, ne0 * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
         HIPCHECK(hipMemcpyAsync(c->recs.data() + ne0, c->d_recs2, (n - ne0) * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         if (hostprof)
             fprintf(stderr, "[fluere] records: %llu to the host (%llu actives sorted on the device) %.1f ms\n",
                     (unsigned long long)n, (unsigned long long)(n - ne0),
@@ -352,7 +352,7 @@ int fetch_records(fluere_ctx* c) {
         HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
     if (n && c->has_aux)
         HIPCHECK(hipMemcpyAsync(c->aux.data(), c->d_recaux, 2 * n * 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     if (hostprof)
         fprintf(stderr, "[fluere] records: %llu to the host %.1f ms\n", (unsigned long long)n,
                 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
@@ -543,7 +543,7 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
 int grow_flow_state(fluere_ctx* c, uint64_t want) {
     const uint64_t mf = std::min<uint64_t>(std::max<uint64_t>(want, (uint64_t)c->fmax * 2), MAX_FLOWS);
     if (mf <= c->fmax) return FLUERE_OK;
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(ctx_sync(c));
     // the larger state is allocated before the current one is released: when
     // HBM cannot hold it, the context keeps its capacity (a run that then
     // overflows reports FLUERE_E_TABLE_FULL, as without the growth)
@@ -627,6 +627,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_recaux);
     hipFree(c->d_okey);
     sweep_free(c);
+    merge_pending_free(c);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -685,6 +686,7 @@ int clear_flows(fluere_ctx* c) {
 // (publish_ctl); now and then ask whether the stream failed instead.
 int wait_published(fluere_ctx* c, uint32_t seq, Glob& g, uint32_t (&nf_err)[2]) {
     volatile uint32_t* seqp = &c->h_ctl->seq;
+    if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) != seq) c->host_waits++;
     static const uint32_t qmask = getenv("FLUERE_QUERY_MASK") ? (uint32_t)atoi(getenv("FLUERE_QUERY_MASK")) : 65535u;
     for (uint32_t spin = 1;; spin++) {
         if (__atomic_load_n(seqp, __ATOMIC_ACQUIRE) == seq) break;
@@ -729,7 +731,7 @@ extern "C" int fluere_reset(fluere_ctx* c) {
     HIPCHECK(hipSetDevice(c->device));
     int rc = clear_flows(c);
     if (rc) return rc;
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(ctx_sync(c));
     free_batches(c);
     c->recs.clear();
     c->have_results = false;
@@ -873,7 +875,7 @@ extern "C" int fluere_parse_batch(fluere_ctx* c, fluere_pkt_meta* d_out, uint64_
         k_parse_batch<<<grid_for(hb.b.n, 256), 256, 0, c->stream>>>(hb.b, d_out + hb.b.first, mode);
     }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(ctx_sync(c));
     return FLUERE_OK;
 }
 
@@ -1771,7 +1773,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         // (a blocking wait would add ~15 us of wake-up latency to every run)
         if ((rc = wait_published(c, P.fa.seq, g, nf_err))) return rc;
     } else {
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         g = c->h_ctl->g;
         nf_err[0] = c->h_ctl->n_flows;
         nf_err[1] = c->h_ctl->err;
@@ -1916,14 +1918,14 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         k_seq_run<<<1, 64, 0, s>>>(sa);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         n_rec = g.n_rec;
         n_ended = g.n_heads;
         c->recs.resize(n_rec);
         if (n_rec)
             HIPCHECK(hipMemcpyAsync(c->recs.data(), c->d_recs, n_rec * sizeof(fluere_record), hipMemcpyDeviceToHost, s));
         HIPCHECK(hipEventRecord(c->ev2, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         for (uint64_t i = n_ended; i < n_rec; i++) c->recs[i].order_key = NONE64;
         hipFree(meta); hipFree(heap); hipFree(cur); hipFree(cdir);
         for (auto& r : c->recs) updates += r.d_pkts;
@@ -2057,7 +2059,7 @@ extern "C" int fluere_debug_dense_ids(fluere_ctx* c, const uint32_t* d_keys, uin
     HIPCHECK(hipSetDevice(c->device));
     if (n) k_dense_test<<<grid_for(n, 256), 256, 0, c->stream>>>(tables_of(c), d_keys, n, d_out, c->acc.slots);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(ctx_sync(c));
     uint32_t nf_err[2];
     HIPCHECK(hipMemcpy(nf_err, c->d_nflows, 8, hipMemcpyDeviceToHost));
     return nf_err[1] ? FLUERE_E_TABLE_FULL : FLUERE_OK;

@@ -320,7 +320,7 @@ static int order_sorted(fluere_ctx* c, uint64_t n, uint64_t n_ended, const unsig
         k_ob_gather_aux<<<g, 256, 0, s>>>(c->d_recaux, v0, n, c->d_recaux2);
         if (hipGetLastError() != hipSuccess) rc = FLUERE_E_HIP;
     }
-    HIPCHECK(hipStreamSynchronize(s));  // (then the scratch is released)
+    HIPCHECK(ctx_sync(c));  // (then the scratch is released)
     hipFree(buf);
     if (rc) return rc;
     std::swap(c->d_recaux, c->d_recaux2);

@@ -116,6 +116,13 @@ struct MergeArgs {
     uint32_t seq;
     unsigned long long timeout_us;
 };
+// a merge enqueued by fluere_merge_gathered_async, completed by _finish
+struct MergePending {
+    MergeArgs ma;
+    uint32_t seq = 0, shards = 0;
+    uint64_t cap = 0;
+    bool pending = false;
+};
 
 // summary i of a merge; null when absent
 __device__ __forceinline__ const fluere_flow_summary* merge_input(const MergeArgs& a, unsigned long long i) {
@@ -633,7 +640,7 @@ int grow_recs_keep(fluere_ctx* c, uint64_t need, uint64_t keep) {
     const uint64_t cap = std::max<uint64_t>(need, 1024);
     if (hipMalloc(&nr, cap * sizeof(fluere_record)) != hipSuccess) return FLUERE_E_NOMEM;
     if (keep) HIPCHECK(hipMemcpyAsync(nr, c->d_recs, keep * sizeof(fluere_record), hipMemcpyDeviceToDevice, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(ctx_sync(c));
     hipFree(c->d_recs);
     c->d_recs = nr;
     c->d_recs_cap = cap;
@@ -676,7 +683,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
     } back;
     HIPCHECK(hipMemcpyAsync(&back.ctl, c->d_glob, sizeof back.ctl, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipMemcpyAsync(back.nd, c->d_need, 16, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     Glob g = back.ctl.g;
     if (!(back.ctl.err & (ERR_TABLE_FULL | ERR_SPIN))) c->last_nf = back.ctl.n_flows;  // (merge owner estimate)
     // 2. order-dependent flows: their annexes (and the records that open and
@@ -693,7 +700,7 @@ extern "C" int fluere_export_device(fluere_ctx* c, void* d_blocks, uint32_t n_ow
         if ((rc = enqueue_export(true))) return rc;
         HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
         HIPCHECK(hipMemcpyAsync(back.nd, c->d_need, 16, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
     }
     if (need) *need = back.nd[0];
     if (need_annex) *need_annex = back.nd[1];
@@ -813,22 +820,40 @@ extern "C" int fluere_wire_unpack(fluere_ctx* c, const void* d_wire, uint32_t n_
     return FLUERE_OK;
 }
 
-extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap,
-                                     uint64_t cap_annex, fluere_stats* st) {
-    if (!c || (!d_blocks && n_shards) || (n_shards && !cap)) return FLUERE_E_ARG;
-    HIPCHECK(hipSetDevice(c->device));
+// the run counters the owner merge starts from (the records this rank's
+// export produced stay first in d_recs) -- a kernel, not a host copy
+__global__ void k_merge_counters(Glob* g, unsigned long long n_rec, unsigned long long updates,
+                                 unsigned long long ended) {
+    if (threadIdx.x) return;
+    g->n_rec = n_rec;
+    g->n_updates = updates;
+    g->n_ended = ended;
+}
+// 1 when the merge just enqueued cannot stand as the step's result: a block
+// was cut short (a shard had more flows for this owner than cap), a flow
+// depends on packet order (annexes needed), the span reaches the timeout (the
+// sweep composition), or the table filled
+__device__ __host__ __forceinline__ bool merge_redo(const Glob& g, uint32_t err, unsigned long long timeout_us) {
+    const bool expiry = g.valid && g.tmax >= g.tmin && g.tmax - g.tmin >= timeout_us;
+    return err != 0 || g.n_complex != 0 || expiry;
+}
+__global__ void k_merge_retry(const Glob* g, const uint32_t* err, unsigned long long timeout_us,
+                              unsigned long long* out) {
+    if (threadIdx.x) return;
+    out[0] = merge_redo(*g, *err, timeout_us) ? 1ull : 0ull;
+}
+
+// Enqueues the owner merge (no host wait unless a buffer grows); seq: the
+// number k_merge_finalize publishes.
+static int merge_enqueue(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap, uint64_t cap_annex,
+                         MergeArgs& ma, uint32_t& seq) {
     hipStream_t s = c->stream;
     int rc;
     const uint64_t n = (uint64_t)n_shards * cap;
     const uint64_t keep = c->local_n_rec;
     if ((rc = clear_flows(c))) return rc;
     c->precleaned = false;
-    {   // the records this rank's export produced stay first in d_recs
-        const unsigned long long cnt[3] = {keep, c->local_updates, c->local_ended};
-        char* gb = (char*)c->d_glob;
-        HIPCHECK(hipMemcpyAsync(gb + offsetof(Glob, n_rec), &cnt[0], 8, hipMemcpyHostToDevice, s));
-        HIPCHECK(hipMemcpyAsync(gb + offsetof(Glob, n_updates), &cnt[1], 16, hipMemcpyHostToDevice, s));
-    }
+    k_merge_counters<<<1, 64, 0, s>>>(c->d_glob, keep, c->local_updates, c->local_ended);
     if (!c->d_pay && hipMalloc(&c->d_pay, (size_t)c->fmax * sizeof(FirstPay)) != hipSuccess) return FLUERE_E_NOMEM;
     if (std::max<uint64_t>(n, 1) > c->d_sd_cap) {
         hipFree(c->d_sd);
@@ -838,17 +863,27 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
         c->d_sd_cap = std::max<uint64_t>(n, 1);
     }
     if ((rc = grow_recs_keep(c, keep + std::min<uint64_t>(std::max<uint64_t>(n, 1), c->fmax), keep))) return rc;
-    const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
-    MergeArgs ma{tables_of(c), c->acc, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
-                 c->d_recs_cap, (const uint8_t*)d_blocks, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
-                 c->h_ctl, seq, c->timeout_ms * 1000ull};
+    c->merge_t0 = std::chrono::steady_clock::now();
+    seq = ++c->run_seq ? c->run_seq : ++c->run_seq;  // never 0 (the initial value)
+    ma = MergeArgs{tables_of(c), c->acc, n, c->d_sd, (FirstPay*)c->d_pay, c->d_glob, c->d_recs, c->d_complex,
+                   c->d_recs_cap, (const uint8_t*)d_blocks, cap, cap_annex, fluere_shard_block_bytes(cap, cap_annex),
+                   c->h_ctl, seq, c->timeout_ms * 1000ull};
     if (n) {
         k_merge_insert<<<grid_for(n, 256), 256, 0, s>>>(ma);
         k_merge_payload<<<grid_for(n, 256), 256, 0, s>>>(ma);
     }
     k_merge_finalize<<<flow_grid(c), 256, 0, s>>>(ma);
     HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
+// The merge's results once k_merge_finalize published: the composition of
+// order-dependent flows (unless `redo`: then FLUERE_RETRY), the stats.
+static int merge_complete(fluere_ctx* c, MergeArgs& ma, uint32_t seq, uint32_t n_shards, uint64_t cap, bool redo,
+                          fluere_stats* st) {
+    hipStream_t s = c->stream;
+    int rc;
+    const uint64_t n = (uint64_t)n_shards * cap;
     Glob g;
     uint32_t nf_err[2];
     if ((rc = wait_published(c, seq, g, nf_err))) return rc;
@@ -856,9 +891,13 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
         c->last_nf = c->h_ctl->pad[0];
         c->async_nf = false;
     }
+    const uint64_t timeout_us = c->timeout_ms * 1000ull;
+    if (redo && merge_redo(g, nf_err[1], timeout_us)) {
+        c->have_results = false;
+        return FLUERE_RETRY;
+    }
     if (nf_err[1] & ERR_CAPACITY) return FLUERE_E_ARG;  // a shard had more flows than its block holds
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
-    const uint64_t timeout_us = c->timeout_ms * 1000ull;
     const bool expiry = g.valid && g.tmax >= g.tmin && g.tmax - g.tmin >= timeout_us;
     if (g.n_complex && !expiry) {
         // the order-dependent flows: compose the shards' pieces in shard order
@@ -876,7 +915,7 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
         k_comp_collect<<<grid_for(n, 256), 256, 0, s>>>(ma, keys, vals);
         unsigned long long nk = 0;
         HIPCHECK(hipMemcpyAsync(&nk, &c->d_glob->n_keys, 8, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         // records: the certified ones + at most one per shard piece
         if ((rc = grow_recs_keep(c, g.n_rec + 2 * nk, g.n_rec))) return rc;
         ma.out = c->d_recs;
@@ -892,7 +931,7 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
         if (nk) k_compose<<<grid_for(nk, 64), 64, 0, s>>>(ma, keys2, vals2, nk);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         hipFree(tmp); hipFree(keys); hipFree(keys2); hipFree(vals); hipFree(vals2);
     }
     const uint32_t nf = std::min(nf_err[0], c->fmax);
@@ -908,7 +947,7 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
     out.records = g.n_rec;
     out.ended = g.n_ended;
     out.complex_flows = g.n_complex;
-    out.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    out.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->merge_t0).count();
     out.updates = g.n_updates;
     if (st) *st = out;
     // the hard-timeout sweep (offline_fluereflows.rs:161-175): the records
@@ -920,6 +959,57 @@ extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32
     if (expiry) return FLUERE_NEED_SWEEP;
     return FLUERE_OK;
 }
+
+extern "C" int fluere_merge_gathered(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap,
+                                     uint64_t cap_annex, fluere_stats* st) {
+    if (!c || (!d_blocks && n_shards) || (n_shards && !cap)) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    MergeArgs ma{};
+    uint32_t seq = 0;
+    int rc;
+    if (c->merge_p) c->merge_p->pending = false;
+    if ((rc = merge_enqueue(c, d_blocks, n_shards, cap, cap_annex, ma, seq))) return rc;
+    return merge_complete(c, ma, seq, n_shards, cap, false, st);
+}
+
+// The device-agreed step (dist.py): the merge enqueued without a host wait,
+// and d_retry (device, one uint64) set to 1 when its result cannot stand (a
+// block cut short, order-dependent flows, the span reaching the timeout) --
+// the ranks reduce it (MAX) on the stream and read it once, the step's one
+// host round trip; fluere_merge_gathered_finish then returns the stats, or
+// FLUERE_RETRY when the step must be redone by the host-driven sequence.
+extern "C" int fluere_merge_gathered_async(fluere_ctx* c, const void* d_blocks, uint32_t n_shards, uint64_t cap,
+                                           uint64_t cap_annex, unsigned long long* d_retry) {
+    if (!c || !d_retry || (!d_blocks && n_shards) || (n_shards && !cap)) return FLUERE_E_ARG;
+    HIPCHECK(hipSetDevice(c->device));
+    int rc;
+    if (!c->merge_p) c->merge_p = new MergePending{};
+    MergePending& M = *c->merge_p;
+    M.pending = false;
+    if ((rc = merge_enqueue(c, d_blocks, n_shards, cap, cap_annex, M.ma, M.seq))) return rc;
+    k_merge_retry<<<1, 64, 0, c->stream>>>(c->d_glob, tables_of(c).err, c->timeout_ms * 1000ull, d_retry);
+    HIPCHECK(hipGetLastError());
+    M.pending = true;
+    M.shards = n_shards;
+    M.cap = cap;
+    return FLUERE_OK;
+}
+
+extern "C" int fluere_merge_gathered_finish(fluere_ctx* c, fluere_stats* st) {
+    if (!c) return FLUERE_E_ARG;
+    if (!c->merge_p || !c->merge_p->pending) return FLUERE_E_STATE;
+    HIPCHECK(hipSetDevice(c->device));
+    MergePending& M = *c->merge_p;
+    M.pending = false;
+    return merge_complete(c, M.ma, M.seq, M.shards, M.cap, true, st);
+}
+
+void merge_pending_free(fluere_ctx* c) {
+    delete c->merge_p;
+    c->merge_p = nullptr;
+}
+
+extern "C" uint64_t fluere_host_waits(fluere_ctx* c) { return c ? c->host_waits : 0; }
 
 // ---------------------------------------------------------------------------
 // sharded Mode B: the hard-timeout sweep composed across shards
@@ -1195,14 +1285,14 @@ extern "C" int fluere_sweep_pack(fluere_ctx* c, uint32_t n_owners, uint64_t* cou
         w->counts.assign(n_owners, 0);
         HIPCHECK(hipMemcpyAsync(w->counts.data(), w->misc, n_owners * 8, hipMemcpyDeviceToHost, s));
         HIPCHECK(hipGetLastError());
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         w->n_owners = n_owners;
     }
     for (uint32_t o = 0; o < n_owners; o++) counts[o] = w->counts[o];
     if (d_send && w->hn) {
         k_sw_pack<<<grid_for(w->hn, 256), 256, 0, s>>>(w->hcm, w->hperm, w->hn, c->d_sumpos, (ExMeta*)d_send);
         HIPCHECK(hipGetLastError());
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
     }
     return FLUERE_OK;
 }
@@ -1228,7 +1318,7 @@ extern "C" int fluere_sweep_load(fluere_ctx* c, const void* d_recv, uint32_t n_s
                                                    c->merge_cap, c->fmax, w->ocm, w->err);
     uint32_t err = 0;
     HIPCHECK(hipMemcpyAsync(&err, w->err, 4, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     if (err) return FLUERE_E_ARG;  // a packet of a flow the merge does not hold
     if (w->es) exact_free(w->es);
     w->es = nullptr;
@@ -1257,7 +1347,7 @@ extern "C" int fluere_sweep_index(fluere_ctx* c, const uint8_t* d_pr, uint64_t* 
     if (rc) return rc;
     unsigned long long root = 0;
     HIPCHECK(hipMemcpyAsync(&root, w->tree + 1, 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     *max_time = n ? root : 0;  // 1 + the latest processed packet's time (0: none)
     return FLUERE_OK;
 }
@@ -1289,7 +1379,7 @@ extern "C" int fluere_sweep_queries(fluere_ctx* c, uint32_t n_ranks, uint32_t ra
             k_sw_kcount<<<grid_for(n_ranks + 1, 256), 256, 0, s>>>(w->k2, n, n_ranks + 1, w->misc + 2048);
             HIPCHECK(hipGetLastError());
             HIPCHECK(hipMemcpyAsync(cnt.data(), w->misc + 2048, (n_ranks + 1) * 8, hipMemcpyDeviceToHost, s));
-            HIPCHECK(hipStreamSynchronize(s));
+            HIPCHECK(ctx_sync(c));
         }
         for (uint32_t r = 0; r < n_ranks; r++) { qcounts[r] = cnt[r]; w->nq += cnt[r]; }
         return FLUERE_OK;
@@ -1298,7 +1388,7 @@ extern "C" int fluere_sweep_queries(fluere_ctx* c, uint32_t n_ranks, uint32_t ra
     uint64_t nq = w->nq;
     if (nq) k_sw_qpack<<<grid_for(nq, 256), 256, 0, s>>>(w->hcm, w->qk, nq, T, (unsigned long long*)d_q);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     return FLUERE_OK;
 }
 
@@ -1311,7 +1401,7 @@ extern "C" int fluere_sweep_answer(fluere_ctx* c, const void* d_q, uint64_t n, v
         k_sw_answer<<<grid_for(n, 256), 256, 0, s>>>((const unsigned long long*)d_q, n, w->tree, w->P, w->hcm, w->hn,
                                                      (unsigned long long*)d_ans);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     return FLUERE_OK;
 }
 
@@ -1323,7 +1413,7 @@ extern "C" int fluere_sweep_points(fluere_ctx* c, const void* d_ans, void* d_f) 
     if (w->nq) k_sw_fill<<<grid_for(w->nq, 256), 256, 0, s>>>((const unsigned long long*)d_ans, w->qk, w->nq, w->hF);
     if (w->hn) k_sw_fpack<<<grid_for(w->hn, 256), 256, 0, s>>>(w->hF, w->hperm, w->hn, (unsigned long long*)d_f);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     return FLUERE_OK;
 }
 
@@ -1357,14 +1447,14 @@ extern "C" int fluere_sweep_seed_requests(fluere_ctx* c, uint32_t n_ranks, const
         HIPCHECK(hipGetLastError());
         std::vector<unsigned long long> cnt(n_ranks);
         HIPCHECK(hipMemcpyAsync(cnt.data(), w->misc + 2048, n_ranks * 8, hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(ctx_sync(c));
         uint64_t tot = 0;
         for (uint32_t r = 0; r < n_ranks; r++) { counts[r] = cnt[r]; tot += cnt[r]; }
         if (tot != w->n_inst) return FLUERE_E_ARG;  // a creating packet outside every shard's range
         return FLUERE_OK;
     }
     if (w->n_inst) HIPCHECK(hipMemcpyAsync(d_req, w->req, (size_t)w->n_inst * 8, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     return FLUERE_OK;
 }
 
@@ -1378,7 +1468,7 @@ extern "C" int fluere_sweep_seeds(fluere_ctx* c, const void* d_req, uint64_t n, 
         k_sw_seed<<<grid_for(n, 256), 256, 0, s>>>(c->d_batches, (int)c->batches.size(), (const unsigned long long*)d_req,
                                                    n, c->use_mac, (Seed*)d_seeds);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     return FLUERE_OK;
 }
 
@@ -1396,7 +1486,7 @@ extern "C" int fluere_sweep_finish(fluere_ctx* c, const void* d_seeds, fluere_st
     // the records of this rank: only the sweep's (the merge emitted none)
     Glob g;
     HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     const uint64_t want = g.n_rec + ni;
     if (want > c->d_recaux_cap) {
         hipFree(c->d_recaux);
@@ -1409,7 +1499,7 @@ extern "C" int fluere_sweep_finish(fluere_ctx* c, const void* d_seeds, fluere_st
     int rc = exact_finish(w->es, w->seeds, c->d_recaux + 2 * g.n_rec);
     if (rc) return rc;
     HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(ctx_sync(c));
     c->dev_n_rec = g.n_rec;
     c->host_recs = false;
     c->dev_ordered = false;

@@ -140,6 +140,8 @@ class _DistComm:
     collective end with their stream drained, and a collective's output is
     waited for before the library reads it)."""
 
+    host_reads = 0  # values read back to the host (each one a round trip)
+
     def __init__(self, group, ctx):
         import torch
         import torch.distributed as dist
@@ -168,6 +170,7 @@ class _DistComm:
         x = t.cpu() if self.gloo else t
         dist.all_reduce(x, op=dist.ReduceOp.MAX, group=self.group)
         self._after()
+        self.host_reads += 1
         return np.asarray(x.tolist(), dtype=np.int64)
 
     def allgather_dev(self, tensors):
@@ -183,6 +186,7 @@ class _DistComm:
         else:
             dist.all_gather_into_tensor(out, x, group=self.group)
         self._after()
+        self.host_reads += 1
         return np.asarray(out.tolist(), dtype=np.int64)
 
     def all_to_all_known(self, sends, send_counts, recv_counts):
@@ -198,6 +202,7 @@ class _DistComm:
         (a,) = arrays
         t = torch.tensor(np.asarray(a, dtype=np.int64), device="cpu" if self.gloo else self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self.host_reads += 1
         return np.asarray(t.tolist(), dtype=np.int64)
 
     def allgather(self, arrays):
@@ -208,6 +213,7 @@ class _DistComm:
         t = torch.tensor(a, device="cpu" if self.gloo else self.device)
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
+        self.host_reads += 1
         return np.stack([np.asarray(o.tolist(), dtype=np.int64) for o in out])
 
     def all_to_all_equal(self, sends, recvs):
@@ -219,6 +225,7 @@ class _DistComm:
     def all_to_all_v(self, sends, counts, elem):
         (s,), (c,) = sends, counts
         self._before()
+        self.host_reads += 1  # (the receive counts)
         r, rc = exchange_var(s, c, elem, self.group)
         self._after()
         return [r], [rc]
@@ -231,6 +238,7 @@ class _LocalComm:
     def __init__(self, n):
         self.world = n
         self.ranks = list(range(n))
+        self.host_reads = 0
 
     @staticmethod
     def _sync():
@@ -239,10 +247,12 @@ class _LocalComm:
 
     def allreduce_max_dev(self, tensors):
         self._sync()
+        self.host_reads += 1
         return np.max(np.stack([np.asarray(t.tolist(), dtype=np.int64) for t in tensors]), axis=0)
 
     def allgather_dev(self, tensors):
         self._sync()
+        self.host_reads += 1
         return np.stack([np.asarray(t.tolist(), dtype=np.int64) for t in tensors])
 
     def all_to_all_known(self, sends, send_counts, recv_counts):
@@ -410,13 +420,85 @@ class _StepState:
         self.wire = wire  # None: by block size (WIRE_MIN_BLOCK); True / False: always / never
         self.bytes_sent = 0  # per local context, last step: the bytes it sent to other ranks
         self.wire_used = False
+        # the device-agreed step (_shard_step_dev): taken after a host-driven
+        # step that needed neither annexes nor the sweep composition
+        self.dev_next = False
+        self.flags = None
+        self.device_agreed = False  # the last step was the device-agreed one
+
+
+def _ensure_blocks(S: _StepState, n_ctx: int, W: int, blk: int):
+    import torch
+    if S.sends is None or S.blk != blk or len(S.sends) != n_ctx:
+        S.sends = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in range(n_ctx)]
+        S.recvs = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in range(n_ctx)]
+        S.blk = blk
+
+
+def _shard_step_dev(comm, ctxs, S: _StepState):
+    """The step agreed on the device: parse + key + aggregate, export without
+    annexes into blocks of the current capacities, one all-to-all of equal
+    blocks, the owner merge -- enqueued back to back on the stream.  Each
+    merge sets a retry word on the device (a block cut short, order-dependent
+    flows, the span reaching the timeout); the ranks reduce it (MAX) and read
+    it once: the step's one host round trip.  Returns the stats, or None when
+    the step must be redone by the host-driven sequence."""
+    import torch
+    L = _lib.lib()
+    W = comm.world
+    for c in ctxs:
+        c.parse_aggregate()
+    blk = int(L.fluere_shard_block_bytes(S.cap, S.cap_annex))
+    _ensure_blocks(S, len(ctxs), W, blk)
+    if S.infos is None or len(S.infos) != len(ctxs) or S.infos[0].numel() < 6:
+        S.infos = [torch.zeros(6, dtype=torch.int64, device="cuda") for _ in ctxs]
+    if S.flags is None or len(S.flags) != len(ctxs):
+        S.flags = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in ctxs]
+    for c, rk, s, info in zip(ctxs, comm.ranks, S.sends, S.infos):
+        check(L.fluere_export_async(c._h, s.data_ptr(), W, rk, S.cap, S.cap_annex, info.data_ptr()),
+              "fluere_export_async")
+    comm.all_to_all_equal(S.sends, S.recvs)
+    for c, r, f in zip(ctxs, S.recvs, S.flags):
+        check(L.fluere_merge_gathered_async(c._h, r.data_ptr(), W, S.cap, S.cap_annex, f.data_ptr()),
+              "fluere_merge_gathered_async")
+    redo = int(comm.allreduce_max_dev(S.flags)[0])
+    stats = []
+    for c in ctxs:
+        st = Stats()
+        rc = L.fluere_merge_gathered_finish(c._h, ctypes.byref(st))
+        if rc == _lib.RETRY and redo:
+            continue
+        check(rc, "fluere_merge_gathered_finish")
+        d = st.as_dict()
+        d["rc"] = rc
+        d["device_agreed"] = 1
+        stats.append(d)
+    if redo:
+        return None
+    S.wire_used = False
+    S.bytes_sent = (W - 1) * blk
+    return stats
 
 
 def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
+    """One sharded pass over every local context: the device-agreed step
+    when the last step allows it (_shard_step_dev), else -- or when it asks
+    for a redo -- the host-driven one."""
+    if S.dev_next and S.wire is not True:
+        stats = _shard_step_dev(comm, ctxs, S)
+        if stats is not None:
+            S.device_agreed = True
+            return stats
+    S.device_agreed = False
+    return _shard_step_host(comm, ctxs, S, rank_first_fn)
+
+
+def _shard_step_host(comm, ctxs, S: _StepState, rank_first_fn):
     """One sharded pass over every local context (parse + key + aggregate,
     export, capacity agreement, all-to-all, owner merge; the sweep
-    composition when the span reaches the timeout).  Returns the merge stats
-    of every local context."""
+    composition when the span reaches the timeout), every decision taken on
+    the host from the gathered export counts.  Returns the merge stats of
+    every local context."""
     import torch
     L = _lib.lib()
     W = comm.world
@@ -428,10 +510,7 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
     while True:
         blk = int(L.fluere_shard_block_bytes(S.cap, S.cap_annex))
         wire = (blk >= WIRE_MIN_BLOCK) if S.wire is None else bool(S.wire)  # (the same on every rank)
-        if S.sends is None or S.blk != blk or len(S.sends) != len(ctxs):
-            S.sends = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in ctxs]
-            S.recvs = [torch.empty(W * blk, dtype=torch.uint8, device="cuda") for _ in ctxs]
-            S.blk = blk
+        _ensure_blocks(S, len(ctxs), W, blk)
         if wire:
             wb = int(L.fluere_wire_bound(S.cap, S.cap_annex))
             if S.wsends is None or S.wbound != wb or len(S.wsends) != len(ctxs):
@@ -504,6 +583,9 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
         stats = _sweep_compose(comm, ctxs, rank_first_fn(), *packed)
         for d in stats:
             d["rc"] = _lib.NEED_SWEEP
+    # the next step agrees on the device unless this one needed annexes or the
+    # sweep (the capacities it grew to stay)
+    S.dev_next = not annexes and not expiry
     return stats
 
 
@@ -544,6 +626,16 @@ class ShardExchange:
     def wire_used(self):
         """The last step moved the compact wire encoding (else equal wide blocks)."""
         return self._S.wire_used
+
+    @property
+    def device_agreed(self):
+        """The last step was agreed on the device (one host read: the retry word)."""
+        return self._S.device_agreed
+
+    @property
+    def host_reads(self):
+        """Values this rank's collectives read back to the host so far."""
+        return self._comm.host_reads if self._comm is not None else 0
 
     def _rank_first_fn(self):
         if self._rank_first is None:
@@ -617,6 +709,14 @@ class LogicalShards:
     @property
     def wire_used(self):
         return self._S.wire_used
+
+    @property
+    def device_agreed(self):
+        return self._S.device_agreed
+
+    @property
+    def host_reads(self):
+        return self._comm.host_reads
 
     def _rank_first(self):
         first = [int(getattr(c, "index_base", 0)) for c in self.ctxs]

@@ -91,6 +91,10 @@ class FlowContext:
     def parse_aggregate(self):
         check(self._L.fluere_parse_aggregate(self._h), "fluere_parse_aggregate")
 
+    def host_waits(self) -> int:
+        """Blocking host waits on the context's stream so far (fluere_host_waits)."""
+        return int(self._L.fluere_host_waits(self._h))
+
     def last_kernel_ms(self) -> float:
         """HIP-event time of the last k_parse_agg launch (the roofline kernel)."""
         return float(self._L.fluere_last_kernel_ms(self._h))

@@ -51,6 +51,10 @@ enum fluere_status {
  * of a capture whose span reaches the timeout; its records come from the
  * sweep composition (fluere_sweep_*). */
 #define FLUERE_NEED_SWEEP 1
+/* Positive status: fluere_merge_gathered_finish found the device-agreed step's
+ * merge unusable (a block cut short, order-dependent flows, or the span
+ * reaching the timeout); redo the step with the host-driven sequence. */
+#define FLUERE_RETRY 2
 
 /* NetError per packet (src/net/mod.rs:28-36). */
 enum fluere_pkt_status {
@@ -303,6 +307,24 @@ int fluere_export_async(fluere_ctx* ctx, void* d_blocks, uint32_t n_owners, uint
  * yet; every rank completes the merge with the fluere_sweep_* sequence. */
 int fluere_merge_gathered(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
                           uint64_t cap_annex, fluere_stats* stats);
+/* The same merge for a step agreed on the device (no host round trip before
+ * it): fluere_merge_gathered_async enqueues the merge and sets d_retry (device,
+ * one uint64) to 1 when its result cannot stand -- a block cut short, a flow
+ * whose record depends on packet order (annexes), the span reaching the
+ * timeout; the ranks reduce it (MAX) on the stream and read it once (the
+ * step's one host round trip).  fluere_merge_gathered_finish then returns
+ * FLUERE_OK with the stats, or FLUERE_RETRY: every rank redoes the step with
+ * fluere_parse_aggregate, fluere_export_async / fluere_export_device and
+ * fluere_merge_gathered (dist.py).  Replaces the host decision on the gathered
+ * export counts (the reference has no sharding: offline_fluereflows.rs:49-191
+ * is one sequential pass). */
+int fluere_merge_gathered_async(fluere_ctx* ctx, const void* d_blocks, uint32_t n_shards, uint64_t cap,
+                                uint64_t cap_annex, unsigned long long* d_retry);
+int fluere_merge_gathered_finish(fluere_ctx* ctx, fluere_stats* stats);
+/* Blocking host waits on the context's stream so far (stream syncs, polls of
+ * a counter copy that was not yet published): the host round trips a step
+ * takes (tests). */
+uint64_t fluere_host_waits(fluere_ctx* ctx);
 
 /* The compact wire encoding of the blocks (what the all-to-all moves): each
  * summary as a variable-length record that leaves out absent and zero fields

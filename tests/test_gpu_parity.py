@@ -470,6 +470,38 @@ def test_sharded_steps_repeat_with_slow_packets(gpu, wire):
         c.close()
 
 
+@pytest.mark.parametrize("G", [2, 4])
+def test_sharded_device_agreed_steps(gpu, G):
+    """Repeated sharded steps: the first is host-driven (it
+    grows the blocks from a small capacity); every later one is agreed on the
+    device -- export, all-to-all and owner merge enqueued back to back, ONE
+    host read (the reduced retry word), no library wait -- and equals the
+    oracle.  A device-agreed step whose blocks are cut short asks for the redo
+    and is completed by the host-driven sequence."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    ls, ctxs = _logical_shards(cfg, G, cap=64, cap_annex=8, wire=False)
+    for step in range(3):
+        r0, w0 = ls.host_reads, [c.host_waits() for c in ctxs]
+        ls.run()
+        reads, waits = ls.host_reads - r0, [c.host_waits() - w for c, w in zip(ctxs, w0)]
+        print(f"G={G} step {step}: device_agreed {ls.device_agreed} host reads {reads} library waits {waits}")
+        if step:
+            assert ls.device_agreed
+            assert reads == 1 and waits == [0] * G, (reads, waits)
+        recs, ne = ls.records()
+        assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"device-agreed G={G} step {step}")
+    # forced onto the device path with blocks too small: the redo
+    ls2 = fluere_amd.dist.LogicalShards(ctxs, cap=64, cap_annex=8, wire=False)
+    ls2._S.dev_next = True
+    ls2.run()
+    assert not ls2.device_agreed
+    recs, ne = ls2.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"device-agreed redo G={G}")
+    for c in ctxs:
+        c.close()
+
+
 def test_sharded_cut_short_block_is_an_error(gpu):
     """A block with more flows than its capacity: the merge refuses it."""
     cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 40_000, 2000, 0xF10E0004)
@@ -1091,12 +1123,14 @@ def _shard_exchange_rank(rank, world, port, q, case):
             ctx.add_device_batch(b, nbytes, o, nb)
         torch.cuda.synchronize()
         ex = fluere_amd.dist.ShardExchange(ctx, cap=128, cap_annex=16, wire=case.endswith("_wire") or None)
-        for _ in range(2):  # the first step grows the blocks, the second reuses them
+        for _ in range(2):  # the first step grows the blocks, the second reuses them (agreed on the device)
+            r0, w0 = ex.host_reads, ctx.host_waits()
             ex.step()
+        last = (ex.device_agreed, ex.host_reads - r0, ctx.host_waits() - w0)
         got = ex.gather_records()
         if rank == 0:
             recs, ne = got
-            q.put((fluere_amd.format_csv(recs), ne))
+            q.put((fluere_amd.format_csv(recs), ne, last))
         ctx.close()
     finally:
         dist.destroy_process_group()
@@ -1120,11 +1154,19 @@ def test_shard_exchange_two_ranks_gloo(gpu, case):
     procs = [ctx.Process(target=_shard_exchange_rank, args=(r, 2, port, q, case)) for r in range(2)]
     for p in procs:
         p.start()
-    csv, ne = q.get(timeout=240)
+    csv, ne, (agreed, reads, waits) = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"ShardExchange gloo x2 {case}")
+    # the second step: agreed on the device with one host read (the reduced
+    # retry word) and no library wait -- unless the capture needs annexes
+    # (order-dependent flows) or the sweep, or the wire encoding is forced
+    print(case, "device_agreed", agreed, "host reads", reads, "library waits", waits)
+    if agreed:
+        assert reads == 1 and waits == 0, (reads, waits)
+    if case.startswith("udp") and not case.endswith("_wire"):
+        assert agreed
 
 
 def test_pcapng_file_ingest(gpu, tmp_path):
