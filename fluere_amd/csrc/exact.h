@@ -98,6 +98,11 @@ struct ExactJob {
     // instead of a parse of the batches.
     const ExMeta* ext_cm = nullptr;
     uint64_t ext_n = 0;
+    // One GPU, Mode B: every packet's replay metadata written by the hot pass
+    // in capture order (AggArgs::exm; every packet valid, none for the general
+    // parser): no k_ex_meta pass; the flows come from the merge's words
+    // (phash + emap, which must be set)
+    const ExMeta* dense_cm = nullptr;
     // Mode A: the complex-flow filter (device.h ckey_bucket), or null
     const uint8_t* cbits = nullptr;
     // pinned mailbox for the host's scalar reads (null: copies + stream syncs)
@@ -130,6 +135,9 @@ struct ExactResult {
 // (timestamps not non-decreasing over the valid packets, or no fixed point
 // within the pass limit): the caller runs the sequential kernel; else FLUERE_E_*.
 constexpr int EXACT_FALLBACK = 1;
+// exact_begin: a packet of the dense metadata has no flow word (exact_run
+// then begins again with k_ex_meta)
+constexpr int EXACT_DENSE_MISS = 2;
 int exact_run(const ExactJob& job, hipStream_t s, ExactResult* res);
 // Grow the job's scratch arena (J.scratch) to what exact_begin lays out for
 // it, ahead of the run (host-side allocation while the GPU works).

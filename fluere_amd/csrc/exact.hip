@@ -225,6 +225,20 @@ __global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta_blk, cons
     }
 }
 
+// one GPU, Mode B over the hot pass's dense metadata: packet k's flow from
+// the merge's word; a packet without one is counted in *bad (then the caller
+// takes the k_ex_meta path)
+__global__ void __launch_bounds__(256) k_ex_pidkeys(uint64_t n, const uint32_t* pid, const uint32_t* emap, uint32_t fmax,
+                                                    uint32_t* key, uint32_t* val, uint32_t* bad) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t d = k < n ? ph_flow(pid[k], emap) : 0u;
+    const bool miss = k < n && (d == FAIL || d >= fmax);
+    if (__ballot(miss) && (threadIdx.x & 63) == 0) atomicAdd(bad, 1u);
+    if (k >= n) return;
+    key[k] = miss ? 0xFFFFFFFFu : d;
+    val[k] = (uint32_t)k;
+}
+
 // sharded Mode B owner: sort keys of the shards' packets (capture order)
 __global__ void __launch_bounds__(256) k_ex_keys(uint64_t n, const ExMeta* cm, uint32_t* key, uint32_t* val) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -239,9 +253,10 @@ __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* s
                                                    unsigned long long* re, unsigned long long* rf) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
-    const ExMeta m = cm[sval[p]];
-    sm[p] = m;
+    ExMeta m = cm[sval[p]];
     const unsigned long long d = skey[p];
+    m.d = (uint32_t)d;  // (the sort key is the flow: dense capture-order metadata carries none)
+    sm[p] = m;
     hf[p] = (p == 0 || skey[p - 1] != skey[p]) ? 1u : 0u;
     // reversed, so an inclusive min-scan gives the first eligible / FIN-RST
     // position at or after p within the key (low PBITS bits MP: none)
@@ -1143,7 +1158,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     uint32_t* bcount = A.take<uint32_t>(nblk + 1);
     uint32_t* bpos = A.take<uint32_t>(nblk + 1);
     // ---- 1. metadata of every packet to replay, compacted in capture order
-    if (!J.ext_cm) {
+    if (!J.ext_cm && !J.dense_cm) {
         uint64_t blk = 0;
         for (int b = 0; b < J.nb; b++) {
             const Batch& B = J.h_batches[b];
@@ -1203,6 +1218,12 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         n = N;
         HIPCHECK(hipMemcpyAsync(cm, J.ext_cm, n * sizeof(ExMeta), hipMemcpyDeviceToDevice, s));
         k_ex_keys<<<gridn(n, 256), 256, 0, s>>>(n, cm, key, val);
+    } else if (J.dense_cm) {  // one GPU, Mode B: the hot pass's metadata, every packet
+        n = N;
+        cm = S->cm = const_cast<ExMeta*>(J.dense_cm);
+        HIPCHECK(hipMemsetAsync(bcount, 0, 4, s));
+        k_ex_pidkeys<<<gridn(n, 256), 256, 0, s>>>(n, J.phash + (J.h_batches[0].first - J.phash_base), J.emap,
+                                                   J.T.fmax, key, val, bcount);
     } else {
         HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, bcount, bpos, (int)nblk, s));
         unsigned long long last[2] = {0, 0};
@@ -1252,15 +1273,16 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     // on the device and the chase's grid covers the replayed packets (every
     // host round trip leaves the GPU idle for ~50-60 us: the wait, then the
     // next submission on an idle queue)
-    unsigned long long hv[5] = {0, 0, 0, 0, 0};
+    unsigned long long hv[6] = {0, 0, 0, 0, 0, 0};
     const bool dev_keys = !J.mode_b && !J.shard_mode;
     if (dev_keys) {
         k_ex_nkeys<<<1, 64, 0, s>>>(hpos + n - 1, hf + n - 1, ctr + 3);
     } else {
-        const void* src[5] = {hpos + n - 1, hf + n - 1, ctr + 1, &cm[0].t, &cm[n - 1].t};
-        const int by[5] = {4, 4, 4, 8, 8};
-        int rc = mail_fetch(J.mail, s, J.mode_b ? 5 : 2, src, by, hv);
+        const void* src[6] = {hpos + n - 1, hf + n - 1, ctr + 1, &cm[0].t, &cm[n - 1].t, bcount};
+        const int by[6] = {4, 4, 4, 8, 8, 4};
+        int rc = mail_fetch(J.mail, s, J.mode_b ? (J.dense_cm ? 6 : 5) : 2, src, by, hv);
         if (rc) return rc;
+        if (J.dense_cm && hv[5]) return EXACT_DENSE_MISS;  // a packet without a flow word: the k_ex_meta path
     }
     S->n_keys = (uint32_t)(hv[0] + hv[1]);
     S->R.keys = S->n_keys;
@@ -1518,6 +1540,13 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
 int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     ExactSession* S = nullptr;
     int rc = exact_begin(J, s, &S);
+    if (rc == EXACT_DENSE_MISS) {
+        exact_free(S);
+        S = nullptr;
+        ExactJob J2 = J;
+        J2.dense_cm = nullptr;
+        rc = exact_begin(J2, s, &S);
+    }
     for (int pass = 0; rc == FLUERE_OK && S->n; pass++) {
         if (pass == MAX_PASSES) {
             rc = EXACT_FALLBACK;

@@ -309,12 +309,21 @@ __global__ void __launch_bounds__(1024) k_scratch_warm(uint8_t* out, uint32_t n)
     if (n == 1u) out[threadIdx.x] = (uint8_t)buf[threadIdx.x & 127u];
 }
 
+// the record counters of a run, zeroed by one launch (eight 8-byte memsets
+// cost a host submission each while the GPU waits for them)
+__global__ void k_reset_records(Glob* g) {
+    if (threadIdx.x) return;
+    g->n_rec = 0;
+    g->n_complex = 0;
+    g->n_complex_pkts = 0;
+    g->n_heads = 0;
+    g->n_updates = 0;
+    g->n_ended = 0;
+    g->n_fdefer = 0;
+    g->n_okey = 0;
+}
 void reset_record_counters(fluere_ctx* c) {
-    char* g = (char*)c->d_glob;
-    for (size_t off : {offsetof(Glob, n_rec), offsetof(Glob, n_complex), offsetof(Glob, n_complex_pkts),
-                       offsetof(Glob, n_heads), offsetof(Glob, n_updates), offsetof(Glob, n_ended),
-                       offsetof(Glob, n_fdefer), offsetof(Glob, n_okey)})
-        hipMemsetAsync(g + off, 0, 8, c->stream);
+    k_reset_records<<<1, 64, 0, c->stream>>>(c->d_glob);
 }
 
 // Host copy of device-resident records, ended prefix first in emission order
@@ -628,6 +637,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     hipFree(c->d_okey);
     sweep_free(c);
     merge_pending_free(c);
+    hipFree(c->d_exm);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -899,6 +909,7 @@ struct PassPlan {
     int spill;     // 1: the hot pass is k_parse_spill (many flows per window), not k_parse_agg
     int lean_merge;  // 1: runs without partials merge their owners in k_merge_spill (0: k_merge_partials, A/B)
     int one_merge;   // 1: one k_merge_spill over every batch of the pass (after all the hot passes)
+    int exm;         // 1: k_parse_spill writes every packet's ExMeta (Mode B predicted: AggArgs::exm)
     MergeSrc ms;     // the owner segments of every batch (k_merge_spill)
     int phash;     // 1: the hot pass writes the per-packet filter words (AggArgs::phash)
     int pid;       // 1: the merge writes each packet's flow over them (AggArgs::pid; k_parse_spill runs)
@@ -1061,6 +1072,21 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
             hipMalloc(&c->d_emap, ((size_t)PLAN_BATCHES << 21) * sizeof(uint32_t)) != hipSuccess)
             return FLUERE_E_NOMEM;
     }
+    // Mode B predicted (the last run's): the hot pass also writes every
+    // packet's replay metadata in capture order, so the exact engine skips its
+    // k_ex_meta pass over the packets (used when every packet was valid and
+    // none needed the general parser; FLUERE_EXM=0: A/B)
+    {
+        static const int exm_env = getenv("FLUERE_EXM") ? atoi(getenv("FLUERE_EXM")) : -1;
+        P.exm = (P.pid && P.spill && !c->use_mac && c->last_mode_b && exm_env != 0) ? 1 : 0;
+        if (P.exm && c->n_total > c->exm_cap) {
+            hipFree(c->d_exm);
+            c->d_exm = nullptr;
+            c->exm_cap = 0;
+            if (hipMalloc(&c->d_exm, c->n_total * sizeof(ExMeta)) != hipSuccess) return FLUERE_E_NOMEM;
+            c->exm_cap = c->n_total;
+        }
+    }
     if (P.phash && c->n_total > c->phash_cap) {
         hipFree(c->d_phash);
         c->d_phash = nullptr;
@@ -1130,6 +1156,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         ab.emap = P.pid ? c->d_emap : nullptr;
         ab.pid_base = c->index_base;
         ab.pid_batch = (uint32_t)P.nb;
+        ab.exm = P.exm ? c->d_exm + (hb.b.first - c->index_base) : nullptr;
         const size_t all = sets + n_slow_sets;
         Stage& S = ab.S;
         // layout (16-byte aligned pieces): parts | owner segments (hot, k_slow) | spill_raw | spill | base | off | soff
@@ -1875,6 +1902,8 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             J.phash_base = c->index_base;
             J.emap = c->d_emap;
         }
+        // every packet's metadata from the hot pass (all valid, none for the general parser)
+        if (P.exm && g.valid == c->n_total && g.dropped == 0 && g.n_slow == 0) J.dense_cm = c->d_exm;
         J.recaux = &c->d_recaux;  // the records' order words (fetch_records orders by them)
         J.recaux_cap = &c->d_recaux_cap;
         ExactResult er{};

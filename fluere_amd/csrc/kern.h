@@ -183,6 +183,10 @@ struct AggArgs {
     uint32_t* emap;
     uint64_t pid_base;
     uint32_t pid_batch;
+    // Mode B predicted (k_parse_spill): every packet's replay metadata, this
+    // batch's first packet first (capture order over the capture: the exact
+    // engine's k_ex_meta pass is skipped), or null
+    ExMeta* exm;
     int tail_only;             // k_merge_partials: no owners (k_merge_spill merged them), only the run
                                // statistics and the tail (overflow list, general-parser packets)
     int slow_all;              // k_slow takes every packet of the batch (no hot kernel: captures of the general
