@@ -249,8 +249,7 @@ __global__ void __launch_bounds__(256) k_ex_keys(uint64_t n, const ExMeta* cm, u
 
 // ---- 2. sorted view, key heads, next-eligible / next-FIN inputs -------------
 __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* skey, const uint32_t* sval,
-                                                   const ExMeta* cm, ExMeta* sm, uint32_t* hf,
-                                                   unsigned long long* re, unsigned long long* rf) {
+                                                   const ExMeta* cm, ExMeta* sm, uint32_t* hf, uint8_t* gbits) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     ExMeta m = cm[sval[p]];
@@ -258,10 +257,8 @@ __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* s
     m.d = (uint32_t)d;  // (the sort key is the flow: dense capture-order metadata carries none)
     sm[p] = m;
     hf[p] = (p == 0 || skey[p - 1] != skey[p]) ? 1u : 0u;
-    // reversed, so an inclusive min-scan gives the first eligible / FIN-RST
-    // position at or after p within the key (low PBITS bits MP: none)
-    re[n - 1 - p] = (d << PBITS) | ((m.bits & 1) ? p : MP);
-    rf[n - 1 - p] = (d << PBITS) | ((m.bits & 2) ? p : MP);
+    // the next eligible / FIN-RST scans read these flags (k_next_scan)
+    gbits[p] = m.bits;
 }
 
 __global__ void __launch_bounds__(256) k_ex_heads(uint64_t n, const uint32_t* hf, const uint32_t* hpos, uint32_t* heads) {
@@ -322,11 +319,185 @@ __global__ void __launch_bounds__(256) k_ex_tscan(uint64_t n, const ExMeta* cm, 
     if (__ballot(back) && (threadIdx.x & 63) == 0) *bad = 1u;
 }
 
-// reversed "k if processed" for the next-processed min-scan
-__global__ void __launch_bounds__(256) k_ex_proc_in(uint64_t n, const uint8_t* pr, unsigned long long* npr) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) npr[n - 1 - k] = pr[k] ? k : MP;
+// ---- next-position scans --------------------------------------------------------
+// out_o[p] = min over p' >= p of v_o(p'), v_o(p) = key(p) << PBITS | (flags[p] & mask_o ?
+// p : MP): for sorted position p, the first position at or after p within its
+// key whose flags have mask_o (the key in the high bits; MP: none) -- the next
+// create-eligible and next FIN/RST packets of a key (two outputs), or with no
+// key the next processed packet.  Replaces a reversed input array and a
+// library min-scan per output: the keys (4 B) and flags (1 B) read twice, one
+// write per output, 16 contiguous items a thread (vector loads and stores).
+// k_next_reduce: each tile's minima; k_next_scan: a tile's suffix is the
+// minimum of the later tiles' (every workgroup reduces them itself: no chained
+// look-back, whose serial cross-XCD waits cost ~0.5 us a tile), then the
+// suffix scan within the tile.
+struct NextScan {
+    uint64_t n;
+    const uint32_t* key;        // sorted keys, or null (0)
+    const uint8_t* flags;
+    uint32_t mask[2];
+    int nout;
+    unsigned long long* out[2];
+    unsigned long long* tagg;   // per tile: its 2 minima
+    uint32_t T;                 // tiles
+};
+constexpr int NSC_ITEMS = 16;
+constexpr uint32_t NSC_TILE = 256 * NSC_ITEMS;
+
+// this thread's 16 items starting at p0 (a multiple of 16): values v[o][k]
+__device__ __forceinline__ void nsc_load(const NextScan& a, uint64_t p0, unsigned long long (&v)[2][NSC_ITEMS]) {
+    uint32_t kk[NSC_ITEMS];
+    uint8_t ff[NSC_ITEMS];
+    if (p0 + NSC_ITEMS <= a.n) {
+        const uint4* kp = reinterpret_cast<const uint4*>(a.key ? a.key + p0 : nullptr);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 x = a.key ? kp[q] : make_uint4(0, 0, 0, 0);
+            kk[4 * q] = x.x; kk[4 * q + 1] = x.y; kk[4 * q + 2] = x.z; kk[4 * q + 3] = x.w;
+        }
+        const uint4 f = *reinterpret_cast<const uint4*>(a.flags + p0);
+        const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+        for (int k = 0; k < NSC_ITEMS; k++) ff[k] = (uint8_t)(fw[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+        for (int k = 0; k < NSC_ITEMS; k++) {
+            const bool in = p0 + k < a.n;
+            kk[k] = (in && a.key) ? a.key[p0 + k] : 0u;
+            ff[k] = in ? a.flags[p0 + k] : (uint8_t)0;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NSC_ITEMS; k++) {
+        const uint64_t p = p0 + k;
+        const unsigned long long hi = (unsigned long long)kk[k] << PBITS;
+        const bool in = p < a.n;
+        v[0][k] = in ? (hi | ((ff[k] & a.mask[0]) ? p : MP)) : ~0ull;
+        v[1][k] = in ? (hi | ((ff[k] & a.mask[1]) ? p : MP)) : ~0ull;
+    }
 }
+// the block's minimum of (x0, x1) into s[0..1] (256 threads; ends with a barrier)
+__device__ __forceinline__ void nsc_block_min(unsigned long long x0, unsigned long long x1, unsigned long long (*s_w)[4],
+                                              unsigned long long* s) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        x0 = min(x0, (unsigned long long)__shfl_xor(x0, d, 64));
+        x1 = min(x1, (unsigned long long)__shfl_xor(x1, d, 64));
+    }
+    if (lane == 0) {
+        s_w[0][wv] = x0;
+        s_w[1][wv] = x1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s[0] = min(min(s_w[0][0], s_w[0][1]), min(s_w[0][2], s_w[0][3]));
+        s[1] = min(min(s_w[1][0], s_w[1][1]), min(s_w[1][2], s_w[1][3]));
+    }
+    __syncthreads();
+}
+__global__ void __launch_bounds__(256) k_next_reduce(NextScan a) {
+    __shared__ unsigned long long s_w[2][4], s_m[2];
+    unsigned long long v[2][NSC_ITEMS];
+    nsc_load(a, (uint64_t)blockIdx.x * NSC_TILE + (uint64_t)threadIdx.x * NSC_ITEMS, v);
+    unsigned long long m0 = ~0ull, m1 = ~0ull;
+#pragma unroll
+    for (int k = 0; k < NSC_ITEMS; k++) {
+        m0 = min(m0, v[0][k]);
+        m1 = min(m1, v[1][k]);
+    }
+    nsc_block_min(m0, m1, s_w, s_m);
+    if (threadIdx.x == 0) {
+        a.tagg[2 * blockIdx.x] = s_m[0];
+        a.tagg[2 * blockIdx.x + 1] = s_m[1];
+    }
+}
+__global__ void __launch_bounds__(256) k_next_scan(NextScan a) {
+    __shared__ unsigned long long s_w[2][4], s_suf[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t tile = blockIdx.x;
+    constexpr unsigned long long ID = ~0ull;
+    // the later tiles' minima
+    unsigned long long q0 = ID, q1 = ID;
+    for (uint32_t t = tile + 1 + tid; t < a.T; t += 256) {
+        q0 = min(q0, a.tagg[2 * t]);
+        q1 = min(q1, a.tagg[2 * t + 1]);
+    }
+    nsc_block_min(q0, q1, s_w, s_suf);
+    const uint64_t p0 = (uint64_t)tile * NSC_TILE + (uint64_t)tid * NSC_ITEMS;
+    unsigned long long v[2][NSC_ITEMS];
+    nsc_load(a, p0, v);
+    unsigned long long after[2];
+#pragma unroll
+    for (int o = 0; o < 2; o++) {
+        // suffix within the thread
+        unsigned long long run = ID;
+#pragma unroll
+        for (int k = NSC_ITEMS - 1; k >= 0; k--) {
+            run = min(run, v[o][k]);
+            v[o][k] = run;
+        }
+        // the later lanes of the wave (inclusive suffix scan, then shift by one)
+        unsigned long long incl = run;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long y = __shfl_down(incl, d, 64);
+            if (lane + d < 64) incl = min(incl, y);
+        }
+        const unsigned long long dn = __shfl_down(incl, 1, 64);
+        after[o] = lane < 63 ? dn : ID;
+        if (lane == 0) s_w[o][wv] = incl;  // (nsc_block_min's barriers are behind us)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < 2; o++) {
+        for (uint32_t q = wv + 1; q < 4; q++) after[o] = min(after[o], s_w[o][q]);
+        after[o] = min(after[o], s_suf[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < 2; o++) {
+        if (o >= a.nout) break;
+        unsigned long long* dst = a.out[o] + p0;
+        if (p0 + NSC_ITEMS <= a.n) {
+#pragma unroll
+            for (int k = 0; k < NSC_ITEMS; k += 2) {
+                ulonglong2 w;
+                w.x = min(after[o], v[o][k]);
+                w.y = min(after[o], v[o][k + 1]);
+                *reinterpret_cast<ulonglong2*>(dst + k) = w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NSC_ITEMS; k++)
+                if (p0 + k < a.n) dst[k] = min(after[o], v[o][k]);
+        }
+    }
+}
+
+// n items; `tmp` holds the tiles' minima (16 bytes a tile of 4096 items: the
+// callers pass an n x 8-byte array)
+static int next_scan(hipStream_t s, uint64_t n, const uint32_t* key, const uint8_t* flags, uint32_t m0, uint32_t m1,
+                     int nout, unsigned long long* o0, unsigned long long* o1, void* tmp) {
+    if (!n) return FLUERE_OK;
+    const uint64_t T = (n + NSC_TILE - 1) / NSC_TILE;
+    if (T >= (1u << 31)) return FLUERE_E_ARG;
+    NextScan a{};
+    a.n = n;
+    a.key = key;
+    a.flags = flags;
+    a.mask[0] = m0;
+    a.mask[1] = m1;
+    a.nout = nout;
+    a.out[0] = o0;
+    a.out[1] = o1;
+    a.tagg = (unsigned long long*)tmp;
+    a.T = (uint32_t)T;
+    k_next_reduce<<<(unsigned)T, 256, 0, s>>>(a);
+    k_next_scan<<<(unsigned)T, 256, 0, s>>>(a);
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
+}
+
 
 }  // namespace
 
@@ -365,12 +536,12 @@ struct ChaseArgs {
     const uint32_t* heads;
     const ExMeta* sm;   // sorted by (key, index)
     const uint32_t* sval;  // sorted position -> capture-order index k (Mode B: into cm)
-    const unsigned long long* ne_rev;  // scans (reversed)
+    const unsigned long long* ne_rev;  // next eligible / FIN-RST position within the key, at each position (k_next_scan)
     const unsigned long long* nf_rev;
     int mode_b;
     uint64_t timeout_us;
     const ExMeta* cm;   // capture order (Mode B sweep points)
-    const unsigned long long* np_rev;  // next processed (reversed min-scan; non-decreasing times)
+    const unsigned long long* np_rev;  // next processed packet at or after each capture position (non-decreasing times)
     const unsigned long long* tree;    // max segment tree (times that go backwards), or null
     uint64_t tree_P;
     const uint32_t* tbl;               // non-decreasing times: lower_bound of t0 + b * bw for every bucket b
@@ -449,7 +620,7 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     }
     const uint64_t k = max((uint64_t)k0, lo);
     if (k >= a.n) return NONE64;
-    const unsigned long long kp = a.np_all ? k : a.np_rev[a.n - 1 - k];
+    const unsigned long long kp = a.np_all ? k : a.np_rev[k];
     if (a.elook) {
         a.elook[c] = (uint32_t)k;
         a.ekp[c] = kp == MP ? NOPOS : (uint32_t)kp;
@@ -485,10 +656,10 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
     // shard mode: from "no flow", the lead piece [p0, min(e0, f0 + 1)) and the
     // roles of the instances (the first one, if created at or before f0, is
     // the head; the one still open at the end, after f0, the tail)
-    const unsigned long long f0 = a.nf_rev[a.n - 1 - p0] & MP;
+    const unsigned long long f0 = a.nf_rev[p0] & MP;
     int n_inst = 0;
     if (a.shard_mode) {
-        const unsigned long long e0 = a.ne_rev[a.n - 1 - p0] & MP;
+        const unsigned long long e0 = a.ne_rev[p0] & MP;
         const uint32_t lead_end = (uint32_t)min(e0 == MP ? (unsigned long long)pend : e0,
                                                 f0 == MP ? (unsigned long long)pend : f0 + 1);  // exclusive
         const uint32_t d = a.sm[p0].d;
@@ -508,13 +679,13 @@ __global__ void __launch_bounds__(64) k_ex_chase(ChaseArgs a) {
         }
     }
     while (pos < pend) {
-        const unsigned long long ce = a.ne_rev[a.n - 1 - pos] & MP;
+        const unsigned long long ce = a.ne_rev[pos] & MP;
         if (ce == MP) break;
         const uint32_t c = (uint32_t)ce;
         const ExMeta mc = a.sm[c];
         const uint32_t o = mc.dir;
         // the loads that depend on c alone, issued before the queue's stores
-        const unsigned long long fe = a.nf_rev[a.n - 1 - c] & MP;
+        const unsigned long long fe = a.nf_rev[c] & MP;
         const unsigned long long fg = fe != MP ? a.sm[fe].gidx : 0;
         unsigned long long jf = NONE64;
         uint32_t front = NOPOS;
@@ -601,7 +772,7 @@ __global__ void __launch_bounds__(256) k_ex_check(uint64_t n, const uint32_t* sf
         const uint64_t k = tree_first(tree, tree_P, L, exp_of(sm[p].t, timeout_us) + 1);
         r = k >= n ? NOPOS : (uint32_t)k;
     } else {
-        const unsigned long long kp = np_rev[n - 1 - L];
+        const unsigned long long kp = np_rev[L];
         r = kp == MP ? NOPOS : (uint32_t)kp;
     }
     if (r != ekp[p]) kdirty[hpos[p] + hf[p] - 1] = 1;
@@ -1245,11 +1416,12 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     while (end_bit < 32 && (1ull << end_bit) < J.T.fmax) end_bit++;
     tb = tmp;
     HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tp, tb, key, skey, val, sval, in, 0, end_bit, s));
-    k_ex_gather<<<gridn(n, 256), 256, 0, s>>>(n, skey, sval, cm, sm, hf, re, rf);
-    tb = tmp;
-    HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, re, ne_rev, hipcub::Min(), in, s));
-    tb = tmp;
-    HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, rf, nf_rev, hipcub::Min(), in, s));
+    // (re's space holds the sorted packets' flag bytes, rf's the scan's tile minima)
+    k_ex_gather<<<gridn(n, 256), 256, 0, s>>>(n, skey, sval, cm, sm, hf, reinterpret_cast<uint8_t*>(re));
+    {
+        int rc = next_scan(s, n, skey, reinterpret_cast<const uint8_t*>(re), 1u, 2u, 2, ne_rev, nf_rev, rf);
+        if (rc) return rc;
+    }
     tb = tmp;
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, hf, hpos, in, s));
     k_ex_heads<<<gridn(n, 256), 256, 0, s>>>(n, hf, hpos, heads);
@@ -1334,9 +1506,8 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     S->ca.np_all = J.mode_b && !fext && S->mono && S->pass_no == 0 && !pr_out ? 1 : 0;
     if (J.mode_b && !fext && !S->ca.np_all) {  // the sweep-point index over this pass's processed packets
         if (S->mono) {
-            k_ex_proc_in<<<gridn(n, 256), 256, 0, s>>>(n, S->pr, S->npr);
-            tb = S->tmp;
-            HIPCHECK(hipcub::DeviceScan::InclusiveScan(S->tp, tb, S->npr, S->np_rev, hipcub::Min(), in, s));
+            int rc = next_scan(s, n, nullptr, S->pr, 0xFFu, 0u, 1, S->np_rev, nullptr, S->npr);
+            if (rc) return rc;
         } else {
             int rc = tree_build(n, S->cm, S->pr, S->tree, S->tree_P, s);
             if (rc) return rc;

@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             }
         }
     };
-    unsigned long long cyc_flush = 0, cyc_flush0 = 0, cyc_wait = 0, cyc_start = clock64(), rt_start = wall_clock64();
+    unsigned long long cyc_flush = 0, cyc_wait = 0, cyc_start = clock64(), rt_start = wall_clock64();
     uint32_t ovf_total = 0;  // (thread 0) overflow records of every window
     auto flush = [&]() {
         // the window's partial aggregates -> this workgroup's staging set
@@ -549,7 +549,6 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
         lds_barrier();
         const unsigned long long f1 = clock64() - f0;
         if (a.dbg && tid == 0 && win == 0) a.dbg[blockIdx.x * 8 + 2] = wall_clock64();
-        if (win == 0) cyc_flush0 = f1;
         cyc_flush += f1;
         wbase += stride * WIN_ITERS;
         win++;
