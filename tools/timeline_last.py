@@ -7,8 +7,9 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 anchor = sys.argv[2] if len(sys.argv) > 2 else "k_parse_agg"
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
-if not idx:  # (a run without the hot kernel: Mode B known ahead starts with k_ex_meta)
-    idx = [i for i, r in enumerate(rows) if "k_ex_meta" in r["Kernel_Name"]]
+for alt in ("k_slow", "k_ex_meta"):  # (a pass without the hot kernel: slow-all starts with k_slow)
+    if not idx:
+        idx = [i for i, r in enumerate(rows) if alt in r["Kernel_Name"]]
 s = idx[-1]
 t0 = int(rows[s]["Start_Timestamp"])
 prev = t0
