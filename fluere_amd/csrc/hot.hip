@@ -758,9 +758,6 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 // The merge, the segments and the sets are k_parse_agg's (no partials).
 // ---------------------------------------------------------------------------
 constexpr int SPB_WORDS = 8192;  // LDS bins: 16-byte words (128 KiB), 2 per record
-__device__ __forceinline__ uint32_t own_add_n(uint32_t* arr, uint32_t o, uint32_t n) {
-    return (atomicAdd(&arr[o >> 1], n << ((o & 1) * 16)) >> ((o & 1) * 16)) & 0xFFFFu;
-}
 
 // MACS (-M): the canonical MAC pair joins the key; a record is four 16-byte
 // words -- key, MAC words + hash, payload, zero (k_parse_agg<MACS>'s spills)

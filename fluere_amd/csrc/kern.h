@@ -312,6 +312,9 @@ __device__ __forceinline__ uint32_t own_get(const uint32_t* arr, uint32_t o) {
 __device__ __forceinline__ uint32_t own_add(uint32_t* arr, uint32_t o) {
     return (atomicAdd(&arr[o >> 1], 1u << ((o & 1) * 16)) >> ((o & 1) * 16)) & 0xFFFFu;
 }
+__device__ __forceinline__ uint32_t own_add_n(uint32_t* arr, uint32_t o, uint32_t n) {
+    return (atomicAdd(&arr[o >> 1], n << ((o & 1) * 16)) >> ((o & 1) * 16)) & 0xFFFFu;
+}
 __device__ __forceinline__ void own_set(uint32_t* arr, uint32_t o, uint32_t v) {  // (no concurrent writer of the word)
     const uint32_t sh = (o & 1) * 16;
     arr[o >> 1] = (arr[o >> 1] & ~(0xFFFFu << sh)) | (v << sh);
@@ -776,7 +779,10 @@ __device__ __forceinline__ void record_of_piece(const fluere_flow_piece& f, unsi
 
 inline unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-constexpr int SB = 256;                      // k_slow block
+#ifndef FLUERE_SB
+#define FLUERE_SB 256
+#endif
+constexpr int SB = FLUERE_SB;                // k_slow block
 constexpr uint32_t SLOW_SET = SPILL_WG / 4;  // slow-list entries per k_slow workgroup (one set)
 
 // kernels of the pass launched from other translation units

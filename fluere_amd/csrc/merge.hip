@@ -764,9 +764,18 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
 // protocol 255) as its dense id from the dictionary.  k_merge_partials then
 // aggregates them with the hot kernel's partials.
 // ---------------------------------------------------------------------------
+// Records of a set's owners are staged in per-owner LDS bins (non-MAC runs;
+// SLB_WORDS 16-byte words, 2 per record): a full bin leaves as one contiguous
+// run of its owner's segment.  A record written straight to its owner
+// segment (one 32-byte store pair per packet, scattered over O segments) cost
+// ~230 us of the slow-all step (FLUERE_SLOW_ABL=3: 1.076 -> 0.691 ms).
+constexpr uint32_t SLB_WORDS = 2048;
+
 __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
     __shared__ uint32_t s_start[MB + 1];
     __shared__ uint32_t s_scnt[OWN_WORDS];  // records per owner (packed 16-bit: a set has <= SLOW_SET)
+    __shared__ uint4 s_bin[SLB_WORDS];       // per-owner bins (BINS records of 2 words each)
+    __shared__ uint32_t s_cl[SLB_WORDS / 2], s_wr[SLB_WORDS / 2];  // per bin: slots claimed / records written
     const int tid = threadIdx.x;
     const bool macs = a.macs != 0;
     const Stage& S = a.S;
@@ -774,6 +783,9 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
     const uint32_t set = S.n_hot + blockIdx.x;
     const int spu = spill_units(macs);
     for (int o = tid; o < OWN_WORDS; o += SB) s_scnt[o] = 0;
+    const uint32_t BINS = macs ? 0u : SLB_WORDS / 2 / O;  // records per bin (< 2: no bins)
+    const bool bins = BINS >= 2;
+    for (uint32_t o = tid; o < SLB_WORDS / 2; o += SB) s_cl[o] = s_wr[o] = 0;
     // the hot workgroups' regions, flattened (wave 0: an exclusive scan, an
     // even run of regions per lane)
     const uint32_t nwg = S.n_wg;  // <= MB
@@ -888,6 +900,55 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             if (gen) a.gen[b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] = gli;
         }
         if (a.slow_abl == 3) rec = false;  // diagnostics: no spill records
+        // the segment position of a record past a full segment: the overflow list below
+        auto seg_put = [&](uint32_t o, uint32_t p, const uint4& k0, const uint4& k1) -> bool {
+            if (p >= S.cap_s) return false;
+            uint4* dst = reinterpret_cast<uint4*>(S.dspill) + (S.slow_rec0 + ((size_t)blockIdx.x * O + o) * S.cap_s + p) * 2;
+            dst[0] = k0;
+            dst[1] = k1;
+            return true;
+        };
+        auto ovf_put = [&](const uint4& k0, uint4 k1) {  // (rare: a key that fills its owner's whole segment)
+            const unsigned long long b0 = atomicAdd(&a.bc[1], 1ull);
+            uint4* dst = reinterpret_cast<uint4*>(S.spill) + b0 * 2;
+            k1.w |= set << 9;
+            dst[0] = k0;
+            dst[1] = k1;
+        };
+        if (bins) {
+            // claim a bin slot, write the record, count it written; the lane that
+            // completes a bin writes it out; a lane whose bin is full retries
+            // once the completer has emptied it
+            bool pend = rec;
+            for (int it = 0; it < (1 << 16); it++) {
+                if (__ballot(pend) == 0) break;
+                uint32_t done = NONE32;
+                if (pend) {
+                    const uint32_t slot = atomicAdd(&s_cl[ow], 1u);
+                    if (slot < BINS) {
+                        uint4* b = &s_bin[(ow * BINS + slot) * 2];
+                        b[0] = wk;
+                        b[1] = wp;
+                        __threadfence_block();
+                        if (atomicAdd(&s_wr[ow], 1u) + 1 == BINS) done = ow;
+                        pend = false;
+                    }
+                }
+                if (done != NONE32) {
+                    const uint32_t p0 = own_add_n(s_scnt, done, BINS);
+                    for (uint32_t r = 0; r < BINS; r++) {
+                        const uint4 k0 = s_bin[(done * BINS + r) * 2], k1 = s_bin[(done * BINS + r) * 2 + 1];
+                        if (seg_put(done, p0 + r, k0, k1)) c_seg++;
+                        else ovf_put(k0, k1);
+                    }
+                    atomicExch(&s_wr[done], 0u);  // (this lane's reads of the bin come first: LDS order)
+                    atomicExch(&s_cl[done], 0u);
+                }
+                if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
+            }
+            if (pend) atomicOr(a.T.err, ERR_SPIN);  // (cannot happen: a full bin's completer empties it)
+            continue;
+        }
         const uint32_t pos = rec ? own_add(s_scnt, ow) : 0u;
         const bool ovf = rec && pos >= S.cap_s;
         if (rec && !ovf) {
@@ -924,6 +985,31 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         }
     }
     __syncthreads();
+    if (bins) {  // the partly filled bins
+        for (uint32_t o = tid; o < O; o += SB) {
+            const uint32_t k = s_wr[o];
+            if (!k) continue;
+            const uint32_t p0 = own_add_n(s_scnt, o, k);
+            for (uint32_t r = 0; r < k; r++) {
+                const uint4 k0 = s_bin[(o * BINS + r) * 2];
+                uint4 k1 = s_bin[(o * BINS + r) * 2 + 1];
+                if (p0 + r < S.cap_s) {
+                    uint4* dst = reinterpret_cast<uint4*>(S.dspill) +
+                                 (S.slow_rec0 + ((size_t)blockIdx.x * O + o) * S.cap_s + p0 + r) * 2;
+                    dst[0] = k0;
+                    dst[1] = k1;
+                    c_seg++;
+                } else {
+                    const unsigned long long b0 = atomicAdd(&a.bc[1], 1ull);
+                    uint4* dst = reinterpret_cast<uint4*>(S.spill) + b0 * 2;
+                    k1.w |= set << 9;
+                    dst[0] = k0;
+                    dst[1] = k1;
+                }
+            }
+        }
+        __syncthreads();
+    }
     // this set's segments: record counts, no partials, positions relative to the batch
     for (uint32_t o = tid; o <= O; o += SB) {
         S.off[(size_t)o * S.n_sets + set] = 0;
