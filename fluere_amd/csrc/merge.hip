@@ -769,7 +769,10 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
 // run of its owner's segment.  A record written straight to its owner
 // segment (one 32-byte store pair per packet, scattered over O segments) cost
 // ~230 us of the slow-all step (FLUERE_SLOW_ABL=3: 1.076 -> 0.691 ms).
-constexpr uint32_t SLB_WORDS = 2048;
+#ifndef FLUERE_SLB_WORDS
+#define FLUERE_SLB_WORDS 2048
+#endif
+constexpr uint32_t SLB_WORDS = FLUERE_SLB_WORDS;
 
 __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
     __shared__ uint32_t s_start[MB + 1];
