@@ -1104,12 +1104,12 @@ EXCHANGE_CASES = {
 }
 
 
-def _shard_exchange_rank(rank, world, port, q, case):
+def _shard_exchange_rank(rank, world, port, q, case, backend="gloo"):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         kind, n_pk, lanes, seed, t = EXCHANGE_CASES[case]
         cfg = fluere_amd.synth_cfg(kind, n_pk, lanes, seed)
@@ -1123,7 +1123,7 @@ def _shard_exchange_rank(rank, world, port, q, case):
             ctx.add_device_batch(b, nbytes, o, nb)
         torch.cuda.synchronize()
         ex = fluere_amd.dist.ShardExchange(ctx, cap=128, cap_annex=16, wire=case.endswith("_wire") or None)
-        for _ in range(2):  # the first step grows the blocks, the second reuses them (agreed on the device)
+        for _ in range(2 if backend == "gloo" else 3):  # the first step grows the blocks, the rest reuse them (agreed on the device)
             r0, w0 = ex.host_reads, ctx.host_waits()
             ex.step()
         last = (ex.device_agreed, ex.host_reads - r0, ctx.host_waits() - w0)
@@ -1167,6 +1167,35 @@ def test_shard_exchange_two_ranks_gloo(gpu, case):
         assert reads == 1 and waits == 0, (reads, waits)
     if case.startswith("udp") and not case.endswith("_wire"):
         assert agreed
+
+
+@pytest.mark.parametrize("case", ["udp", "tcp"])
+def test_shard_exchange_rccl_one_rank(gpu, case):
+    """ShardExchange over the nccl backend (RCCL) with one rank: the RCCL code
+    path of the step -- the device-agreed exchange (all_to_all_single, the
+    retry word's all_reduce) and, for realistic TCP, the host-driven one with
+    annexes -- on the card this box has (two ranks on one GPU are refused by
+    RCCL).  Records equal the oracle; the last step of the UDP capture was
+    agreed on the device with one host read."""
+    import socket
+    import torch.multiprocessing as mp
+    kind, n_pk, lanes, seed, t = EXCHANGE_CASES[case]
+    want = pyoracle.offline(fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n_pk, lanes, seed)), t)
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_shard_exchange_rank, args=(0, 1, port, q, case, "nccl"))
+    p.start()
+    csv, ne, (agreed, reads, waits) = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"ShardExchange rccl x1 {case}")
+    print(case, "device_agreed", agreed, "host reads", reads, "library waits", waits)
+    if case == "udp":
+        assert agreed and reads == 1 and waits == 0, (agreed, reads, waits)
 
 
 def test_pcapng_file_ingest(gpu, tmp_path):
