@@ -1174,8 +1174,8 @@ def test_shard_exchange_rccl_one_rank(gpu, case):
     """ShardExchange over the nccl backend (RCCL) with one rank: the RCCL code
     path of the step -- the device-agreed exchange (all_to_all_single, the
     retry word's all_reduce) and, for realistic TCP, the host-driven one with
-    annexes -- on the card this box has (two ranks on one GPU are refused by
-    RCCL).  Records equal the oracle; the last step of the UDP capture was
+    annexes -- on the one card this box has (two RCCL ranks would need two
+    devices).  Records equal the oracle; the last step of the UDP capture was
     agreed on the device with one host read."""
     import socket
     import torch.multiprocessing as mp
