@@ -10,7 +10,7 @@ same work split into phases through the FlowContext API:
   records  fluere_get_records (D2H + ordering)
   csv      fluere_write_csv
 
-  python tools/host_inclusive.py [--config c2|c3] [--packets N] [--reps R]
+  python tools/host_inclusive.py [--config c2|c3|tcp|tcp_t1] [--packets N] [--reps R]
 """
 import argparse
 import json
@@ -22,7 +22,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CONFIGS = {"c2": (0, 1000, 0xF10E0002), "c3": (1, 100_000, 0xF10E0003)}
+# (kind, flows, seed, timeout ms): bench.py's configs
+CONFIGS = {"c2": (0, 1000, 0xF10E0002, 600000), "c3": (1, 100_000, 0xF10E0003, 600000),
+           "tcp": (4, 100_000, 0xF10E0007, 600000), "tcp_t1": (4, 100_000, 0xF10E0007, 1000)}
 
 
 def main():
@@ -34,7 +36,7 @@ def main():
     import fluere_amd
     from fluere_amd import offline
 
-    kind, flows, seed = CONFIGS[args.config]
+    kind, flows, seed, timeout_ms = CONFIGS[args.config]
     cfg = fluere_amd.synth_cfg(kind, args.packets, flows, seed)
     data = fluere_amd.synth_pcap(cfg)
     tmp = tempfile.mkdtemp(prefix="fluere_hi_")
@@ -43,12 +45,13 @@ def main():
         f.write(data)
     del data
     out_dir = os.path.join(tmp, "output")
-    res = {"config": args.config, "packets": args.packets, "file_bytes": os.path.getsize(path)}
+    res = {"config": args.config, "packets": args.packets, "timeout_ms": timeout_ms, "file_bytes": os.path.getsize(path)}
     # whole call, file in the page cache (the first call also warms the runtime)
     walls = []
     for _ in range(args.reps + 1):
         t0 = time.perf_counter()
-        st = offline.fluereflow_fileparse(offline.Args(offline.Files(file=path)), out_dir=out_dir)
+        st = offline.fluereflow_fileparse(offline.Args(offline.Files(file=path), offline.Parameters(timeout=timeout_ms)),
+                                          out_dir=out_dir)
         walls.append(time.perf_counter() - t0)
     best = min(walls[1:])
     res["offline_file_s"] = round(best, 4)
@@ -57,7 +60,7 @@ def main():
     # phases
     ph = {k: [] for k in ("ingest", "run", "records", "csv")}
     for _ in range(args.reps):
-        with fluere_amd.FlowContext(max_flows=max(1 << 16, 2 * flows)) as ctx:
+        with fluere_amd.FlowContext(timeout_ms=timeout_ms, max_flows=max(1 << 16, 2 * flows, args.packets // 2 if kind == 4 else 0)) as ctx:
             t = time.perf_counter()
             ctx.add_pcap_file(path)  # file -> pinned chunks -> HBM, host-side record index
             ph["ingest"].append(time.perf_counter() - t)
