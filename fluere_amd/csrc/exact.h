@@ -121,6 +121,10 @@ struct ExactJob {
     // or null: the words also carry the merge's flows (PH_ID / PH_EREF,
     // device.h), emap its entries' dense ids (Mode A and Mode B)
     const uint32_t* emap = nullptr;
+    // or null: the hot pass's per-packet replay metadata, indexed like phash
+    // (AggArgs::exm; d == 0 marks a packet the hot parser took): k_ex_meta
+    // copies it for a packet with a merge word instead of parsing it again
+    const ExMeta* hot_meta = nullptr;
 };
 
 struct ExactResult {

@@ -106,7 +106,8 @@ constexpr uint32_t EXM_PKTS = 1024;
 constexpr int EXM_R = EXM_PKTS / 256;
 __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, int all, const uint8_t* cplx,
                                                  const uint8_t* cbits, ExMeta* meta_blk, uint32_t* bcount,
-                                                 uint64_t blk0, const uint32_t* phash, const uint32_t* emap) {
+                                                 uint64_t blk0, const uint32_t* phash, const uint32_t* emap,
+                                                 const ExMeta* hmeta) {
     __shared__ uint32_t s_c[EXM_PKTS];
     __shared__ uint32_t s_w[2][4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -159,17 +160,33 @@ __global__ void __launch_bounds__(256) k_ex_meta(Batch B, TableSet T, int macs, 
             const uint64_t li = base + s_c[i];
             const uint32_t wd = words ? phash[li] : PH_PARSE;
             const bool known = emap && wd != PH_PARSE && (wd & (PH_ID | PH_EREF));
+            // a packet the hot parser took: its metadata from the hot pass
+            // (32 bytes instead of a window and a parse)
+            bool copied = false;
+            if (known && hmeta) {
+                const ExMeta h = hmeta[li];
+                if (h.d == 0) {
+                    copied = true;
+                    const uint32_t d = ph_flow(wd, emap);
+                    if (d < T.fmax && (all || cplx[d])) {
+                        take = 1;
+                        m = h;
+                        m.d = d;
+                    }
+                }
+            }
             // the register parser first (an 80-byte window), the general one
             // only for the classes it declines
             Parsed P;
-            {
+            P.cls = 1;
+            if (!copied) {
                 const uint32_t off = B.offs[li];
                 Win W;
                 load_win(B, off, W);
                 parse_loaded_fast(B, off, W, macs != 0, P);
             }
-            if (P.cls == 2) parse_record(B, li, macs != 0, 0, P);
-            if (P.cls == 0) {
+            if (!copied && P.cls == 2) parse_record(B, li, macs != 0, 0, P);
+            if (!copied && P.cls == 0) {
                 uint8_t dir;
                 uint32_t d;
                 if (known) {  // the merge resolved this packet's flow
@@ -1335,8 +1352,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
             const uint32_t* ph = J.phash && (!J.mode_b || J.emap) ? J.phash + (B.first - J.phash_base) : nullptr;
+            const ExMeta* hm = ph && J.emap && J.hot_meta ? J.hot_meta + (B.first - J.phash_base) : nullptr;
             k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, J.mode_b, J.complex, J.cbits, meta, bcount, blk, ph,
-                                                           J.emap);
+                                                           J.emap, hm);
             blk += gridn(B.n, EXM_PKTS);
         }
     }
@@ -1689,7 +1707,7 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
             const Batch& B = J.h_batches[b];
             if (!B.n) continue;
             k_ex_meta<<<gridn(B.n, EXM_PKTS), 256, 0, s>>>(B, J.T, J.macs, 1, nullptr, nullptr, meta, bcount, blk, nullptr,
-                                                           nullptr);
+                                                           nullptr, nullptr);
             blk += gridn(B.n, EXM_PKTS);
         }
         unsigned long long last[2] = {0, 0};

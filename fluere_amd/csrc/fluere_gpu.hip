@@ -1075,10 +1075,17 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
     // Mode B predicted (the last run's): the hot pass also writes every
     // packet's replay metadata in capture order, so the exact engine skips its
     // k_ex_meta pass over the packets (used when every packet was valid and
-    // none needed the general parser; FLUERE_EXM=0: A/B)
+    // none needed the general parser; FLUERE_EXM=0: A/B).  Complex flows
+    // predicted in Mode A: the same metadata, which k_ex_meta copies for the
+    // replayed packets the hot parser took instead of parsing them again
+    // (FLUERE_EXMA=1, forced on; off by default: on the realistic TCP mix
+    // k_ex_meta went from 249 to 194 us but the hot pass's 320 MB of extra
+    // writes cost 68 us)
     {
         static const int exm_env = getenv("FLUERE_EXM") ? atoi(getenv("FLUERE_EXM")) : -1;
-        P.exm = (P.pid && P.spill && !c->use_mac && c->last_mode_b && exm_env != 0) ? 1 : 0;
+        const char* exma = getenv("FLUERE_EXMA");
+        const bool want = c->last_mode_b ? exm_env != 0 : (exma && atoi(exma) > 0);
+        P.exm = (P.pid && P.spill && !c->use_mac && want) ? 1 : 0;
         if (P.exm && c->n_total > c->exm_cap) {
             hipFree(c->d_exm);
             c->d_exm = nullptr;
@@ -1860,6 +1867,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
                 J.phash = c->d_phash;
                 J.phash_base = c->index_base;
                 J.emap = P.pid ? c->d_emap : nullptr;
+                if (P.exm && P.pid) J.hot_meta = c->d_exm;
             }
             ExactResult er{};
             if ((rc = exact_run(J, s, &er))) return rc < 0 ? rc : FLUERE_E_HIP;
@@ -1904,6 +1912,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         }
         // every packet's metadata from the hot pass (all valid, none for the general parser)
         if (P.exm && g.valid == c->n_total && g.dropped == 0 && g.n_slow == 0) J.dense_cm = c->d_exm;
+        if (P.exm && P.pid) J.hot_meta = c->d_exm;  // (k_ex_meta, when the dense path is not taken)
         J.recaux = &c->d_recaux;  // the records' order words (fetch_records orders by them)
         J.recaux_cap = &c->d_recaux_cap;
         ExactResult er{};

@@ -863,11 +863,11 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
             const uint4 w_mac = make_uint4(m0, m1, m2, hk);
             const uint32_t o = owner_of(hk, O);
             if (!MACS && a.phash && live) a.phash[li] = valid ? ckey_bucket_v4(w_key.x, w_key.y, w_key.z, h.proto) : PH_PARSE;
-            if (!MACS && a.exm && live) {  // Mode B: the exact engine's ExMeta of this packet (k_ex_meta's fields)
+            if (!MACS && a.exm && live) {  // the exact engine's ExMeta of this packet (k_ex_meta's fields)
                 ExMeta m;
                 m.t = h.t;
                 m.gidx = B.first + li;
-                m.d = 0;  // (the merge's flow word gives it)
+                m.d = valid ? 0u : FAIL;  // (the merge's flow word gives it; FAIL: not this parser's packet)
                 m.pkt = h.pkt;
                 m.doct = h.doct;
                 m.dir = gt ? 1 : 0;

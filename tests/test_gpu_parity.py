@@ -235,6 +235,23 @@ def test_merge_flow_words_realistic_tcp(gpu, pid, t, cap, monkeypatch):
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp pid={pid} t={t} cap={cap}")
 
 
+@pytest.mark.parametrize("t", [600000, 1000])
+def test_hot_metadata_copied_by_ex_meta(gpu, t, monkeypatch):
+    """Mode A with the hot pass's replay metadata (FLUERE_EXMA=1): k_ex_meta
+    copies a complex flow's packet's 32 bytes from the hot pass instead of
+    parsing it; the packets the general parser took (mutated headers inside
+    TCP flows: merge words without hot metadata) are parsed as before.  The
+    result equals the oracle."""
+    monkeypatch.setenv("FLUERE_EXMA", "1")
+    monkeypatch.setenv("FLUERE_PID", "1")
+    monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
+    data = _mutated_pcap(fluere_amd.synth_pcap(fluere_amd.synth_cfg(_lib.SYNTH_TCP, 1_000_000, 10_000, 0xF10E0061)),
+                         13, 1)
+    want = pyoracle.offline(data, t)
+    csv, ne, st = _gpu_csv(data, t, max_flows=1 << 20)
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"tcp exma t={t}")
+
+
 def test_phash_chosen_on_rerun(gpu):
     """A context whose last run replayed complex flows in Mode A writes the
     filter words on the next runs (the prediction); every run equals the oracle."""

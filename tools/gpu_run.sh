@@ -32,6 +32,10 @@ for st in "$@"; do
       c=${st#cfg:}
       timeout -k 10 240 python -u bench.py --config $c --no-cpu-baseline > "$O/bench_$c.log" 2>&1
       tail -1 "$O/bench_$c.log" | cut -c1-300 ;;
+    ecfg:*)  # ecfg:<VAR=VALUE>:<config>: cfg with one environment setting (A/B)
+      v=${st#ecfg:}; c=${v#*:}; v=${v%%:*}
+      env "$v" timeout -k 10 240 python -u bench.py --config $c --no-cpu-baseline > "$O/bench_${c}_${v%%=*}.log" 2>&1
+      tail -1 "$O/bench_${c}_${v%%=*}.log" | cut -c1-300 ;;
     cold:*)
       c=${st#cold:}
       FLUERE_HOSTPROF=1 timeout -k 10 120 python -u tools/cold_probe.py $c 3 > "$O/cold_$c.log" 2>&1
