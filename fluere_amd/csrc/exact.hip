@@ -265,17 +265,38 @@ __global__ void __launch_bounds__(256) k_ex_keys(uint64_t n, const ExMeta* cm, u
 }
 
 // ---- 2. sorted view, key heads, next-eligible / next-FIN inputs -------------
+// GATHER_ITEMS positions per thread (256 apart: coalesced), every random
+// 32-byte load issued before the first store
+#ifndef FLUERE_GATHER_ITEMS
+#define FLUERE_GATHER_ITEMS 1  // (4: 369 vs 327 us on tcp_t1 -- more loads in flight per lane did not pay)
+#endif
+constexpr uint32_t GATHER_ITEMS = FLUERE_GATHER_ITEMS;
 __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* skey, const uint32_t* sval,
-                                                   const ExMeta* cm, ExMeta* sm, uint32_t* hf, uint8_t* gbits) {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    ExMeta m = cm[sval[p]];
-    const unsigned long long d = skey[p];
-    m.d = (uint32_t)d;  // (the sort key is the flow: dense capture-order metadata carries none)
-    sm[p] = m;
-    hf[p] = (p == 0 || skey[p - 1] != skey[p]) ? 1u : 0u;
-    // the next eligible / FIN-RST scans read these flags (k_next_scan)
-    gbits[p] = m.bits;
+                                                   const ExMeta* cm, ExMeta* sm, uint32_t* hf, uint8_t* gbits,
+                                                   uint8_t* prp) {
+    const uint64_t p0 = (uint64_t)blockIdx.x * (256 * GATHER_ITEMS) + threadIdx.x;
+    uint32_t v[GATHER_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < GATHER_ITEMS; j++) {
+        const uint64_t p = p0 + j * 256;
+        v[j] = p < n ? sval[p] : 0u;
+    }
+    ExMeta m[GATHER_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < GATHER_ITEMS; j++)
+        if (p0 + j * 256 < n) m[j] = cm[v[j]];
+#pragma unroll
+    for (uint32_t j = 0; j < GATHER_ITEMS; j++) {
+        const uint64_t p = p0 + j * 256;
+        if (p >= n) break;
+        const uint32_t d = skey[p];
+        m[j].d = d;  // (the sort key is the flow: dense capture-order metadata carries none)
+        sm[p] = m[j];
+        hf[p] = (p == 0 || skey[p - 1] != d) ? 1u : 0u;
+        // the next eligible / FIN-RST scans read these flags (k_next_scan)
+        gbits[p] = m[j].bits;
+        if (prp) prp[p] = 1;  // (Mode B: the first guess, every packet processed)
+    }
 }
 
 __global__ void __launch_bounds__(256) k_ex_heads(uint64_t n, const uint32_t* hf, const uint32_t* hpos, uint32_t* heads) {
@@ -809,19 +830,22 @@ __global__ void __launch_bounds__(256) k_ex_starts(uint64_t n, const uint32_t* s
 
 // Mode B: the processed flag of each replayed packet (the members of an
 // instance are processed); *changed when the set moved (one store per wave:
-// an atomic per changed packet serialised on the one word)
+// an atomic per changed packet serialised on the one word).  The flags are
+// compared in sorted order (prp, coalesced) and only a changed one is
+// scattered to its capture position (pr[sval[p]]): reading pr at capture
+// positions cost a random line per packet.
 __global__ void __launch_bounds__(256) k_ex_members(uint64_t n, const uint32_t* incl, const uint32_t* ist,
                                                     const uint32_t* iend, const uint32_t* sval, uint8_t* pr,
-                                                    uint32_t* changed) {
+                                                    uint8_t* prp, uint32_t* changed) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool ch = false;
     if (p < n) {
         const uint32_t q1 = incl[p];  // instances starting at or before p
         const bool member = q1 > 0 && p <= iend[ist[q1 - 1]];
         const uint8_t v = member ? 1 : 0;
-        const uint32_t k = sval[p];
-        if (pr[k] != v) {
-            pr[k] = v;
+        if (prp[p] != v) {
+            prp[p] = v;
+            pr[sval[p]] = v;
             ch = true;
         }
     }
@@ -894,7 +918,17 @@ __global__ void __launch_bounds__(256) k_ex_agg(uint32_t n_inst, const uint32_t*
         if (len <= AGG_THREAD) {
             Agg a;
             agg_clear(a);
-            for (uint32_t p = c; p <= e; p++) agg_add(a, sm[p]);
+            // four records' loads in flight before the first is added (one at a
+            // time, each lane waited out a load per packet of its run)
+            uint32_t p = c;
+            for (; p + 3 <= e; p += 4) {
+                const ExMeta m0 = sm[p], m1 = sm[p + 1], m2 = sm[p + 2], m3 = sm[p + 3];
+                agg_add(a, m0);
+                agg_add(a, m1);
+                agg_add(a, m2);
+                agg_add(a, m3);
+            }
+            for (; p <= e; p++) agg_add(a, sm[p]);
             aggs[q] = a;
         } else {
             wide = len <= AGG_WAVE;
@@ -994,7 +1028,30 @@ struct RecArgs {
     const uint32_t* ikey;
     fluere_flow_annex* annex;
     const Seed* seeds;       // sharded Mode B: FluereRecord seed of each instance's creating packet
+    // every instance one record (no annex pieces): instance q's record at
+    // base0 + q (base0: the records before, known to the host), so no
+    // workgroup takes a position with an atomic on the one record counter;
+    // k_ex_records_t<true> adds the instances to it
+    int fixed;
+    uint64_t base0;
 };
+
+// fixed positions: the block's records [pos0, pos0 + EMIT_BLOCK), thread t's
+// built in S.rec[t] (S.slot[t] = 1 when it is one: the slots of instances
+// left to the general parser are skipped, the second kernel fills them),
+// written out as coalesced 8-byte words
+__device__ __forceinline__ void emit_fixed_block(EmitLds& S, fluere_record* out, uint64_t cap, bool live,
+                                                 unsigned long long pos0) {
+    S.slot[threadIdx.x] = live ? 1 : 0;
+    __syncthreads();
+    constexpr uint32_t RW = sizeof(fluere_record) / 8;
+    const unsigned long long n = pos0 < cap ? min((unsigned long long)EMIT_BLOCK, cap - pos0) : 0ull;
+    uint2* dst = reinterpret_cast<uint2*>(out + pos0);
+    const uint2* src = reinterpret_cast<const uint2*>(S.rec);
+    for (uint32_t i = threadIdx.x; i < n * RW; i += EMIT_BLOCK)
+        if (S.slot[i / RW]) dst[i] = src[i];
+    __syncthreads();
+}
 
 __device__ __forceinline__ void piece_of(const Agg& g, fluere_flow_piece& pc) {
     pc.pkts[0] = g.pk[0]; pc.pkts[1] = g.pk[1];
@@ -1023,8 +1080,14 @@ template <bool GEN>
 __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records_t(RecArgs a) {
     __shared__ EmitLds S;
     unsigned long long tot[2] = {0, 0};  // thread 0: the workgroup's updates / ended (one atomic pair at the end)
+    unsigned long long upd = 0, ended = 0;  // fixed positions: this thread's
     const uint32_t n_inst = a.p_ninst ? *a.p_ninst : a.n_inst;
     const uint32_t n_items = GEN ? min(*a.n_defer, n_inst) : n_inst;
+    if (GEN && a.fixed && blockIdx.x == 0 && threadIdx.x == 0) {  // every instance's record counted
+        const unsigned long long nok = okey_count(okey_ref(a.g), a.out_cap, a.base0, n_inst);
+        if (nok) atomicAdd(&a.g->n_okey, nok);
+        atomicAdd(&a.g->n_rec, (unsigned long long)n_inst);
+    }
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n_items; i0 += gridDim.x * blockDim.x) {  // (uniform)
         const uint32_t i = i0 + threadIdx.x;
         const bool lane_live = i < n_items;
@@ -1122,10 +1185,47 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_ex_records_t(RecArgs a) {
                     a.defer[b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] = q;
             }
         }
+        if (a.fixed) {  // (uniform) the record at base0 + q
+            const unsigned long long pos = a.base0 + q;
+            if (rec_live) {
+                const OkeyRef o = okey_ref(a.g);
+                if (okey_count(o, a.out_cap, pos, 1)) o.p[pos] = rec.order_key;
+                if (a.mode_b && a.aux && pos < a.out_cap)
+                    *reinterpret_cast<ulonglong2*>(a.aux + 2 * pos) =
+                        make_ulonglong2(kind == K_SWEEP ? cex + 1 : 0ull, kind == K_SWEEP ? cie : 0ull);
+                upd += rec.d_pkts;
+                ended += rec.order_key != NONE64 ? 1 : 0;
+            }
+            if (GEN) {  // (few: each thread its own record)
+                if (rec_live && pos < a.out_cap) {
+                    const uint2* src = reinterpret_cast<const uint2*>(&rec);
+                    uint2* dst = reinterpret_cast<uint2*>(a.out + pos);
+                    for (uint32_t k = 0; k < sizeof(fluere_record) / 8; k++) dst[k] = src[k];
+                }
+                __syncthreads();  // (S.rec[t] is rebuilt by the next item)
+            } else {
+                emit_fixed_block(S, a.out, a.out_cap, rec_live, a.base0 + i0);
+            }
+            continue;
+        }
         // (uniform: every thread of the block emits)
         emit_inplace_block(S, a.g, a.out, a.out_cap, rec_live, rec_live ? rec.d_pkts : 0u,
                            rec_live && rec.order_key != NONE64, a.mode_b ? a.aux : nullptr,
                            kind == K_SWEEP ? cex + 1 : 0ull, kind == K_SWEEP ? cie : 0ull, tot);
+    }
+    if (a.fixed) {  // the workgroup's updates / ended: one atomic pair
+        upd = wave_sum(upd);
+        ended = wave_sum(ended);
+        if ((threadIdx.x & 63) == 0) {
+            S.w[threadIdx.x >> 6][1] = upd;
+            S.w[threadIdx.x >> 6][2] = ended;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int k = 0; k < EMIT_BLOCK / 64; k++) {
+                tot[0] += S.w[k][1];
+                tot[1] += S.w[k][2];
+            }
     }
     if (threadIdx.x == 0) {
         if (tot[0]) atomicAdd(&a.g->n_updates, tot[0]);
@@ -1231,6 +1331,7 @@ struct ExactSession {
     uint32_t *val, *sval, *hf, *hpos, *heads, *link, *plink, *sflag, *iend, *incl, *ist, *alist, *ctr, *tbl;
     uint32_t *idx, *ikey;
     uint8_t *pr, *ikind, *irole;
+    uint8_t* prp;  // the processed flags by sorted position (k_ex_members' own copy of pr)
     uint8_t *stamp, *kpass, *kdirty;
     uint32_t *elook, *ekp;
     uint32_t pass_no = 0;
@@ -1263,6 +1364,7 @@ static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* 
         add(n * sizeof(Agg)); add(16);                                // aggs, nruns/counters
         add(n * 4); add(n * 8);                                       // idx, hi2 (seed requests)
         add(n); add(n * 4);                                           // irole, ikey
+        add(n);                                                       // prp
         add(n); add(n); add(n); add(n * 4); add(n * 4);               // stamp, kpass, kdirty, elook, ekp
         if (J.mode_b) add(2 * P * 8);                                 // tree
         add((n / 16 + 4) * 4);                                        // tbl
@@ -1398,6 +1500,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     S->hi2 = A.take<unsigned long long>(N);
     S->irole = A.take<uint8_t>(N);
     S->ikey = A.take<uint32_t>(N);
+    S->prp = A.take<uint8_t>(N);
     S->tree = J.mode_b ? A.take<unsigned long long>(2 * P) : nullptr;
     S->tbl = A.take<uint32_t>(N / 16 + 4);
     S->tree_P = P;
@@ -1435,7 +1538,8 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     tb = tmp;
     HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tp, tb, key, skey, val, sval, in, 0, end_bit, s));
     // (re's space holds the sorted packets' flag bytes, rf's the scan's tile minima)
-    k_ex_gather<<<gridn(n, 256), 256, 0, s>>>(n, skey, sval, cm, sm, hf, reinterpret_cast<uint8_t*>(re));
+    k_ex_gather<<<gridn(n, 256 * GATHER_ITEMS), 256, 0, s>>>(n, skey, sval, cm, sm, hf, reinterpret_cast<uint8_t*>(re),
+                                                                J.mode_b ? S->prp : nullptr);
     {
         int rc = next_scan(s, n, skey, reinterpret_cast<const uint8_t*>(re), 1u, 2u, 2, ne_rev, nf_rev, rf);
         if (rc) return rc;
@@ -1457,7 +1561,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     } else if (J.mode_b) {
         k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1);
     }
-    if (J.mode_b) HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed
+    if (J.mode_b) HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed (k_ex_gather: prp)
     // one host read: key count, monotonicity, the first and last times.  Mode
     // A (not shard mode) needs none of them on the host: the key count stays
     // on the device and the chase's grid covers the replayed packets (every
@@ -1565,7 +1669,7 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->incl, S->ist);
     HIPCHECK(hipMemsetAsync(S->ctr + 2, 0, 4, s));
     if (J.mode_b)  // the processed set (Mode A needs none: every run is a record or a piece)
-        k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->sval, S->pr, S->ctr + 2);
+        k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->sval, S->pr, S->prp, S->ctr + 2);
     HIPCHECK(hipGetLastError());
     if (pr_out) HIPCHECK(hipMemcpyAsync(pr_out, S->pr, n, hipMemcpyDeviceToDevice, s));
     if (!J.mode_b) return FLUERE_OK;
@@ -1667,6 +1771,11 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, n_inst, S->aggs, S->ist, S->sm, S->iend, S->ikind,
                S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, aux, p_ninst, S->idx, S->ctr + 3,
                J.shard_mode, S->irole, S->ikey, S->annex, seeds};
+    {
+        const char* e = getenv("FLUERE_REC_FIXED");  // (A/B)
+        ra.fixed = !J.shard_mode && !(e && atoi(e) == 0);
+        ra.base0 = n_rec0;
+    }
     // runs <= n (every run holds a packet); records appended per block, Mode B
     // with their order words (fetch_records orders them: no device sort).
     // The instances whose creating packet needs the general parser are listed

@@ -51,6 +51,10 @@ for st in "$@"; do
       c=${st#trace:}
       bash tools/trace.sh $TAG $c
       cp gpurun_out/trace_${TAG}_$c/timeline.txt "$O/timeline_$c.txt" ;;
+    etrace:*)  # etrace:<VAR=VALUE>:<config>: trace with one environment setting (A/B)
+      v=${st#etrace:}; c=${v#*:}; v=${v%%:*}
+      env "$v" bash tools/trace.sh ${TAG}_e $c
+      cp gpurun_out/trace_${TAG}_e_$c/timeline.txt "$O/timeline_${c}_${v%%=*}.txt" ;;
     vtrace:*)  # vtrace:<variant>:<config>: the kernel timeline of a variant build (tools/variants.sh)
       v=${st#vtrace:}; c=${v#*:}; v=${v%%:*}
       FLUERE_LIB=$R/fluere_amd/variants/libfluere_gpu_$v.so bash tools/trace.sh ${v} $c
