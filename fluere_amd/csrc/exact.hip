@@ -299,11 +299,6 @@ __global__ void __launch_bounds__(256) k_ex_gather(uint64_t n, const uint32_t* s
     }
 }
 
-__global__ void __launch_bounds__(256) k_ex_heads(uint64_t n, const uint32_t* hf, const uint32_t* hpos, uint32_t* heads) {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < n && hf[p]) heads[hpos[p]] = (uint32_t)p;
-}
-
 __global__ void k_ex_nkeys(const uint32_t* hpos_last, const uint32_t* hf_last, uint32_t* out) {
     if (threadIdx.x == 0) *out = *hpos_last + *hf_last;
 }
@@ -510,6 +505,103 @@ __global__ void __launch_bounds__(256) k_next_scan(NextScan a) {
                 if (p0 + k < a.n) dst[k] = min(after[o], v[o][k]);
         }
     }
+}
+
+// ---- flag counts ---------------------------------------------------------------
+// out[p] = the flags before p (exclusive) or up to p (inclusive), flags 0/1
+// words; with a list, list[c] = p for the c-th flagged position (the key
+// heads, the instance starts: the scatter the separate k_ex_heads /
+// k_ex_starts passes did).  k_next_*'s structure: a reduce, then each tile
+// adds the earlier tiles' totals itself (no look-back chain) and scans its
+// 4096 items, 16 contiguous a thread (vector loads and stores).  Replaces a
+// library scan (~50 us for 10M words) and the scatter pass (~20 us).
+__global__ void __launch_bounds__(256) k_fc_reduce(uint64_t n, const uint32_t* flags, uint32_t* tsum) {
+    __shared__ uint32_t s_w[4];
+    const uint64_t p0 = (uint64_t)blockIdx.x * NSC_TILE + (uint64_t)threadIdx.x * NSC_ITEMS;
+    uint32_t t = 0;
+    if (p0 + NSC_ITEMS <= n) {
+        const uint4* fp = reinterpret_cast<const uint4*>(flags + p0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 x = fp[q];
+            t += x.x + x.y + x.z + x.w;
+        }
+    } else {
+        for (uint64_t p = p0; p < n && p < p0 + NSC_ITEMS; p++) t += flags[p];
+    }
+    t = wave_sum(t);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) tsum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+__global__ void __launch_bounds__(256) k_fc_scan(uint64_t n, const uint32_t* flags, uint32_t* out, int inclusive,
+                                                 uint32_t* list, const uint32_t* tsum) {
+    __shared__ uint32_t s_w[4], s_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, tile = blockIdx.x;
+    // the earlier tiles' totals
+    uint32_t b = 0;
+    for (uint32_t t = tid; t < tile; t += 256) b += tsum[t];
+    b = wave_sum(b);
+    if (lane == 0) s_w[wv] = b;
+    __syncthreads();
+    if (tid == 0) s_base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    const uint64_t p0 = (uint64_t)tile * NSC_TILE + (uint64_t)tid * NSC_ITEMS;
+    uint32_t f[NSC_ITEMS];
+    const bool full = p0 + NSC_ITEMS <= n;
+    if (full) {
+        const uint4* fp = reinterpret_cast<const uint4*>(flags + p0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 x = fp[q];
+            f[4 * q] = x.x; f[4 * q + 1] = x.y; f[4 * q + 2] = x.z; f[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NSC_ITEMS; k++) f[k] = p0 + k < n ? flags[p0 + k] : 0u;
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < NSC_ITEMS; k++) run += f[k];
+    // exclusive prefix of the thread totals: within the wave, then the waves before
+    uint32_t incl = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    __syncthreads();  // (s_w's totals above are read)
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t ex = s_base + incl - run;
+    for (uint32_t q = 0; q < wv; q++) ex += s_w[q];
+    uint32_t o[NSC_ITEMS];
+#pragma unroll
+    for (int k = 0; k < NSC_ITEMS; k++) {
+        if (list && f[k] && p0 + k < n) list[ex] = (uint32_t)(p0 + k);
+        ex += f[k];
+        o[k] = inclusive ? ex : ex - f[k];
+    }
+    if (full) {
+        uint4* dp = reinterpret_cast<uint4*>(out + p0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) dp[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NSC_ITEMS; k++)
+            if (p0 + k < n) out[p0 + k] = o[k];
+    }
+}
+// tmp: a word per tile of 4096 items
+static int flag_count(hipStream_t s, uint64_t n, const uint32_t* flags, uint32_t* out, bool inclusive, uint32_t* list,
+                      void* tmp) {
+    if (!n) return FLUERE_OK;
+    const uint64_t T = (n + NSC_TILE - 1) / NSC_TILE;
+    if (T >= (1u << 31)) return FLUERE_E_ARG;
+    k_fc_reduce<<<(unsigned)T, 256, 0, s>>>(n, flags, (uint32_t*)tmp);
+    k_fc_scan<<<(unsigned)T, 256, 0, s>>>(n, flags, out, inclusive ? 1 : 0, list, (const uint32_t*)tmp);
+    HIPCHECK(hipGetLastError());
+    return FLUERE_OK;
 }
 
 // n items; `tmp` holds the tiles' minima (16 bytes a tile of 4096 items: the
@@ -823,11 +915,6 @@ __global__ void __launch_bounds__(256) k_ex_flags(uint64_t n, const uint8_t* sta
 }
 
 // ---- 5. members, processed set, reduction keys ------------------------------
-__global__ void __launch_bounds__(256) k_ex_starts(uint64_t n, const uint32_t* sflag, const uint32_t* incl, uint32_t* ist) {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < n && sflag[p]) ist[incl[p] - 1] = (uint32_t)p;
-}
-
 // Mode B: the processed flag of each replayed packet (the members of an
 // instance are processed); *changed when the set moved (one store per wave:
 // an atomic per changed packet serialised on the one word).  The flags are
@@ -1544,9 +1631,10 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         int rc = next_scan(s, n, skey, reinterpret_cast<const uint8_t*>(re), 1u, 2u, 2, ne_rev, nf_rev, rf);
         if (rc) return rc;
     }
-    tb = tmp;
-    HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, hf, hpos, in, s));
-    k_ex_heads<<<gridn(n, 256), 256, 0, s>>>(n, hf, hpos, heads);
+    {  // key positions and heads (rf: the tile totals, after next_scan's use)
+        int rc = flag_count(s, n, hf, hpos, false, heads, rf);
+        if (rc) return rc;
+    }
     HIPCHECK(hipMemsetAsync(ctr, 0, 16, s));
     // Mode B: monotonicity and the time-bucket index in one pass (a max-scan
     // of range starts, no binary searches); small runs: the two kernels
@@ -1619,8 +1707,6 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     const uint64_t n = S->n;
     if (changed) *changed = false;
     if (!n) return FLUERE_OK;
-    const int in = (int)n;
-    size_t tb;
     S->R.iterations++;
     S->ca.fext = fext;
     // the first pass guesses every replayed packet processed (exact_begin's
@@ -1664,9 +1750,10 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
         HIPCHECK(hipMemsetAsync(S->sflag, 0, n * 4, s));
         k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
     }
-    tb = S->tmp;
-    HIPCHECK(hipcub::DeviceScan::InclusiveSum(S->tp, tb, S->sflag, S->incl, in, s));
-    k_ex_starts<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->incl, S->ist);
+    {  // instance ordinals and starts (npr: the tile totals, after next_scan's use)
+        int rc = flag_count(s, n, S->sflag, S->incl, true, S->ist, S->npr);
+        if (rc) return rc;
+    }
     HIPCHECK(hipMemsetAsync(S->ctr + 2, 0, 4, s));
     if (J.mode_b)  // the processed set (Mode A needs none: every run is a record or a piece)
         k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->sval, S->pr, S->prp, S->ctr + 2);
