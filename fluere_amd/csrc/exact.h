@@ -173,4 +173,10 @@ const ExactResult& exact_result(const ExactSession* S);
 int exact_collect(const ExactJob& job, hipStream_t s, ExMeta* cm, uint64_t* n);
 void exact_free(ExactSession* S);
 
+// out[p] = the sum of flags[0..p) (or [0..p] inclusive), 32-bit words; with a
+// list, list[out_exclusive[p]] = p where flags[p] != 0 (0/1 flags).  tmp: one
+// word per 4096 items.  Stream-ordered (a reduce and a scan kernel).
+int flag_count(hipStream_t s, uint64_t n, const uint32_t* flags, uint32_t* out, bool inclusive, uint32_t* list,
+               void* tmp);
+
 }  // namespace fl

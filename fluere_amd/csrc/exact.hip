@@ -592,8 +592,8 @@ __global__ void __launch_bounds__(256) k_fc_scan(uint64_t n, const uint32_t* fla
             if (p0 + k < n) out[p0 + k] = o[k];
     }
 }
-// tmp: a word per tile of 4096 items
-static int flag_count(hipStream_t s, uint64_t n, const uint32_t* flags, uint32_t* out, bool inclusive, uint32_t* list,
+// tmp: a word per tile of 4096 items (exact.h's flag_count)
+static int fc_run(hipStream_t s, uint64_t n, const uint32_t* flags, uint32_t* out, bool inclusive, uint32_t* list,
                       void* tmp) {
     if (!n) return FLUERE_OK;
     const uint64_t T = (n + NSC_TILE - 1) / NSC_TILE;
@@ -1632,7 +1632,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         if (rc) return rc;
     }
     {  // key positions and heads (rf: the tile totals, after next_scan's use)
-        int rc = flag_count(s, n, hf, hpos, false, heads, rf);
+        int rc = fc_run(s, n, hf, hpos, false, heads, rf);
         if (rc) return rc;
     }
     HIPCHECK(hipMemsetAsync(ctr, 0, 16, s));
@@ -1751,7 +1751,7 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
         k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
     }
     {  // instance ordinals and starts (npr: the tile totals, after next_scan's use)
-        int rc = flag_count(s, n, S->sflag, S->incl, true, S->ist, S->npr);
+        int rc = fc_run(s, n, S->sflag, S->incl, true, S->ist, S->npr);
         if (rc) return rc;
     }
     HIPCHECK(hipMemsetAsync(S->ctr + 2, 0, 4, s));
@@ -1945,6 +1945,11 @@ int exact_run(const ExactJob& J, hipStream_t s, ExactResult* res) {
     if (res && S) *res = S->R;
     exact_free(S);
     return rc;
+}
+
+int flag_count(hipStream_t s, uint64_t n, const uint32_t* flags, uint32_t* out, bool inclusive, uint32_t* list,
+               void* tmp) {
+    return fc_run(s, n, flags, out, inclusive, list, tmp);
 }
 
 }  // namespace fl

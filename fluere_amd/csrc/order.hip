@@ -395,8 +395,8 @@ int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint
         k_ord_move<<<gn, 256, 0, s>>>(c->d_recs, nullptr, n, base, okey, cb, ps, nullptr, nullptr, blk_pre, n_ended,
                                       c->d_recs2, nullptr);
     } else {
-        t = tb;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, cb, ps, (int)(N + 1), s));
+        // the groups' starts (pc, unused in Mode B: the tile totals)
+        if ((rc = flag_count(s, N + 1, cb, ps, false, nullptr, pc))) return rc;
         // the largest group: a sweep that ends thousands of flows at one packet
         // (an idle gap) would make the members' rank scans quadratic
         unsigned long long g = 0;
