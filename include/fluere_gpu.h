@@ -103,7 +103,13 @@ typedef struct fluere_opts {
     void* stream;          /* hipStream_t to run on (NULL: the library creates one) */
     uint64_t timeout_ms;   /* -t (Args.parameters.timeout), default 600000 */
     int use_mac;           /* -M (Args.parameters.use_mac) */
-    uint64_t max_flows;    /* flow dictionary capacity (0: 1<<21) */
+    uint64_t max_flows;    /* initial flow dictionary capacity (0: 1<<21).  Like the
+                              reference's HashMap (offline_fluereflows.rs:61, no bound),
+                              a capture whose sampled census shows more flows grows it
+                              before its first pass, up to 2^26 (kept when HBM cannot
+                              hold the larger tables); live sessions keep it fixed, and
+                              so does FLUERE_NO_GROW=1 (then a run past it fails with
+                              FLUERE_E_TABLE_FULL) */
 } fluere_opts;
 
 typedef struct fluere_stats {
