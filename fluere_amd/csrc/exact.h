@@ -125,6 +125,9 @@ struct ExactJob {
     // (AggArgs::exm; d == 0 marks a packet the hot parser took): k_ex_meta
     // copies it for a packet with a merge word instead of parsing it again
     const ExMeta* hot_meta = nullptr;
+    // the run's flow count when the host knows it (every dense id below it),
+    // else 0 (T.fmax bounds them): the sort by flow takes only its bits
+    uint64_t key_bound = 0;
 };
 
 struct ExactResult {

@@ -1429,6 +1429,26 @@ struct ExactSession {
 
 void exact_free(ExactSession* S) { delete S; }
 
+// The replayed packets' stable sort by flow (32-bit keys of at most end_bit
+// bits, 32-bit values).  FLUERE_SORT_BITS > 0: rocprim's onesweep with that
+// many bits a pass (10: two passes for up to 20-bit flow ids, where the
+// gfx950 default of 8 takes three); 0: the library default.  The bits are
+// the run's flow count's (ExactJob::key_bound), not the table capacity's.
+#ifndef FLUERE_SORT_BITS
+#define FLUERE_SORT_BITS 10  // (tcp_t1, 20-bit flow ids: 8 bits 3 passes ~300 us, 10 bits 2 passes ~254 us, 11 bits ~271 us)
+#endif
+static hipError_t sort_by_flow(void* tmp, size_t& tb, const uint32_t* key, uint32_t* skey, const uint32_t* val,
+                               uint32_t* sval, int n, int end_bit, hipStream_t s) {
+#if FLUERE_SORT_BITS > 0
+    using OS = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
+                                                   FLUERE_SORT_BITS, rocprim::block_radix_rank_algorithm::match>;
+    using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OS>;
+    return rocprim::radix_sort_pairs<Cfg>(tmp, tb, key, skey, val, sval, (size_t)n, 0u, (unsigned)end_bit, s);
+#else
+    return hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, skey, val, sval, n, 0, end_bit, s);
+#endif
+}
+
 // The arena exact_begin lays out for a job: phase 1 over every packet, phase
 // 2 over at most every packet, and the hipCUB temp storage at that size.
 static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* tmp_out) {
@@ -1469,6 +1489,8 @@ static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* 
         tmp = std::max(tmp, t);
         (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 32, s);
+        tmp = std::max(tmp, t);
+        (void)sort_by_flow(nullptr, t, nullptr, nullptr, nullptr, nullptr, n, 32, s);
         tmp = std::max(tmp, t);
         (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                           hipcub::Min(), n, s);
@@ -1621,9 +1643,10 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     // packets (LSD radix: ceil(log2 fmax) bits, not key + index); key heads;
     // next eligible / FIN-RST
     int end_bit = 1;
-    while (end_bit < 32 && (1ull << end_bit) < J.T.fmax) end_bit++;
+    const uint64_t kb = J.key_bound ? std::min<uint64_t>(J.key_bound, J.T.fmax) : J.T.fmax;
+    while (end_bit < 32 && (1ull << end_bit) < kb) end_bit++;
     tb = tmp;
-    HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tp, tb, key, skey, val, sval, in, 0, end_bit, s));
+    HIPCHECK(sort_by_flow(tp, tb, key, skey, val, sval, in, end_bit, s));
     // (re's space holds the sorted packets' flag bytes, rf's the scan's tile minima)
     k_ex_gather<<<gridn(n, 256 * GATHER_ITEMS), 256, 0, s>>>(n, skey, sval, cm, sm, hf, reinterpret_cast<uint8_t*>(re),
                                                                 J.mode_b ? S->prp : nullptr);

@@ -1863,6 +1863,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             J.cbits = c->d_cbits;
             J.mail = c->h_mail;
             J.n_rec_known = g.n_rec;  // (g: this run's counters after finalize)
+            J.key_bound = nf;
             if (P.phash) {
                 J.phash = c->d_phash;
                 J.phash_base = c->index_base;
@@ -1905,6 +1906,7 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
         ExactJob J{c->d_batches, hb.data(), nb, T, c->use_mac, 1, timeout_us, c->d_complex, c->d_glob,
                    &c->d_recs, &c->d_recs_cap, &c->d_exact, &c->d_exact_bytes};
         J.mail = c->h_mail;
+        J.key_bound = nf;
         if (P.pid) {  // every valid packet's flow from the merge (AggArgs::pid)
             J.phash = c->d_phash;
             J.phash_base = c->index_base;
