@@ -155,6 +155,7 @@ struct fluere_ctx {
     fl::MergePending* merge_p = nullptr;
     std::chrono::steady_clock::time_point merge_t0{};
     uint64_t host_waits = 0;
+    unsigned long long* d_exm_t = nullptr;  // Mode B predicted: the packets' times beside d_exm (AggArgs::exm_t)
     ExMeta* d_exm = nullptr;         // Mode B predicted: the hot pass's per-packet replay metadata (AggArgs::exm)
     uint64_t exm_cap = 0;         // blocking host waits on the stream (ctx_sync, wait_published polls)
     bool so_next = false;            // the last run was complete with ended records: enqueue the ordering

@@ -103,6 +103,8 @@ struct ExactJob {
     // parser): no k_ex_meta pass; the flows come from the merge's words
     // (phash + emap, which must be set)
     const ExMeta* dense_cm = nullptr;
+    // or null: with dense_cm, the packets' times alone (AggArgs::exm_t)
+    const unsigned long long* dense_t = nullptr;
     // Mode A: the complex-flow filter (device.h ckey_bucket), or null
     const uint8_t* cbits = nullptr;
     // pinned mailbox for the host's scalar reads (null: copies + stream syncs)

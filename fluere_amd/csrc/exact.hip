@@ -331,18 +331,20 @@ __global__ void __launch_bounds__(256) k_ex_tindex(uint64_t n, const ExMeta* cm,
 // inclusive max-scan.  The buckets are k_ex_tindex's: t0 = t_0, nb given,
 // bw = (t_last - t0) / nb + 1 (the host computes the same from the same
 // times); with times that go backwards the index is not used.
-__global__ void __launch_bounds__(256) k_ex_tscan(uint64_t n, const ExMeta* cm, uint64_t nb, uint32_t* starts,
-                                                  uint32_t* bad) {
+__global__ void __launch_bounds__(256) k_ex_tscan(uint64_t n, const ExMeta* cm, const unsigned long long* ct,
+                                                  uint64_t nb, uint32_t* starts, uint32_t* bad) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long t0 = cm[0].t, tl = cm[n - 1].t;
+    // (ct: the times alone, 8 of every 32 bytes of cm)
+    auto tm = [&](uint64_t q) -> unsigned long long { return ct ? ct[q] : cm[q].t; };
+    const unsigned long long t0 = tm(0), tl = tm(n - 1);
     const uint64_t bw = max((uint64_t)1, (tl > t0 ? tl - t0 : 0) / nb + 1);
     auto bucket = [&](unsigned long long v) -> uint64_t { return v <= t0 ? 0 : min(nb, (uint64_t)((v - t0) / bw)); };
     bool back = false;
     if (k < n) {
-        const unsigned long long t = cm[k].t;
+        const unsigned long long t = tm(k);
         const uint64_t bk = bucket(t);
         if (k > 0) {
-            const unsigned long long tp = cm[k - 1].t;
+            const unsigned long long tp = tm(k - 1);
             back = t < tp;
             const uint64_t bp = bucket(tp);
             if (bk > bp) starts[bp + 1] = (uint32_t)k;  // buckets (bp, bk] start at k
@@ -706,6 +708,7 @@ struct ChaseArgs {
     uint32_t* ekp = nullptr;          //               the answer (capture index; NOPOS: none)
     uint32_t pass_id = 0;
     int np_all = 0;  // every replayed packet processed (the first pass's guess): next processed = itself
+    const unsigned long long* ct = nullptr;  // or null: cm's times alone (the sweep points' searches)
 };
 
 __device__ __forceinline__ unsigned long long exp_of(uint64_t t, uint64_t timeout_us) {
@@ -745,7 +748,7 @@ __device__ __forceinline__ unsigned long long sweep_point(const ChaseArgs& a, ui
     // the next processed packet
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (a.cm[mid].t < exp) lo = mid + 1;
+        if ((a.ct ? a.ct[mid] : a.cm[mid].t) < exp) lo = mid + 1;
         else hi = mid;
     }
     const uint64_t k = max((uint64_t)k0, lo);
@@ -1411,6 +1414,7 @@ struct ExactSession {
     size_t tmp = 0;
     void* tp = nullptr;
     ExMeta *cm, *sm;
+    const unsigned long long* ct = nullptr;  // or null: the replayed packets' times alone (capture order; J.dense_t)
     uint32_t *key, *skey;
     unsigned long long *re, *rf, *ne_rev, *nf_rev, *npr, *np_rev, *ej, *ij, *iie, *iex;
     unsigned long long *hi2, *tree;
@@ -1622,6 +1626,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     } else if (J.dense_cm) {  // one GPU, Mode B: the hot pass's metadata, every packet
         n = N;
         cm = S->cm = const_cast<ExMeta*>(J.dense_cm);
+        S->ct = J.dense_t;
         HIPCHECK(hipMemsetAsync(bcount, 0, 4, s));
         k_ex_pidkeys<<<gridn(n, 256), 256, 0, s>>>(n, J.phash + (J.h_batches[0].first - J.phash_base), J.emap,
                                                    J.T.fmax, key, val, bcount);
@@ -1666,7 +1671,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     if (tscan) {
         uint32_t* starts = S->idx;  // (free until the seed requests; n >= nb + 1)
         HIPCHECK(hipMemsetAsync(starts, 0, (nb_dev + 1) * 4, s));
-        k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, nb_dev, starts, ctr + 1);
+        k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, S->ct, nb_dev, starts, ctr + 1);
         tb = tmp;
         HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, starts, S->tbl, hipcub::Max(), (int)(nb_dev + 1), s));
     } else if (J.mode_b) {
@@ -1719,6 +1724,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
                       S->sflag, S->iend, S->ikind, S->ij, S->iie, S->iex, S->ej, S->link, S->plink,
                       J.shard_mode, S->irole, S->ikey, S->annex, J.annex_of, J.T.flow_key};
     if (dev_keys) S->ca.d_nkeys = ctr + 3;  // (ctr[3] is the records' defer count only after the chase)
+    S->ca.ct = S->ct;
     return FLUERE_OK;
 }
 

@@ -638,6 +638,7 @@ extern "C" int fluere_close(fluere_ctx* c) {
     sweep_free(c);
     merge_pending_free(c);
     hipFree(c->d_exm);
+    hipFree(c->d_exm_t);
     hipFree(c->d_sd);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -910,6 +911,7 @@ struct PassPlan {
     int lean_merge;  // 1: runs without partials merge their owners in k_merge_spill (0: k_merge_partials, A/B)
     int one_merge;   // 1: one k_merge_spill over every batch of the pass (after all the hot passes)
     int exm;         // 1: k_parse_spill writes every packet's ExMeta (Mode B predicted: AggArgs::exm)
+    int exm_t;       // 1: and every packet's time (AggArgs::exm_t; Mode B predicted)
     MergeSrc ms;     // the owner segments of every batch (k_merge_spill)
     int phash;     // 1: the hot pass writes the per-packet filter words (AggArgs::phash)
     int pid;       // 1: the merge writes each packet's flow over them (AggArgs::pid; k_parse_spill runs)
@@ -1086,11 +1088,16 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         const char* exma = getenv("FLUERE_EXMA");
         const bool want = c->last_mode_b ? exm_env != 0 : (exma && atoi(exma) > 0);
         P.exm = (P.pid && P.spill && !c->use_mac && want) ? 1 : 0;
+        P.exm_t = P.exm && c->last_mode_b ? 1 : 0;
         if (P.exm && c->n_total > c->exm_cap) {
             hipFree(c->d_exm);
+            hipFree(c->d_exm_t);
             c->d_exm = nullptr;
+            c->d_exm_t = nullptr;
             c->exm_cap = 0;
-            if (hipMalloc(&c->d_exm, c->n_total * sizeof(ExMeta)) != hipSuccess) return FLUERE_E_NOMEM;
+            if (hipMalloc(&c->d_exm, c->n_total * sizeof(ExMeta)) != hipSuccess ||
+                hipMalloc(&c->d_exm_t, c->n_total * 8) != hipSuccess)
+                return FLUERE_E_NOMEM;
             c->exm_cap = c->n_total;
         }
     }
@@ -1164,6 +1171,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         ab.pid_base = c->index_base;
         ab.pid_batch = (uint32_t)P.nb;
         ab.exm = P.exm ? c->d_exm + (hb.b.first - c->index_base) : nullptr;
+        ab.exm_t = P.exm_t ? c->d_exm_t + (hb.b.first - c->index_base) : nullptr;
         const size_t all = sets + n_slow_sets;
         Stage& S = ab.S;
         // layout (16-byte aligned pieces): parts | owner segments (hot, k_slow) | spill_raw | spill | base | off | soff
@@ -1913,7 +1921,10 @@ extern "C" int fluere_run(fluere_ctx* c, fluere_stats* st) {
             J.emap = c->d_emap;
         }
         // every packet's metadata from the hot pass (all valid, none for the general parser)
-        if (P.exm && g.valid == c->n_total && g.dropped == 0 && g.n_slow == 0) J.dense_cm = c->d_exm;
+        if (P.exm && g.valid == c->n_total && g.dropped == 0 && g.n_slow == 0) {
+            J.dense_cm = c->d_exm;
+            if (P.exm_t) J.dense_t = c->d_exm_t;
+        }
         if (P.exm && P.pid) J.hot_meta = c->d_exm;  // (k_ex_meta, when the dense path is not taken)
         J.recaux = &c->d_recaux;  // the records' order words (fetch_records orders by them)
         J.recaux_cap = &c->d_recaux_cap;

@@ -875,6 +875,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                 m.ttl = (uint8_t)h.ttl;
                 m.bits = (elig ? 1 : 0) | ((h.tf & 5u) ? 2 : 0);
                 a.exm[li] = m;
+                if (a.exm_t) a.exm_t[li] = h.t;
             }
             if (valid) {
                 c_valid++;

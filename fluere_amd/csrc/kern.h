@@ -187,6 +187,7 @@ struct AggArgs {
     // batch's first packet first (capture order over the capture: the exact
     // engine's k_ex_meta pass is skipped), or null
     ExMeta* exm;
+    unsigned long long* exm_t;  // or null: the packets' times alone (8 B, capture order) beside exm
     int tail_only;             // k_merge_partials: no owners (k_merge_spill merged them), only the run
                                // statistics and the tail (overflow list, general-parser packets)
     int slow_all;              // k_slow takes every packet of the batch (no hot kernel: captures of the general
