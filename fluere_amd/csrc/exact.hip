@@ -1455,7 +1455,25 @@ static hipError_t sort_by_flow(void* tmp, size_t& tb, const uint32_t* key, uint3
 
 // The arena exact_begin lays out for a job: phase 1 over every packet, phase
 // 2 over at most every packet, and the hipCUB temp storage at that size.
+static size_t arena_bytes_calc(const ExactJob& J, uint64_t N, hipStream_t s, size_t* tmp_out);
+// (the library's temp-size queries cost the host ~10 us a run, between the
+// pass and the engine's first launch: the last sizes are kept)
 static size_t arena_bytes(const ExactJob& J, uint64_t N, hipStream_t s, size_t* tmp_out) {
+    struct Memo {
+        uint64_t N;
+        int nb, mode_b;
+        size_t need, tmp;
+    };
+    static thread_local Memo memo = {~0ull, 0, 0, 0, 0};
+    if (memo.N != N || memo.nb != J.nb || memo.mode_b != J.mode_b) {
+        size_t t = 0;
+        const size_t need = arena_bytes_calc(J, N, s, &t);
+        memo = Memo{N, J.nb, J.mode_b, need, t};
+    }
+    if (tmp_out) *tmp_out = memo.tmp;
+    return memo.need;
+}
+static size_t arena_bytes_calc(const ExactJob& J, uint64_t N, hipStream_t s, size_t* tmp_out) {
     const uint64_t P = J.mode_b ? tree_leaves(N) : 1;
     // ---- arena sizing: phase 1 (all packets) + phase 2 (replayed packets, at most N)
     auto bytes_for = [&](uint64_t n_all, uint64_t n, size_t tmp) {

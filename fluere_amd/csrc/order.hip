@@ -47,6 +47,15 @@ __global__ void __launch_bounds__(256) k_ord_keys(const fluere_record* r, uint64
     __syncthreads();
     if (threadIdx.x == 0) blk_act[blockIdx.x] = s_act;
 }
+__global__ void __launch_bounds__(256) k_ord_zero(uint32_t* cb, uint64_t nk, uint32_t* gmax) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 + 4 <= nk && (nk & 3) == 0) {
+        *reinterpret_cast<uint4*>(cb + i0) = make_uint4(0, 0, 0, 0);
+    } else {
+        for (uint64_t i = i0; i < i0 + 4 && i < nk; i++) cb[i] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *gmax = 0;
+}
 __global__ void __launch_bounds__(256) k_ord_popc(const uint32_t* bits, uint64_t nw, uint32_t* pc) {
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w < nw) pc[w] = __popc(bits[w]);
@@ -372,8 +381,8 @@ int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint
     uint32_t* blk_pre = (uint32_t*)take(gn * 4);
     uint32_t* gmax = (uint32_t*)take(16);
     void* tmp = p;
-    HIPCHECK(hipMemsetAsync(cb, 0, nk * 4, s));
-    HIPCHECK(hipMemsetAsync(gmax, 0, 4, s));
+    // (one launch for both clears: each host submission here leaves the GPU idle)
+    k_ord_zero<<<(unsigned)std::max<uint64_t>(1, (nk + 1023) / 1024), 256, 0, s>>>(cb, nk, gmax);
     k_ord_keys<<<gn, 256, 0, s>>>(c->d_recs, n, base, mode_b ? 1 : 0, have_okey ? c->d_okey : nullptr, okey, cb, cb,
                                   gmax, blk);
     size_t t = tb;
