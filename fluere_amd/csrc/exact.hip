@@ -250,9 +250,9 @@ __global__ void __launch_bounds__(256) k_ex_pidkeys(uint64_t n, const uint32_t* 
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t d = k < n ? ph_flow(pid[k], emap) : 0u;
     const bool miss = k < n && (d == FAIL || d >= fmax);
-    if (__ballot(miss) && (threadIdx.x & 63) == 0) atomicAdd(bad, 1u);
+    if (bad && __ballot(miss) && (threadIdx.x & 63) == 0) atomicAdd(bad, 1u);
     if (k >= n) return;
-    key[k] = miss ? 0xFFFFFFFFu : d;
+    key[k] = miss ? 0xFFFFFFFFu : d;  // (bad null: k_ex_tscan / k_ex_mono count the misses)
     val[k] = (uint32_t)k;
 }
 
@@ -304,10 +304,12 @@ __global__ void k_ex_nkeys(const uint32_t* hpos_last, const uint32_t* hf_last, u
 }
 
 // ---- 3. Mode B: timestamps non-decreasing over the valid packets? ---------
-__global__ void __launch_bounds__(256) k_ex_mono(uint64_t n, const ExMeta* cm, uint32_t* bad) {
+__global__ void __launch_bounds__(256) k_ex_mono(uint64_t n, const ExMeta* cm, uint32_t* bad, const uint32_t* mkey,
+                                                 uint32_t* miss) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool back = k > 0 && k < n && cm[k].t < cm[k - 1].t;
     if (__ballot(back) && (threadIdx.x & 63) == 0) *bad = 1u;  // (one store per wave, not an atomic per packet)
+    if (mkey && __ballot(k < n && mkey[k] == 0xFFFFFFFFu) && (threadIdx.x & 63) == 0) *miss = 1u;  // (k_ex_tscan's)
 }
 
 // lower_bound of t0 + b * bw over the non-decreasing times, b = 0..nb
@@ -332,7 +334,8 @@ __global__ void __launch_bounds__(256) k_ex_tindex(uint64_t n, const ExMeta* cm,
 // bw = (t_last - t0) / nb + 1 (the host computes the same from the same
 // times); with times that go backwards the index is not used.
 __global__ void __launch_bounds__(256) k_ex_tscan(uint64_t n, const ExMeta* cm, const unsigned long long* ct,
-                                                  uint64_t nb, uint32_t* starts, uint32_t* bad) {
+                                                  uint64_t nb, uint32_t* starts, uint32_t* bad, const uint32_t* mkey,
+                                                  uint32_t* miss) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // (ct: the times alone, 8 of every 32 bytes of cm)
     auto tm = [&](uint64_t q) -> unsigned long long { return ct ? ct[q] : cm[q].t; };
@@ -352,6 +355,8 @@ __global__ void __launch_bounds__(256) k_ex_tscan(uint64_t n, const ExMeta* cm, 
         if (k == n - 1 && bk + 1 <= nb) starts[bk + 1] = (uint32_t)n;  // the buckets past the last time
     }
     if (__ballot(back) && (threadIdx.x & 63) == 0) *bad = 1u;
+    // (mkey: k_ex_pidkeys' keys, capture order -- a packet without a flow word)
+    if (mkey && __ballot(k < n && mkey[k] == 0xFFFFFFFFu) && (threadIdx.x & 63) == 0) *miss = 1u;
 }
 
 // ---- next-position scans --------------------------------------------------------
@@ -1645,9 +1650,9 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         n = N;
         cm = S->cm = const_cast<ExMeta*>(J.dense_cm);
         S->ct = J.dense_t;
-        HIPCHECK(hipMemsetAsync(bcount, 0, 4, s));
+        // (no counter to clear before it: k_ex_tscan / k_ex_mono count the misses)
         k_ex_pidkeys<<<gridn(n, 256), 256, 0, s>>>(n, J.phash + (J.h_batches[0].first - J.phash_base), J.emap,
-                                                   J.T.fmax, key, val, bcount);
+                                                   J.T.fmax, key, val, nullptr);
     } else {
         HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, bcount, bpos, (int)nblk, s));
         unsigned long long last[2] = {0, 0};
@@ -1689,11 +1694,12 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     if (tscan) {
         uint32_t* starts = S->idx;  // (free until the seed requests; n >= nb + 1)
         HIPCHECK(hipMemsetAsync(starts, 0, (nb_dev + 1) * 4, s));
-        k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, S->ct, nb_dev, starts, ctr + 1);
+        k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, S->ct, nb_dev, starts, ctr + 1, J.dense_cm ? key : nullptr,
+                                                 ctr + 2);
         tb = tmp;
         HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, starts, S->tbl, hipcub::Max(), (int)(nb_dev + 1), s));
     } else if (J.mode_b) {
-        k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1);
+        k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1, J.dense_cm ? key : nullptr, ctr + 2);
     }
     if (J.mode_b) HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed (k_ex_gather: prp)
     // one host read: key count, monotonicity, the first and last times.  Mode
@@ -1706,7 +1712,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     if (dev_keys) {
         k_ex_nkeys<<<1, 64, 0, s>>>(hpos + n - 1, hf + n - 1, ctr + 3);
     } else {
-        const void* src[6] = {hpos + n - 1, hf + n - 1, ctr + 1, &cm[0].t, &cm[n - 1].t, bcount};
+        const void* src[6] = {hpos + n - 1, hf + n - 1, ctr + 1, &cm[0].t, &cm[n - 1].t, ctr + 2};  // (ctr[2]: dense misses)
         const int by[6] = {4, 4, 4, 8, 8, 4};
         int rc = mail_fetch(J.mail, s, J.mode_b ? (J.dense_cm ? 6 : 5) : 2, src, by, hv);
         if (rc) return rc;
