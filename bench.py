@@ -9,9 +9,10 @@ aggregates its shard and the step adds the flow-table merge: every rank
 exports its flows into one block per owner rank, one RCCL all_to_all over
 xGMI, and each owner merges / finalizes its own flows (fluere_amd/dist.py).
 Weak scaling: every rank owns a fixed per-GPU shard of one global capture
-(packet-range sharding with global packet indices).
+(packet-range sharding with global packet indices); c4 (BASELINE configs[3],
+a fixed 100M-packet capture) scales strong: N ranks share its packets.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5u|tcp|tcp_t1|tcp_t1_backtime|slow]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c4_shard|c5|c5u|tcp|tcp_t1|tcp_t1_backtime|slow]
   torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
 """
 from __future__ import annotations
@@ -31,10 +32,15 @@ CONFIGS = {
                workload="10M x 64B UDP, 1k 5-tuples per GPU (BASELINE configs[1])"),
     "c3": dict(kind=1, per_gpu=10_000_000, flows=100_000, seed=0xF10E0003, use_mac=False,
                workload="10M IMIX 64/576/1500 TCP+UDP, 100k flows per GPU (BASELINE configs[2])"),
-    # BASELINE configs[3]: 100M IMIX packets, 1M flows over 8 GPUs; the flow
-    # count is global, so every 12.5M-packet shard sees nearly all 1M flows
-    "c4": dict(kind=1, per_gpu=12_500_000, flows=1_000_000, seed=0xF10E0004, use_mac=False,
-               workload="IMIX TCP+UDP, 12.5M packets per GPU, 1M flows in the whole capture (BASELINE configs[3])"),
+    # BASELINE configs[3]: 100M IMIX packets, 1M flows, sharded across 2/4/8
+    # GPUs -- a fixed capture (strong scaling: N ranks take 100M / N packets
+    # each); the flow count is global, so every shard sees nearly all 1M flows
+    "c4": dict(kind=1, total=100_000_000, flows=1_000_000, seed=0xF10E0004, use_mac=False,
+               workload="100M IMIX TCP+UDP packets, 1M flows, sharded over the GPUs (BASELINE configs[3])"),
+    # one 8-GPU shard of it on one GPU (the per-GPU work of c4 at N = 8; weak)
+    "c4_shard": dict(kind=1, per_gpu=12_500_000, flows=1_000_000, seed=0xF10E0004, use_mac=False,
+                     workload="IMIX TCP+UDP, 12.5M packets per GPU, 1M flows in the whole capture "
+                              "(BASELINE configs[3]'s per-GPU shard at N = 8)"),
     "c5": dict(kind=2, per_gpu=10_000_000, flows=50_000, seed=0xF10E0005, use_mac=True,
                workload="10M x 64B VLAN-tagged, 50k MAC pairs, --useMAC (BASELINE configs[4]; header-only CSV)",
                note="drop-only path: the reference's vlan_keys misparse (keys.rs:417-435) skips every frame, "
@@ -66,11 +72,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_COPY_GBS = 6290.0  # measured device copy rate (MI355X_MICROARCH.md)
 
 
+def packets_total(C, world):
+    """Packets of the whole job: a fixed capture shared by the ranks (strong,
+    c4), else the per-GPU shard times the ranks (weak)."""
+    return C["total"] if "total" in C else C["per_gpu"] * world
+
+
 def measure(name, args, world, rank, local, stream, torch, dist, fluere_amd, fdist):
     """Warmup + timed steps of one config on this rank; every rank returns its
     numbers, the max over ranks already taken for the times."""
     C = CONFIGS[name]
-    n_total = C["per_gpu"] * world
+    n_total = packets_total(C, world)
     cfg = fluere_amd.synth_cfg(C["kind"], n_total, C["flows"], C["seed"])
     first, n = fdist.shard_range(n_total, rank, world)
 
@@ -227,7 +239,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(m["ms_per_step"], 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if "total" in C else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (counter-based generator, device-resident)",

@@ -119,7 +119,7 @@ ANNEX_DTYPE = np.dtype([("key", "<u4", 14), ("flags", "<u4"), ("pad", "<u4"), ("
                         ("head", PIECE_DTYPE), ("tail", PIECE_DTYPE), ("mid_last", "<u8")])
 SHARD_HEADER_DTYPE = np.dtype([("n_flows", "<u8"), ("n_annex", "<u8"), ("tmin", "<u8"), ("tmax", "<u8"),
                                ("valid", "<u8"), ("dropped", "<u8"), ("err", "<u4"), ("shard", "<u4"),
-                               ("reserved", "<u8")])
+                               ("n_bare_complex", "<u8")])
 SHARD_HEADER_BYTES = 64  # fluere_shard_header
 SUMMARY_BYTES = SUMMARY_DTYPE.itemsize  # struct fluere_flow_summary
 assert SUMMARY_BYTES == 256 and PIECE_DTYPE.itemsize == 144 and ANNEX_DTYPE.itemsize == 512

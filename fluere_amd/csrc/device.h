@@ -77,6 +77,7 @@ struct Glob {
     unsigned long long fin_done;                          // k_finalize: workgroups finished
     unsigned long long n_fdefer;                          // k_finalize: certified flows left to k_finalize_gen
     unsigned long long n_okey;                            // emitters: order keys written beside the records
+    unsigned long long n_bare;                            // owner merge: order-dependent flows gathered without annexes
 };
 static_assert(offsetof(Glob, n_spill) == offsetof(Glob, n_slow) + 8 && offsetof(Glob, n_dspill) == offsetof(Glob, n_slow) + 16 &&
                   offsetof(Glob, n_gen) == offsetof(Glob, n_slow) + 24 && offsetof(Glob, n_owner) == offsetof(Glob, n_slow) + 32,

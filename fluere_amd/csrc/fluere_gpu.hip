@@ -321,6 +321,7 @@ __global__ void k_reset_records(Glob* g) {
     g->n_ended = 0;
     g->n_fdefer = 0;
     g->n_okey = 0;
+    g->n_bare = 0;
 }
 void reset_record_counters(fluere_ctx* c) {
     k_reset_records<<<1, 64, 0, c->stream>>>(c->d_glob);

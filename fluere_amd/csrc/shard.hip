@@ -41,6 +41,8 @@ __global__ void k_export_hdr(ExportArgs a) {
     h.tmin = g->tmin; h.tmax = g->tmax; h.valid = g->valid; h.dropped = g->dropped;
     h.err = *a.fa.T.err;
     h.shard = a.shard;
+    // (k_local_cert counted them: exported without annexes, the owner cannot compose them)
+    h.n_bare_complex = a.annex ? 0ull : g->n_complex;
     *blk_hdr(a.blocks, a.block_bytes, o) = h;
 }
 
@@ -149,6 +151,7 @@ __global__ void __launch_bounds__(256) k_merge_insert(MergeArgs a) {
         if (h->dropped) atomicAdd(&a.g->dropped, (unsigned long long)h->dropped);
         if (h->err) atomicOr(a.T.err, h->err);
         if (h->n_flows > a.cap || h->n_annex > a.cap_annex) atomicOr(a.T.err, ERR_CAPACITY);  // cut short
+        if (h->n_bare_complex) atomicAdd(&a.g->n_bare, (unsigned long long)h->n_bare_complex);
     }
     const fluere_flow_summary* sp = merge_input(a, i);
     if (!sp) {
@@ -830,12 +833,16 @@ __global__ void k_merge_counters(Glob* g, unsigned long long n_rec, unsigned lon
     g->n_ended = ended;
 }
 // 1 when the merge just enqueued cannot stand as the step's result: a block
-// was cut short (a shard had more flows for this owner than cap), a flow
-// depends on packet order (annexes needed), the span reaches the timeout (the
-// sweep composition), or the table filled
+// was cut short (a shard had more flows for this owner than cap), a shard's
+// flow depends on packet order inside the shard (its annex is needed:
+// ERR_BARE), the span reaches the timeout (the sweep composition), or the
+// table filled.  Flows that are order-free on every shard but order-dependent
+// once merged (a FIN ending shard 0's part, trailing ACKs in shard 1) need no
+// redo: merge_complete composes them from the summaries (k_compose), as after
+// the host-driven step.
 __device__ __host__ __forceinline__ bool merge_redo(const Glob& g, uint32_t err, unsigned long long timeout_us) {
     const bool expiry = g.valid && g.tmax >= g.tmin && g.tmax - g.tmin >= timeout_us;
-    return err != 0 || g.n_complex != 0 || expiry;
+    return err != 0 || g.n_bare != 0 || expiry;
 }
 __global__ void k_merge_retry(const Glob* g, const uint32_t* err, unsigned long long timeout_us,
                               unsigned long long* out) {
@@ -899,6 +906,9 @@ static int merge_complete(fluere_ctx* c, MergeArgs& ma, uint32_t seq, uint32_t n
     if (nf_err[1] & ERR_CAPACITY) return FLUERE_E_ARG;  // a shard had more flows than its block holds
     if (nf_err[1]) return FLUERE_E_TABLE_FULL;
     const bool expiry = g.valid && g.tmax >= g.tmin && g.tmax - g.tmin >= timeout_us;
+    // order-dependent shard flows without annexes cannot be composed (the sweep
+    // composition, with expiry, rebuilds every record from the packets instead)
+    if (g.n_bare && !expiry) return FLUERE_E_ARG;
     if (g.n_complex && !expiry) {
         // the order-dependent flows: compose the shards' pieces in shard order
         unsigned long long *keys = nullptr, *keys2 = nullptr;

@@ -273,7 +273,9 @@ typedef struct {
     uint64_t n_annex;           /* annexes for this owner (> cap_annex: cut short) */
     uint64_t tmin, tmax, valid, dropped;
     uint32_t err, shard;
-    uint64_t reserved;
+    uint64_t n_bare_complex;    /* order-dependent flows of this shard exported WITHOUT their annexes
+                                   (fluere_export_async): the owner cannot compose them, the step is
+                                   redone with annexes (fluere_merge_gathered_async's retry word) */
 } fluere_shard_header;          /* 64 bytes */
 
 /* Flow capacity of the context (max_flows clamped to the table size). */

@@ -163,3 +163,21 @@ def test_order_records_sweep_words():
     assert ne == 4
     assert list(recs["order_key"]) == [20, 50, 50, 50, fdist.NONE64]
     assert list(recs["first"]) == [9, 0, 2, 1, 3]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_bench_c4_is_the_fixed_100m_capture(world):
+    """bench.py --config c4 is BASELINE configs[3] as named --
+    100M IMIX packets sharded over N GPUs (strong scaling), every packet in
+    exactly one rank's shard; c4_shard keeps the 12.5M-per-GPU shard (weak)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from fluere_amd import dist as fdist
+    C = bench.CONFIGS["c4"]
+    n = bench.packets_total(C, world)
+    assert n == 100_000_000
+    assert sum(fdist.shard_range(n, r, world)[1] for r in range(world)) == n
+    assert bench.packets_total(bench.CONFIGS["c4_shard"], world) == 12_500_000 * world

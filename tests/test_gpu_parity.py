@@ -519,6 +519,77 @@ def test_sharded_device_agreed_steps(gpu, G):
         c.close()
 
 
+def _split_tcp_capture(n_flows=300, seed=5):
+    """TCP flows that are order-free inside each of two shards but
+    order-dependent once merged: SYN .. FIN as shard 0's last packets of the
+    flow, then ACKs (no SYN) in shard 1 -- and plain UDP flows beside them.
+    Returns (whole pcap, shard 0 pcap, shard 1 pcap, shard 0's packet count)."""
+    import pktbuild as pb
+    rng = np.random.default_rng(seed)
+    first, second = [], []
+
+    def frame(src, dst, l4, proto):
+        return pb.eth() + pb.ipv4(src, dst, proto, l4)
+    for f in range(n_flows):
+        a, b = f"10.1.{f // 250}.{f % 250 + 1}", f"10.2.{f // 250}.{f % 250 + 1}"
+        sp, dp = 20000 + f, 443
+        first.append(frame(a, b, pb.tcp(sp, dp, pb.SYN), 6))
+        for _ in range(int(rng.integers(0, 3))):
+            first.append(frame(b, a, pb.tcp(dp, sp, pb.ACK, b"x" * int(rng.integers(0, 40))), 6))
+        first.append(frame(a, b, pb.tcp(sp, dp, pb.FIN | pb.ACK), 6))
+        for _ in range(int(rng.integers(1, 3))):
+            second.append(frame(b, a, pb.tcp(dp, sp, pb.ACK), 6))
+        u = frame(f"10.3.{f // 250}.{f % 250 + 1}", "10.4.0.1", pb.udp(5000 + f, 53), 17)
+        (first if f % 2 else second).append(u)
+    # capture order: shard 0's packets, then shard 1's; rising timestamps
+    pk = [(1_700_000_000 + (7 * i) // 1_000_000, (7 * i) % 1_000_000, fr) for i, fr in enumerate(first + second)]
+    n0 = len(first)
+    return pb.pcap(pk), pb.pcap(pk[:n0]), pb.pcap(pk[n0:]), n0
+
+
+def test_device_agreed_merged_complex_no_redo(gpu):
+    """flows order-free on every shard but order-dependent once
+    merged (the FIN ends shard 0's part, trailing ACKs land in shard 1) are
+    composed by the owner from the summaries: the device-agreed step does not
+    ask for a redo, and its records equal the oracle's (step 2 and 3)."""
+    whole, p0, p1, n0 = _split_tcp_capture()
+    want = pyoracle.offline(whole)
+    ctxs = []
+    for first, data in ((0, p0), (n0, p1)):
+        ctx = fluere_amd.FlowContext(max_flows=1 << 16)
+        fluere_amd.dist.set_index_base(ctx, first)
+        ctx.add_host_pcap(data)
+        ctxs.append(ctx)
+    ls = fluere_amd.dist.LogicalShards(ctxs, cap=1024, cap_annex=64, wire=False)
+    for step in range(3):
+        st = ls.run()
+        recs, ne = ls.records()
+        print(f"step {step}: device_agreed {ls.device_agreed} complex {[x['complex_flows'] for x in st]}")
+        assert sum(x["complex_flows"] for x in st) > 0
+        if step:
+            assert ls.device_agreed, "merged-complex flows must not force the host-driven redo"
+        assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"merged complex step {step}")
+    for c in ctxs:
+        c.close()
+
+
+def test_device_agreed_bare_complex_redo(gpu):
+    """A shard whose flows depend on packet order inside it exports them
+    without annexes on the device-agreed step (n_bare_complex in the block
+    header): the owner asks for the redo and the host-driven step (annexes)
+    gives the oracle's records."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_TCP, 200_000, 2_000, 0xF10E0017)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    ls, ctxs = _logical_shards(cfg, 2, max_flows=1 << 18, wire=False)
+    ls._S.dev_next = True
+    st = ls.run()
+    assert not ls.device_agreed
+    recs, ne = ls.records()
+    assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], "bare complex redo")
+    for c in ctxs:
+        c.close()
+
+
 def test_sharded_cut_short_block_is_an_error(gpu):
     """A block with more flows than its capacity: the merge refuses it."""
     cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 40_000, 2000, 0xF10E0004)
