@@ -189,6 +189,8 @@ def lib() -> ctypes.CDLL:
         "fluere_wire_bound": (U64, [U64, U64]),
         "fluere_wire_pack": (I, [P, P, U32, U64, U64, P, P]),
         "fluere_wire_unpack": (I, [P, P, U32, P, U64, U64, P]),
+        "fluere_wire_pack_slots": (I, [P, P, U32, U64, U64, U64, P]),
+        "fluere_wire_unpack_slots": (I, [P, P, U32, U64, U64, U64, P]),
         "fluere_sweep_pack": (I, [P, U32, P, P]),
         "fluere_sweep_load": (I, [P, P, U32, P]),
         "fluere_sweep_index": (I, [P, P, ctypes.POINTER(U64)]),

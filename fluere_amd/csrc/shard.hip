@@ -517,7 +517,14 @@ struct WireArgs {
     unsigned long long* woff;    // [n_blocks + 1]: offset of each wire block (device)
     unsigned long long* sizes;   // pack: [n_blocks] bytes of each wire block (the caller's device buffer)
     unsigned long long off_h[WIRE_MAX_BLOCKS + 1];  // unpack: offset of each received wire block, then the end
+    // slotted form (the device-agreed step, no host-known sizes): block b in
+    // the fixed slot [b * slot, (b + 1) * slot), a 16-byte prefix {bytes,
+    // 0} before it; a block that does not fit sends only the prefix with
+    // bytes = WIRE_OVER, which the owner unpacks as a block cut short
+    uint64_t slot;               // 0: the contiguous form
 };
+constexpr unsigned long long WIRE_OVER = ~0ull;
+constexpr uint64_t WIRE_SLOT_PREFIX = 16;
 __device__ __forceinline__ uint64_t wire_table_bytes(uint64_t n) { return (4 * n + 15) & ~15ull; }
 __device__ __forceinline__ uint64_t blk_count(const uint8_t* blocks, uint64_t block_bytes, uint32_t b, uint64_t cap) {
     return min((unsigned long long)reinterpret_cast<const fluere_shard_header*>(blocks + (size_t)b * block_bytes)->n_flows,
@@ -555,11 +562,19 @@ __global__ void k_wire_offsets(WireArgs a) {
         const uint64_t rec = a.scan[(size_t)(b + 1) * a.cap] - a.scan[(size_t)b * a.cap];
         const uint64_t bytes = sizeof(fluere_shard_header) + wire_table_bytes(n) + ((rec + 15) & ~15ull) +
                                na * sizeof(fluere_flow_annex);
+        if (a.slot) {  // fixed slots: the prefix, then the block when it fits
+            const bool fits = bytes <= a.slot - WIRE_SLOT_PREFIX;
+            reinterpret_cast<unsigned long long*>(a.wwire + (size_t)b * a.slot)[0] = fits ? bytes : WIRE_OVER;
+            reinterpret_cast<unsigned long long*>(a.wwire + (size_t)b * a.slot)[1] = 0ull;
+            a.woff[b] = (unsigned long long)b * a.slot + WIRE_SLOT_PREFIX;
+            a.sizes[b] = fits ? bytes : WIRE_OVER;
+            continue;
+        }
         a.woff[b] = off;
         a.sizes[b] = bytes;
         off += bytes;
     }
-    a.woff[a.n_blocks] = off;
+    a.woff[a.n_blocks] = a.slot ? (unsigned long long)a.n_blocks * a.slot : off;
 }
 // pack 3: header, offset table and record of each summary (thread per summary slot)
 __global__ void __launch_bounds__(256) k_wire_pack(WireArgs a) {
@@ -568,6 +583,7 @@ __global__ void __launch_bounds__(256) k_wire_pack(WireArgs a) {
     const uint32_t b = (uint32_t)(i / a.cap);
     const uint64_t j = i % a.cap;
     const uint8_t* wb = a.blocks + (size_t)b * a.block_bytes;
+    if (a.slot && a.sizes[b] == WIRE_OVER) return;  // (does not fit its slot: the prefix says so)
     uint8_t* out = a.wwire + a.woff[b];
     const uint64_t n = blk_count(a.blocks, a.block_bytes, b, a.cap);
     if (j == 0) *reinterpret_cast<fluere_shard_header*>(out) = *reinterpret_cast<const fluere_shard_header*>(wb);
@@ -580,6 +596,10 @@ __global__ void __launch_bounds__(256) k_wire_pack(WireArgs a) {
 // pack 4 / unpack 2: the annexes, verbatim (thread per 16-byte word)
 __global__ void __launch_bounds__(256) k_wire_annex(WireArgs a, int unpack) {
     const uint32_t b = blockIdx.y;
+    // slotted form: the block's bytes from its prefix (WIRE_OVER: nothing sent)
+    const unsigned long long sbytes =
+        !a.slot ? 0ull : unpack ? reinterpret_cast<const unsigned long long*>(a.wire + (size_t)b * a.slot)[0] : a.sizes[b];
+    if (a.slot && sbytes == WIRE_OVER) return;
     const uint8_t* hdrp = unpack ? a.wire + a.off_h[b] : a.blocks + (size_t)b * a.block_bytes;
     const fluere_shard_header& h = *reinterpret_cast<const fluere_shard_header*>(hdrp);
     const uint64_t n = min((unsigned long long)h.n_flows, (unsigned long long)a.cap);
@@ -594,7 +614,8 @@ __global__ void __launch_bounds__(256) k_wire_annex(WireArgs a, int unpack) {
             reinterpret_cast<uint4*>(wax)[k] = reinterpret_cast<const uint4*>(wide_ax)[k];
         } else {
             // the received block's records end at the start of its annexes: total - annex bytes
-            const uint8_t* wax = a.wire + a.off_h[b + 1] - na * sizeof(fluere_flow_annex);
+            const uint8_t* wend = a.slot ? a.wire + a.off_h[b] + sbytes : a.wire + a.off_h[b + 1];
+            const uint8_t* wax = wend - na * sizeof(fluere_flow_annex);
             reinterpret_cast<uint4*>(const_cast<uint8_t*>(wide_ax))[k] = reinterpret_cast<const uint4*>(wax)[k];
         }
     }
@@ -606,8 +627,18 @@ __global__ void __launch_bounds__(256) k_wire_unpack(WireArgs a) {
     const uint32_t b = (uint32_t)(i / a.cap);
     const uint64_t j = i % a.cap;
     const uint8_t* in = a.wire + a.off_h[b];
-    const fluere_shard_header& h = *reinterpret_cast<const fluere_shard_header*>(in);
     uint8_t* wb = a.wblocks + (size_t)b * a.block_bytes;
+    if (a.slot && reinterpret_cast<const unsigned long long*>(a.wire + (size_t)b * a.slot)[0] == WIRE_OVER) {
+        // the sender's block did not fit its slot: a block cut short (the merge asks for the redo)
+        if (j == 0) {
+            fluere_shard_header h{};
+            h.n_annex = a.cap_annex + 1;  // (no summary is read; k_merge_insert flags ERR_CAPACITY)
+            h.shard = b;
+            *reinterpret_cast<fluere_shard_header*>(wb) = h;
+        }
+        return;
+    }
+    const fluere_shard_header& h = *reinterpret_cast<const fluere_shard_header*>(in);
     if (j == 0) *reinterpret_cast<fluere_shard_header*>(wb) = h;
     const uint64_t n = min((unsigned long long)h.n_flows, (unsigned long long)a.cap);
     if (j >= n) return;
@@ -755,9 +786,8 @@ extern "C" uint64_t fluere_wire_bound(uint64_t cap, uint64_t cap_annex) {
            cap_annex * sizeof(fluere_flow_annex);
 }
 
-extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uint64_t cap, uint64_t cap_annex,
-                                void* d_wire, unsigned long long* d_sizes) {
-    if (!c || !d_blocks || !d_wire || !d_sizes || !n_owners || !cap) return FLUERE_E_ARG;
+static int wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uint64_t cap, uint64_t cap_annex,
+                     void* d_wire, unsigned long long* d_sizes, uint64_t slot) {
     if (cap * WIRE_REC_MAX >= (1ull << 32)) return FLUERE_E_ARG;  // u32 record offsets within a block
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -765,7 +795,8 @@ extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(n + 1), s);
-    const size_t need = 2 * (n + 1) * 8 + (size_t)(n_owners + 1) * 8 + ((tb + 255) & ~(size_t)255);
+    // (+ n_owners words: the slotted form's block sizes when the caller has no buffer for them)
+    const size_t need = 2 * (n + 1) * 8 + (size_t)(n_owners + 1) * 8 + (size_t)n_owners * 8 + ((tb + 255) & ~(size_t)255);
     if (need > c->d_wire_tmp_bytes) {
         hipFree(c->d_wire_tmp);
         c->d_wire_tmp = nullptr;
@@ -780,12 +811,13 @@ extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_
     a.cap_annex = cap_annex;
     a.block_bytes = fluere_shard_block_bytes(cap, cap_annex);
     a.n_blocks = n_owners;
+    a.slot = slot;
     char* t = (char*)c->d_wire_tmp;
     void* tmp = t;
     a.sz = (unsigned long long*)(t + ((tb + 255) & ~(size_t)255));
     a.scan = a.sz + (n + 1);
     a.woff = a.scan + (n + 1);
-    a.sizes = d_sizes;
+    a.sizes = d_sizes ? d_sizes : a.woff + (n_owners + 1);
     k_wire_size<<<grid_for(n + 1, 256), 256, 0, s>>>(a);
     HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.sz, a.scan, (int)(n + 1), s));
     k_wire_offsets<<<1, 64, 0, s>>>(a);
@@ -796,9 +828,22 @@ extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_
     return FLUERE_OK;
 }
 
-extern "C" int fluere_wire_unpack(fluere_ctx* c, const void* d_wire, uint32_t n_shards, const uint64_t* sizes,
-                                  uint64_t cap, uint64_t cap_annex, void* d_blocks) {
-    if (!c || !d_wire || !d_blocks || !sizes || !n_shards || n_shards > WIRE_MAX_BLOCKS || !cap) return FLUERE_E_ARG;
+extern "C" int fluere_wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uint64_t cap, uint64_t cap_annex,
+                                void* d_wire, unsigned long long* d_sizes) {
+    if (!c || !d_blocks || !d_wire || !d_sizes || !n_owners || !cap) return FLUERE_E_ARG;
+    return wire_pack(c, d_blocks, n_owners, cap, cap_annex, d_wire, d_sizes, 0);
+}
+
+extern "C" int fluere_wire_pack_slots(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uint64_t cap,
+                                      uint64_t cap_annex, uint64_t slot_bytes, void* d_slots) {
+    if (!c || !d_blocks || !d_slots || !n_owners || !cap || slot_bytes < WIRE_SLOT_PREFIX + sizeof(fluere_shard_header) ||
+        slot_bytes % 16)
+        return FLUERE_E_ARG;
+    return wire_pack(c, d_blocks, n_owners, cap, cap_annex, d_slots, nullptr, slot_bytes);
+}
+
+static int wire_unpack(fluere_ctx* c, const void* d_wire, uint32_t n_shards, const uint64_t* sizes, uint64_t slot,
+                       uint64_t cap, uint64_t cap_annex, void* d_blocks) {
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     WireArgs a{};
@@ -808,19 +853,38 @@ extern "C" int fluere_wire_unpack(fluere_ctx* c, const void* d_wire, uint32_t n_
     a.cap_annex = cap_annex;
     a.block_bytes = fluere_shard_block_bytes(cap, cap_annex);
     a.n_blocks = n_shards;
+    a.slot = slot;
     unsigned long long off = 0;
     for (uint32_t b = 0; b < n_shards; b++) {
+        if (slot) {
+            a.off_h[b] = (unsigned long long)b * slot + WIRE_SLOT_PREFIX;
+            continue;
+        }
         if (sizes[b] < sizeof(fluere_shard_header)) return FLUERE_E_ARG;
         a.off_h[b] = off;
         off += sizes[b];
     }
-    a.off_h[n_shards] = off;
+    a.off_h[n_shards] = slot ? (unsigned long long)n_shards * slot : off;
     const uint64_t n = (uint64_t)n_shards * cap;
     k_wire_unpack<<<grid_for(n, 256), 256, 0, s>>>(a);
     const unsigned ax = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(64, cap_annex * 32 / 256));
     k_wire_annex<<<dim3(ax, n_shards), 256, 0, s>>>(a, 1);
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
+}
+
+extern "C" int fluere_wire_unpack(fluere_ctx* c, const void* d_wire, uint32_t n_shards, const uint64_t* sizes,
+                                  uint64_t cap, uint64_t cap_annex, void* d_blocks) {
+    if (!c || !d_wire || !d_blocks || !sizes || !n_shards || n_shards > WIRE_MAX_BLOCKS || !cap) return FLUERE_E_ARG;
+    return wire_unpack(c, d_wire, n_shards, sizes, 0, cap, cap_annex, d_blocks);
+}
+
+extern "C" int fluere_wire_unpack_slots(fluere_ctx* c, const void* d_slots, uint32_t n_shards, uint64_t slot_bytes,
+                                        uint64_t cap, uint64_t cap_annex, void* d_blocks) {
+    if (!c || !d_slots || !d_blocks || !n_shards || n_shards > WIRE_MAX_BLOCKS || !cap ||
+        slot_bytes < WIRE_SLOT_PREFIX + sizeof(fluere_shard_header) || slot_bytes % 16)
+        return FLUERE_E_ARG;
+    return wire_unpack(c, d_slots, n_shards, nullptr, slot_bytes, cap, cap_annex, d_blocks);
 }
 
 // the run counters the owner merge starts from (the records this rank's

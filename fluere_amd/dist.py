@@ -40,6 +40,8 @@ SPAN_BIAS = 1 << 62  # fluere_export_async d_info[4] = SPAN_BIAS - earliest vali
 # (fluere_wire_pack / fluere_wire_unpack): variable-length summaries, split
 # sizes exact per owner; smaller ones go as equal wide blocks (one fewer pass)
 WIRE_MIN_BLOCK = 1 << 20
+WIRE_SLOT_PREFIX = 16       # fluere_wire_pack_slots: the size word before each slot's block
+WIRE_SLOT_HEADROOM = 1 / 16  # slot = largest block of the last host-driven step + this share
 
 
 def shard_range(n_packets: int, rank: int, world: int):
@@ -425,6 +427,11 @@ class _StepState:
         self.dev_next = False
         self.flags = None
         self.device_agreed = False  # the last step was the device-agreed one
+        # the device-agreed step's wire slots (fluere_wire_pack_slots): bytes
+        # per owner, sized from the last host-driven wire step's largest block
+        # (+ WIRE_SLOT_HEADROOM); 0 until a host-driven step used the wire
+        self.wslot = 0
+        self.wslot_sends = self.wslot_recvs = None
 
 
 def _ensure_blocks(S: _StepState, n_ctx: int, W: int, blk: int):
@@ -454,10 +461,26 @@ def _shard_step_dev(comm, ctxs, S: _StepState):
         S.infos = [torch.zeros(6, dtype=torch.int64, device="cuda") for _ in ctxs]
     if S.flags is None or len(S.flags) != len(ctxs):
         S.flags = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in ctxs]
+    # the compact wire encoding in fixed slots when the blocks are large (the
+    # host-driven step's rule), sized by the last host-driven wire step
+    wire = (blk >= WIRE_MIN_BLOCK) if S.wire is None else bool(S.wire)
+    slot = S.wslot if wire else 0
     for c, rk, s, info in zip(ctxs, comm.ranks, S.sends, S.infos):
         check(L.fluere_export_async(c._h, s.data_ptr(), W, rk, S.cap, S.cap_annex, info.data_ptr()),
               "fluere_export_async")
-    comm.all_to_all_equal(S.sends, S.recvs)
+    if slot:
+        if S.wslot_sends is None or S.wslot_sends[0].numel() != W * slot or len(S.wslot_sends) != len(ctxs):
+            S.wslot_sends = [torch.empty(W * slot, dtype=torch.uint8, device="cuda") for _ in ctxs]
+            S.wslot_recvs = [torch.empty(W * slot, dtype=torch.uint8, device="cuda") for _ in ctxs]
+        for c, s, ws in zip(ctxs, S.sends, S.wslot_sends):
+            check(L.fluere_wire_pack_slots(c._h, s.data_ptr(), W, S.cap, S.cap_annex, slot, ws.data_ptr()),
+                  "fluere_wire_pack_slots")
+        comm.all_to_all_equal(S.wslot_sends, S.wslot_recvs)
+        for c, wr, r in zip(ctxs, S.wslot_recvs, S.recvs):
+            check(L.fluere_wire_unpack_slots(c._h, wr.data_ptr(), W, slot, S.cap, S.cap_annex, r.data_ptr()),
+                  "fluere_wire_unpack_slots")
+    else:
+        comm.all_to_all_equal(S.sends, S.recvs)
     for c, r, f in zip(ctxs, S.recvs, S.flags):
         check(L.fluere_merge_gathered_async(c._h, r.data_ptr(), W, S.cap, S.cap_annex, f.data_ptr()),
               "fluere_merge_gathered_async")
@@ -475,8 +498,8 @@ def _shard_step_dev(comm, ctxs, S: _StepState):
         stats.append(d)
     if redo:
         return None
-    S.wire_used = False
-    S.bytes_sent = (W - 1) * blk
+    S.wire_used = bool(slot)
+    S.bytes_sent = (W - 1) * (slot if slot else blk)
     return stats
 
 
@@ -484,7 +507,9 @@ def _shard_step(comm, ctxs, S: _StepState, rank_first_fn):
     """One sharded pass over every local context: the device-agreed step
     when the last step allows it (_shard_step_dev), else -- or when it asks
     for a redo -- the host-driven one."""
-    if S.dev_next and S.wire is not True:
+    blk = int(_lib.lib().fluere_shard_block_bytes(S.cap, S.cap_annex))
+    wire = (blk >= WIRE_MIN_BLOCK) if S.wire is None else bool(S.wire)
+    if S.dev_next and (not wire or S.wslot):
         stats = _shard_step_dev(comm, ctxs, S)
         if stats is not None:
             S.device_agreed = True
@@ -564,6 +589,9 @@ def _shard_step_host(comm, ctxs, S: _StepState, rank_first_fn):
             check(L.fluere_wire_unpack(c._h, wr.data_ptr(), W, _arr(rs), S.cap, S.cap_annex, r.data_ptr()),
                   "fluere_wire_unpack")
         S.bytes_sent = int(sizes[rks[0]].sum() - sizes[rks[0], rks[0]])
+        # the next device-agreed step's fixed slots: this step's largest block + headroom
+        big = int(sizes.max()) + WIRE_SLOT_PREFIX
+        S.wslot = (big + int(big * WIRE_SLOT_HEADROOM) + 255) // 256 * 256
     else:
         S.bytes_sent = (W - 1) * blk
         comm.all_to_all_equal(S.sends, S.recvs)

@@ -353,6 +353,17 @@ int fluere_wire_pack(fluere_ctx* ctx, const void* d_blocks, uint32_t n_owners, u
                      void* d_wire, unsigned long long* d_sizes);
 int fluere_wire_unpack(fluere_ctx* ctx, const void* d_wire, uint32_t n_shards, const uint64_t* sizes, uint64_t cap,
                        uint64_t cap_annex, void* d_blocks);
+/* The same in fixed slots, for the device-agreed step (no split sizes on the
+ * host): block b of d_slots (n x slot_bytes, slot_bytes a multiple of 16) in
+ * [b * slot_bytes, (b + 1) * slot_bytes) behind a 16-byte prefix holding its
+ * bytes; a block that does not fit sends only the prefix (bytes = UINT64_MAX),
+ * and its owner unpacks it as a block cut short (the merge's retry word asks
+ * for the redo).  The caller sizes the slots from the last host-driven step's
+ * wire sizes; the all-to-all moves equal slot_bytes blocks. */
+int fluere_wire_pack_slots(fluere_ctx* ctx, const void* d_blocks, uint32_t n_owners, uint64_t cap, uint64_t cap_annex,
+                           uint64_t slot_bytes, void* d_slots);
+int fluere_wire_unpack_slots(fluere_ctx* ctx, const void* d_slots, uint32_t n_shards, uint64_t slot_bytes, uint64_t cap,
+                             uint64_t cap_annex, void* d_blocks);
 
 /* ---- the hard-timeout sweep across shards (offline_fluereflows.rs:103-119,
  * 161-175): an expiry entry pushed at a flow's creation fires at the first

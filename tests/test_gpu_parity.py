@@ -519,6 +519,27 @@ def test_sharded_device_agreed_steps(gpu, G):
         c.close()
 
 
+def test_device_agreed_wire_slots(gpu):
+    """The device-agreed step with the wire encoding in fixed slots (sized by
+    the last host-driven step): records equal the oracle's; a slot too small
+    for a block sends only its size word, the owner sees a block cut short and
+    the step is redone host-driven (which sizes the slots again)."""
+    cfg = fluere_amd.synth_cfg(_lib.SYNTH_IMIX, 160_000, 4000, 0xF10E0004)
+    want = pyoracle.offline(fluere_amd.synth_pcap(cfg))
+    ls, ctxs = _logical_shards(cfg, 3, cap=64, cap_annex=8, wire=True)
+    for step in range(4):
+        if step == 2:
+            ls._S.wslot = 256  # too small for any block: every slot overflows
+        ls.run()
+        print(f"step {step}: device_agreed {ls.device_agreed} wire {ls.wire_used} slot {ls._S.wslot} sent {ls.bytes_sent}")
+        assert ls.wire_used
+        assert ls.device_agreed == (step in (1, 3))
+        recs, ne = ls.records()
+        assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"wire slots step {step}")
+    for c in ctxs:
+        c.close()
+
+
 def _split_tcp_capture(n_flows=300, seed=5):
     """TCP flows that are order-free inside each of two shards but
     order-dependent once merged: SYN .. FIN as shard 0's last packets of the
@@ -1162,14 +1183,25 @@ def test_c4_recipe_8_shards_1m_flows(gpu, G):
     cap = 1 << max(17, (int(1.3e6 / G) - 1).bit_length())
     ls, ctxs = _logical_shards(cfg, G, max_flows=1 << 21, cap=cap, cap_annex=1 << 10)
     st = ls.run()
-    recs, ne = ls.records()
-    for c in ctxs:
-        c.close()
+    assert not ls.device_agreed
+    host_bytes = ls.bytes_sent
     # the compact wire encoding (32 MiB blocks): at least 2.5x fewer bytes than
     # the equal wide blocks would move
     wide = (G - 1) * _lib.lib().fluere_shard_block_bytes(ls.cap, ls.cap_annex)
     print(f"c4 recipe, {G} shards: shard 0 sent {ls.bytes_sent} B (wide blocks: {wide} B, {wide / ls.bytes_sent:.2f}x)")
     assert ls.wire_used and ls.bytes_sent * 2.5 <= wide
+    # the second step is agreed on the device and keeps the wire encoding, in
+    # fixed slots sized by the first (VERDICT r5 #4a): one host read,
+    # at most 1.1x the host-driven step's bytes
+    r0 = ls.host_reads
+    ls.run()
+    print(f"  device-agreed step: {ls.bytes_sent} B ({ls.bytes_sent / host_bytes:.3f}x), host reads {ls.host_reads - r0}")
+    assert ls.device_agreed and ls.wire_used
+    assert ls.host_reads - r0 == 1
+    assert ls.bytes_sent <= 1.1 * host_bytes
+    recs, ne = ls.records()
+    for c in ctxs:
+        c.close()
     assert len(recs) == 1_000_000
     assert int(recs["d_pkts"].sum()) == cfg.n_packets
     if "want" not in _C4_WANT:  # (one oracle run for the three splits)
@@ -1249,11 +1281,12 @@ def test_shard_exchange_two_ranks_gloo(gpu, case):
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], f"ShardExchange gloo x2 {case}")
     # the second step: agreed on the device with one host read (the reduced
     # retry word) and no library wait -- unless the capture needs annexes
-    # (order-dependent flows) or the sweep, or the wire encoding is forced
+    # (order-dependent flows) or the sweep; the wire encoding travels in fixed
+    # slots sized by the first step (fluere_wire_pack_slots)
     print(case, "device_agreed", agreed, "host reads", reads, "library waits", waits)
     if agreed:
         assert reads == 1 and waits == 0, (reads, waits)
-    if case.startswith("udp") and not case.endswith("_wire"):
+    if case.startswith("udp"):
         assert agreed
 
 
