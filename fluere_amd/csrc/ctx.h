@@ -154,10 +154,11 @@ struct fluere_ctx {
     // the owner merge of the device-agreed sharded step (shard.hip)
     fl::MergePending* merge_p = nullptr;
     std::chrono::steady_clock::time_point merge_t0{};
-    uint64_t host_waits = 0;
+    uint64_t host_waits = 0;                    // blocking host waits on the stream (ctx_sync, wait_published polls)
     unsigned long long* d_exm_t = nullptr;  // Mode B predicted: the packets' times beside d_exm (AggArgs::exm_t)
     ExMeta* d_exm = nullptr;         // Mode B predicted: the hot pass's per-packet replay metadata (AggArgs::exm)
-    uint64_t exm_cap = 0;         // blocking host waits on the stream (ctx_sync, wait_published polls)
+    uint64_t exm_t_cap = 0;       // packets d_exm_t holds
+    uint64_t exm_cap = 0;         // packets d_exm holds
     bool so_next = false;            // the last run was complete with ended records: enqueue the ordering
     uint64_t so_last_n = 0, so_last_ne = 0;
 };

@@ -44,7 +44,7 @@
 // (fluere_gpu.hip, fluere_sweep_*).
 #include "exact.h"
 
-#include <hipcub/hipcub.hpp>
+#include "prim.h"
 
 #include <algorithm>
 #include <vector>
@@ -452,18 +452,82 @@ __global__ void __launch_bounds__(256) k_next_reduce(NextScan a) {
         a.tagg[2 * blockIdx.x + 1] = s_m[1];
     }
 }
+// The tiles' totals scanned once, by one workgroup (each tile used
+// to combine every earlier / later tile's total itself, O(T^2) loads -- ~300M
+// at 100M items): each thread folds a contiguous run of tiles, the runs'
+// results are scanned across the block, then written back in place.
+constexpr int TSC_B = 1024;
+// tsum[t] <- the sum of tsum[0 .. t) (exclusive prefix, in place)
+__global__ void __launch_bounds__(TSC_B) k_tile_prefix(uint32_t* tsum, uint32_t T) {
+    __shared__ uint32_t s_w[TSC_B / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t per = (T + TSC_B - 1) / TSC_B, t0 = tid * per, t1 = min(T, t0 + per);
+    uint32_t run = 0;
+    for (uint32_t t = t0; t < t1; t++) run += tsum[t];
+    uint32_t incl = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t ex = incl - run;
+    for (uint32_t q = 0; q < wv; q++) ex += s_w[q];
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t v = tsum[t];
+        tsum[t] = ex;
+        ex += v;
+    }
+}
+// tagg[2t + o] <- the minimum of tagg[2u + o] over u > t (exclusive suffix, in place)
+__global__ void __launch_bounds__(TSC_B) k_tile_suffix_min(unsigned long long* tagg, uint32_t T) {
+    __shared__ unsigned long long s_w[2][TSC_B / 64];
+    constexpr unsigned long long ID = ~0ull;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t per = (T + TSC_B - 1) / TSC_B, t0 = tid * per, t1 = min(T, t0 + per);
+    unsigned long long run[2] = {ID, ID}, incl[2], after[2];
+    for (uint32_t t = t0; t < t1; t++) {
+        run[0] = min(run[0], tagg[2 * t]);
+        run[1] = min(run[1], tagg[2 * t + 1]);
+    }
+#pragma unroll
+    for (int o = 0; o < 2; o++) {
+        incl[o] = run[o];  // inclusive suffix over the lanes, then the later waves
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long y = __shfl_down(incl[o], d, 64);
+            if (lane + d < 64) incl[o] = min(incl[o], y);
+        }
+        const unsigned long long dn = __shfl_down(incl[o], 1, 64);
+        after[o] = lane < 63 ? dn : ID;
+        if (lane == 0) s_w[o][wv] = incl[o];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < 2; o++)
+        for (uint32_t q = wv + 1; q < TSC_B / 64; q++) after[o] = min(after[o], s_w[o][q]);
+    for (uint32_t t = t1; t-- > t0;) {
+        const unsigned long long v0 = tagg[2 * t], v1 = tagg[2 * t + 1];
+        tagg[2 * t] = after[0];
+        tagg[2 * t + 1] = after[1];
+        after[0] = min(after[0], v0);
+        after[1] = min(after[1], v1);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_next_scan(NextScan a) {
-    __shared__ unsigned long long s_w[2][4], s_suf[2];
+    __shared__ unsigned long long s_suf[2];
+    __shared__ unsigned long long s_w[2][4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t tile = blockIdx.x;
     constexpr unsigned long long ID = ~0ull;
-    // the later tiles' minima
-    unsigned long long q0 = ID, q1 = ID;
-    for (uint32_t t = tile + 1 + tid; t < a.T; t += 256) {
-        q0 = min(q0, a.tagg[2 * t]);
-        q1 = min(q1, a.tagg[2 * t + 1]);
+    // the later tiles' minima (k_tile_suffix_min)
+    if (tid == 0) {
+        s_suf[0] = a.tagg[2 * tile];
+        s_suf[1] = a.tagg[2 * tile + 1];
     }
-    nsc_block_min(q0, q1, s_w, s_suf);
+    __syncthreads();
     const uint64_t p0 = (uint64_t)tile * NSC_TILE + (uint64_t)tid * NSC_ITEMS;
     unsigned long long v[2][NSC_ITEMS];
     nsc_load(a, p0, v);
@@ -543,16 +607,10 @@ __global__ void __launch_bounds__(256) k_fc_reduce(uint64_t n, const uint32_t* f
 }
 __global__ void __launch_bounds__(256) k_fc_scan(uint64_t n, const uint32_t* flags, uint32_t* out, int inclusive,
                                                  uint32_t* list, const uint32_t* tsum) {
-    __shared__ uint32_t s_w[4], s_base;
+    __shared__ uint32_t s_w[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, tile = blockIdx.x;
-    // the earlier tiles' totals
-    uint32_t b = 0;
-    for (uint32_t t = tid; t < tile; t += 256) b += tsum[t];
-    b = wave_sum(b);
-    if (lane == 0) s_w[wv] = b;
-    __syncthreads();
-    if (tid == 0) s_base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    __syncthreads();
+    // the earlier tiles' totals (k_tile_prefix)
+    const uint32_t s_base = tsum[tile];
     const uint64_t p0 = (uint64_t)tile * NSC_TILE + (uint64_t)tid * NSC_ITEMS;
     uint32_t f[NSC_ITEMS];
     const bool full = p0 + NSC_ITEMS <= n;
@@ -606,6 +664,7 @@ static int fc_run(hipStream_t s, uint64_t n, const uint32_t* flags, uint32_t* ou
     const uint64_t T = (n + NSC_TILE - 1) / NSC_TILE;
     if (T >= (1u << 31)) return FLUERE_E_ARG;
     k_fc_reduce<<<(unsigned)T, 256, 0, s>>>(n, flags, (uint32_t*)tmp);
+    k_tile_prefix<<<1, TSC_B, 0, s>>>((uint32_t*)tmp, (uint32_t)T);
     k_fc_scan<<<(unsigned)T, 256, 0, s>>>(n, flags, out, inclusive ? 1 : 0, list, (const uint32_t*)tmp);
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
@@ -630,6 +689,7 @@ static int next_scan(hipStream_t s, uint64_t n, const uint32_t* key, const uint8
     a.tagg = (unsigned long long*)tmp;
     a.T = (uint32_t)T;
     k_next_reduce<<<(unsigned)T, 256, 0, s>>>(a);
+    k_tile_suffix_min<<<1, TSC_B, 0, s>>>(a.tagg, a.T);
     k_next_scan<<<(unsigned)T, 256, 0, s>>>(a);
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
@@ -1466,12 +1526,12 @@ static hipError_t sort_by_flow(void* tmp, size_t& tb, const uint32_t* key, uint3
     using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OS>;
     return rocprim::radix_sort_pairs<Cfg>(tmp, tb, key, skey, val, sval, (size_t)n, 0u, (unsigned)end_bit, s);
 #else
-    return hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, skey, val, sval, n, 0, end_bit, s);
+    return prim_sort_pairs(tmp, tb, key, skey, val, sval, n, 0, end_bit, s);
 #endif
 }
 
 // The arena exact_begin lays out for a job: phase 1 over every packet, phase
-// 2 over at most every packet, and the hipCUB temp storage at that size.
+// 2 over at most every packet, and the rocPRIM temp storage at that size.
 static size_t arena_bytes_calc(const ExactJob& J, uint64_t N, hipStream_t s, size_t* tmp_out);
 // (the library's temp-size queries cost the host ~10 us a run, between the
 // pass and the engine's first launch: the last sizes are kept)
@@ -1517,24 +1577,23 @@ static size_t arena_bytes_calc(const ExactJob& J, uint64_t N, hipStream_t s, siz
         add(tmp);
         return b;
     };
-    // hipcub temp storage: the largest of the primitives at size N
+    // rocPRIM temp storage: the largest of the primitives at size N
     size_t tmp = 0, t = 0;
     {
         const int n = (int)N;
-        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, n, s); tmp = std::max(tmp, t);
-        (void)hipcub::DeviceScan::InclusiveSum(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, n, s); tmp = std::max(tmp, t);
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+        (void)prim_exclusive_sum(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, n, s); tmp = std::max(tmp, t);
+        (void)prim_inclusive_sum(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, n, s); tmp = std::max(tmp, t);
+        (void)prim_sort_pairs(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 64, s);
         tmp = std::max(tmp, t);
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr,
+        (void)prim_sort_pairs(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 32, s);
         tmp = std::max(tmp, t);
         (void)sort_by_flow(nullptr, t, nullptr, nullptr, nullptr, nullptr, n, 32, s);
         tmp = std::max(tmp, t);
-        (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                          hipcub::Min(), n, s);
+        (void)prim_inclusive_min(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n, s);
         tmp = std::max(tmp, t);
-        (void)hipcub::DeviceScan::InclusiveScan(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, hipcub::Max(),
+        (void)prim_inclusive_max(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                                 n / 16 + 2, s);
         tmp = std::max(tmp, t);
     }
@@ -1666,7 +1725,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         k_ex_pidkeys<<<gridn(n, 256), 256, 0, s>>>(n, J.phash + (J.h_batches[0].first - J.phash_base), J.emap,
                                                    J.T.fmax, key, val, nullptr);
     } else {
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tp, tb, bcount, bpos, (int)nblk, s));
+        HIPCHECK(prim_exclusive_sum(tp, tb, bcount, bpos, (int)nblk, s));
         unsigned long long last[2] = {0, 0};
         const void* src[2] = {bpos + nblk - 1, bcount + nblk - 1};
         const int by[2] = {4, 4};
@@ -1709,7 +1768,7 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, S->ct, nb_dev, starts, ctr + 1, J.dense_cm ? key : nullptr,
                                                  ctr + 2);
         tb = tmp;
-        HIPCHECK(hipcub::DeviceScan::InclusiveScan(tp, tb, starts, S->tbl, hipcub::Max(), (int)(nb_dev + 1), s));
+        HIPCHECK(prim_inclusive_max(tp, tb, starts, S->tbl, (int)(nb_dev + 1), s));
     } else if (J.mode_b) {
         k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1, J.dense_cm ? key : nullptr, ctr + 2);
     }
@@ -1846,7 +1905,7 @@ int exact_seed_requests(ExactSession* S, unsigned long long* req, uint32_t* q, u
         // (creation index, instance) sorted by index: grouped by holder shard
         k_ex_seed_req<<<gridn(ni, 256), 256, 0, s>>>(ni, S->ist, S->sm, S->hi2, S->idx);
         size_t tb = S->tmp;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(S->tp, tb, S->hi2, req, S->idx, q, (int)ni, 0, 64, s));
+        HIPCHECK(prim_sort_pairs(S->tp, tb, S->hi2, req, S->idx, q, (int)ni, 0, 64, s));
     }
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(s));
@@ -1955,7 +2014,7 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
     uint32_t* val = nullptr;
     void* tp = nullptr;
     size_t tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, bcount, bpos, (int)nblk, s);
+    (void)prim_exclusive_sum(nullptr, tb, bcount, bpos, (int)nblk, s);
     int rc = FLUERE_OK;
     const uint64_t N = nblk * EXM_PKTS;
     if (hipMalloc(&meta, N * sizeof(ExMeta)) != hipSuccess || hipMalloc(&bcount, nblk * 4) != hipSuccess ||
@@ -1974,7 +2033,7 @@ int exact_collect(const ExactJob& J, hipStream_t s, ExMeta* cm, uint64_t* n_out)
         unsigned long long last[2] = {0, 0};
         const void* src[2] = {bpos + nblk - 1, bcount + nblk - 1};
         const int by[2] = {4, 4};
-        if (hipcub::DeviceScan::ExclusiveSum(tp, tb, bcount, bpos, (int)nblk, s) != hipSuccess ||
+        if (prim_exclusive_sum(tp, tb, bcount, bpos, (int)nblk, s) != hipSuccess ||
             mail_fetch(J.mail, s, 2, src, by, last) != FLUERE_OK)
             rc = FLUERE_E_HIP;
         else {

@@ -1090,17 +1090,24 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         const bool want = c->last_mode_b ? exm_env != 0 : (exma && atoi(exma) > 0);
         P.exm = (P.pid && P.spill && !c->use_mac && want) ? 1 : 0;
         P.exm_t = P.exm && c->last_mode_b ? 1 : 0;
+        // (an optional speed-up: without the memory the run goes on without it;
+        // the times array only where Mode B reads it)
         if (P.exm && c->n_total > c->exm_cap) {
             hipFree(c->d_exm);
-            hipFree(c->d_exm_t);
             c->d_exm = nullptr;
-            c->d_exm_t = nullptr;
             c->exm_cap = 0;
-            if (hipMalloc(&c->d_exm, c->n_total * sizeof(ExMeta)) != hipSuccess ||
-                hipMalloc(&c->d_exm_t, c->n_total * 8) != hipSuccess)
-                return FLUERE_E_NOMEM;
-            c->exm_cap = c->n_total;
+            if (hipMalloc(&c->d_exm, c->n_total * sizeof(ExMeta)) == hipSuccess) c->exm_cap = c->n_total;
+            else (void)hipGetLastError();
         }
+        if (P.exm_t && c->n_total > c->exm_t_cap) {
+            hipFree(c->d_exm_t);
+            c->d_exm_t = nullptr;
+            c->exm_t_cap = 0;
+            if (hipMalloc(&c->d_exm_t, c->n_total * 8) == hipSuccess) c->exm_t_cap = c->n_total;
+            else (void)hipGetLastError();
+        }
+        if (c->n_total > c->exm_cap) P.exm = 0;
+        if (!P.exm || c->n_total > c->exm_t_cap) P.exm_t = 0;
     }
     if (P.phash && c->n_total > c->phash_cap) {
         hipFree(c->d_phash);
@@ -1311,7 +1318,10 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         static const bool hostprof = getenv("FLUERE_HOSTPROF") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         hipEvent_t e0 = c->evh[2 * i], e1 = c->evh[2 * i + 1];
-        if (grid)
+        static const int ev_abl = diag_knob("FLUERE_EV_ABL");  // diagnostics: 1 no timing events (kernel_ms invalid)
+        if (grid && ev_abl == 1)
+            HIPCHECK(hipLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s));
+        else if (grid)
             HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, e0, e1, 0));
         const auto t1 = std::chrono::steady_clock::now();
         // the slow list into k_slow's owner segments, before the merge reads them
@@ -1675,7 +1685,7 @@ int prepare_capture(fluere_ctx* c) {
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
         const uint64_t n = c->d_recs_cap, gn = (n + 255) / 256, nw = N / 32 + 1;
         size_t tb = 0;
-        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(N + 1),
+        (void)prim_exclusive_sum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(N + 1),
                                                c->stream);
         (void)ord_scratch(c, al(n * 8) + 2 * al((N + 1) * 4) + al(nw * 4) + al(n * 4) + 2 * al(gn * 4) + al(16) +
                                  al(tb));
@@ -2095,9 +2105,9 @@ extern "C" int fluere_synth_device(const fluere_synth_cfg* cfg, uint64_t first, 
     k_synth_len<<<grid_for(n, 256), 256, 0, s>>>(*cfg, first, n, lens);
     size_t tb = 0;
     void* tmp = nullptr;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lens, d_offsets, (int)n, s);
+    prim_exclusive_sum(nullptr, tb, lens, d_offsets, (int)n, s);
     if (hipMalloc(&tmp, std::max<size_t>(tb, 16)) != hipSuccess) { hipFree(lens); return FLUERE_E_NOMEM; }
-    hipcub::DeviceScan::ExclusiveSum(tmp, tb, lens, d_offsets, (int)n, s);
+    prim_exclusive_sum(tmp, tb, lens, d_offsets, (int)n, s);
     k_synth_write<<<grid_for(n, 256), 256, 0, s>>>(*cfg, first, n, d_bytes, d_offsets);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(s));

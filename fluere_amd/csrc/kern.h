@@ -4,7 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
-#include <hipcub/hipcub.hpp>
+#include "prim.h"
 
 #include <fcntl.h>
 #include <sys/stat.h>

@@ -253,7 +253,7 @@ int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m) {
     if (rc || c->d_recs2_cap < m) return rc ? rc : FLUERE_E_NOMEM;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+    (void)prim_sort_pairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                              (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, 64, s);
     if ((rc = ord_scratch(c, 2 * al(m * 8) + 2 * al(m * 4) + al(tb)))) return rc;
     char* p = (char*)c->d_ord;
@@ -265,7 +265,7 @@ int sort_actives(fluere_ctx* c, uint64_t ne, uint64_t m) {
     const fluere_record* act = c->d_recs + ne;
     k_act_keys<<<grid_for(m, 256), 256, 0, s>>>(act, m, k0, v0);
     size_t t = tb;
-    HIPCHECK(hipcub::DeviceRadixSort::SortPairs(p, t, k0, k1, v0, v1, (int)m, 0, 64, s));
+    HIPCHECK(prim_sort_pairs(p, t, k0, k1, v0, v1, (int)m, 0, 64, s));
     k_act_gather<<<grid_for(m * REC_WORDS, 256), 256, 0, s>>>(act, v1, m, c->d_recs2);
     HIPCHECK(hipGetLastError());
     return FLUERE_OK;
@@ -302,7 +302,7 @@ static int order_sorted(fluere_ctx* c, uint64_t n, uint64_t n_ended, const unsig
     hipStream_t s = c->stream;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+    (void)prim_sort_pairs(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                              (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64, s);
     // (okey lives in the ordering scratch or the emitters' array: the keys get a buffer of their own)
     void* buf = nullptr;
@@ -321,7 +321,7 @@ static int order_sorted(fluere_ctx* c, uint64_t n, uint64_t n_ended, const unsig
         if (word == 1) k_ob_keys<<<g, 256, 0, s>>>(okey, c->d_recaux, n, w, k0, v0);
         else k_ob_rekey<<<g, 256, 0, s>>>(okey, c->d_recaux, v0, n, w, k0);
         size_t t = tb;
-        if (hipcub::DeviceRadixSort::SortPairs(tmp, t, k0, k1, v0, v1, (int)n, 0, 64, s) != hipSuccess) rc = FLUERE_E_HIP;
+        if (prim_sort_pairs(tmp, t, k0, k1, v0, v1, (int)n, 0, 64, s) != hipSuccess) rc = FLUERE_E_HIP;
         std::swap(v0, v1);  // the permutation so far (stable: ties keep the last pass's order)
     }
     if (rc == FLUERE_OK) {
@@ -361,8 +361,8 @@ int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint
     const uint64_t nw = N / 32 + 1;                 // Mode A: bit words
     const uint64_t nk = mode_b ? N + 1 : nw;        // the scanned array: Mode A bit counts, Mode B group counts
     size_t tb = 0, tb2 = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nk, s);
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)gn, s);
+    (void)prim_exclusive_sum(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nk, s);
+    (void)prim_exclusive_sum(nullptr, tb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)gn, s);
     tb = std::max(tb, tb2);
     // scratch: okey[n] | cnt-or-bits[nk] | pc[nw] | pre-or-start[nk] | mem[n] | blk[gn] | blk_pre[gn] | gmax | tmp
     if ((rc = ord_scratch(c, al(n * 8) + 2 * al(nk * 4) + al(nw * 4) + al(n * 4) + 2 * al(gn * 4) + al(16) + al(tb))))
@@ -386,11 +386,11 @@ int order_records(fluere_ctx* c, uint64_t n, uint64_t n_ended, bool mode_b, uint
     k_ord_keys<<<gn, 256, 0, s>>>(c->d_recs, n, base, mode_b ? 1 : 0, have_okey ? c->d_okey : nullptr, okey, cb, cb,
                                   gmax, blk);
     size_t t = tb;
-    HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, blk, blk_pre, (int)gn, s));
+    HIPCHECK(prim_exclusive_sum(tmp, t, blk, blk_pre, (int)gn, s));
     if (!mode_b) {
         k_ord_popc<<<grid_for(nw, 256), 256, 0, s>>>(cb, nw, pc);
         t = tb;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, t, pc, ps, (int)nw, s));
+        HIPCHECK(prim_exclusive_sum(tmp, t, pc, ps, (int)nw, s));
         static const bool all_move = getenv("FLUERE_ORD_MOVE_ALL") != nullptr;
         if (!all_move && n_ended * 4 <= n) {  // few ended: only they and the head's actives move (k_ord_out)
             k_ord_out<<<gn, 256, 0, s>>>(c->d_recs, n, base, okey, cb, ps, blk_pre, n_ended, c->d_recs2, mem, gmax);

@@ -793,7 +793,7 @@ static int wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uin
     hipStream_t s = c->stream;
     const uint64_t n = (uint64_t)n_owners * cap;
     size_t tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+    (void)prim_exclusive_sum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(n + 1), s);
     // (+ n_owners words: the slotted form's block sizes when the caller has no buffer for them)
     const size_t need = 2 * (n + 1) * 8 + (size_t)(n_owners + 1) * 8 + (size_t)n_owners * 8 + ((tb + 255) & ~(size_t)255);
@@ -819,7 +819,7 @@ static int wire_pack(fluere_ctx* c, const void* d_blocks, uint32_t n_owners, uin
     a.woff = a.scan + (n + 1);
     a.sizes = d_sizes ? d_sizes : a.woff + (n_owners + 1);
     k_wire_size<<<grid_for(n + 1, 256), 256, 0, s>>>(a);
-    HIPCHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.sz, a.scan, (int)(n + 1), s));
+    HIPCHECK(prim_exclusive_sum(tmp, tb, a.sz, a.scan, (int)(n + 1), s));
     k_wire_offsets<<<1, 64, 0, s>>>(a);
     k_wire_pack<<<grid_for(n, 256), 256, 0, s>>>(a);
     const unsigned ax = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(64, cap_annex * 32 / 256));
@@ -996,12 +996,12 @@ static int merge_complete(fluere_ctx* c, MergeArgs& ma, uint32_t seq, uint32_t n
         ma.out_cap = c->d_recs_cap;
         int end_bit = 8;
         while (end_bit < 64 && (1ull << (end_bit - 8)) <= c->fmax) end_bit++;
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys2, vals, vals2, (int)nk, 0, end_bit, s);
+        (void)prim_sort_pairs(nullptr, tb, keys, keys2, vals, vals2, (int)nk, 0, end_bit, s);
         if (hipMalloc(&tmp, std::max<size_t>(tb, 16)) != hipSuccess) {
             hipFree(keys); hipFree(keys2); hipFree(vals); hipFree(vals2);
             return FLUERE_E_NOMEM;
         }
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, (int)nk, 0, end_bit, s));
+        HIPCHECK(prim_sort_pairs(tmp, tb, keys, keys2, vals, vals2, (int)nk, 0, end_bit, s));
         if (nk) k_compose<<<grid_for(nk, 64), 64, 0, s>>>(ma, keys2, vals2, nk);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipMemcpyAsync(&g, c->d_glob, sizeof g, hipMemcpyDeviceToHost, s));
@@ -1348,10 +1348,10 @@ extern "C" int fluere_sweep_pack(fluere_ctx* c, uint32_t n_owners, uint64_t* cou
         if (n) {
             k_sw_owner<<<grid_for(n, 256), 256, 0, s>>>(w->hcm, n, c->d_flow_key, n_owners, w->k1, w->v1);
             size_t tb = 0;
-            (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, w->k1, w->k2, w->v1, w->hperm, (int)n, 0,
+            (void)prim_sort_pairs(nullptr, tb, w->k1, w->k2, w->v1, w->hperm, (int)n, 0,
                                                      bits_for(n_owners), s);
             if ((rc = sw_tmp(w, tb))) return rc;
-            HIPCHECK(hipcub::DeviceRadixSort::SortPairs(w->tmp, tb, w->k1, w->k2, w->v1, w->hperm, (int)n, 0,
+            HIPCHECK(prim_sort_pairs(w->tmp, tb, w->k1, w->k2, w->v1, w->hperm, (int)n, 0,
                                                         bits_for(n_owners), s));
             k_sw_kcount<<<grid_for(n_owners, 256), 256, 0, s>>>(w->k2, n, n_owners, w->misc);
             HIPCHECK(hipMemsetAsync(w->hpr, 1, n, s));  // first guess: every valid packet is processed
@@ -1444,11 +1444,11 @@ extern "C" int fluere_sweep_queries(fluere_ctx* c, uint32_t n_ranks, uint32_t ra
                                                          w->k1, w->v1);
             // queries grouped by target shard (n_ranks: none), capture order within one
             size_t tb = 0;
-            (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, w->k1, w->k2, w->v1, w->qk, (int)n, 0,
+            (void)prim_sort_pairs(nullptr, tb, w->k1, w->k2, w->v1, w->qk, (int)n, 0,
                                                      bits_for(n_ranks), s);
             int rc = sw_tmp(w, tb);
             if (rc) return rc;
-            HIPCHECK(hipcub::DeviceRadixSort::SortPairs(w->tmp, tb, w->k1, w->k2, w->v1, w->qk, (int)n, 0,
+            HIPCHECK(prim_sort_pairs(w->tmp, tb, w->k1, w->k2, w->v1, w->qk, (int)n, 0,
                                                         bits_for(n_ranks), s));
             k_sw_kcount<<<grid_for(n_ranks + 1, 256), 256, 0, s>>>(w->k2, n, n_ranks + 1, w->misc + 2048);
             HIPCHECK(hipGetLastError());
