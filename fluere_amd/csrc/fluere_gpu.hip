@@ -521,8 +521,14 @@ extern "C" int fluere_open(const fluere_opts* o, fluere_ctx** out) {
         hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreate(&c->ev_ctl) != hipSuccess)
         return fail(FLUERE_E_HIP);
+    // the hot kernels' timing events (carried by their dispatches): timing
+    // only, so no system-scope fence when they are recorded -- with it the
+    // stop event wrote back and invalidated the caches behind the hot kernel
+    // (FLUERE_EV_FENCE=1: the default events, A/B)
+    static const bool ev_fence = getenv("FLUERE_EV_FENCE") && atoi(getenv("FLUERE_EV_FENCE")) != 0;
     for (hipEvent_t& e : c->evh)
-        if (hipEventCreate(&e) != hipSuccess) return fail(FLUERE_E_HIP);
+        if (hipEventCreateWithFlags(&e, ev_fence ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess)
+            return fail(FLUERE_E_HIP);
     hipStream_t s = c->stream;
     if (hipMemsetAsync(c->d_cbits, 0, 1u << CBITS_LOG2, s) != hipSuccess) return fail(FLUERE_E_HIP);
     // the stream's scratch (private memory) backing, sized now: the first
