@@ -526,16 +526,22 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
             const size_t o = (size_t)set * NS + (FLUERE_FLUSH_LINEAR ? e : own_add(s_own, own[k]));
             uint4* dst = reinterpret_cast<uint4*>(S.part + o);
             if (FLUERE_FLUSH_LINEAR == 2 && kk.x != 0x12345678u) continue;  // diagnostics: no stores
-            const uint4 mm = s_mm[e];
-            const uint4 pv[5] = {make_uint4(kk.x, kk.y, kk.z, tag),
-                                 make_uint4(h, (uint32_t)(p0 & 0xFFFF) | ((uint32_t)(p1 & 0xFFFF) << 16),
-                                            (uint32_t)(p0 >> 32), (uint32_t)(p1 >> 32)),
-                                 make_uint4(mm.x, mm.y, mm.z, mm.w),
-                                 make_uint4(s_fl[0][e], s_fl[1][e], s_fl[2][e], s_fl[3][e]), s_pos[e]};
+            const uint4 mm = s_mm[e], ps = s_pos[e];
+            const uint4 fw = make_uint4(s_fl[0][e], s_fl[1][e], s_fl[2][e], s_fl[3][e]);
+            // lean (kern.h PART_LEAN): no flag, no FIN/RST, first packet creates
+            const bool lean = !MACS && (fw.x | fw.y | fw.z | fw.w) == 0 && ps.z == NONE32 && ps.y == ps.x;
+            dst[0] = make_uint4(kk.x, kk.y, kk.z, tag | (lean ? PART_LEAN : 0u));
+            dst[1] = make_uint4(h, (uint32_t)(p0 & 0xFFFF) | ((uint32_t)(p1 & 0xFFFF) << 16), (uint32_t)(p0 >> 32),
+                                (uint32_t)(p1 >> 32));
             // (plain stores: nontemporal ones, measured, made the kernel ~20 us
             // longer -- 20 MB written through at once at the end of the pass)
-#pragma unroll
-            for (int q = 0; q < 5; q++) dst[q] = pv[q];
+            if (lean) {
+                dst[2] = make_uint4(mm.x | (mm.z << 16), mm.y | (mm.w << 8), ps.x, ps.w);
+            } else {
+                dst[2] = make_uint4(mm.x, mm.y, mm.z, mm.w);
+                dst[3] = fw;
+                dst[4] = ps;
+            }
             if (MACS) {  // (re-read from LDS: registers are scarce across the spill scatter)
                 const uint4 xs = s_key[LKL + s_sk[e]];
                 S.partx[o] = make_uint4(xs.x, xs.y, xs.z, h);

@@ -55,6 +55,12 @@ struct alignas(16) Part {
     uint32_t pos[4];              // first any / first create / first FIN-RST (NONE32) and last+1 (0), window-relative
 };
 static_assert(sizeof(Part) == 80, "Part layout");
+// A lean partial (k_parse_agg without MACs): a flow whose window carried no TCP
+// flag, no FIN/RST and whose first packet could create it (every UDP flow)
+// is staged as its first 48 bytes only -- tag | PART_LEAN; word 2 = {min pkt |
+// max pkt << 16, min ttl | max ttl << 8, first, last + 1} -- 40 % fewer flush
+// bytes (20 -> 12 MB for C2) and dirty lines behind the kernel.
+constexpr uint32_t PART_LEAN = 2u;
 
 // A spilled packet: a valid hot-path packet whose key found no LDS slot (more
 // flows in a workgroup's window than the table holds).  32 bytes; written
@@ -410,6 +416,22 @@ __device__ __forceinline__ void part_store_global(const Acc& A, uint32_t d, cons
 }
 
 __device__ __forceinline__ void part_of_stage(const Part& p, unsigned long long base, FlowPart& f) {
+    if (p.tag & PART_LEAN) {  // {min | max pkt << 16, min | max ttl << 8, first, last + 1}
+        f.pk[0] = p.pk & 0xFFFF;
+        f.pk[1] = p.pk >> 16;
+        f.by[0] = p.by0;
+        f.by[1] = p.by1;
+        f.mn[0] = p.mn0 & 0xFFFF;
+        f.mx[0] = p.mn0 >> 16;
+        f.mn[1] = p.mn1 & 0xFF;
+        f.mx[1] = (p.mn1 >> 8) & 0xFF;
+#pragma unroll
+        for (int q = 0; q < 8; q++) f.fl[q] = 0;
+        f.fa = f.fc = base + p.mx0;
+        f.fr = NONE64;
+        f.la = base + p.mx1;
+        return;
+    }
     f.pk[0] = p.pk & 0xFFFF;
     f.pk[1] = p.pk >> 16;
     f.by[0] = p.by0;

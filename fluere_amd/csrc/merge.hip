@@ -459,8 +459,8 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     uint4 v[5];
     #pragma unroll
                     for (int q = 0; q < 5; q++) v[q] = src[q];
-                    __builtin_memcpy(&p, v, sizeof p);
-                    h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag;
+                    __builtin_memcpy(&p, v, sizeof p);  // (a lean partial's last two words are stale: unused)
+                    h = p.h; k0 = p.k0; k1 = p.k1; k2 = p.k2; tag = p.tag & ~PART_LEAN;
                     if (macs) {
                         const uint4 xx = S.partx[o];
                         x0 = xx.x; x1 = xx.y; x2 = xx.z;
