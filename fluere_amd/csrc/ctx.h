@@ -203,7 +203,12 @@ struct SoLaunch {
 inline int diag_knob(const char* name) {
     if (!FLUERE_DIAG) return 0;
     const char* v = getenv(name);
-    return v ? (atoi(v) ? atoi(v) : 1) : 0;
+    if (!v) return 0;
+    // a number is taken as given (FLUERE_ABLATE=0: the full kernel); any other
+    // value switches the knob on
+    char* end = nullptr;
+    const long x = strtol(v, &end, 10);
+    return end != v ? (int)x : 1;
 }
 
 // host helpers shared by the translation units
