@@ -26,7 +26,7 @@ __device__ __forceinline__ void load_acc(const Acc& A, uint32_t d, AccVals& v) {
 // k_finalize_gen, whose general parser would cost k_finalize its occupancy).
 template <bool GEN>
 __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, const AccVals& v, fluere_record& r,
-                                              bool& cplx, unsigned long long& cplx_pkts) {
+                                              bool& cplx, unsigned long long& cplx_pkts, bool one = false, Batch bone = Batch{}) {
     const unsigned long long fa = v.fa, fc = v.fc, fr = v.fr, la = v.la;
     if (fc == NONE64) return false;  // TCP flow without any SYN: every packet is dropped (:101-113)
     bool certified = fc == fa && (fr == NONE64 || fr == la);
@@ -42,9 +42,13 @@ __device__ __forceinline__ bool finalize_vals(const FinArgs& a, uint32_t d, cons
     }
     const bool macs = a.macs != 0;
     // the first and the last packet: both offsets, then both windows, in flight together
-    const int bp = find_batch(a.bs, a.nb, fc), bq = find_batch(a.bs, a.nb, la);
-    const Batch& BP = a.bs[bp];
-    const Batch& BQ = a.bs[bq];
+    // (one: a single batch, its descriptor `bone` loaded by the caller ahead of
+    // the chain; passed by value -- a pointer to it would live in scratch)
+    Batch BP = bone, BQ = bone;
+    if (!one) {
+        BP = a.bs[find_batch(a.bs, a.nb, fc)];
+        BQ = a.bs[find_batch(a.bs, a.nb, la)];
+    }
     const uint32_t op = BP.offs[fc - BP.first], oq = BQ.offs[la - BQ.first];
     Win WP;
     load_win(BP, op, WP);
@@ -1040,6 +1044,13 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
 // The record is built in place in the block's LDS staging (S.rec[thread]):
 // held in registers it took the kernel to 250 VGPRs (2 waves per SIMD).
 __global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
+    // loaded together, ahead of the flow count they would otherwise wait for:
+    // the first flow's accumulators (every dense id below fmax is allocated)
+    // and, with one batch, its descriptor -- one dependent round trip less
+    const uint32_t d_pre = blockIdx.x * blockDim.x + threadIdx.x;
+    AccVals v_pre;
+    if (d_pre < a.T.fmax) load_acc(a.A, d_pre, v_pre);
+    const Batch b_pre = a.bs[0];
     const Glob& gg = *a.g;
     const bool mode_b = a.timeout_us && gg.valid && gg.tmax - gg.tmin >= a.timeout_us;
     const uint32_t nf = mode_b ? 0u : min(*a.T.n_flows, a.T.fmax);
@@ -1052,7 +1063,12 @@ __global__ void __launch_bounds__(EMIT_BLOCK) k_finalize(FinArgs a) {
         fluere_record& r = S.rec[threadIdx.x];
         bool cplx = false;
         unsigned long long cplx_pkts = 0;
-        const bool want = d < nf && finalize_one<false>(a, d, r, cplx, cplx_pkts);
+        bool want = false;
+        if (d < nf) {
+            AccVals v = v_pre;
+            if (d != d_pre) load_acc(a.A, d, v);
+            want = finalize_vals<false>(a, d, v, r, cplx, cplx_pkts, a.nb == 1, b_pre);
+        }
         const unsigned long long ok = want ? r.order_key : NONE64;
         emit_inplace_block(S, a.g, a.out, a.out_cap, want, want ? r.d_pkts : 0u, ok != NONE64, nullptr, 0, 0, tot,
                            a.rbits);
