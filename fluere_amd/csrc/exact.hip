@@ -242,6 +242,47 @@ __global__ void __launch_bounds__(256) k_ex_compact(const ExMeta* meta_blk, cons
     }
 }
 
+// Several small fills in one launch (each hipMemsetAsync is a kernel of its
+// own, ~5 us on the stream): up to FILL_MAX (pointer, bytes, byte value),
+// 16-byte stores where a range allows them.
+constexpr int FILL_MAX = 4;
+struct Fills {
+    uint8_t* p[FILL_MAX];
+    uint64_t n[FILL_MAX];
+    uint32_t v[FILL_MAX];  // the byte value, replicated to a word
+    int k = 0;
+    void add(void* ptr, uint64_t bytes, uint8_t value) {
+        if (!bytes) return;
+        p[k] = (uint8_t*)ptr;
+        n[k] = bytes;
+        v[k] = value * 0x01010101u;
+        k++;
+    }
+};
+__global__ void __launch_bounds__(256) k_fill_many(Fills f) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    for (int j = 0; j < f.k; j++) {
+        uint8_t* p = f.p[j];
+        const uint64_t n = f.n[j];
+        const uint32_t v = f.v[j];
+        // byte head up to 16-byte alignment, 16-byte body, byte tail
+        const uint64_t head = min(n, (uint64_t)((16 - ((uintptr_t)p & 15)) & 15));
+        const uint64_t body = (n - head) / 16;
+        if (tid < head) p[tid] = (uint8_t)v;
+        uint4* q = reinterpret_cast<uint4*>(p + head);
+        for (uint64_t i = tid; i < body; i += nt) q[i] = make_uint4(v, v, v, v);
+        const uint64_t t0 = head + body * 16;
+        if (tid < n - t0) p[t0 + tid] = (uint8_t)v;
+    }
+}
+static hipError_t fill_many(const Fills& f, hipStream_t s) {
+    if (!f.k) return hipSuccess;
+    uint64_t big = 0;
+    for (int j = 0; j < f.k; j++) big = std::max<uint64_t>(big, f.n[j] / 16 + 16);
+    k_fill_many<<<(unsigned)std::min<uint64_t>(1024, (big + 255) / 256), 256, 0, s>>>(f);
+    return hipGetLastError();
+}
+
 // one GPU, Mode B over the hot pass's dense metadata: packet k's flow from
 // the merge's word; a packet without one is counted in *bad (then the caller
 // takes the k_ex_meta path)
@@ -1757,14 +1798,20 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
         int rc = fc_run(s, n, hf, hpos, false, heads, rf);
         if (rc) return rc;
     }
-    HIPCHECK(hipMemsetAsync(ctr, 0, 16, s));
     // Mode B: monotonicity and the time-bucket index in one pass (a max-scan
     // of range starts, no binary searches); small runs: the two kernels
     const uint64_t nb_dev = n / 16 + 1;
     const bool tscan = J.mode_b && n >= 64;
+    {   // the counters, the range starts, the first guess of the processed set
+        // (every valid packet; k_ex_gather set prp): one launch
+        Fills f;
+        f.add(ctr, 16, 0);
+        if (tscan) f.add(S->idx, (nb_dev + 1) * 4, 0);
+        if (J.mode_b) f.add(pr, n, 1);
+        HIPCHECK(fill_many(f, s));
+    }
     if (tscan) {
         uint32_t* starts = S->idx;  // (free until the seed requests; n >= nb + 1)
-        HIPCHECK(hipMemsetAsync(starts, 0, (nb_dev + 1) * 4, s));
         k_ex_tscan<<<gridn(n, 256), 256, 0, s>>>(n, cm, S->ct, nb_dev, starts, ctr + 1, J.dense_cm ? key : nullptr,
                                                  ctr + 2);
         tb = tmp;
@@ -1772,7 +1819,6 @@ int exact_begin(const ExactJob& J, hipStream_t s, ExactSession** out) {
     } else if (J.mode_b) {
         k_ex_mono<<<gridn(n, 256), 256, 0, s>>>(n, cm, ctr + 1, J.dense_cm ? key : nullptr, ctr + 2);
     }
-    if (J.mode_b) HIPCHECK(hipMemsetAsync(pr, 1, n, s));  // first guess: every valid packet is processed (k_ex_gather: prp)
     // one host read: key count, monotonicity, the first and last times.  Mode
     // A (not shard mode) needs none of them on the host: the key count stays
     // on the device and the chase's grid covers the replayed packets (every
@@ -1849,12 +1895,17 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
     static const bool no_inc = getenv("FLUERE_EXACT_NO_INC") != nullptr;  // (A/B)
     const bool inc = J.mode_b && !fext && !J.shard_mode && !no_inc;
     const uint32_t pid = ++S->pass_no;
+    // this pass's fills in one launch: the changed counter k_ex_members counts
+    // into, and the stamps (first pass), the dirty keys, or the start flags
+    Fills fills;
+    fills.add(S->ctr + 2, 4, 0);
+    if (inc && pid < 255) fills.add(pid == 1 ? (void*)S->stamp : (void*)S->kdirty, pid == 1 ? n : S->n_keys, 0);
+    else fills.add(S->sflag, n * 4, 0);
+    HIPCHECK(fill_many(fills, s));
     if (inc && pid < 255) {
         if (pid == 1) {
-            HIPCHECK(hipMemsetAsync(S->stamp, 0, n, s));
             S->ca.kdirty = nullptr;
         } else {
-            HIPCHECK(hipMemsetAsync(S->kdirty, 0, S->n_keys, s));
             k_ex_check<<<gridn(n, 256), 256, 0, s>>>(n, S->sflag, S->elook, S->ekp, S->np_rev, S->hf, S->hpos, S->kdirty,
                                                      S->mono ? nullptr : S->tree, S->tree_P, S->sm, J.timeout_us);
             S->ca.kdirty = S->kdirty;
@@ -1871,14 +1922,12 @@ int exact_pass(ExactSession* S, const unsigned long long* fext, uint8_t* pr_out,
         S->ca.kpass = nullptr;
         S->ca.kdirty = nullptr;
         S->ca.elook = S->ca.ekp = nullptr;
-        HIPCHECK(hipMemsetAsync(S->sflag, 0, n * 4, s));
         k_ex_chase<<<gridn(S->ca.d_nkeys ? n : S->n_keys, 64), 64, 0, s>>>(S->ca);
     }
     {  // instance ordinals and starts (npr: the tile totals, after next_scan's use)
         int rc = fc_run(s, n, S->sflag, S->incl, true, S->ist, S->npr);
         if (rc) return rc;
     }
-    HIPCHECK(hipMemsetAsync(S->ctr + 2, 0, 4, s));
     if (J.mode_b)  // the processed set (Mode A needs none: every run is a record or a piece)
         k_ex_members<<<gridn(n, 256), 256, 0, s>>>(n, S->incl, S->ist, S->iend, S->sval, S->pr, S->prp, S->ctr + 2);
     HIPCHECK(hipGetLastError());
@@ -1938,16 +1987,8 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     }
     const uint32_t n_inst = (uint32_t)hv[0];
     const uint64_t n_rec0 = hv[1];
-    // ---- 6. per-instance aggregates over each instance's contiguous run
-    HIPCHECK(hipMemsetAsync(S->ctr, 0, 8, s));
-    if (n_inst) {
-        k_ex_agg<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
-        k_ex_agg_wave<<<1024, 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
-        k_ex_agg_block<<<256, 1024, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
-    }
-    HIPCHECK(hipGetLastError());
-    S->R.instances = dev_inst ? 0 : n_inst;
-    // ---- 7. records
+    // ---- 7a. the record buffer and (Mode B) the order words: grown first,
+    // so that the counters and the order words are cleared in one launch
     const uint64_t want = n_rec0 + n_inst;
     if (want > *J.d_recs_cap) {  // grow, keeping the records already there
         fluere_record* nr = nullptr;
@@ -1962,6 +2003,8 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     // Mode B: the order words beside the records (indexed like them); the
     // caller's aux_out is the slot of record n_rec0
     unsigned long long* aux = nullptr;
+    Fills fills;
+    fills.add(S->ctr, 16, 0);  // aggregate lists [0..1], the records' defer count [3]
     if (J.mode_b) {
         if (aux_out) {
             aux = aux_out - 2 * n_rec0;
@@ -1975,10 +2018,20 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
                 if (hipMalloc(J.recaux, std::max<uint64_t>(want, 1) * 16) != hipSuccess) return FLUERE_E_NOMEM;
                 *J.recaux_cap = std::max<uint64_t>(want, 1);
             }
-            if (n_rec0) HIPCHECK(hipMemsetAsync(*J.recaux, 0, n_rec0 * 16, s));
+            fills.add(*J.recaux, n_rec0 * 16, 0);
             aux = *J.recaux;
         }
     }
+    HIPCHECK(fill_many(fills, s));
+    // ---- 6. per-instance aggregates over each instance's contiguous run
+    if (n_inst) {
+        k_ex_agg<<<gridn(n_inst, 256), 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
+        k_ex_agg_wave<<<1024, 256, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
+        k_ex_agg_block<<<256, 1024, 0, s>>>(n_inst, S->ist, S->iend, S->sm, S->aggs, S->alist, S->ctr, p_ninst);
+    }
+    HIPCHECK(hipGetLastError());
+    S->R.instances = dev_inst ? 0 : n_inst;
+    // ---- 7. records
     RecArgs ra{J.d_batches, J.nb, J.macs, J.mode_b, n_inst, S->aggs, S->ist, S->sm, S->iend, S->ikind,
                S->ij, S->iie, S->iex, J.g, *J.d_recs, *J.d_recs_cap, aux, p_ninst, S->idx, S->ctr + 3,
                J.shard_mode, S->irole, S->ikey, S->annex, seeds};
@@ -1992,7 +2045,6 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     // The instances whose creating packet needs the general parser are listed
     // by the first kernel and done by the second (grid-stride over the count).
     if (n_inst) {
-        HIPCHECK(hipMemsetAsync(S->ctr + 3, 0, 4, s));
         k_ex_records_t<false><<<std::min<unsigned>(gridn(n_inst, 256), 1024), 256, 0, s>>>(ra);
         k_ex_records_t<true><<<std::min<unsigned>(gridn(n_inst, 256), 64), 256, 0, s>>>(ra);
     }

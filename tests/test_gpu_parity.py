@@ -693,6 +693,10 @@ FULL_SIZE = {
     # CSV, keys.rs:417-435) and the same frames untagged (50k MAC-keyed rows)
     "c5": (_lib.SYNTH_VLAN64, 10_000_000, 50_000, 0xF10E0005, True),
     "c5u": (_lib.SYNTH_MAC64, 10_000_000, 50_000, 0xF10E0005, True),
+    # BASELINE configs[3]'s per-GPU shard as bench.py --config c4_shard runs it
+    # (12.5M IMIX packets, 1M flows: two 4-GiB batches, one owner merge over
+    # both, 2048 merge owners) -- VERDICT r5 missing #4
+    "c4_shard": (_lib.SYNTH_IMIX, 12_500_000, 1_000_000, 0xF10E0004, False),
 }
 
 
@@ -703,18 +707,22 @@ def test_full_size_parity(gpu, name):
     kind, n, flows, seed, use_mac = FULL_SIZE[name]
     cfg = fluere_amd.synth_cfg(kind, n, flows, seed)
     with fluere_amd.FlowContext(use_mac=use_mac, max_flows=max(1 << 16, 2 * flows)) as ctx:
-        for b, o, nbytes, nb in fluere_amd.synth_device_batches(cfg, 0, n):
+        batches = fluere_amd.synth_device_batches(cfg, 0, n)
+        for b, o, nbytes, nb in batches:
             ctx.add_device_batch(b, nbytes, o, nb)
         torch.cuda.synchronize()
         st = ctx.run()
         recs, ne = ctx.records()
+        if name == "c4_shard":
+            assert len(batches) == 2 and ctx.last_hot_kernel() == "k_parse_spill"
+        del batches
     want = pyoracle.offline(fluere_amd.synth_pcap(cfg), use_mac=use_mac)
     assert st["packets"] == n
     assert_csv_equal(fluere_amd.format_csv(recs), ne, want["csv"], want["n_ended"], f"{name} full size")
     if name == "c5":
         assert len(recs) == 0  # the vlan_keys misparse drops every frame
     else:
-        assert len(recs) >= flows if name == "c3" else len(recs) == flows
+        assert len(recs) >= flows if name in ("c3", "c4_shard") else len(recs) == flows
 
 
 @pytest.mark.parametrize("n_keys,dup", [(64, 1), (5000, 1), (5000, 4), (100_000, 3)])
