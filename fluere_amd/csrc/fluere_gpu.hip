@@ -940,7 +940,9 @@ struct PassPlan {
 // record indices of the segments fit u32 (k_merge_partials' set tables).
 static uint32_t owner_cap(size_t sets, uint32_t O) {
     const char* force = getenv("FLUERE_OWNER_CAP");  // tests: a small capacity sends spills to the overflow list
-    uint64_t cap = force ? (uint64_t)std::max(1, atoi(force)) : (uint64_t)SPILL_WG / O * 5 / 4 + 32;
+    // (a multiple of 32 records: every owner segment starts on a whole 128-B
+    // line for the 24-byte records, so k_parse_spill's bins land as whole lines)
+    uint64_t cap = force ? (uint64_t)std::max(1, atoi(force)) : ((uint64_t)SPILL_WG / O * 5 / 4 + 32 + 31) & ~31ull;
     while (cap > 16 && (uint64_t)sets * O * cap >= (1ull << 32)) cap /= 2;
     return (uint32_t)cap;
 }
@@ -951,7 +953,8 @@ static uint32_t owner_cap(size_t sets, uint32_t O) {
 static void slow_shape(uint64_t n, size_t sets, uint32_t O, uint32_t& n_slow_sets, uint32_t& cap_s) {
     n_slow_sets = (uint32_t)((n + SLOW_SET - 1) / SLOW_SET);
     const char* force = getenv("FLUERE_OWNER_CAP");  // tests: a small capacity sends records to the overflow list
-    cap_s = force ? (uint32_t)std::max(1, atoi(force)) : SLOW_SET / O * 5 / 4 + 32;
+    // (a multiple of 32 records, as owner_cap: line-aligned segments of 24-byte records)
+    cap_s = force ? (uint32_t)std::max(1, atoi(force)) : ((uint32_t)SLOW_SET / O * 5 / 4 + 32 + 31) & ~31u;
     const uint64_t rec0 = (uint64_t)sets * O * owner_cap(sets, O);
     while (cap_s > 8 && rec0 + (uint64_t)n_slow_sets * O * cap_s >= (1ull << 32)) cap_s /= 2;
     if (rec0 + (uint64_t)n_slow_sets * O * cap_s >= (1ull << 32)) n_slow_sets = 0;
@@ -979,7 +982,7 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     // enough owners that each one's share of the flows (the last run's count
     // as the estimate) fits its merge workgroup's 1024-entry LDS table at
     // <= 85 % load; at least one per CU.  No more than that: k_parse_spill's
-    // per-owner LDS bins shrink as owners grow (BIN = 4096 / O records), and
+    // per-owner LDS bins shrink as owners grow (BIN = 5461 / O records), and
     // at 2048 owners the 2-record bins cost realistic TCP (847k flows) 85 us of
     // hot kernel over 1024 owners (827 flows each); 1M flows at 1024 owners
     // (977 each) overflow the merge tables and cost 0.5 ms (r03ah)
@@ -989,7 +992,7 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     static const int o_max = getenv("FLUERE_MAX_OWNERS") ? atoi(getenv("FLUERE_MAX_OWNERS")) : MAX_OWNERS;  // diagnostics
     const int cap = std::min(o_max, c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS);
     // a power of two: k_parse_spill writes a wave's completed bins in groups of
-    // 64 / (2 * BIN) lanes with BIN = 4096 / O (a CU count such as 304 rounds up)
+    // 64 / (3 * BIN) lanes with BIN = 5461 / O (a CU count such as 304 rounds up)
     uint32_t r = (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
     while (r & (r - 1)) r += r & (~r + 1);
     return std::min<uint32_t>(r, (uint32_t)MAX_OWNERS);

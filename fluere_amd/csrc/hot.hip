@@ -282,14 +282,14 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                     dst[0] = w_key;
                     dst[1] = w_pay;
                 } else if (pos < a.S.cap_o) {
-                    uint4* dst = reinterpret_cast<uint4*>(a.S.dspill) +
-                                 (((size_t)(blockIdx.x * a.S.W + win) * a.S.O + ow) * a.S.cap_o + pos) * (2 * SPU);
-                    dst[0] = w_key;
+                    const size_t rec = ((size_t)(blockIdx.x * a.S.W + win) * a.S.O + ow) * a.S.cap_o + pos;
                     if (MACS) {
+                        uint4* dst = reinterpret_cast<uint4*>(a.S.dspill) + rec * (2 * SPU);
+                        dst[0] = w_key;
                         dst[1] = make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]);
                         dst[2] = w_pay;
                     } else {
-                        dst[1] = w_pay;
+                        seg_store(reinterpret_cast<uint2*>(a.S.dspill), rec, w_key, w_pay);
                     }
                 } else {
                     ovf = true;
@@ -758,22 +758,27 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 // k_parse_spill: the hot pass for captures with many flows per window (the
 // last run sent more than half of its packets past k_parse_agg's LDS table:
 // C3/C4-like IMIX with 100k-1M flows).  No key table: every valid packet
-// becomes a 32-byte record for its merge owner, staged in an LDS bin per
-// owner (O x BIN records, 128 KiB); a full bin leaves as one contiguous run
-// of its owner's segment, written cooperatively by the wave that completed
-// it (2*BIN lanes per bin: 16-byte pieces, whole lines per instruction).
+// becomes a 24-byte record for its merge owner (seg_pack, kern.h), staged in
+// an LDS bin per owner (O x BIN records, 128 KiB); a full bin leaves as one
+// contiguous run of its owner's segment, written cooperatively by the wave
+// that completed it (3*BIN lanes per bin: 8-byte pieces).
 // k_parse_agg's scattered per-packet 32-byte stores into the owner segments
 // were ~90 us of C3's 0.44-ms kernel (ablation: the same stores coalesced).
 // The merge, the segments and the sets are k_parse_agg's (no partials).
 // ---------------------------------------------------------------------------
-constexpr int SPB_WORDS = 8192;  // LDS bins: 16-byte words (128 KiB), 2 per record
+constexpr int SPB_WORDS = 8192;  // LDS bins: 16-byte words (128 KiB); a record is 24 B (MACS: 64 B)
 
 // MACS (-M): the canonical MAC pair joins the key; a record is four 16-byte
 // words -- key, MAC words + hash, payload, zero (k_parse_agg<MACS>'s spills)
 template <bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
-    constexpr uint32_t RU = MACS ? 4u : 2u;  // 16-byte words per record
+    constexpr uint32_t RU = MACS ? 4u : 2u;  // 16-byte words per record (the raw overflow buffer's form)
+    // a bin record as it leaves for its owner segment: MACS four 16-byte
+    // pieces, otherwise the packed 24-byte form (seg_pack, kern.h), three 8-byte pieces
+    constexpr uint32_t PQ = MACS ? RU : SEG_Q;
+    typedef typename std::conditional<MACS, uint4, uint2>::type Piece;
     __shared__ uint4 s_bin[SPB_WORDS];
+    Piece* const s_bp = reinterpret_cast<Piece*>(s_bin);
     __shared__ uint32_t s_cl[MAX_OWNERS], s_wr[MAX_OWNERS];  // per bin: slots claimed / records written
     __shared__ uint32_t s_scnt[OWN_WORDS];                   // per owner: records in its segment (packed)
     __shared__ uint32_t s_chunk, s_nspill, s_slow;
@@ -782,8 +787,19 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
     const Stage& S = a.S;
     const Batch& B = a.B;
     const uint32_t O = S.O;
-    const uint32_t BIN = (uint32_t)(SPB_WORDS / RU) / O;  // records per bin: 16 (256 owners) .. 2 (2048); MACS: 8 .. 1
-    const uint32_t PPB = RU * BIN;                         // 16-byte pieces per bin
+    // records per bin: 21 (256 owners) .. 2 (2048); MACS: 8 .. 1
+    // A completed bin leaves as 16-byte pieces, at most one wave's lanes of
+    // them (MACS: RU per record; otherwise the bin's BIN * 24 contiguous bytes,
+    // BIN a power of two: 16 records = 384 B = three whole 128-B lines at
+    // line-aligned segment positions)
+    uint32_t BIN;
+    if constexpr (MACS) {
+        BIN = min((uint32_t)(SPB_WORDS / RU) / O, 64u / RU);
+    } else {
+        const uint32_t fit = min((uint32_t)(SPB_WORDS * 2 / SEG_Q) / O, 64u * 2 / 3);
+        BIN = fit >= 2 ? 1u << (31 - __builtin_clz(fit)) : 2u;  // (O <= 2048: fit >= 2)
+    }
+    const uint32_t PPB = MACS ? RU * BIN : BIN * 3 / 2;  // 16-byte pieces per bin
     for (uint32_t o = tid; o < MAX_OWNERS; o += BLOCK) s_cl[o] = s_wr[o] = 0;
     for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
     if (tid < 3) s_cnt[tid] = 0;
@@ -807,7 +823,20 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
     for (uint64_t ws = 0; ws < nsteps; ws += WIN_ITERS) {
         const uint32_t set = blockIdx.x * S.W + win;
         const uint32_t nch = (uint32_t)min<uint64_t>(WIN_ITERS, nsteps - ws) * WAVES;
-        uint4* seg0 = reinterpret_cast<uint4*>(S.dspill) + (size_t)set * O * S.cap_o * RU;
+        Piece* seg0 = reinterpret_cast<Piece*>(S.dspill) + (size_t)set * O * S.cap_o * PQ;
+        // record r of bin o, from LDS, in the 32-byte form (its piece h: the raw overflow buffer)
+        auto bin_rec = [&](uint32_t o, uint32_t r, uint32_t h) -> uint4 {
+            if constexpr (MACS) {
+                return s_bin[(o * BIN + r) * RU + h];
+            } else {
+                uint2 qq[SEG_Q];
+#pragma unroll
+                for (uint32_t i = 0; i < SEG_Q; i++) qq[i] = s_bp[(o * BIN + r) * SEG_Q + i];
+                uint4 key, pay;
+                seg_unpack(qq, key, pay);
+                return h ? pay : key;
+            }
+        };
         auto li_of = [&](uint32_t c) -> uint64_t {
             return beg + (ws + c / WAVES) * stride + (uint64_t)(c % WAVES) * 64 + lane;
         };
@@ -900,14 +929,17 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                 if (pend) {
                     const uint32_t slot = atomicAdd(&s_cl[o], 1u);
                     if (slot < BIN) {
-                        uint4* b = &s_bin[(o * BIN + slot) * RU];
-                        b[0] = w_key;
-                        if (MACS) {
+                        if constexpr (MACS) {
+                            uint4* b = &s_bin[(o * BIN + slot) * RU];
+                            b[0] = w_key;
                             b[1] = w_mac;
                             b[2] = w_pay;
                             b[3] = make_uint4(0, 0, 0, 0);
                         } else {
-                            b[1] = w_pay;
+                            uint2 qq[SEG_Q];
+                            seg_pack(w_key, w_pay, qq);
+#pragma unroll
+                            for (uint32_t i = 0; i < SEG_Q; i++) s_bp[(o * BIN + slot) * SEG_Q + i] = qq[i];
                         }
                         __threadfence_block();
                         if (atomicAdd(&s_wr[o], 1u) + 1 == BIN) done = o;
@@ -915,7 +947,7 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                     }
                 }
                 // the bins completed this round: their segment positions, then
-                // the wave writes them out, 2*BIN lanes per bin
+                // the wave writes them out, PPB lanes per bin
                 uint32_t pos = 0;
                 if (done != NONE32) pos = own_add_n(s_scnt, done, BIN);
                 uint64_t fm = __ballot(done != NONE32);
@@ -926,15 +958,34 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                     const bool act = m != 0 && j < 64 / PPB;  // (64 % PPB != 0: the spare lanes idle)
                     const uint32_t src = act ? (uint32_t)__builtin_ctzll(m) : 0u;
                     const uint32_t bo = __shfl(done, src, 64), bp = __shfl(pos, src, 64);
-                    const uint32_t r = pc / RU, hh = pc % RU;
-                    const bool ovf = act && bp + r >= S.cap_o;
-                    uint32_t q = 0;  // (the overflow slot: from the record's first lane, every lane shuffling)
-                    if (ovf && hh == 0) q = atomicAdd(&s_nspill, 1u);
-                    q = __shfl(q, lane & ~(RU - 1), 64);
-                    if (act) {
-                        const uint4 v = s_bin[(bo * BIN + r) * RU + hh];
-                        if (!ovf) seg0[((size_t)bo * S.cap_o + bp + r) * RU + hh] = v;
-                        else overflow(q, hh, v);  // past the segment's capacity: the overflow list
+                    if constexpr (MACS) {
+                        const uint32_t r = pc / RU, hh = pc % RU;
+                        const bool ovf = act && bp + r >= S.cap_o;
+                        uint32_t q = 0;  // (the overflow slot: from the record's first lane, every lane shuffling)
+                        if (ovf && hh == 0) q = atomicAdd(&s_nspill, 1u);
+                        q = __shfl(q, lane & ~(RU - 1), 64);
+                        if (act) {
+                            if (!ovf) seg0[((size_t)bo * S.cap_o + bp + r) * RU + hh] = s_bin[(bo * BIN + r) * RU + hh];
+                            else overflow(q, hh, s_bin[(bo * BIN + r) * RU + hh]);  // past the segment's capacity
+                        }
+                    } else {
+                        // the whole bin inside the segment (an even capacity keeps
+                        // the 16-byte pieces aligned): its bytes as they are in LDS
+                        const bool whole = (S.cap_o & 1u) == 0 && bp + BIN <= S.cap_o;
+                        if (act && whole) {
+                            reinterpret_cast<uint4*>(S.dspill)[((size_t)set * O * S.cap_o + (size_t)bo * S.cap_o + bp) * 3 / 2 + pc] =
+                                s_bin[bo * BIN * 3 / 2 + pc];
+                        } else if (act && pc < BIN) {  // (rare) record by record; past the capacity: the overflow list
+                            if (bp + pc < S.cap_o) {
+#pragma unroll
+                                for (uint32_t i = 0; i < SEG_Q; i++)
+                                    seg0[((size_t)bo * S.cap_o + bp + pc) * SEG_Q + i] = s_bp[(bo * BIN + pc) * SEG_Q + i];
+                            } else {
+                                const uint32_t q = atomicAdd(&s_nspill, 1u);
+                                overflow(q, 0, bin_rec(bo, pc, 0));
+                                overflow(q, 1, bin_rec(bo, pc, 1));
+                            }
+                        }
                     }
                     // drop the group's bins (the first 64 / PPB set bits)
                     for (uint32_t k = 0; k < 64 / PPB && fm; k++) fm &= fm - 1;
@@ -967,15 +1018,14 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
             if (!k) continue;
             const uint32_t p0 = own_add_n(s_scnt, o, k);
             for (uint32_t r = 0; r < k; r++) {
-                const uint4* v = &s_bin[(o * BIN + r) * RU];
                 if (p0 + r < S.cap_o) {
-                    uint4* d = seg0 + ((size_t)o * S.cap_o + p0 + r) * RU;
+                    Piece* d = seg0 + ((size_t)o * S.cap_o + p0 + r) * PQ;
 #pragma unroll
-                    for (uint32_t u = 0; u < RU; u++) d[u] = v[u];
+                    for (uint32_t u = 0; u < PQ; u++) d[u] = s_bp[(o * BIN + r) * PQ + u];
                 } else {
                     const uint32_t q = atomicAdd(&s_nspill, 1u);
 #pragma unroll
-                    for (uint32_t u = 0; u < RU; u++) overflow(q, u, v[u]);
+                    for (uint32_t u = 0; u < RU; u++) overflow(q, u, bin_rec(o, r, u));
                 }
             }
             s_cl[o] = s_wr[o] = 0;

@@ -351,27 +351,29 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 };
                 // one record ahead: the next iteration's record is loaded
                 // while this one is probed and aggregated in LDS
-                constexpr uint32_t RW = MACS ? 4u : 2u;  // 16-byte words per record
+                // (MACS: four 16-byte words per record; otherwise the packed 24-byte form)
+                auto load_rec = [&](size_t rix, uint4& k, uint4& p, uint4& x) {
+                    if constexpr (MACS) {
+                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + rix * 4;
+                        k = src[0];
+                        x = src[1];
+                        p = src[2];
+                    } else {
+                        seg_load(reinterpret_cast<const uint2*>(S.dspill), rix, k, p);
+                    }
+                };
                 uint32_t lo_n = 0;
                 uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, nx = n0;
                 if ((uint32_t)tid < total) {
                     lo_n = set_of(tid);
-                    const uint4* src = reinterpret_cast<const uint4*>(S.dspill) +
-                                       ((size_t)m_lo[lo_n] + ((uint32_t)tid - m_start[lo_n])) * RW;
-                    n0 = src[0];
-                    n1 = src[MACS ? 2 : 1];
-                    if (MACS) nx = src[1];
+                    load_rec((size_t)m_lo[lo_n] + ((uint32_t)tid - m_start[lo_n]), n0, n1, nx);
                 }
                 for (uint32_t idx = tid; idx < total; idx += MB) {
                     const uint32_t lo_i = lo_n;
                     const uint4 v0 = n0, v1 = n1, vx = nx;  // key, payload, (MACS) MAC words + hash
                     if (idx + MB < total) {
                         lo_n = set_of(idx + MB);
-                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) +
-                                           ((size_t)m_lo[lo_n] + (idx + MB - m_start[lo_n])) * RW;
-                        n0 = src[0];
-                        n1 = src[MACS ? 2 : 1];
-                        if (MACS) nx = src[1];
+                        load_rec((size_t)m_lo[lo_n] + (idx + MB - m_start[lo_n]), n0, n1, nx);
                     }
                     const unsigned long long gi = a.B.first + m_wb[lo_i] + v1.z;
                     const uint32_t k0 = v0.x, k1 = v0.y, k2 = v0.z, tag = v0.w;
@@ -472,15 +474,17 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     part_of_stage(p, base, f);
                 } else {
                     const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                    const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)(macs ? 4 : 2);
-                    const uint4 v0 = src[0], v1 = src[1];
-                    k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
                     if (macs) {  // {key}, {MAC words, hash}, {payload}
-                        const uint4 v2 = src[2];
+                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)4;
+                        const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+                        k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
                         x0 = v1.x; x1 = v1.y; x2 = v1.z;
                         h = v1.w;
                         spill_to_part(v2.x, v2.y, v2.z, v2.w, base, f);
-                    } else {
+                    } else {  // the packed 24-byte form (kern.h seg_pack)
+                        uint4 v0, v1;
+                        seg_load(reinterpret_cast<const uint2*>(S.dspill), o, v0, v1);
+                        k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
                         h = lt_hash(k0, k1, k2, tag);
                         spill_to_part(v1.x, v1.y, v1.z, v1.w, base, f);
                     }
@@ -908,11 +912,10 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         }
         if (a.slow_abl == 3) rec = false;  // diagnostics: no spill records
         // the segment position of a record past a full segment: the overflow list below
+        // (bins: runs without MACs; the segment holds the packed 24-byte form)
         auto seg_put = [&](uint32_t o, uint32_t p, const uint4& k0, const uint4& k1) -> bool {
             if (p >= S.cap_s) return false;
-            uint4* dst = reinterpret_cast<uint4*>(S.dspill) + (S.slow_rec0 + ((size_t)blockIdx.x * O + o) * S.cap_s + p) * 2;
-            dst[0] = k0;
-            dst[1] = k1;
+            seg_store(reinterpret_cast<uint2*>(S.dspill), S.slow_rec0 + ((size_t)blockIdx.x * O + o) * S.cap_s + p, k0, k1);
             return true;
         };
         auto ovf_put = [&](const uint4& k0, uint4 k1) {  // (rare: a key that fills its owner's whole segment)
@@ -922,6 +925,12 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             dst[0] = k0;
             dst[1] = k1;
         };
+        // a length the packed segment form cannot hold (none from 16-bit IP
+        // length fields): the overflow list, before any segment count is taken
+        if (rec && !macs && wp.x >= SEG_DOCT_MAX) {
+            ovf_put(wk, wp);
+            rec = false;
+        }
         if (bins) {
             // claim a bin slot, write the record, count it written; the lane that
             // completes a bin writes it out; a lane whose bin is full retries
@@ -943,10 +952,21 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
                 }
                 if (done != NONE32) {
                     const uint32_t p0 = own_add_n(s_scnt, done, BINS);
-                    for (uint32_t r = 0; r < BINS; r++) {
+                    // two records at a time (three 16-byte stores at an even position)
+                    for (uint32_t r = 0; r < BINS; r += 2) {
                         const uint4 k0 = s_bin[(done * BINS + r) * 2], k1 = s_bin[(done * BINS + r) * 2 + 1];
-                        if (seg_put(done, p0 + r, k0, k1)) c_seg++;
-                        else ovf_put(k0, k1);
+                        if (r + 1 < BINS && p0 + r + 1 < S.cap_s) {
+                            const uint4 j0 = s_bin[(done * BINS + r + 1) * 2], j1 = s_bin[(done * BINS + r + 1) * 2 + 1];
+                            seg_store2(reinterpret_cast<uint2*>(S.dspill),
+                                       S.slow_rec0 + ((size_t)blockIdx.x * O + done) * S.cap_s + p0 + r, k0, k1, j0, j1);
+                            c_seg += 2;
+                            continue;
+                        }
+                        for (uint32_t u = r; u < min(r + 2, BINS); u++) {
+                            const uint4 x0 = s_bin[(done * BINS + u) * 2], x1 = s_bin[(done * BINS + u) * 2 + 1];
+                            if (seg_put(done, p0 + u, x0, x1)) c_seg++;
+                            else ovf_put(x0, x1);
+                        }
                     }
                     atomicExch(&s_wr[done], 0u);  // (this lane's reads of the bin come first: LDS order)
                     atomicExch(&s_cl[done], 0u);
@@ -959,14 +979,14 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
         const uint32_t pos = rec ? own_add(s_scnt, ow) : 0u;
         const bool ovf = rec && pos >= S.cap_s;
         if (rec && !ovf) {
-            uint4* dst = reinterpret_cast<uint4*>(S.dspill) +
-                         (S.slow_rec0 + ((size_t)blockIdx.x * O + ow) * S.cap_s + pos) * (2 * spu);
-            dst[0] = wk;
+            const size_t rix = S.slow_rec0 + ((size_t)blockIdx.x * O + ow) * S.cap_s + pos;
             if (macs) {
+                uint4* dst = reinterpret_cast<uint4*>(S.dspill) + rix * (2 * spu);
+                dst[0] = wk;
                 dst[1] = wx;
                 dst[2] = wp;
             } else {
-                dst[1] = wp;
+                seg_store(reinterpret_cast<uint2*>(S.dspill), rix, wk, wp);
             }
             c_seg++;
         }
@@ -1001,10 +1021,8 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
                 const uint4 k0 = s_bin[(o * BINS + r) * 2];
                 uint4 k1 = s_bin[(o * BINS + r) * 2 + 1];
                 if (p0 + r < S.cap_s) {
-                    uint4* dst = reinterpret_cast<uint4*>(S.dspill) +
-                                 (S.slow_rec0 + ((size_t)blockIdx.x * O + o) * S.cap_s + p0 + r) * 2;
-                    dst[0] = k0;
-                    dst[1] = k1;
+                    seg_store(reinterpret_cast<uint2*>(S.dspill), S.slow_rec0 + ((size_t)blockIdx.x * O + o) * S.cap_s + p0 + r,
+                              k0, k1);
                     c_seg++;
                 } else {
                     const unsigned long long b0 = atomicAdd(&a.bc[1], 1ull);
@@ -1443,7 +1461,7 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a, MergeSrc ms) {
         for (int bi = 0; bi < ms.nb; bi++)
         for (uint32_t c0s = 0; c0s < ms.b[bi].n_sets; c0s += MCH) {
             const SegSrc& S = ms.b[bi];
-            const uint4* recs = reinterpret_cast<const uint4*>(S.dspill);
+            const uint2* recs = reinterpret_cast<const uint2*>(S.dspill);  // the packed 24-byte form (seg_pack)
             const uint32_t bshift = (uint32_t)(S.first - bfirst);  // the batch's first packet in the pass
             const uint32_t nset = min((uint32_t)MCH, S.n_sets - c0s);
             // this owner's segment of each set of the chunk: count, record base, window base
@@ -1513,8 +1531,7 @@ __global__ void __launch_bounds__(MB) k_merge_spill(AggArgs a, MergeSrc ms) {
 #pragma unroll
                 for (int u = 0; u < MS_STRIP; u++) {
                     const uint32_t idx = sd[u].x + fc[u];
-                    v0[u] = recs[(size_t)idx * 2];
-                    v1[u] = recs[(size_t)idx * 2 + 1];
+                    seg_load(recs, idx, v0[u], v1[u]);
                     wbr[u] = sd[u].y;
                 }
             };
