@@ -284,10 +284,11 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
                 } else if (pos < a.S.cap_o) {
                     const size_t rec = ((size_t)(blockIdx.x * a.S.W + win) * a.S.O + ow) * a.S.cap_o + pos;
                     if (MACS) {
-                        uint4* dst = reinterpret_cast<uint4*>(a.S.dspill) + rec * (2 * SPU);
-                        dst[0] = w_key;
-                        dst[1] = make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]);
-                        dst[2] = w_pay;
+                        uint4 pk[SEGM_U];
+                        segm_pack(w_key, make_uint4(q[u].m0, q[u].m1, q[u].m2, hk[u]), w_pay, pk);
+                        uint4* dst = reinterpret_cast<uint4*>(a.S.dspill) + rec * SEGM_U;
+#pragma unroll
+                        for (uint32_t i = 0; i < SEGM_U; i++) dst[i] = pk[i];
                     } else {
                         seg_store(reinterpret_cast<uint2*>(a.S.dspill), rec, w_key, w_pay);
                     }
@@ -768,14 +769,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int SPB_WORDS = 8192;  // LDS bins: 16-byte words (128 KiB); a record is 24 B (MACS: 64 B)
 
-// MACS (-M): the canonical MAC pair joins the key; a record is four 16-byte
-// words -- key, MAC words + hash, payload, zero (k_parse_agg<MACS>'s spills)
+// MACS (-M): the canonical MAC pair joins the key; a segment record is the
+// packed MAC form (segm_pack, kern.h: three 16-byte words), the raw overflow
+// buffer's four words -- key, MAC words + hash, payload, zero
 template <bool MACS>
 __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
     constexpr uint32_t RU = MACS ? 4u : 2u;  // 16-byte words per record (the raw overflow buffer's form)
-    // a bin record as it leaves for its owner segment: MACS four 16-byte
-    // pieces, otherwise the packed 24-byte form (seg_pack, kern.h), three 8-byte pieces
-    constexpr uint32_t PQ = MACS ? RU : SEG_Q;
+    // a bin record as it leaves for its owner segment: MACS the packed 48-byte
+    // form (three 16-byte pieces), otherwise the packed 24-byte form (three 8-byte pieces)
+    constexpr uint32_t PQ = MACS ? SEGM_U : SEG_Q;
     typedef typename std::conditional<MACS, uint4, uint2>::type Piece;
     __shared__ uint4 s_bin[SPB_WORDS];
     Piece* const s_bp = reinterpret_cast<Piece*>(s_bin);
@@ -787,19 +789,20 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
     const Stage& S = a.S;
     const Batch& B = a.B;
     const uint32_t O = S.O;
-    // records per bin: 21 (256 owners) .. 2 (2048); MACS: 8 .. 1
+    // Records per bin: a power of two, 16 (256 owners) .. 2 (2048); MACS 8 .. 1.
     // A completed bin leaves as 16-byte pieces, at most one wave's lanes of
-    // them (MACS: RU per record; otherwise the bin's BIN * 24 contiguous bytes,
-    // BIN a power of two: 16 records = 384 B = three whole 128-B lines at
-    // line-aligned segment positions)
+    // them (MACS: three per record; otherwise the bin's BIN * 24 contiguous
+    // bytes): 16 records (8 with MACS) = 384 B = three whole 128-B lines at
+    // line-aligned segment positions
     uint32_t BIN;
     if constexpr (MACS) {
-        BIN = min((uint32_t)(SPB_WORDS / RU) / O, 64u / RU);
+        const uint32_t fit = min((uint32_t)(SPB_WORDS / SEGM_U) / O, 64u / SEGM_U);
+        BIN = fit >= 1 ? 1u << (31 - __builtin_clz(fit)) : 1u;  // (O <= 2048: fit >= 1)
     } else {
         const uint32_t fit = min((uint32_t)(SPB_WORDS * 2 / SEG_Q) / O, 64u * 2 / 3);
         BIN = fit >= 2 ? 1u << (31 - __builtin_clz(fit)) : 2u;  // (O <= 2048: fit >= 2)
     }
-    const uint32_t PPB = MACS ? RU * BIN : BIN * 3 / 2;  // 16-byte pieces per bin
+    const uint32_t PPB = MACS ? SEGM_U * BIN : BIN * 3 / 2;  // 16-byte pieces per bin
     for (uint32_t o = tid; o < MAX_OWNERS; o += BLOCK) s_cl[o] = s_wr[o] = 0;
     for (uint32_t o = tid; o < OWN_WORDS; o += BLOCK) s_scnt[o] = 0;
     if (tid < 3) s_cnt[tid] = 0;
@@ -824,10 +827,15 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
         const uint32_t set = blockIdx.x * S.W + win;
         const uint32_t nch = (uint32_t)min<uint64_t>(WIN_ITERS, nsteps - ws) * WAVES;
         Piece* seg0 = reinterpret_cast<Piece*>(S.dspill) + (size_t)set * O * S.cap_o * PQ;
-        // record r of bin o, from LDS, in the 32-byte form (its piece h: the raw overflow buffer)
+        // record r of bin o, from LDS, in the raw overflow buffer's form (its word h)
         auto bin_rec = [&](uint32_t o, uint32_t r, uint32_t h) -> uint4 {
             if constexpr (MACS) {
-                return s_bin[(o * BIN + r) * RU + h];
+                uint4 uu[SEGM_U];
+#pragma unroll
+                for (uint32_t i = 0; i < SEGM_U; i++) uu[i] = s_bin[(o * BIN + r) * SEGM_U + i];
+                uint4 key, mac, pay;
+                segm_unpack(uu, key, mac, pay);
+                return h == 0 ? key : h == 1 ? mac : h == 2 ? pay : make_uint4(0, 0, 0, 0);
             } else {
                 uint2 qq[SEG_Q];
 #pragma unroll
@@ -930,11 +938,10 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                     const uint32_t slot = atomicAdd(&s_cl[o], 1u);
                     if (slot < BIN) {
                         if constexpr (MACS) {
-                            uint4* b = &s_bin[(o * BIN + slot) * RU];
-                            b[0] = w_key;
-                            b[1] = w_mac;
-                            b[2] = w_pay;
-                            b[3] = make_uint4(0, 0, 0, 0);
+                            uint4 uu[SEGM_U];
+                            segm_pack(w_key, w_mac, w_pay, uu);
+#pragma unroll
+                            for (uint32_t i = 0; i < SEGM_U; i++) s_bin[(o * BIN + slot) * SEGM_U + i] = uu[i];
                         } else {
                             uint2 qq[SEG_Q];
                             seg_pack(w_key, w_pay, qq);
@@ -959,14 +966,18 @@ __global__ void __launch_bounds__(BLOCK) k_parse_spill(AggArgs a) {
                     const uint32_t src = act ? (uint32_t)__builtin_ctzll(m) : 0u;
                     const uint32_t bo = __shfl(done, src, 64), bp = __shfl(pos, src, 64);
                     if constexpr (MACS) {
-                        const uint32_t r = pc / RU, hh = pc % RU;
+                        const uint32_t r = pc / SEGM_U, hh = pc % SEGM_U;
                         const bool ovf = act && bp + r >= S.cap_o;
                         uint32_t q = 0;  // (the overflow slot: from the record's first lane, every lane shuffling)
                         if (ovf && hh == 0) q = atomicAdd(&s_nspill, 1u);
-                        q = __shfl(q, lane & ~(RU - 1), 64);
+                        q = __shfl(q, lane - hh, 64);
                         if (act) {
-                            if (!ovf) seg0[((size_t)bo * S.cap_o + bp + r) * RU + hh] = s_bin[(bo * BIN + r) * RU + hh];
-                            else overflow(q, hh, s_bin[(bo * BIN + r) * RU + hh]);  // past the segment's capacity
+                            if (!ovf) {
+                                seg0[((size_t)bo * S.cap_o + bp + r) * SEGM_U + hh] = s_bin[(bo * BIN + r) * SEGM_U + hh];
+                            } else {  // past the segment's capacity: the raw buffer's four words
+                                overflow(q, hh, bin_rec(bo, r, hh));
+                                if (hh == 0) overflow(q, 3, make_uint4(0, 0, 0, 0));
+                            }
                         }
                     } else {
                         // the whole bin inside the segment (an even capacity keeps

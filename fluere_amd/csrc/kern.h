@@ -127,8 +127,24 @@ __device__ __forceinline__ void seg_load(const uint2* seg, size_t rec, uint4& ke
     for (uint32_t i = 0; i < SEG_Q; i++) q[i] = seg[rec * SEG_Q + i];
     seg_unpack(q, key, pay);
 }
-// MAC kernels: a spilled packet takes two records: {k0, k1, k2, tag},
+// MAC runs: in an owner segment a spilled packet is 48 bytes, three 16-byte
+// words -- the packed form's 24 bytes, then {m0, m1}, {m2, key hash}, 8 zero
+// bytes (a bin of 8 records: 384 B, three 128-B lines); the raw buffers and
+// the overflow list keep 64 bytes: {k0, k1, k2, tag},
 // {m0, m1, m2, key hash}, {doct, pt, loc, fl}, padding.
+constexpr uint32_t SEGM_U = 3;  // 16-byte words per packed MAC record
+__host__ __device__ __forceinline__ void segm_pack(const uint4& key, const uint4& mac, const uint4& pay, uint4 (&u)[SEGM_U]) {
+    uint2 q[SEG_Q];
+    seg_pack(key, pay, q);
+    u[0] = make_uint4(q[0].x, q[0].y, q[1].x, q[1].y);
+    u[1] = make_uint4(q[2].x, q[2].y, mac.x, mac.y);
+    u[2] = make_uint4(mac.z, mac.w, 0u, 0u);
+}
+__host__ __device__ __forceinline__ void segm_unpack(const uint4 (&u)[SEGM_U], uint4& key, uint4& mac, uint4& pay) {
+    const uint2 q[SEG_Q] = {make_uint2(u[0].x, u[0].y), make_uint2(u[0].z, u[0].w), make_uint2(u[1].x, u[1].y)};
+    seg_unpack(q, key, pay);
+    mac = make_uint4(u[1].z, u[1].w, u[2].x, u[2].y);
+}
 __host__ __device__ constexpr int spill_units(bool macs) { return macs ? 2 : 1; }
 
 struct Stage {

@@ -351,13 +351,14 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                 };
                 // one record ahead: the next iteration's record is loaded
                 // while this one is probed and aggregated in LDS
-                // (MACS: four 16-byte words per record; otherwise the packed 24-byte form)
+                // (MACS: the packed 48-byte form; otherwise the packed 24-byte form)
                 auto load_rec = [&](size_t rix, uint4& k, uint4& p, uint4& x) {
                     if constexpr (MACS) {
-                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + rix * 4;
-                        k = src[0];
-                        x = src[1];
-                        p = src[2];
+                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + rix * SEGM_U;
+                        uint4 uu[SEGM_U];
+#pragma unroll
+                        for (uint32_t i = 0; i < SEGM_U; i++) uu[i] = src[i];
+                        segm_unpack(uu, k, x, p);
                     } else {
                         seg_load(reinterpret_cast<const uint2*>(S.dspill), rix, k, p);
                     }
@@ -474,9 +475,12 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     part_of_stage(p, base, f);
                 } else {
                     const size_t o = (size_t)m_lo[lo_i] + (idx - m_start[lo_i]);
-                    if (macs) {  // {key}, {MAC words, hash}, {payload}
-                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)4;
-                        const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+                    if (macs) {  // the packed MAC form (segm_pack)
+                        const uint4* src = reinterpret_cast<const uint4*>(S.dspill) + o * (size_t)SEGM_U;
+                        uint4 uu[SEGM_U], v0, v1, v2;
+#pragma unroll
+                        for (uint32_t i = 0; i < SEGM_U; i++) uu[i] = src[i];
+                        segm_unpack(uu, v0, v1, v2);
                         k0 = v0.x; k1 = v0.y; k2 = v0.z; tag = v0.w;
                         x0 = v1.x; x1 = v1.y; x2 = v1.z;
                         h = v1.w;
@@ -925,9 +929,10 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             dst[0] = k0;
             dst[1] = k1;
         };
-        // a length the packed segment form cannot hold (none from 16-bit IP
+        // a length the packed segment forms cannot hold (none from 16-bit IP
         // length fields): the overflow list, before any segment count is taken
-        if (rec && !macs && wp.x >= SEG_DOCT_MAX) {
+        const bool big = rec && wp.x >= SEG_DOCT_MAX;
+        if (big && bins) {
             ovf_put(wk, wp);
             rec = false;
         }
@@ -976,15 +981,16 @@ __global__ void __launch_bounds__(SB) k_slow(AggArgs a) {
             if (pend) atomicOr(a.T.err, ERR_SPIN);  // (cannot happen: a full bin's completer empties it)
             continue;
         }
-        const uint32_t pos = rec ? own_add(s_scnt, ow) : 0u;
-        const bool ovf = rec && pos >= S.cap_s;
+        const uint32_t pos = rec && !big ? own_add(s_scnt, ow) : 0u;
+        const bool ovf = rec && (big || pos >= S.cap_s);
         if (rec && !ovf) {
             const size_t rix = S.slow_rec0 + ((size_t)blockIdx.x * O + ow) * S.cap_s + pos;
-            if (macs) {
-                uint4* dst = reinterpret_cast<uint4*>(S.dspill) + rix * (2 * spu);
-                dst[0] = wk;
-                dst[1] = wx;
-                dst[2] = wp;
+            if (macs) {  // the packed MAC form (segm_pack)
+                uint4 uu[SEGM_U];
+                segm_pack(wk, wx, wp, uu);
+                uint4* dst = reinterpret_cast<uint4*>(S.dspill) + rix * SEGM_U;
+#pragma unroll
+                for (uint32_t i = 0; i < SEGM_U; i++) dst[i] = uu[i];
             } else {
                 seg_store(reinterpret_cast<uint2*>(S.dspill), rix, wk, wp);
             }
