@@ -989,12 +989,16 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     static const uint32_t o_min = getenv("FLUERE_MIN_OWNERS") ? (uint32_t)atoi(getenv("FLUERE_MIN_OWNERS")) : 256u;
     uint32_t o = o_min;
     while (o < (uint32_t)MAX_OWNERS && c->last_nf > 870ull * o) o *= 2;
+    // between two powers of two: the smallest multiple of 256 owners whose mean
+    // share stays <= 800 flows (1M flows: 1280 owners, bins of 4 records, not
+    // 2048 owners with bins of 2)
+    const uint64_t alt = ((c->last_nf + 799) / 800 + 255) / 256 * 256;
+    if (alt > o_min && alt < o) o = (uint32_t)alt;
     static const int o_max = getenv("FLUERE_MAX_OWNERS") ? atoi(getenv("FLUERE_MAX_OWNERS")) : MAX_OWNERS;  // diagnostics
     const int cap = std::min(o_max, c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS);
-    // a power of two: k_parse_spill writes a wave's completed bins in groups of
-    // 64 / (3 * BIN) lanes with BIN = 5461 / O (a CU count such as 304 rounds up)
-    uint32_t r = (uint32_t)std::max(1, std::min(std::max((int)o, c->n_cu), cap));
-    while (r & (r - 1)) r += r & (~r + 1);
+    // even: the flush's per-owner counters are 16-bit pairs (a CU count such as 304 stays)
+    uint32_t r = (uint32_t)std::max(2, std::min(std::max((int)o, c->n_cu), cap));
+    r = (r + 1) & ~1u;
     return std::min<uint32_t>(r, (uint32_t)MAX_OWNERS);
 }
 
@@ -1255,7 +1259,7 @@ static int spill_mode(const fluere_ctx* c) {
     return F * (1.0 - std::exp(-w / F)) > 2.0 * (c->use_mac ? NS_MAC : NS) ? 1 : 0;
 }
 
-// k_merge_spill for the runs without partials (not MAC runs: their 64-byte
+// k_merge_spill for the runs without partials (not MAC runs: their 48-byte
 // records stay with k_merge_partials); FLUERE_LEAN_MERGE=0: k_merge_partials
 // for every run (A/B)
 static int lean_merge(const fluere_ctx* c) {
