@@ -670,7 +670,8 @@ unsigned flow_grid(fluere_ctx* c) {
 // k_finalize): grid-stride over n flows with at most 4 workgroups per CU, so
 // a million-flow run counts ~1k workgroups done on the one word, not ~4k.
 unsigned done_grid(fluere_ctx* c, uint64_t n) {
-    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->n_cu * 4));
+    static const uint64_t wpc = getenv("FLUERE_DONE_WPC") ? std::max(1, atoi(getenv("FLUERE_DONE_WPC"))) : 4;  // (A/B)
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->n_cu * wpc));
 }
 
 // Sequential clear of the IPv4 chain's tables when the flows to clear would
