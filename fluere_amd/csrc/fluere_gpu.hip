@@ -1333,10 +1333,17 @@ static int enqueue_batches(fluere_ctx* c, const PassPlan& P) {
         const auto t0 = std::chrono::steady_clock::now();
         hipEvent_t e0 = c->evh[2 * i], e1 = c->evh[2 * i + 1];
         static const int ev_abl = diag_knob("FLUERE_EV_ABL");  // diagnostics: 1 no timing events (kernel_ms invalid)
-        if (grid && ev_abl == 1)
+        // FLUERE_EV_REC=1 (A/B): the events recorded on the stream around a plain launch
+        static const bool ev_rec = getenv("FLUERE_EV_REC") && atoi(getenv("FLUERE_EV_REC")) != 0;
+        if (grid && ev_abl == 1) {
             HIPCHECK(hipLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s));
-        else if (grid)
+        } else if (grid && ev_rec) {
+            HIPCHECK(hipEventRecord(e0, s));
+            HIPCHECK(hipLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s));
+            HIPCHECK(hipEventRecord(e1, s));
+        } else if (grid) {
             HIPCHECK(hipExtLaunchKernel(fn, dim3(grid), dim3(BLOCK), args, 0, s, e0, e1, 0));
+        }
         const auto t1 = std::chrono::steady_clock::now();
         // the slow list into k_slow's owner segments, before the merge reads them
         // (every packet without a hot kernel: k_slow carries the timing events)
