@@ -2045,7 +2045,8 @@ int exact_finish(ExactSession* S, const Seed* seeds, unsigned long long* aux_out
     // The instances whose creating packet needs the general parser are listed
     // by the first kernel and done by the second (grid-stride over the count).
     if (n_inst) {
-        k_ex_records_t<false><<<std::min<unsigned>(gridn(n_inst, 256), 1024), 256, 0, s>>>(ra);
+        static const unsigned rec_wgs = getenv("FLUERE_REC_WGS") ? (unsigned)std::max(1, atoi(getenv("FLUERE_REC_WGS"))) : 1024u;  // (A/B)
+        k_ex_records_t<false><<<std::min<unsigned>(gridn(n_inst, 256), rec_wgs), 256, 0, s>>>(ra);
         k_ex_records_t<true><<<std::min<unsigned>(gridn(n_inst, 256), 64), 256, 0, s>>>(ra);
     }
     HIPCHECK(hipGetLastError());
