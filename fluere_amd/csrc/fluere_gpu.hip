@@ -998,7 +998,9 @@ static uint32_t merge_owners(const fluere_ctx* c) {
     static const int o_max = getenv("FLUERE_MAX_OWNERS") ? atoi(getenv("FLUERE_MAX_OWNERS")) : MAX_OWNERS;  // diagnostics
     const int cap = std::min(o_max, c->use_mac ? std::min(FLUERE_MAC_OWNERS, MAX_OWNERS) : MAX_OWNERS);
     // even: the flush's per-owner counters are 16-bit pairs (a CU count such as 304 stays)
-    uint32_t r = (uint32_t)std::max(2, std::min(std::max((int)o, c->n_cu), cap));
+    // (at least one per CU, unless FLUERE_MIN_OWNERS sets the floor itself)
+    const int floor_o = getenv("FLUERE_MIN_OWNERS") ? (int)o_min : c->n_cu;
+    uint32_t r = (uint32_t)std::max(2, std::min(std::max((int)o, floor_o), cap));
     r = (r + 1) & ~1u;
     return std::min<uint32_t>(r, (uint32_t)MAX_OWNERS);
 }
