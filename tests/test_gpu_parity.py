@@ -164,6 +164,23 @@ def test_spill_overflow_list(gpu, name, monkeypatch):
     assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
 
 
+@pytest.mark.parametrize("name", ["c3_imix_small", "c5u_mac_small", "many_flows", "slow_many_flows"])
+@pytest.mark.parametrize("cap", ["40", "41"])
+def test_spill_bins_straddle_capacity(gpu, name, cap, monkeypatch):
+    """k_parse_spill's packed records (seg.h): with 40 records a segment the
+    first full bins of an owner leave whole (16-byte pieces of 16 x 24-B or
+    8 x 48-B records) and a later one straddles the capacity (its first
+    records into the segment, the rest to the overflow list, record by
+    record); 41 (odd) sends every bin record by record."""
+    monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
+    monkeypatch.setenv("FLUERE_OWNER_CAP", cap)
+    kind, n, f, seed, use_mac = SYNTH[name]
+    data = fluere_amd.synth_pcap(fluere_amd.synth_cfg(kind, n, f, seed))
+    want = pyoracle.offline(data, use_mac=use_mac)
+    csv, ne, st = _gpu_csv(data, use_mac=use_mac, max_flows=max(1 << 16, 2 * f))
+    assert_csv_equal(csv, ne, want["csv"], want["n_ended"], name)
+
+
 @pytest.mark.parametrize("name", ["c1_udp64_1flow", "c2_udp64_small", "c3_imix_small", "many_flows", "slow_small",
                                   "slow_many_flows", "c3_imix_2m", "c5u_mac_small", "c5_vlan_small", "slow_mac"])
 @pytest.mark.parametrize("cap", [None, "3"])
@@ -171,7 +188,7 @@ def test_spill_kernel_matches_oracle(gpu, name, cap, monkeypatch):
     """k_parse_spill (the hot pass for many flows per window: every valid
     packet through the per-owner LDS bins into its owner's segment, full bins
     written out by the wave) forced on every capture kind -- MAC keys (-M)
-    with 64-byte records -- also with owner segments of 3 records (nearly
+    with 48-byte records -- also with owner segments of 3 records (nearly
     every record through the overflow list)."""
     monkeypatch.setenv("FLUERE_SPILL_MODE", "1")
     if cap:
