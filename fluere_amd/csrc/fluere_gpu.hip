@@ -1206,7 +1206,7 @@ static int plan_batches(fluere_ctx* c, PassPlan& P, bool allow_pid = true) {
         S.dspill = (Spill*)(S.part + cells);
         S.spill_raw = S.dspill + (sets * O * S.cap_o + (size_t)n_slow_sets * O * cap_s) * spill_units(c->use_mac);
         S.spill = S.spill_raw + (size_t)grid * SPILL_WG * spill_units(c->use_mac);
-        S.spill_cap = hb.b.n;  // records (32 B, or 64 B with MACs)
+        S.spill_cap = hb.b.n;  // overflow-list records (32 B, or 64 B with MACs; the segments' are packed, seg.h)
         S.base = (unsigned long long*)(S.spill + hb.b.n * spill_units(c->use_mac));
         S.off = (uint32_t*)(S.base + all);
         S.soff = S.off + (size_t)(O + 1) * all;

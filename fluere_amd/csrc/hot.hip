@@ -260,8 +260,8 @@ __global__ void __launch_bounds__(BLOCK) k_parse_agg(AggArgs a) {
 #pragma unroll
         for (int u = 0; u < PK; u++) {
             agg[u] = q[u].valid & (q[u].state == 1) & (q[u].slot < NSL);
-            // a valid packet whose key has no LDS slot spills: a 32-byte record
-            // (64 with MACs) straight into its merge owner's segment of this
+            // a valid packet whose key has no LDS slot spills: a packed 24-byte
+            // record (48 with MACs; seg.h) straight into its merge owner's segment of this
             // set; past the segment's capacity, to this workgroup's raw
             // overflow buffer (wave-aggregated append; listed at the flush)
             const bool miss = q[u].valid & !agg[u];

@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(MB) k_merge_partials(AggArgs a) {
                     }
             };
             if (pass == 1) {
-                // Spilled packets, the lean path (MAC runs: 64-byte records,
+                // Spilled packets, the lean path (MAC runs: 48-byte records,
                 // the MAC words and the hash beside the key): the merge is
                 // instruction-bound (PMC on C3: 28 % of wave time issuing at
                 // 4 waves per SIMD, 14k VALU + 7k SALU instructions per wave),
@@ -1303,11 +1303,12 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
 
 // ---------------------------------------------------------------------------
 // k_merge_spill: the owner merge of runs whose hot pass staged no partials
-// (k_parse_spill, k_slow): every record is one packet (Spill, 32 B) in its
-// owner's segment of a set.  Lean per record, and loads kept in flight:
+// (k_parse_spill, k_slow): every record is one packet (packed 24 B, seg.h) in
+// its owner's segment of a set.  Lean per record, and loads kept in flight:
 //  * an owner's segments of a chunk of sets are flattened (exclusive scan of
-//    their counts); a wave takes strips of 256 consecutive flattened records,
-//    four per lane, all eight 16-byte loads issued before the first is used;
+//    their counts); a wave takes strips of 128 consecutive flattened records,
+//    two per lane, and the next strip's loads are issued before this one is
+//    probed and aggregated;
 //  * a record's set comes from a 64-record group map (every lane of a
 //    64-aligned group starts from the same set) and a forward step;
 //  * one LDS read per record gives the segment's record base and the window's
