@@ -1306,8 +1306,8 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
 // (k_parse_spill, k_slow): every record is one packet (packed 24 B, seg.h) in
 // its owner's segment of a set.  Lean per record, and loads kept in flight:
 //  * an owner's segments of a chunk of sets are flattened (exclusive scan of
-//    their counts); a wave takes strips of 128 consecutive flattened records,
-//    two per lane, and the next strip's loads are issued before this one is
+//    their counts); a wave takes strips of 64 consecutive flattened records,
+//    one per lane, and the next strip's loads are issued before this one is
 //    probed and aggregated;
 //  * a record's set comes from a 64-record group map (every lane of a
 //    64-aligned group starts from the same set) and a forward step;
@@ -1322,7 +1322,7 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
 // chain (dense_of_key, up to 12 levels) puts tens of KiB of code between the
 // instructions of the record loop.
 #ifndef FLUERE_MS_STRIP
-#define FLUERE_MS_STRIP 2
+#define FLUERE_MS_STRIP 1  // records per lane per strip (r06: 1 -- no spills, 121 VGPRs -- beat 2 by 5 us on C3, 20 on C4)
 #endif
 #ifndef FLUERE_MS_BATCH
 #define FLUERE_MS_BATCH 1  // the strip's first probes issued together (0: each record's probe loop alone; A/B)
